@@ -1,0 +1,132 @@
+"""ctypes binding of the C-ABI library libfgp_hip.so (include/fgp_hip.h).
+
+The library is built in-tree by `python -m fastgaussianprocesses_amd.build` (or
+__graft_entry__.build()) into fastgaussianprocesses_amd/_lib/.  There is no fallback: if the
+library is missing or a call fails, a RuntimeError is raised.
+"""
+import ctypes
+import os
+import threading
+
+import torch
+
+_LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
+LIB_PATH = os.path.join(_LIB_DIR, "libfgp_hip.so")
+ABI_VERSION = 2
+
+_lock = threading.Lock()
+_lib = None
+
+_c_i64 = ctypes.c_int64
+_c_int = ctypes.c_int
+_c_dbl = ctypes.c_double
+_c_vp = ctypes.c_void_p
+
+_c_pi = ctypes.POINTER(ctypes.c_int)
+_c_pd = ctypes.POINTER(ctypes.c_double)
+
+
+class NllDesc(ctypes.Structure):
+    """Mirror of fgp_nll_desc (include/fgp_hip.h)."""
+    _fields_ = [
+        ("family", _c_int), ("log2n", _c_int), ("d", _c_int), ("G", _c_int),
+        ("parts", _c_vp), ("parts_stride", _c_i64),
+        ("ysq", _c_vp), ("ysq_stride", _c_i64),
+        ("raw", _c_vp),
+        ("scale_off", _c_int), ("scale_pp", _c_int),
+        ("ls_off", _c_int), ("ls_pp", _c_int), ("ls_pd", _c_int),
+        ("noise_off", _c_int), ("noise_pp", _c_int),
+        ("logdet_weight", _c_dbl),
+        ("grad_lam", _c_vp), ("work", _c_vp), ("partials", _c_vp),
+    ]
+
+
+class FitDesc(ctypes.Structure):
+    """Mirror of fgp_fit_desc (include/fgp_hip.h)."""
+    _fields_ = [
+        ("n_params", _c_int),
+        ("raw", _c_vp), ("rprop_prev", _c_vp), ("rprop_step", _c_vp), ("grad_out", _c_vp),
+        ("loss_hist", _c_vp), ("raw_hist", _c_vp),
+        ("scale_rg", _c_int), ("ls_rg", _c_int), ("noise_rg", _c_int),
+        ("mll_const", _c_dbl), ("eta_minus", _c_dbl), ("eta_plus", _c_dbl),
+        ("step_min", _c_dbl), ("step_max", _c_dbl),
+    ]
+
+
+_P_NLL = ctypes.POINTER(NllDesc)
+_P_FIT = ctypes.POINTER(FitDesc)
+
+# name -> argtypes (all return int status); must match include/fgp_hip.h
+_SIGNATURES = {
+    "fgp_init": [_c_vp],
+    "fgp_fftbr": [_c_vp, _c_i64, _c_int, _c_vp, _c_i64, _c_int, _c_int, _c_vp],
+    "fgp_ifftbr": [_c_vp, _c_i64, _c_vp, _c_int, _c_vp, _c_i64, _c_int, _c_int, _c_vp],
+    "fgp_fwht": [_c_vp, _c_i64, _c_vp, _c_i64, _c_int, _c_int, _c_vp],
+    "fgp_lattice_parts": [_c_vp, _c_i64, _c_vp, _c_i64, _c_int, _c_pi, _c_pd, _c_vp, _c_vp],
+    "fgp_net_parts": [_c_vp, _c_i64, _c_vp, _c_i64, _c_int, _c_int, _c_vp, _c_vp],
+    "fgp_nll_fwd": [_P_NLL, _c_vp],
+    "fgp_nll_bwd": [_P_NLL, _c_vp],
+    "fgp_fit_step": [_P_NLL, _P_FIT, _c_int, _c_int, _c_vp],
+    "fgp_fit_run": [_P_NLL, _P_FIT, _c_int, _c_int, _c_int, _c_vp],
+    "fgp_post_mean": [_c_int, _c_vp, _c_i64, _c_vp, _c_i64, _c_int, _c_int, _c_pi, _c_pd, _c_vp, _c_int, _c_vp,
+                      _c_i64, _c_int, _c_vp, _c_i64, _c_vp, _c_i64, _c_vp],
+    "fgp_kernel_rows": [_c_int, _c_vp, _c_i64, _c_vp, _c_i64, _c_int, _c_int, _c_pi, _c_pd, _c_vp, _c_int, _c_vp,
+                        _c_vp],
+}
+
+
+def int_array(vals):
+    return (ctypes.c_int * max(1, len(vals)))(*[int(v) for v in vals])
+
+
+def double_array(vals):
+    return (ctypes.c_double * max(1, len(vals)))(*[float(v) for v in vals])
+
+
+def _load():
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.isfile(LIB_PATH):
+            raise RuntimeError(
+                "fastgaussianprocesses_amd: native library %s is missing; build it with "
+                "`python -m fastgaussianprocesses_amd.build` (hipcc, gfx950). There is no CPU fallback." % LIB_PATH)
+        lib = ctypes.CDLL(LIB_PATH)
+        lib.fgp_last_error.restype = ctypes.c_char_p
+        lib.fgp_abi_version.restype = ctypes.c_int
+        if lib.fgp_abi_version() != ABI_VERSION:
+            raise RuntimeError("libfgp_hip.so ABI version %d != expected %d; rebuild"
+                               % (lib.fgp_abi_version(), ABI_VERSION))
+        for name, argt in _SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.argtypes = argt
+            fn.restype = ctypes.c_int
+        _lib = lib
+        return lib
+
+
+def lib():
+    return _lib if _lib is not None else _load()
+
+
+def exported_symbols():
+    return ["fgp_abi_version", "fgp_last_error"] + list(_SIGNATURES.keys())
+
+
+def call(name, *args):
+    """Invoke a C-ABI entry point; raise RuntimeError with the library's message on failure."""
+    L = lib()
+    rc = getattr(L, name)(*args)
+    if rc != 0:
+        msg = L.fgp_last_error().decode(errors="replace")
+        raise RuntimeError("%s failed (%d): %s" % (name, rc, msg))
+    return rc
+
+
+def stream_ptr(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)

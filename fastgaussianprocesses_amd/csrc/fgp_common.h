@@ -1,0 +1,235 @@
+// Shared device code for the fast-transform GP kernels (gfx950 / CDNA4).
+//
+// Transform engine: every in-LDS transform works on a 4096-element tile per 256-thread workgroup
+// (16 elements per thread, 4 wave64s).  A length-L = 2^P transform (4 <= P <= 12) is run by
+// TL = L/16 threads; a tile holds 4096/L such transforms (rows or columns of a larger transform).
+//
+//   forward  (fftbr, qmcpy.fftbr_torch):  bit-reversed-order input, natural-order output  = radix-2
+//            DIT network  x[a], x[a+h] <- x[a] + w x[a+h], x[a] - w x[a+h],  w = exp(-2 pi i pos/2h)
+//   adjoint  (ifftbr, qmcpy.ifftbr_torch): the exact transpose-conjugate of that network = DIF with
+//            conj twiddles, natural input, bit-reversed output.
+//   WHT      (fwht, qmcpy.fwht_torch): same network with w = 1 (self-adjoint, Sylvester order).
+//
+// Stages are executed as radix-16 register passes (4 radix-2 stages per LDS round trip).
+// LDS index padding i + (i >> 4) keeps every pass's 16-byte (double2) / 8-byte (double) accesses
+// bank-conflict free.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fgp {
+
+constexpr int kWG = 256;         // threads per workgroup
+constexpr int kTileLog = 12;
+constexpr int kTile = 1 << kTileLog;   // elements per workgroup tile
+constexpr int kLds = 4608;       // >= every padded tile layout used below (max 4480)
+
+__device__ __forceinline__ int padi(int i) { return i + (i >> 4); }
+
+// ---------------------------------------------------------------- scalar / complex arithmetic
+__device__ __forceinline__ double2 operator+(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ double2 operator-(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ double2 operator*(double2 a, double s) { return make_double2(a.x * s, a.y * s); }
+__device__ __forceinline__ double2& operator+=(double2& a, double2 b) { a.x += b.x; a.y += b.y; return a; }
+__device__ __forceinline__ double2& operator-=(double2& a, double2 b) { a.x -= b.x; a.y -= b.y; return a; }
+__device__ __forceinline__ double2 cmul(double2 a, double2 b) {
+  return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ double2 cmulc(double2 a, double2 w) {  // a * conj(w)
+  return make_double2(a.x * w.x + a.y * w.y, a.y * w.x - a.x * w.y);
+}
+
+template <typename T> __device__ __forceinline__ T zero_v();
+template <> __device__ __forceinline__ double zero_v<double>() { return 0.0; }
+template <> __device__ __forceinline__ double2 zero_v<double2>() { return make_double2(0.0, 0.0); }
+
+// ---------------------------------------------------------------- butterflies
+// tw = exp(-2 pi i k / 4096), k < 4096 (full circle); a stage of span 2h = 2^(s+1) uses
+// w = exp(-2 pi i pos / 2h) = tw[pos << (11 - s)].
+__device__ __forceinline__ void bfly_dit(double2& a, double2& b, const double2* __restrict__ tw, int k) {
+  const double2 bw = cmul(b, tw[k]);
+  b = a - bw;
+  a = a + bw;
+}
+__device__ __forceinline__ void bfly_dit(double& a, double& b, const double2* __restrict__, int) {
+  const double t = a;
+  a = t + b;
+  b = t - b;
+}
+__device__ __forceinline__ void bfly_dif(double2& a, double2& b, const double2* __restrict__ tw, int k) {
+  const double2 d = a - b;
+  a = a + b;
+  b = cmulc(d, tw[k]);
+}
+__device__ __forceinline__ void bfly_dif(double& a, double& b, const double2* __restrict__, int) {
+  const double t = a;
+  a = t + b;
+  b = t - b;
+}
+
+// One radix-2^RL register pass over stages [S, S+RL) of a length-2^P transform held in LDS
+// (padded layout, base pointer s), run by TL = 2^P/16 threads (tt = thread index in the group).
+template <int P, int S, int RL, bool ADJ, typename T>
+__device__ __forceinline__ void lds_pass(T* s, int tt, const double2* __restrict__ tw) {
+  constexpr int R = 1 << RL;
+  constexpr int GPT = 16 / R;      // register groups per thread
+  constexpr int TL = (1 << P) / 16;
+#pragma unroll
+  for (int j = 0; j < GPT; ++j) {
+    const int q = tt + j * TL;
+    const int blo = q & ((1 << S) - 1);
+    const int base = blo + ((q >> S) << (S + RL));
+    T v[R];
+#pragma unroll
+    for (int t = 0; t < R; ++t) v[t] = s[padi(base + (t << S))];
+    if constexpr (!ADJ) {
+#pragma unroll
+      for (int q2 = 0; q2 < RL; ++q2) {
+#pragma unroll
+        for (int t = 0; t < R; ++t) {
+          if (t & (1 << q2)) continue;
+          const int pos = blo + ((t & ((1 << q2) - 1)) << S);
+          bfly_dit(v[t], v[t | (1 << q2)], tw, pos << (11 - S - q2));
+        }
+      }
+    } else {
+#pragma unroll
+      for (int q2 = RL - 1; q2 >= 0; --q2) {
+#pragma unroll
+        for (int t = 0; t < R; ++t) {
+          if (t & (1 << q2)) continue;
+          const int pos = blo + ((t & ((1 << q2) - 1)) << S);
+          bfly_dif(v[t], v[t | (1 << q2)], tw, pos << (11 - S - q2));
+        }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < R; ++t) s[padi(base + (t << S))] = v[t];
+  }
+}
+
+template <int P, int S, typename T>
+__device__ __forceinline__ void lds_dit_all(T* s, int tt, const double2* __restrict__ tw) {
+  if constexpr (S < P) {
+    constexpr int RL = (P - S) < 4 ? (P - S) : 4;
+    lds_pass<P, S, RL, false>(s, tt, tw);
+    __syncthreads();
+    lds_dit_all<P, S + 4>(s, tt, tw);
+  }
+}
+
+template <int P, int S, typename T>
+__device__ __forceinline__ void lds_dif_all(T* s, int tt, const double2* __restrict__ tw) {
+  constexpr int RL = (P - S) < 4 ? (P - S) : 4;
+  lds_pass<P, S, RL, true>(s, tt, tw);
+  __syncthreads();
+  if constexpr (S >= 4) lds_dif_all<P, S - 4>(s, tt, tw);
+}
+
+// Full in-LDS transform of length 2^P (4 <= P <= 12).  Caller syncs before; ends with a sync.
+template <int P, bool ADJ, typename T>
+__device__ __forceinline__ void lds_transform(T* s, int tt, const double2* __restrict__ tw) {
+  static_assert(P >= 4 && P <= 12, "in-LDS transforms cover 2^4..2^12");
+  if constexpr (ADJ) {
+    lds_dif_all<P, ((P - 1) / 4) * 4>(s, tt, tw);
+  } else {
+    lds_dit_all<P, 0>(s, tt, tw);
+  }
+}
+
+// ---------------------------------------------------------------- reductions
+__device__ __forceinline__ double shfl_xor_d(double v, int o) { return __shfl_xor(v, o, 64); }
+__device__ __forceinline__ double2 shfl_xor_d(double2 v, int o) {
+  return make_double2(__shfl_xor(v.x, o, 64), __shfl_xor(v.y, o, 64));
+}
+
+// Sum over a group of TL consecutive threads (TL a power of two, groups aligned to TL).
+// Every thread of the group receives the total.  `red` is LDS scratch of >= kWG/64 entries.
+// Must be called by all threads of the workgroup (contains barriers when TL > 64).
+template <int TL, typename T>
+__device__ __forceinline__ T group_sum(T v, T* red) {
+  if constexpr (TL <= 64) {
+#pragma unroll
+    for (int o = TL / 2; o > 0; o >>= 1) v += shfl_xor_d(v, o);
+    return v;
+  } else {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += shfl_xor_d(v, o);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    constexpr int NW = TL / 64;
+    const int g0 = (w / NW) * NW;
+    T tot = red[g0];
+#pragma unroll
+    for (int i = 1; i < NW; ++i) tot += red[g0 + i];
+    __syncthreads();
+    return tot;
+  }
+}
+
+// Whole-workgroup sum of a double (result valid in every thread).
+__device__ __forceinline__ double block_sum(double v, double* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  double tot = 0.0;
+#pragma unroll
+  for (int i = 0; i < kWG / 64; ++i) tot += red[i];
+  __syncthreads();
+  return tot;
+}
+
+__device__ __forceinline__ unsigned brev_bits(unsigned u, int bits) {
+  return bits == 0 ? 0u : (__builtin_bitreverse32(u) >> (32 - bits));
+}
+
+// ---------------------------------------------------------------- generic element I/O
+template <typename T> __device__ __forceinline__ T load_in(const void* p, int64_t i, int in_real);
+template <> __device__ __forceinline__ double2 load_in<double2>(const void* p, int64_t i, int in_real) {
+  if (in_real) return make_double2(static_cast<const double*>(p)[i], 0.0);
+  return static_cast<const double2*>(p)[i];
+}
+template <> __device__ __forceinline__ double load_in<double>(const void* p, int64_t i, int) {
+  return static_cast<const double*>(p)[i];
+}
+
+__device__ __forceinline__ void store_out(void* p, int64_t i, double2 v, int out_real) {
+  if (out_real) static_cast<double*>(p)[i] = v.x;
+  else static_cast<double2*>(p)[i] = v;
+}
+__device__ __forceinline__ void store_out(void* p, int64_t i, double v, int) { static_cast<double*>(p)[i] = v; }
+
+template <typename T> __device__ __forceinline__ T tw_mul(T v, double2 w, bool conj);
+template <> __device__ __forceinline__ double2 tw_mul<double2>(double2 v, double2 w, bool conj) {
+  return conj ? cmulc(v, w) : cmul(v, w);
+}
+template <> __device__ __forceinline__ double tw_mul<double>(double v, double2, bool) { return v; }
+
+
+// Centre (optional) -> in-LDS transform -> add the mean back to bin 0, for one length-2^P
+// transform at LDS base s run by TL = 2^P/16 threads.  Caller syncs before; ends synced.
+// The mean-centring mirrors AbstractFastGP.ft/ift (abstract_fast_gp.py:209-211, 225-227).
+template <int P, bool ADJ, typename T>
+__device__ __forceinline__ void center_transform(T* s, int tt, int stable, T* red, const double2* __restrict__ tw) {
+  constexpr int L = 1 << P;
+  constexpr int TL = L / 16;
+  T mean = zero_v<T>();
+  if (stable) {
+    T acc = zero_v<T>();
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc += s[padi(tt + j * TL)];
+    mean = group_sum<TL>(acc, red) * (1.0 / L);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) s[padi(tt + j * TL)] -= mean;
+    __syncthreads();
+  }
+  lds_transform<P, ADJ>(s, tt, tw);
+  if (stable && tt == 0) s[0] += mean * (double)L;
+  __syncthreads();
+}
+
+}  // namespace fgp

@@ -1,0 +1,663 @@
+// Fused fit path: kernel parts, MLL forward (k1 -> lambda -> eigenvalue terms), adjoint backward
+// (gradient w.r.t. raw scale / lengthscales / noise) and the Rprop step, all on device.
+//
+// Reference path replaced (single task, beta=kappa=0, loss_metric="MLL"):
+//   k1     = scale * prod_j(1 + l_j parts_j)                  fastgps/abstract_fast_gp.py:181-191
+//   lam    = ft(k1)                                           fastgps/util.py:102-112
+//   ev     = sqrt(n) lam + noise; logdet = sum log|ev|        fastgps/util.py:285,292-299
+//   norm   = Re sum conj(yt) yt/ev                            fastgps/util.py:354-370
+//   loss   = 1/2 (norm + w logdet + d_out n log 2 pi)         fastgps/abstract_gp.py:235,253-261
+//   grads  = autograd of the above                            fastgps/abstract_gp.py:294
+//   Rprop  = torch.optim.Rprop(lr=0.1)                        fastgps/abstract_fast_gp.py:53-57
+//
+// Analytic gradient (G_e = dL/dRe(ev) + i dL/dIm(ev), Y = sum_b |yt_b|^2, w = logdet weight):
+//   G_e = 1/2 conj(w/ev - Y/ev^2);  dL/dlam = sqrt(n) G_e;  g = Re(ft^H(dL/dlam)) = dL/dk1
+//   dL/draw_scale = sum_i g_i k1_i;  dL/draw_l_j = sum_i g_i scale l_j p_ij prod_{m!=j}(1 + l_m p_im)
+//   dL/draw_noise = noise * sum_k Re(G_e,k)
+// (digital nets: everything real, ft = ft^H = fwht.)
+//
+// Launch structure per iteration:
+//   n <= 4096 : k_iter_single  (forward + eigen terms + adjoint + gradient in ONE kernel, in LDS)
+//   n >  4096 : k_fwd_rows (k1 load + row transform + twiddle) -> k_fwd_cols (column transform +
+//               eigen terms) -> k_cols<ADJ> / k_rows (adjoint column pass) -> k_bwd_rows (adjoint
+//               row transform + gradient terms)
+//   then k_fit_step (one workgroup: deterministic reduction of the per-block partials, loss
+//   assembly, histories, Rprop update).
+#include <cmath>
+
+#include "fgp_common.h"
+#include "fgp_runtime.h"
+#include "../../include/fgp_hip.h"
+
+namespace fgp {
+
+// ------------------------------------------------------------------------------------------------
+// kernel parts
+struct PartsSpec {
+  int order[FGP_MAX_D];
+  double coef[FGP_MAX_D];
+};
+
+// torch.remainder(v, 1.0) for floating point (fmod, then shift negative results by the divisor)
+__device__ __forceinline__ double mod1(double v) {
+  double r = fmod(v, 1.0);
+  if (r != 0.0 && r < 0.0) r += 1.0;
+  return r;
+}
+
+// Bernoulli polynomial B_order(x), Horner form with the standard rational coefficients.
+__device__ __forceinline__ double bernoulli(int order, double x) {
+  switch (order) {
+    case 2: return (x - 1.0) * x + 1.0 / 6.0;
+    case 4: return (((x - 2.0) * x + 1.0) * x + 0.0) * x - 1.0 / 30.0;
+    case 6: return (((((x - 3.0) * x + 5.0 / 2.0) * x + 0.0) * x - 1.0 / 2.0) * x + 0.0) * x + 1.0 / 42.0;
+    case 8:
+      return (((((((x - 4.0) * x + 14.0 / 3.0) * x + 0.0) * x - 7.0 / 3.0) * x + 0.0) * x + 2.0 / 3.0) * x + 0.0) * x -
+             1.0 / 30.0;
+    default: return __builtin_nan("");
+  }
+}
+
+// Order-1 Walsh part for an XOR distance (fast_gp_digital_net_b2.py:297-298).
+__device__ __forceinline__ double walsh1(unsigned long long delta, int t) {
+  if (delta == 0ull) return 6.0 * (1.0 / 6.0 - 0.0);
+  const int fl = 63 - __clzll((long long)delta);   // floor(log2(delta)), exact
+  return 6.0 * (1.0 / 6.0 - ldexp(1.0, fl - t - 1));
+}
+
+__global__ __launch_bounds__(kWG) void k_lattice_parts(const double* __restrict__ x, int64_t xs,
+                                                        const double* __restrict__ z, int64_t n, int d,
+                                                        PartsSpec spec, double* __restrict__ parts) {
+  const int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x;
+  if (i >= n) return;
+  for (int j = 0; j < d; ++j) {
+    const double delta = mod1(x[i * xs + j] - z[j]);
+    parts[(int64_t)j * n + i] = spec.coef[j] * bernoulli(spec.order[j], delta);
+  }
+}
+
+__global__ __launch_bounds__(kWG) void k_net_parts(const int64_t* __restrict__ xb, int64_t xs,
+                                                    const int64_t* __restrict__ z, int64_t n, int d, int t,
+                                                    double* __restrict__ parts) {
+  const int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x;
+  if (i >= n) return;
+  for (int j = 0; j < d; ++j) {
+    const unsigned long long delta = (unsigned long long)(xb[i * xs + j] ^ z[j]);
+    parts[(int64_t)j * n + i] = walsh1(delta, t);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// fused MLL
+struct Nll {
+  int log2n, d, G, nb, nq;
+  const double* parts;
+  int64_t parts_stride;
+  const double* ysq;
+  int64_t ysq_stride;
+  const double* raw;
+  int scale_off, scale_pp, ls_off, ls_pp, ls_pd, noise_off, noise_pp;
+  double logdet_weight;
+  void* grad_lam;
+  void* work;
+  double* partials;
+};
+
+struct Hyp {
+  double scale, noise;
+  double ls[FGP_MAX_D];
+};
+
+__device__ __forceinline__ void load_hyp(const Nll& a, int g, Hyp& h) {
+  h.scale = exp(a.raw[a.scale_off + (a.scale_pp ? g : 0)]);
+  h.noise = exp(a.raw[a.noise_off + (a.noise_pp ? g : 0)]);
+  const int lb = a.ls_off + (a.ls_pp ? g : 0) * (a.ls_pd ? a.d : 1);
+#pragma unroll
+  for (int j = 0; j < FGP_MAX_D; ++j) h.ls[j] = (j < a.d) ? exp(a.raw[lb + (a.ls_pd ? j : 0)]) : 0.0;
+}
+
+// k1_i = scale * prod_j (1 + l_j p_ij)   (product in j order, as torch.prod)
+// (loops fully unrolled to FGP_MAX_D with predicates so every per-dimension array stays in registers)
+__device__ __forceinline__ double k1_at(const Nll& a, const Hyp& h, const double* __restrict__ pg, int64_t n, int64_t i) {
+  double p = 1.0;
+#pragma unroll
+  for (int j = 0; j < FGP_MAX_D; ++j)
+    if (j < a.d) p *= 1.0 + h.ls[j] * pg[(int64_t)j * n + i];
+  return h.scale * p;
+}
+
+// gradient terms at element i: acc[0] += g k1, acc[1+j] += g scale l_j p_j prod_{m != j} f_m
+__device__ __forceinline__ void grad_terms(const Nll& a, const Hyp& h, const double* __restrict__ pg, int64_t n,
+                                           int64_t i, double gi, double* acc) {
+  double f[FGP_MAX_D], pj[FGP_MAX_D];
+#pragma unroll
+  for (int j = 0; j < FGP_MAX_D; ++j) {
+    pj[j] = (j < a.d) ? pg[(int64_t)j * n + i] : 0.0;
+    f[j] = 1.0 + h.ls[j] * pj[j];     // padded dims: l = 0 -> f = 1 exactly
+  }
+  double suf[FGP_MAX_D + 1];
+  suf[FGP_MAX_D] = 1.0;
+#pragma unroll
+  for (int j = FGP_MAX_D - 1; j >= 0; --j) suf[j] = suf[j + 1] * f[j];
+  acc[0] += gi * (h.scale * suf[0]);
+  double pre = 1.0;
+#pragma unroll
+  for (int j = 0; j < FGP_MAX_D; ++j) {
+    acc[1 + j] += gi * (h.scale * h.ls[j] * pj[j] * (pre * suf[j + 1]));
+    pre *= f[j];
+  }
+}
+
+// eigenvalue terms for one frequency: returns dL/dlambda, accumulates norm / logdet / dnoise
+__device__ __forceinline__ double2 eig_terms(double2 lam, double rootn, double noise, double Y, double w,
+                                             double& norm, double& logdet, double& dnoise) {
+  const double ar = rootn * lam.x + noise, ai = rootn * lam.y;    // ev = sqrt(n) lam + noise
+  const double den = ar * ar + ai * ai;
+  const double rr = ar / den, ri = -ai / den;                      // 1/ev
+  norm += Y * rr;
+  logdet += log(hypot(ar, ai));
+  // G_e = 1/2 conj(w/ev - Y/ev^2) ; 1/ev^2 = (rr^2 - ri^2, 2 rr ri)
+  const double qr = w * rr - Y * (rr * rr - ri * ri);
+  const double qi = w * ri - Y * (2.0 * rr * ri);
+  const double ger = 0.5 * qr, gei = -0.5 * qi;
+  dnoise += ger;
+  return make_double2(rootn * ger, rootn * gei);
+}
+__device__ __forceinline__ double eig_terms(double lam, double rootn, double noise, double Y, double w, double& norm,
+                                            double& logdet, double& dnoise) {
+  const double e = rootn * lam + noise;
+  const double r = 1.0 / e;
+  norm += Y * r;
+  logdet += log(fabs(e));
+  const double ge = 0.5 * (w * r - Y * r * r);
+  dnoise += ge;
+  return rootn * ge;
+}
+
+template <typename T> __device__ __forceinline__ T real_to_T(double v);
+template <> __device__ __forceinline__ double2 real_to_T<double2>(double v) { return make_double2(v, 0.0); }
+template <> __device__ __forceinline__ double real_to_T<double>(double v) { return v; }
+__device__ __forceinline__ double re(double2 v) { return v.x; }
+__device__ __forceinline__ double re(double v) { return v; }
+
+__device__ __forceinline__ double* part_ptr(const Nll& a, int g, int q, int blk) {
+  return a.partials + ((int64_t)g * a.nq + q) * a.nb + blk;
+}
+
+// ---------------------------------------------------------------- n <= 4096: one kernel
+template <int P, typename T>
+__global__ __launch_bounds__(kWG) void k_iter_single(Nll a, const double2* __restrict__ tw) {
+  constexpr int L = 1 << P, TL = L / 16, TPW = kTile / L;
+  __shared__ T lds[kTile + kTile / 16];
+  __shared__ T red[kWG / 64];
+  __shared__ double redd[kWG / 64];
+  const int tid = threadIdx.x;
+  const int tr = tid / TL, tt = tid % TL;
+  const int gq = blockIdx.x * TPW + tr;
+  const bool live = gq < a.G;
+  const int g = live ? gq : a.G - 1;
+  Hyp h;
+  load_hyp(a, g, h);
+  const double* pg = a.parts + (int64_t)g * a.parts_stride;
+  T* s = lds + tr * (L + L / 16);
+  // k1 into LDS (each thread its own 16 strided elements of its transform)
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int i = tt + j * TL;
+    s[padi(i)] = real_to_T<T>(k1_at(a, h, pg, L, i));
+  }
+  __syncthreads();
+  center_transform<P, false>(s, tt, 1, red, tw);
+  const double rootn = sqrt((double)L), inv_rootn = 1.0 / rootn;
+  const double* yg = a.ysq + (int64_t)g * a.ysq_stride;
+  double norm = 0.0, logdet = 0.0, dnoise = 0.0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int k = tt + j * TL;
+    const T lam = s[padi(k)] * inv_rootn;
+    s[padi(k)] = eig_terms(lam, rootn, h.noise, yg[k], a.logdet_weight, norm, logdet, dnoise);
+  }
+  norm = group_sum<TL>(norm, redd);
+  logdet = group_sum<TL>(logdet, redd);
+  dnoise = group_sum<TL>(dnoise, redd);
+  __syncthreads();
+  center_transform<P, true>(s, tt, 1, red, tw);
+  double acc[1 + FGP_MAX_D];
+#pragma unroll
+  for (int q = 0; q < 1 + FGP_MAX_D; ++q) acc[q] = 0.0;
+#pragma unroll 4
+  for (int j = 0; j < 16; ++j) {
+    const int i = tt + j * TL;
+    grad_terms(a, h, pg, L, i, re(s[padi(i)]) * inv_rootn, acc);
+  }
+#pragma unroll
+  for (int q = 0; q < 1 + FGP_MAX_D; ++q)
+    if (q <= a.d) acc[q] = group_sum<TL>(acc[q], redd);
+  if (live && tt == 0) {
+    *part_ptr(a, g, 0, 0) = norm;
+    *part_ptr(a, g, 1, 0) = logdet;
+    *part_ptr(a, g, 2, 0) = dnoise;
+#pragma unroll
+    for (int q = 0; q < 1 + FGP_MAX_D; ++q)
+      if (q <= a.d) *part_ptr(a, g, 3 + q, 0) = acc[q];
+  }
+}
+
+// ---------------------------------------------------------------- n > 4096: forward row pass
+template <int P2, typename T>
+__global__ __launch_bounds__(kWG) void k_fwd_rows(Nll a, const double2* __restrict__ tw, const double2* __restrict__ twm) {
+  constexpr int N2 = 1 << P2, TL = N2 / 16, RPW = kTile / N2;
+  __shared__ T lds[kTile + kTile / 16];
+  __shared__ T red[kWG / 64];
+  const int m = a.log2n, m1 = m - P2;
+  const int64_t n = (int64_t)1 << m;
+  const int64_t tiles = n >> kTileLog;
+  const int g = (int)(blockIdx.x / tiles);
+  const int row0 = (int)(blockIdx.x % tiles) * RPW;
+  const int tid = threadIdx.x;
+  Hyp h;
+  load_hyp(a, g, h);
+  const double* pg = a.parts + (int64_t)g * a.parts_stride;
+  const int64_t base = (int64_t)row0 * N2;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int e = tid + k * kWG;
+    lds[padi(e)] = real_to_T<T>(k1_at(a, h, pg, n, base + e));
+  }
+  __syncthreads();
+  T* s = lds + (tid / TL) * (N2 + N2 / 16);
+  center_transform<P2, false>(s, tid % TL, 1, red, tw);
+  T* out = static_cast<T*>(a.work) + (int64_t)g * n + base;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int e = tid + k * kWG;
+    T v = lds[padi(e)];
+    if constexpr (sizeof(T) == 16) {
+      const unsigned u = (unsigned)(row0 + (e >> P2));
+      const unsigned ex = brev_bits(u, m1) * (unsigned)(e & (N2 - 1));
+      v = tw_mul<T>(v, cmul(twm[ex & (N2 - 1)], tw[(ex >> P2) << (kTileLog - m1)]), false);
+    }
+    out[e] = v;
+  }
+}
+
+// ---------------------------------------------------------------- n > 4096: forward column pass + eigen terms
+template <int P1, typename T>
+struct ColLay {
+  static constexpr int N1 = 1 << P1;
+  static constexpr int C = kTile / N1;
+  static constexpr int PADLEN = N1 + N1 / 16;
+  static constexpr int CS = (PADLEN % 2 == 0) ? PADLEN + 1 : PADLEN;
+};
+
+template <int P1, typename T>
+__global__ __launch_bounds__(kWG) void k_fwd_cols(Nll a, const double2* __restrict__ tw) {
+  using Lay = ColLay<P1, T>;
+  constexpr int N1 = Lay::N1, C = Lay::C, CS = Lay::CS, TL = N1 / 16;
+  __shared__ T lds[kLds];
+  __shared__ T red[kWG / 64];
+  __shared__ double redd[kWG / 64];
+  const int m = a.log2n;
+  const int64_t n = (int64_t)1 << m, N2 = n >> P1;
+  const int64_t tiles = n >> kTileLog;
+  const int g = (int)(blockIdx.x / tiles);
+  const int blk = (int)(blockIdx.x % tiles);
+  const int64_t c0 = (int64_t)blk * C;
+  const int tid = threadIdx.x;
+  const T* in = static_cast<const T*>(a.work) + (int64_t)g * n + c0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int e = tid + k * kWG;
+    const int c = e % C, u = e / C;
+    lds[c * CS + padi(u)] = in[(int64_t)u * N2 + c];
+  }
+  __syncthreads();
+  T* s = lds + (tid / TL) * CS;
+  center_transform<P1, false>(s, tid % TL, 1, red, tw);
+  Hyp h;
+  load_hyp(a, g, h);
+  const double rootn = sqrt((double)n), inv_rootn = 1.0 / rootn;
+  const double* yg = a.ysq + (int64_t)g * a.ysq_stride + c0;
+  T* gl = static_cast<T*>(a.grad_lam) + (int64_t)g * n + c0;
+  double norm = 0.0, logdet = 0.0, dnoise = 0.0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int e = tid + k * kWG;
+    const int c = e % C, r = e / C;
+    const int64_t off = (int64_t)r * N2 + c;
+    const T lam = lds[c * CS + padi(r)] * inv_rootn;
+    gl[off] = eig_terms(lam, rootn, h.noise, yg[off], a.logdet_weight, norm, logdet, dnoise);
+  }
+  norm = block_sum(norm, redd);
+  logdet = block_sum(logdet, redd);
+  dnoise = block_sum(dnoise, redd);
+  if (tid == 0) {
+    *part_ptr(a, g, 0, blk) = norm;
+    *part_ptr(a, g, 1, blk) = logdet;
+    *part_ptr(a, g, 2, blk) = dnoise;
+  }
+}
+
+// ---------------------------------------------------------------- n > 4096: adjoint row pass + gradient terms
+template <int P2, typename T>
+__global__ __launch_bounds__(kWG) void k_bwd_rows(Nll a, const double2* __restrict__ tw) {
+  constexpr int N2 = 1 << P2, TL = N2 / 16;
+  constexpr bool ADJ = sizeof(T) == 16;   // FFT: adjoint network; WHT: self-adjoint
+  __shared__ T lds[kTile + kTile / 16];
+  __shared__ T red[kWG / 64];
+  __shared__ double redd[kWG / 64];
+  const int m = a.log2n;
+  const int64_t n = (int64_t)1 << m;
+  const int64_t tiles = n >> kTileLog;
+  const int g = (int)(blockIdx.x / tiles);
+  const int blk = (int)(blockIdx.x % tiles);
+  const int64_t base = (int64_t)blk * kTile;
+  const int tid = threadIdx.x;
+  const T* in = static_cast<const T*>(a.work) + (int64_t)g * n + base;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int e = tid + k * kWG;
+    lds[padi(e)] = in[e];
+  }
+  __syncthreads();
+  T* s = lds + (tid / TL) * (N2 + N2 / 16);
+  center_transform<P2, ADJ>(s, tid % TL, 1, red, tw);
+  Hyp h;
+  load_hyp(a, g, h);
+  const double* pg = a.parts + (int64_t)g * a.parts_stride;
+  const double inv_rootn = 1.0 / sqrt((double)n);
+  double acc[1 + FGP_MAX_D];
+#pragma unroll
+  for (int q = 0; q < 1 + FGP_MAX_D; ++q) acc[q] = 0.0;
+#pragma unroll 4
+  for (int k = 0; k < 16; ++k) {
+    const int e = tid + k * kWG;
+    grad_terms(a, h, pg, n, base + e, re(lds[padi(e)]) * inv_rootn, acc);
+  }
+#pragma unroll
+  for (int q = 0; q < 1 + FGP_MAX_D; ++q) {
+    if (q <= a.d) {
+      const double v = block_sum(acc[q], redd);
+      if (tid == 0) *part_ptr(a, g, 3 + q, blk) = v;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- fit step (one workgroup)
+struct Fit {
+  int n_params;
+  double* raw;
+  double* prev;
+  double* step;
+  double* grad_out;
+  double* loss_hist;
+  double* raw_hist;
+  int scale_rg, ls_rg, noise_rg;
+  double mll_const, eta_minus, eta_plus, step_min, step_max;
+};
+
+__device__ __forceinline__ double* red_ptr(const Nll& a, int g, int q) {
+  return a.partials + (int64_t)a.G * a.nq * a.nb + (int64_t)g * a.nq + q;
+}
+
+// one workgroup per problem: deterministic (fixed-order) reduction of its per-block partials
+__global__ __launch_bounds__(kWG) void k_fit_reduce(Nll a) {
+  __shared__ double redd[kWG / 64];
+  const int g = blockIdx.x;
+  for (int q = 0; q < a.nq; ++q) {
+    double v = 0.0;
+    for (int b = threadIdx.x; b < a.nb; b += kWG) v += *part_ptr(a, g, q, b);
+    v = block_sum(v, redd);
+    if (threadIdx.x == 0) *red_ptr(a, g, q) = v;
+  }
+}
+
+// loss assembly, histories and the Rprop update (torch.optim.Rprop single-tensor semantics)
+__global__ __launch_bounds__(kWG) void k_fit_step(Nll a, Fit f, int iter, int do_update) {
+  extern __shared__ double grad[];   // [n_params]
+  const int tid = threadIdx.x;
+  for (int p = tid; p < f.n_params; p += kWG) {
+    grad[p] = 0.0;
+    f.raw_hist[(int64_t)iter * f.n_params + p] = f.raw[p];
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double term1 = 0.0, logdet_sum = 0.0;
+    for (int g = 0; g < a.G; ++g) {
+      term1 += *red_ptr(a, g, 0);
+      logdet_sum += *red_ptr(a, g, 1);
+      const int ni = a.noise_off + (a.noise_pp ? g : 0);
+      grad[ni] += exp(a.raw[ni]) * *red_ptr(a, g, 2);
+      grad[a.scale_off + (a.scale_pp ? g : 0)] += *red_ptr(a, g, 3);
+      const int lb = a.ls_off + (a.ls_pp ? g : 0) * (a.ls_pd ? a.d : 1);
+      for (int j = 0; j < a.d; ++j) grad[lb + (a.ls_pd ? j : 0)] += *red_ptr(a, g, 4 + j);
+    }
+    const double term2 = a.logdet_weight * logdet_sum;
+    f.loss_hist[(int64_t)iter * 3 + 0] = 0.5 * (term1 + term2 + f.mll_const);
+    f.loss_hist[(int64_t)iter * 3 + 1] = term1;
+    f.loss_hist[(int64_t)iter * 3 + 2] = term2;
+  }
+  __syncthreads();
+  const int scale_cnt = a.scale_pp ? a.G : 1;
+  const int ls_cnt = (a.ls_pp ? a.G : 1) * (a.ls_pd ? a.d : 1);
+  for (int p = tid; p < f.n_params; p += kWG) {
+    const double gp = grad[p];
+    f.grad_out[p] = gp;
+    if (!do_update) continue;
+    bool rg;
+    if (p >= a.scale_off && p < a.scale_off + scale_cnt) rg = f.scale_rg;
+    else if (p >= a.ls_off && p < a.ls_off + ls_cnt) rg = f.ls_rg;
+    else rg = f.noise_rg;
+    if (!rg) continue;
+    const double prod = gp * f.prev[p];
+    const double sgn = prod > 0.0 ? f.eta_plus : (prod < 0.0 ? f.eta_minus : 1.0);
+    const double st = fmin(fmax(f.step[p] * sgn, f.step_min), f.step_max);
+    f.step[p] = st;
+    const double gg = (sgn == f.eta_minus) ? 0.0 : gp;
+    const double gs = gg > 0.0 ? 1.0 : (gg < 0.0 ? -1.0 : 0.0);
+    f.raw[p] = f.raw[p] + (-1.0) * (gs * st);
+    f.prev[p] = gg;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// host-side launch logic
+static int to_nll(const fgp_nll_desc* d, Nll& a) {
+  if (!d) return set_error(kErrInvalid, "null nll desc");
+  if (d->family != FGP_FAMILY_LATTICE && d->family != FGP_FAMILY_NET) return set_error(kErrInvalid, "bad family");
+  if (d->log2n < 4 || d->log2n > kMaxLog2N) return set_error(kErrUnsupported, "fused fit needs 4 <= log2n <= 24");
+  if (d->d < 1 || d->d > FGP_MAX_D) return set_error(kErrUnsupported, "d=%d outside [1, %d]", d->d, FGP_MAX_D);
+  if (d->G < 1) return set_error(kErrInvalid, "G < 1");
+  if (!d->parts || !d->ysq || !d->raw || !d->grad_lam || !d->partials || (d->log2n > 12 && !d->work))
+    return set_error(kErrInvalid, "null pointer in nll desc");
+  a.log2n = d->log2n;
+  a.d = d->d;
+  a.G = d->G;
+  a.nb = d->log2n > 12 ? 1 << (d->log2n - 12) : 1;
+  a.nq = 4 + d->d;
+  a.parts = d->parts;
+  a.parts_stride = d->parts_stride;
+  a.ysq = d->ysq;
+  a.ysq_stride = d->ysq_stride;
+  a.raw = d->raw;
+  a.scale_off = d->scale_off;
+  a.scale_pp = d->scale_pp;
+  a.ls_off = d->ls_off;
+  a.ls_pp = d->ls_pp;
+  a.ls_pd = d->ls_pd;
+  a.noise_off = d->noise_off;
+  a.noise_pp = d->noise_pp;
+  a.logdet_weight = d->logdet_weight;
+  a.grad_lam = d->grad_lam;
+  a.work = d->work;
+  a.partials = d->partials;
+  return kOk;
+}
+
+template <typename T>
+static int launch_iter_single(const Nll& a, const Tables* tb, hipStream_t st) {
+  const int P = a.log2n;
+  const unsigned grid = (unsigned)((a.G + (kTile >> P) - 1) / (kTile >> P));
+  switch (P) {
+#define FGP_C(PP) case PP: k_iter_single<PP, T><<<grid, kWG, 0, st>>>(a, tb->tw4096); break;
+    FGP_C(4) FGP_C(5) FGP_C(6) FGP_C(7) FGP_C(8) FGP_C(9) FGP_C(10) FGP_C(11) FGP_C(12)
+#undef FGP_C
+    default: return set_error(kErrInvalid, "bad log2n");
+  }
+  return check_launch("k_iter_single");
+}
+
+template <typename T>
+static int launch_fwd2(const Nll& a, const Tables* tb, hipStream_t st) {
+  const int m = a.log2n, m2 = split_m2(m), m1 = m - m2;
+  const unsigned grid = (unsigned)((int64_t)a.G << (m - kTileLog));
+  switch (m2) {
+#define FGP_C(PP) case PP: k_fwd_rows<PP, T><<<grid, kWG, 0, st>>>(a, tb->tw4096, tb->twm[m]); break;
+    FGP_C(9) FGP_C(10) FGP_C(11) FGP_C(12)
+#undef FGP_C
+    default: return set_error(kErrInvalid, "bad m2");
+  }
+  int rc = check_launch("k_fwd_rows");
+  if (rc != kOk) return rc;
+  switch (m1) {
+#define FGP_C(PP) case PP: k_fwd_cols<PP, T><<<grid, kWG, 0, st>>>(a, tb->tw4096); break;
+    FGP_C(4) FGP_C(5) FGP_C(6) FGP_C(7) FGP_C(8) FGP_C(9) FGP_C(10) FGP_C(11) FGP_C(12)
+#undef FGP_C
+    default: return set_error(kErrInvalid, "bad m1");
+  }
+  return check_launch("k_fwd_cols");
+}
+
+template <typename T>
+static int launch_bwd2(const Nll& a, const Tables* tb, hipStream_t st) {
+  const int m = a.log2n, m2 = split_m2(m);
+  const unsigned grid = (unsigned)((int64_t)a.G << (m - kTileLog));
+  // adjoint column pass: grad_lam -> work (generic column kernel; conj twiddle for the FFT)
+  int rc = cols_adjoint_launch(sizeof(T) == 16, m, a.grad_lam, a.work, a.G, tb, st);
+  if (rc != kOk) return rc;
+  switch (m2) {
+#define FGP_C(PP) case PP: k_bwd_rows<PP, T><<<grid, kWG, 0, st>>>(a, tb->tw4096); break;
+    FGP_C(9) FGP_C(10) FGP_C(11) FGP_C(12)
+#undef FGP_C
+    default: return set_error(kErrInvalid, "bad m2");
+  }
+  return check_launch("k_bwd_rows");
+}
+
+static int nll_fwd(const Nll& a, hipStream_t st, bool lattice) {
+  const Tables* tb = get_tables(st);
+  if (!tb) return set_error(kErrHip, "twiddle table initialisation failed");
+  if (a.log2n <= 12) return lattice ? launch_iter_single<double2>(a, tb, st) : launch_iter_single<double>(a, tb, st);
+  return lattice ? launch_fwd2<double2>(a, tb, st) : launch_fwd2<double>(a, tb, st);
+}
+
+static int nll_bwd(const Nll& a, hipStream_t st, bool lattice) {
+  if (a.log2n <= 12) return kOk;   // fused into the forward kernel
+  const Tables* tb = get_tables(st);
+  if (!tb) return set_error(kErrHip, "twiddle table initialisation failed");
+  return lattice ? launch_bwd2<double2>(a, tb, st) : launch_bwd2<double>(a, tb, st);
+}
+
+static int to_fit(const fgp_fit_desc* d, Fit& f) {
+  if (!d || !d->raw || !d->rprop_prev || !d->rprop_step || !d->grad_out || !d->loss_hist || !d->raw_hist)
+    return set_error(kErrInvalid, "null pointer in fit desc");
+  if (d->n_params < 1 || d->n_params > 8192) return set_error(kErrInvalid, "bad n_params (1..8192)");
+  f.n_params = d->n_params;
+  f.raw = d->raw;
+  f.prev = d->rprop_prev;
+  f.step = d->rprop_step;
+  f.grad_out = d->grad_out;
+  f.loss_hist = d->loss_hist;
+  f.raw_hist = d->raw_hist;
+  f.scale_rg = d->scale_rg;
+  f.ls_rg = d->ls_rg;
+  f.noise_rg = d->noise_rg;
+  f.mll_const = d->mll_const;
+  f.eta_minus = d->eta_minus;
+  f.eta_plus = d->eta_plus;
+  f.step_min = d->step_min;
+  f.step_max = d->step_max;
+  return kOk;
+}
+
+static int fit_step(const Nll& a, const Fit& f, int iter, int do_update, hipStream_t st) {
+  k_fit_reduce<<<a.G, kWG, 0, st>>>(a);
+  int rc = check_launch("k_fit_reduce");
+  if (rc != kOk) return rc;
+  k_fit_step<<<1, kWG, f.n_params * sizeof(double), st>>>(a, f, iter, do_update);
+  return check_launch("k_fit_step");
+}
+
+}  // namespace fgp
+
+using namespace fgp;
+
+extern "C" {
+
+int fgp_lattice_parts(const double* x, int64_t x_row_stride, const double* z, int64_t n, int d, const int* order,
+                      const double* coef, double* parts, void* stream) {
+  if (n < 0 || d < 1 || d > FGP_MAX_D) return set_error(kErrInvalid, "fgp_lattice_parts: bad n/d");
+  if (n == 0) return kOk;
+  if (!x || !z || !parts || !order || !coef) return set_error(kErrInvalid, "fgp_lattice_parts: null pointer");
+  PartsSpec spec;
+  for (int j = 0; j < FGP_MAX_D; ++j) {
+    spec.order[j] = j < d ? order[j] : 0;
+    spec.coef[j] = j < d ? coef[j] : 0.0;
+    if (j < d && (order[j] < 2 || order[j] > 8 || (order[j] & 1)))
+      return set_error(kErrUnsupported, "Bernoulli order %d unsupported", order[j]);
+  }
+  k_lattice_parts<<<(unsigned)((n + kWG - 1) / kWG), kWG, 0, (hipStream_t)stream>>>(x, x_row_stride, z, n, d, spec, parts);
+  return check_launch("k_lattice_parts");
+}
+
+int fgp_net_parts(const int64_t* xb, int64_t xb_row_stride, const int64_t* z, int64_t n, int d, int t, double* parts,
+                  void* stream) {
+  if (n < 0 || d < 1 || d > FGP_MAX_D || t < 1 || t > 63) return set_error(kErrInvalid, "fgp_net_parts: bad n/d/t");
+  if (n == 0) return kOk;
+  if (!xb || !z || !parts) return set_error(kErrInvalid, "fgp_net_parts: null pointer");
+  k_net_parts<<<(unsigned)((n + kWG - 1) / kWG), kWG, 0, (hipStream_t)stream>>>(xb, xb_row_stride, z, n, d, t, parts);
+  return check_launch("k_net_parts");
+}
+
+int fgp_nll_fwd(const fgp_nll_desc* desc, void* stream) {
+  Nll a;
+  int rc = to_nll(desc, a);
+  if (rc != kOk) return rc;
+  return nll_fwd(a, (hipStream_t)stream, desc->family == FGP_FAMILY_LATTICE);
+}
+
+int fgp_nll_bwd(const fgp_nll_desc* desc, void* stream) {
+  Nll a;
+  int rc = to_nll(desc, a);
+  if (rc != kOk) return rc;
+  return nll_bwd(a, (hipStream_t)stream, desc->family == FGP_FAMILY_LATTICE);
+}
+
+int fgp_fit_step(const fgp_nll_desc* nll, const fgp_fit_desc* fit, int iter, int do_update, void* stream) {
+  Nll a;
+  Fit f;
+  int rc = to_nll(nll, a);
+  if (rc == kOk) rc = to_fit(fit, f);
+  if (rc != kOk) return rc;
+  return fit_step(a, f, iter, do_update, (hipStream_t)stream);
+}
+
+int fgp_fit_run(const fgp_nll_desc* nll, const fgp_fit_desc* fit, int iter0, int iters, int final_no_update,
+                void* stream) {
+  Nll a;
+  Fit f;
+  int rc = to_nll(nll, a);
+  if (rc == kOk) rc = to_fit(fit, f);
+  if (rc != kOk) return rc;
+  const bool lat = nll->family == FGP_FAMILY_LATTICE;
+  hipStream_t st = (hipStream_t)stream;
+  for (int it = 0; it < iters; ++it) {
+    if ((rc = nll_fwd(a, st, lat)) != kOk) return rc;
+    if ((rc = nll_bwd(a, st, lat)) != kOk) return rc;
+    const int upd = !(final_no_update && it == iters - 1);
+    if ((rc = fit_step(a, f, iter0 + it, upd, st)) != kOk) return rc;
+  }
+  return kOk;
+}
+
+}  // extern "C"

@@ -1,0 +1,350 @@
+// Batched orthonormal transforms of the fast-GP hot path (drop-in for qmcpy.fftbr_torch,
+// qmcpy.ifftbr_torch, qmcpy.fwht_torch as injected at fast_gp_lattice.py:224-225 and
+// fast_gp_digital_net_b2.py:226, wrapped by AbstractFastGP.ft/ift, abstract_fast_gp.py:197-228).
+//
+// Length n = 2^m, 0 <= m <= 24, transform along the last (contiguous) axis of a [batch, n] array.
+//   m <= 3       : k_tiny   (one thread per transform, registers only)
+//   4 <= m <= 12 : k_single (one LDS pass: 4096/n transforms per 256-thread workgroup)
+//   13 <= m <= 24: two passes over an N1 x N2 view (N2 = 2^m2 contiguous rows, N1 = 2^(m-m2)):
+//        fftbr  = rows(fftbr_N2) -> twiddle w_n^{brev(u) k2} -> columns(fftbr_N1)
+//        ifftbr = columns(ifftbr_N1) -> conj twiddle -> rows(ifftbr_N2)      (exact adjoint)
+//        fwht   = rows(fwht_N2) -> columns(fwht_N1)
+//      The bit-reversal of fftbr's input is never materialised: for i = u*N2 + v,
+//      brev_m(i) = brev(v)*N1 + brev(u), so the row pass is itself a bit-reversed-input transform
+//      of each contiguous row and the column pass one of each column (natural-order output).
+//
+// "stable" reproduces AbstractFastGP.ft's mean-centring (abstract_fast_gp.py:209-211) inside the
+// kernels: every row / column is centred by its own mean before its transform and the mean is
+// added back to its frequency-0 bin afterwards (exact in exact arithmetic: the transform of a
+// constant vector is supported on bin 0), keeping large DC components out of the butterflies.
+#include "fgp_common.h"
+#include "fgp_runtime.h"
+#include "../../include/fgp_hip.h"
+
+namespace fgp {
+
+// ------------------------------------------------------------------ m <= 3: registers only
+template <int P, typename T, bool ADJ>
+__global__ __launch_bounds__(kWG) void k_tiny(const void* in, int64_t in_bs, int in_real, void* out,
+                                               int64_t out_bs, int out_real, int64_t batch, int stable,
+                                               double scale, const double2* __restrict__ tw) {
+  constexpr int L = 1 << P;
+  const int64_t b = (int64_t)blockIdx.x * kWG + threadIdx.x;
+  if (b >= batch) return;
+  T v[L];
+  T mean = zero_v<T>();
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+    v[i] = load_in<T>(in, b * in_bs + i, in_real);
+    mean += v[i];
+  }
+  mean = mean * (1.0 / L);
+  if (stable) {
+#pragma unroll
+    for (int i = 0; i < L; ++i) v[i] -= mean;
+  }
+  if constexpr (!ADJ) {
+#pragma unroll
+    for (int s = 0; s < P; ++s)
+#pragma unroll
+      for (int a = 0; a < L; ++a)
+        if (!(a & (1 << s))) bfly_dit(v[a], v[a | (1 << s)], tw, (a & ((1 << s) - 1)) << (11 - s));
+  } else {
+#pragma unroll
+    for (int s = P - 1; s >= 0; --s)
+#pragma unroll
+      for (int a = 0; a < L; ++a)
+        if (!(a & (1 << s))) bfly_dif(v[a], v[a | (1 << s)], tw, (a & ((1 << s) - 1)) << (11 - s));
+  }
+  if (stable) v[0] += mean * (double)L;
+#pragma unroll
+  for (int i = 0; i < L; ++i) store_out(out, b * out_bs + i, v[i] * scale, out_real);
+}
+
+// ------------------------------------------------------------------ 4 <= m <= 12: one LDS pass
+template <int P, typename T, bool ADJ>
+__global__ __launch_bounds__(kWG) void k_single(const void* in, int64_t in_bs, int in_real, void* out,
+                                                 int64_t out_bs, int out_real, int64_t batch, int stable,
+                                                 double scale, const double2* __restrict__ tw) {
+  constexpr int L = 1 << P;
+  constexpr int TL = L / 16;
+  constexpr int TPW = kTile / L;
+  __shared__ T lds[kTile + kTile / 16];
+  __shared__ T red[kWG / 64];
+  const int tid = threadIdx.x;
+  const int64_t b0 = (int64_t)blockIdx.x * TPW;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int e = tid + k * kWG;
+    const int64_t b = b0 + (e >> P);
+    T v = zero_v<T>();
+    if (b < batch) v = load_in<T>(in, b * in_bs + (e & (L - 1)), in_real);
+    lds[padi(e)] = v;
+  }
+  __syncthreads();
+  const int tt = tid % TL;
+  T* s = lds + (tid / TL) * (L + L / 16);
+  center_transform<P, ADJ>(s, tt, stable, red, tw);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int e = tid + k * kWG;
+    const int64_t b = b0 + (e >> P);
+    if (b < batch) store_out(out, b * out_bs + (e & (L - 1)), lds[padi(e)] * scale, out_real);
+  }
+}
+
+// ------------------------------------------------------------------ m > 12: row pass
+// View of one batch item: N1 rows of N2 = 2^P2 contiguous elements.  4096/N2 rows per workgroup.
+// Forward (!ADJ): row transform, then (twiddle) multiply position (u, k2) by w_n^{brev_m1(u) k2}.
+// Adjoint  (ADJ): row transform of the column pass' output (no twiddle here).
+template <int P2, typename T, bool ADJ>
+__global__ __launch_bounds__(kWG) void k_rows(const void* in, int64_t in_bs, int in_real, void* out,
+                                               int64_t out_bs, int out_real, int m, int stable, double scale,
+                                               int twiddle, const double2* __restrict__ tw,
+                                               const double2* __restrict__ twm) {
+  constexpr int N2 = 1 << P2;
+  constexpr int TL = N2 / 16;
+  constexpr int RPW = kTile / N2;
+  __shared__ T lds[kTile + kTile / 16];
+  __shared__ T red[kWG / 64];
+  const int m1 = m - P2;
+  const int64_t tiles = (int64_t)1 << (m - kTileLog);
+  const int64_t b = blockIdx.x / tiles;
+  const int row0 = (int)(blockIdx.x % tiles) * RPW;
+  const int tid = threadIdx.x;
+  const int64_t ibase = b * in_bs + (int64_t)row0 * N2;   // rows are contiguous: the tile is one slab
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int e = tid + k * kWG;
+    lds[padi(e)] = load_in<T>(in, ibase + e, in_real);
+  }
+  __syncthreads();
+  const int tt = tid % TL;
+  T* s = lds + (tid / TL) * (N2 + N2 / 16);
+  center_transform<P2, ADJ>(s, tt, stable, red, tw);
+  const int64_t obase = b * out_bs + (int64_t)row0 * N2;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int e = tid + k * kWG;
+    T v = lds[padi(e)];
+    if (twiddle) {
+      const unsigned u = (unsigned)(row0 + (e >> P2));
+      const unsigned k2 = (unsigned)(e & (N2 - 1));
+      const unsigned ex = brev_bits(u, m1) * k2;   // < 2^m
+      const double2 w = cmul(twm[ex & (N2 - 1)], tw[(ex >> P2) << (kTileLog - m1)]);
+      v = tw_mul<T>(v, w, false);
+    }
+    store_out(out, obase + e, v * scale, out_real);
+  }
+}
+
+// ------------------------------------------------------------------ m > 12: column pass
+// C = 4096/N1 adjacent columns (k2 in [c0, c0+C)) of length N1 = 2^P1 per workgroup, staged
+// column-major in LDS with an odd column stride (conflict-free transposing ds_write_b128).
+// Forward (!ADJ): plain column transform (natural-order output rows k1).
+// Adjoint  (ADJ): column transform, then (twiddle) multiply output row u by conj(w_n^{brev(u) k2}).
+// In-place safe (in == out): each workgroup reads its whole tile before writing it.
+template <int P1>
+struct ColLayout {
+  static constexpr int N1 = 1 << P1;
+  static constexpr int C = kTile / N1;
+  static constexpr int PADLEN = N1 + N1 / 16;
+  static constexpr int CS = (PADLEN % 2 == 0) ? PADLEN + 1 : PADLEN;
+  static_assert(C * CS <= kLds, "column tile exceeds LDS budget");
+};
+
+template <int P1, typename T, bool ADJ>
+__global__ __launch_bounds__(kWG) void k_cols(const void* in, int64_t in_bs, int in_real, void* out,
+                                               int64_t out_bs, int out_real, int m, int stable, double scale,
+                                               int twiddle, const double2* __restrict__ tw,
+                                               const double2* __restrict__ twm) {
+  using Lay = ColLayout<P1>;
+  constexpr int N1 = Lay::N1, C = Lay::C, CS = Lay::CS, TL = N1 / 16;
+  __shared__ T lds[kLds];
+  __shared__ T red[kWG / 64];
+  const int P2 = m - P1;
+  const int64_t N2 = (int64_t)1 << P2;
+  const int64_t tiles = (int64_t)1 << (m - kTileLog);
+  const int64_t b = blockIdx.x / tiles;
+  const int64_t c0 = (blockIdx.x % tiles) * C;
+  const int tid = threadIdx.x;
+  const int64_t ibase = b * in_bs + c0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int e = tid + k * kWG;
+    const int c = e % C, u = e / C;
+    lds[c * CS + padi(u)] = load_in<T>(in, ibase + (int64_t)u * N2 + c, in_real);
+  }
+  __syncthreads();
+  const int tt = tid % TL;
+  const int col = tid / TL;
+  T* s = lds + col * CS;
+  center_transform<P1, ADJ>(s, tt, stable, red, tw);
+  const int64_t obase = b * out_bs + c0;
+  const int m2 = P2;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int e = tid + k * kWG;
+    const int c = e % C, r = e / C;
+    T v = lds[c * CS + padi(r)];
+    if (twiddle) {
+      const unsigned k2 = (unsigned)(c0 + c);
+      const unsigned ex = brev_bits((unsigned)r, P1) * k2;
+      const double2 w = cmul(twm[ex & (unsigned)(N2 - 1)], tw[(ex >> m2) << (kTileLog - P1)]);
+      v = tw_mul<T>(v, w, true);
+    }
+    store_out(out, obase + (int64_t)r * N2 + c, v * scale, out_real);
+  }
+}
+
+// ------------------------------------------------------------------ launch helpers
+template <typename T, bool ADJ>
+static int launch_tiny(int m, const void* in, int64_t in_bs, int in_real, void* out, int out_real, int64_t batch,
+                       int stable, double scale, const double2* tw, hipStream_t st) {
+  const dim3 g((unsigned)((batch + kWG - 1) / kWG));
+  const int64_t n = (int64_t)1 << m;
+  switch (m) {
+    case 0: k_tiny<0, T, ADJ><<<g, kWG, 0, st>>>(in, in_bs, in_real, out, n, out_real, batch, stable, scale, tw); break;
+    case 1: k_tiny<1, T, ADJ><<<g, kWG, 0, st>>>(in, in_bs, in_real, out, n, out_real, batch, stable, scale, tw); break;
+    case 2: k_tiny<2, T, ADJ><<<g, kWG, 0, st>>>(in, in_bs, in_real, out, n, out_real, batch, stable, scale, tw); break;
+    case 3: k_tiny<3, T, ADJ><<<g, kWG, 0, st>>>(in, in_bs, in_real, out, n, out_real, batch, stable, scale, tw); break;
+    default: return set_error(kErrInvalid, "launch_tiny: bad m");
+  }
+  return check_launch("k_tiny");
+}
+
+#define FGP_SINGLE_CASE(P)                                                                                   \
+  case P:                                                                                                    \
+    k_single<P, T, ADJ><<<dim3((unsigned)((batch + (kTile >> P) - 1) / (kTile >> P))), kWG, 0, st>>>(      \
+        in, in_bs, in_real, out, (int64_t)1 << P, out_real, batch, stable, scale, tw);                       \
+    break;
+
+template <typename T, bool ADJ>
+static int launch_single(int m, const void* in, int64_t in_bs, int in_real, void* out, int out_real,
+                         int64_t batch, int stable, double scale, const double2* tw, hipStream_t st) {
+  switch (m) {
+    FGP_SINGLE_CASE(4) FGP_SINGLE_CASE(5) FGP_SINGLE_CASE(6) FGP_SINGLE_CASE(7) FGP_SINGLE_CASE(8)
+    FGP_SINGLE_CASE(9) FGP_SINGLE_CASE(10) FGP_SINGLE_CASE(11) FGP_SINGLE_CASE(12)
+    default: return set_error(kErrInvalid, "launch_single: bad m");
+  }
+  return check_launch("k_single");
+}
+#undef FGP_SINGLE_CASE
+
+#define FGP_ROWS_CASE(P)                                                                                       \
+  case P:                                                                                                      \
+    k_rows<P, T, ADJ><<<g, kWG, 0, st>>>(in, in_bs, in_real, out, out_bs, out_real, m, stable, scale, twiddle, \
+                                         tw, twm);                                                             \
+    break;
+
+template <typename T, bool ADJ>
+static int launch_rows(int m, const void* in, int64_t in_bs, int in_real, void* out, int64_t out_bs, int out_real,
+                       int64_t batch, int stable, double scale, int twiddle, const Tables* tb, hipStream_t st) {
+  const int m2 = split_m2(m);
+  const dim3 g((unsigned)(batch << (m - kTileLog)));
+  const double2* tw = tb->tw4096;
+  const double2* twm = tb->twm[m];
+  switch (m2) {
+    FGP_ROWS_CASE(9) FGP_ROWS_CASE(10) FGP_ROWS_CASE(11) FGP_ROWS_CASE(12)
+    default: return set_error(kErrInvalid, "launch_rows: bad m2");
+  }
+  return check_launch("k_rows");
+}
+#undef FGP_ROWS_CASE
+
+#define FGP_COLS_CASE(P)                                                                                       \
+  case P:                                                                                                      \
+    k_cols<P, T, ADJ><<<g, kWG, 0, st>>>(in, in_bs, in_real, out, out_bs, out_real, m, stable, scale, twiddle, \
+                                         tw, twm);                                                             \
+    break;
+
+template <typename T, bool ADJ>
+static int launch_cols(int m, const void* in, int64_t in_bs, int in_real, void* out, int64_t out_bs, int out_real,
+                       int64_t batch, int stable, double scale, int twiddle, const Tables* tb, hipStream_t st) {
+  const int m1 = m - split_m2(m);
+  const dim3 g((unsigned)(batch << (m - kTileLog)));
+  const double2* tw = tb->tw4096;
+  const double2* twm = tb->twm[m];
+  switch (m1) {
+    FGP_COLS_CASE(4) FGP_COLS_CASE(5) FGP_COLS_CASE(6) FGP_COLS_CASE(7) FGP_COLS_CASE(8)
+    FGP_COLS_CASE(9) FGP_COLS_CASE(10) FGP_COLS_CASE(11) FGP_COLS_CASE(12)
+    default: return set_error(kErrInvalid, "launch_cols: bad m1");
+  }
+  return check_launch("k_cols");
+}
+#undef FGP_COLS_CASE
+
+static int validate(const void* in, const void* out, int64_t batch, int log2n, int64_t in_bs) {
+  if (log2n < 0 || log2n > kMaxLog2N)
+    return set_error(kErrUnsupported, "log2n=%d outside supported range [0, %d]", log2n, kMaxLog2N);
+  if (batch < 0) return set_error(kErrInvalid, "negative batch");
+  if (batch > 0 && (in == nullptr || out == nullptr)) return set_error(kErrInvalid, "null data pointer");
+  if (batch > 1 && in_bs < ((int64_t)1 << log2n)) return set_error(kErrInvalid, "in_batch_stride < n");
+  if ((batch << log2n) >= ((int64_t)1 << 31) * kTile) return set_error(kErrUnsupported, "batch*n too large");
+  return kOk;
+}
+
+int cols_adjoint_launch(bool fft, int m, const void* in, void* out, int64_t batch, const Tables* tb,
+                        hipStream_t st) {
+  const int64_t n = (int64_t)1 << m;
+  if (fft) return launch_cols<double2, true>(m, in, n, 0, out, n, 0, batch, 1, 1.0, 1, tb, st);
+  return launch_cols<double, false>(m, in, n, 0, out, n, 0, batch, 1, 1.0, 0, tb, st);
+}
+
+}  // namespace fgp
+
+using namespace fgp;
+
+extern "C" {
+
+int fgp_fftbr(const void* in, int64_t in_batch_stride, int in_is_real, void* out, int64_t batch, int log2n,
+              int stable, void* stream) {
+  int rc = validate(in, out, batch, log2n, in_batch_stride);
+  if (rc != kOk || batch == 0) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  const Tables* tb = get_tables(st);
+  if (!tb) return set_error(kErrHip, "twiddle table initialisation failed");
+  const int64_t n = (int64_t)1 << log2n;
+  const double scale = 1.0 / sqrt((double)n);
+  if (log2n <= 3) return launch_tiny<double2, false>(log2n, in, in_batch_stride, in_is_real, out, 0, batch, stable, scale, tb->tw4096, st);
+  if (log2n <= 12) return launch_single<double2, false>(log2n, in, in_batch_stride, in_is_real, out, 0, batch, stable, scale, tb->tw4096, st);
+  rc = launch_rows<double2, false>(log2n, in, in_batch_stride, in_is_real, out, n, 0, batch, stable, 1.0, 1, tb, st);
+  if (rc != kOk) return rc;
+  return launch_cols<double2, false>(log2n, out, n, 0, out, n, 0, batch, stable, scale, 0, tb, st);
+}
+
+int fgp_ifftbr(const void* in, int64_t in_batch_stride, void* out, int out_real, void* work, int64_t batch,
+               int log2n, int stable, void* stream) {
+  int rc = validate(in, out, batch, log2n, in_batch_stride);
+  if (rc != kOk || batch == 0) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  const Tables* tb = get_tables(st);
+  if (!tb) return set_error(kErrHip, "twiddle table initialisation failed");
+  const int64_t n = (int64_t)1 << log2n;
+  const double scale = 1.0 / sqrt((double)n);
+  if (log2n <= 3) return launch_tiny<double2, true>(log2n, in, in_batch_stride, 0, out, out_real, batch, stable, scale, tb->tw4096, st);
+  if (log2n <= 12) return launch_single<double2, true>(log2n, in, in_batch_stride, 0, out, out_real, batch, stable, scale, tb->tw4096, st);
+  void* mid = out_real ? work : out;
+  if (mid == nullptr) return set_error(kErrInvalid, "fgp_ifftbr: out_real with n > 4096 needs a complex work buffer");
+  rc = launch_cols<double2, true>(log2n, in, in_batch_stride, 0, mid, n, 0, batch, stable, 1.0, 1, tb, st);
+  if (rc != kOk) return rc;
+  return launch_rows<double2, true>(log2n, mid, n, 0, out, n, out_real, batch, stable, scale, 0, tb, st);
+}
+
+int fgp_fwht(const double* in, int64_t in_batch_stride, double* out, int64_t batch, int log2n, int stable,
+             void* stream) {
+  int rc = validate(in, out, batch, log2n, in_batch_stride);
+  if (rc != kOk || batch == 0) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  const Tables* tb = get_tables(st);
+  if (!tb) return set_error(kErrHip, "twiddle table initialisation failed");
+  const int64_t n = (int64_t)1 << log2n;
+  const double scale = 1.0 / sqrt((double)n);
+  if (log2n <= 3) return launch_tiny<double, false>(log2n, in, in_batch_stride, 0, out, 0, batch, stable, scale, tb->tw4096, st);
+  if (log2n <= 12) return launch_single<double, false>(log2n, in, in_batch_stride, 0, out, 0, batch, stable, scale, tb->tw4096, st);
+  rc = launch_rows<double, false>(log2n, in, in_batch_stride, 0, out, n, 0, batch, stable, 1.0, 0, tb, st);
+  if (rc != kOk) return rc;
+  return launch_cols<double, false>(log2n, out, n, 0, out, n, 0, batch, stable, scale, 0, tb, st);
+}
+
+}  // extern "C"

@@ -1,0 +1,1002 @@
+"""Drop-in FastGPLattice / FastGPDigitalNetB2 on MI355X.
+
+Host-side mirror of the reference's Python interface (alegresor/FastGaussianProcesses, fastgps
+0.0.4.1a): same constructor keywords (fast_gp_lattice.py:125-158, fast_gp_digital_net_b2.py:120-153),
+same methods and return shapes (abstract_gp.py, abstract_fast_gp.py), same assertion messages for
+misuse.  Every numerical hot spot runs in the HIP library (include/fgp_hip.h):
+
+  ft / ift                  -> fgp_fftbr / fgp_ifftbr / fgp_fwht (stable, differentiable)
+  k1 parts                  -> fgp_lattice_parts / fgp_net_parts
+  fit (MLL, default Rprop)  -> fgp_fit_run: fused forward / adjoint / Rprop on device, histories read
+                               back in chunks to apply the reference's early-stopping rule exactly
+  post_mean                 -> fgp_post_mean (matrix-free cross-kernel contraction)
+  post_var / post_cov       -> fgp_kernel_rows + the transform solve
+
+Scope of this round: single-task GPs (num_tasks=None or 1) without derivative information
+(beta = kappa = 0); multitask / derivative-informed GPs are the next row of SURVEY.md §8(f) and
+raise NotImplementedError.  Hyper-parameter fits other than (MLL, default optimizer, no masks,
+default log/exp transforms) run a generic path: torch autograd through the HIP transforms and
+torch device ops, with the caller's torch optimizer.
+"""
+import math
+import os
+
+import numpy as np
+import scipy.stats
+import torch
+
+from . import ops
+from . import seqs as _seqs
+from .fit_engine import FusedMLL, mll_constant
+
+
+def _log(x):
+    return torch.log(x)
+
+
+def _exp(x):
+    return torch.exp(x)
+
+
+_DEFAULT_TFS = (_log, _exp)
+_IDENTITY_TFS = ((lambda x: x), (lambda x: x))
+
+
+def _as_size(s):
+    if s is None or isinstance(s, torch.Size):
+        return s
+    return torch.Size(s)
+
+
+class _Hyper(object):
+    """Resolves one hyper-parameter's shape exactly as AbstractGP.__init__ (abstract_gp.py:78-139)."""
+
+    @staticmethod
+    def make(value, shape, shape_batch, last_ok, name, positive, device):
+        assert np.isscalar(value) or isinstance(value, torch.Tensor), "%s must be a scalar or torch.Tensor" % name
+        if isinstance(value, torch.Tensor):
+            shape = value.shape
+        shape = _as_size(shape)
+        assert isinstance(shape, torch.Size) and last_ok(shape[-1])
+        if len(shape) > 1:
+            assert shape[:-1] == shape_batch[-(len(shape) - 1):]
+        if np.isscalar(value):
+            value = value * torch.ones(shape, device=device)
+        value = value.to(device=device, dtype=torch.float64)
+        if positive == "pos":
+            assert (value > 0).all(), "%s must be positive" % name
+        elif positive == "nonneg":
+            assert (value >= 0).all(), "%s must be positive" % name
+        return value
+
+
+class AbstractFastGP(torch.nn.Module):
+    """Shared machinery of FastGPLattice / FastGPDigitalNetB2 (single task, beta=kappa=0)."""
+
+    _FAMILY = None
+    _XBDTYPE = None
+    _FTOUTDTYPE = None
+
+    def __init__(self, seqs, num_tasks, seed_for_seq, alpha, scale, lengthscales, noise, factor_task_kernel,
+                 rank_factor_task_kernel, noise_task_kernel, device, tfs_scale, tfs_lengthscales, tfs_noise,
+                 tfs_factor_task_kernel, tfs_noise_task_kernel, requires_grad_scale, requires_grad_lengthscales,
+                 requires_grad_noise, requires_grad_factor_task_kernel, requires_grad_noise_task_kernel, shape_batch,
+                 shape_scale, shape_lengthscales, shape_noise, shape_factor_task_kernel, shape_noise_task_kernel,
+                 derivatives, derivatives_coeffs, compile_fts, compile_fts_kwargs, adaptive_nugget):
+        super().__init__()
+        assert torch.get_default_dtype() == torch.float64, \
+            "fast transforms do not work without torch.float64 precision"
+        if num_tasks is None:
+            self.solo_task, self.default_task, num_tasks = True, 0, 1
+        else:
+            assert isinstance(num_tasks, int) and num_tasks > 0
+            self.solo_task, self.default_task = False, torch.arange(num_tasks)
+        if num_tasks != 1:
+            raise NotImplementedError("multi-task fast GPs (num_tasks > 1) are the next build row (SURVEY §8f)")
+        if derivatives is not None or derivatives_coeffs is not None:
+            raise NotImplementedError("derivative-informed kernels are not built yet (SURVEY §8f)")
+        self.num_tasks = 1
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise RuntimeError("fastgaussianprocesses_amd runs on a HIP device (device='cuda'); got %s" % device)
+        self.seq = self._resolve_seq(seqs, seed_for_seq)
+        self.seqs = np.array([self.seq], dtype=object)
+        self.d = int(self.seq.d)
+        # shape_batch / hyper-parameters (abstract_gp.py:73-139)
+        shape_batch = _as_size(shape_batch)
+        assert isinstance(shape_batch, torch.Size)
+        self.shape_batch = shape_batch
+        self.ndim_batch = len(shape_batch)
+        d = self.d
+        dev = self.device
+        scale = _Hyper.make(scale, shape_scale, shape_batch, lambda v: v == 1, "scale", "pos", dev)
+        if shape_lengthscales is None and not isinstance(lengthscales, torch.Tensor):
+            shape_lengthscales = torch.Size([d])
+        lengthscales = _Hyper.make(lengthscales, shape_lengthscales, shape_batch, lambda v: v in (1, d),
+                                   "lengthscales", "pos", dev)
+        noise = _Hyper.make(noise, shape_noise, shape_batch, lambda v: v == 1, "noise", "pos", dev)
+        if shape_factor_task_kernel is None and not isinstance(factor_task_kernel, torch.Tensor):
+            if rank_factor_task_kernel is None:
+                rank_factor_task_kernel = 0
+            shape_factor_task_kernel = torch.Size([1, rank_factor_task_kernel])
+        factor_task_kernel = _Hyper.make(factor_task_kernel, shape_factor_task_kernel, shape_batch,
+                                         lambda v: 0 <= v <= 1, "factor_task_kernel", None, dev)
+        if shape_noise_task_kernel is None and not isinstance(noise_task_kernel, torch.Tensor):
+            shape_noise_task_kernel = torch.Size([1])
+        noise_task_kernel = _Hyper.make(noise_task_kernel, shape_noise_task_kernel, shape_batch, lambda v: v == 1,
+                                        "noise_task_kernel", "nonneg", dev)
+        for tfs in (tfs_scale, tfs_lengthscales, tfs_noise, tfs_factor_task_kernel, tfs_noise_task_kernel):
+            assert len(tfs) == 2 and callable(tfs[0]) and callable(tfs[1]), \
+                "tfs should be a tuple of two callables, the transform and inverse transform"
+        self._tfs = dict(scale=tfs_scale, lengthscales=tfs_lengthscales, noise=tfs_noise)
+        self.tf_scale, self.tf_lengthscales, self.tf_noise = tfs_scale[1], tfs_lengthscales[1], tfs_noise[1]
+        self.tf_factor_task_kernel, self.tf_noise_task_kernel = tfs_factor_task_kernel[1], tfs_noise_task_kernel[1]
+        self.raw_scale = torch.nn.Parameter(tfs_scale[0](scale), requires_grad=requires_grad_scale)
+        self.raw_lengthscales = torch.nn.Parameter(tfs_lengthscales[0](lengthscales),
+                                                   requires_grad=requires_grad_lengthscales)
+        self.raw_noise = torch.nn.Parameter(tfs_noise[0](noise), requires_grad=requires_grad_noise)
+        self.raw_factor_task_kernel = torch.nn.Parameter(tfs_factor_task_kernel[0](factor_task_kernel),
+                                                         requires_grad=bool(requires_grad_factor_task_kernel))
+        self.raw_noise_task_kernel = torch.nn.Parameter(tfs_noise_task_kernel[0](noise_task_kernel),
+                                                        requires_grad=bool(requires_grad_noise_task_kernel))
+        self.adaptive_nugget = adaptive_nugget
+        self.compile_fts, self.compile_fts_kwargs = compile_fts, compile_fts_kwargs   # accepted; HIP kernels are native
+        # alpha (abstract_fast_gp.py:21-24)
+        assert (np.isscalar(alpha) and alpha % 1 == 0) or (isinstance(alpha, torch.Tensor) and alpha.shape == (self.d,)), \
+            "alpha should be an int or a torch.Tensor of length d"
+        if np.isscalar(alpha):
+            alpha = int(alpha) * torch.ones(self.d, dtype=torch.int64, device=dev)
+        self.alpha = alpha
+        self._alphas = [int(a) for a in alpha.tolist()]
+        # data
+        self.n = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.m = -torch.ones(1, dtype=torch.int64, device=dev)
+        self._y = [torch.empty(0, device=dev)]
+        self._pts_n = 0
+        self._x = torch.empty((0, self.d), device=dev)
+        self._xb = torch.empty((0, self.d), dtype=self._XBDTYPE, device=dev)
+        self._parts = {}       # n -> [d, n] first-column parts
+        self._cache = {}       # derived quantities keyed by (name, n) + parameter snapshot
+        self._snap = None
+
+    # ------------------------------------------------------------------ construction helpers
+    def _resolve_seq(self, seqs, seed_for_seq):
+        if isinstance(seqs, (int, np.integer)):
+            seed = np.random.SeedSequence(seed_for_seq).spawn(1)[0]
+            return self._default_seq(int(seqs), seed)
+        if isinstance(seqs, (list, np.ndarray)):
+            seqs = list(seqs)
+            assert len(seqs) == 1, "seqs should be a length num_tasks=1 list"
+            seqs = seqs[0]
+        self._check_seq(seqs)
+        return seqs
+
+    # ------------------------------------------------------------------ hyper-parameters
+    @property
+    def scale(self):
+        return self.tf_scale(self.raw_scale)
+
+    @property
+    def lengthscales(self):
+        return self.tf_lengthscales(self.raw_lengthscales)
+
+    @property
+    def noise(self):
+        return self.tf_noise(self.raw_noise)
+
+    @property
+    def factor_task_kernel(self):
+        return self.tf_factor_task_kernel(self.raw_factor_task_kernel)
+
+    @property
+    def noise_task_kernel(self):
+        return self.tf_noise_task_kernel(self.raw_noise_task_kernel)
+
+    @property
+    def gram_matrix_tasks(self):
+        """F F^T + diag(noise_task_kernel) (util.py:157-162)."""
+        F = self.factor_task_kernel
+        k = torch.einsum("...il,...kl->...ik", F, F)
+        return k + self.noise_task_kernel[..., None] * torch.eye(1, device=self.device)
+
+    @property
+    def total_parameters(self):
+        return sum(p.numel() for p in self.parameters())
+
+    @property
+    def total_tuneable_parameters(self):
+        return sum((p.numel() if p.requires_grad else 0) for p in self.parameters())
+
+    def get_default_optimizer(self, lr):
+        return torch.optim.Rprop(self.parameters(), lr=1e-1 if lr is None else lr)
+
+    def _snapshot(self):
+        return tuple(p.detach().clone() for p in (self.raw_scale, self.raw_lengthscales, self.raw_noise,
+                                                   self.raw_factor_task_kernel, self.raw_noise_task_kernel))
+
+    def _params_changed(self):
+        cur = (self.raw_scale, self.raw_lengthscales, self.raw_noise, self.raw_factor_task_kernel,
+               self.raw_noise_task_kernel)
+        if self._snap is None or any(a.shape != b.shape or not torch.equal(a.detach(), b) for a, b in zip(cur, self._snap)):
+            self._snap = self._snapshot()
+            return True
+        return False
+
+    def _cached(self, key, fn, grad_sensitive=True):
+        """Cache a derived quantity until n or the hyper-parameters change (the reference's
+        _frozen_equal / FASTGP_FORCE_RECOMPILE invalidation, util.py:81-94,185-205)."""
+        if self._params_changed():
+            self._cache = {k: v for k, v in self._cache.items() if not k[2]}
+        k = (key[0], key[1], grad_sensitive)
+        if k not in self._cache:
+            self._cache[k] = fn()
+        return self._cache[k]
+
+    def _task_scalar(self):
+        kt = self.gram_matrix_tasks
+        if not torch.equal(kt.detach(), torch.ones_like(kt)):
+            raise NotImplementedError("single-task GPs with a non-unit task kernel are not supported")
+        return 1.0
+
+    # ------------------------------------------------------------------ points and data
+    def _ensure_points(self, n):
+        n = int(n)
+        if n <= self._pts_n:
+            return
+        x, xb = self._sample(self._pts_n, n)
+        self._x = torch.cat([self._x, x], 0)
+        self._xb = x if self._XBDTYPE == torch.float64 else torch.cat([self._xb, xb], 0)
+        if self._XBDTYPE == torch.float64:
+            self._xb = self._x
+        self._pts_n = n
+
+    def get_x(self, task=0, n=None):
+        assert task == 0
+        n = int(self.n[0]) if n is None else int(n)
+        assert n >= 0
+        self._ensure_points(n)
+        return self._x[:n]
+
+    def get_xb(self, task=0, n=None):
+        assert task == 0
+        n = int(self.n[0]) if n is None else int(n)
+        assert n >= 0
+        self._ensure_points(n)
+        return self._xb[:n]
+
+    def get_x_next(self, n, task=None):
+        n_og = n
+        if isinstance(n, (int, np.int64)):
+            n = torch.tensor([n], dtype=torch.int64)
+        if isinstance(n, list):
+            n = torch.tensor(n, dtype=torch.int64)
+        assert isinstance(n, torch.Tensor) and torch.logical_or(n == 0, n & (n - 1) == 0).all(), \
+            "maximum sequence index must be a power of 2"
+        if task is None:
+            task = self.default_task
+        inttask = isinstance(task, int)
+        ns = n.tolist()
+        assert all(v >= int(self.n[0]) for v in ns), \
+            "maximum sequence index must be greater than the current number of samples"
+        out = [self.get_x(0, v)[int(self.n[0]):v] for v in ns]
+        return out[0] if inttask else out
+
+    def add_y_next(self, y_next, task=None):
+        if isinstance(y_next, torch.Tensor):
+            y_next = [y_next]
+        assert isinstance(y_next, list) and len(y_next) == 1
+        assert all(y.shape[:-1] == self.shape_batch for y in y_next)
+        y = y_next[0].to(device=self.device, dtype=torch.float64)
+        self._y[0] = torch.cat([self._y[0], y], -1)
+        self.n = torch.tensor([self._y[0].size(-1)], dtype=torch.int64, device=self.device)
+        self.m = torch.where(self.n == 0, -1, torch.log2(self.n.double())).to(torch.int64)
+        self._cache = {}
+        assert torch.logical_or(self.n == 0, (self.n & (self.n - 1) == 0)).all(), "total samples must be power of 2"
+
+    @property
+    def x(self):
+        return self.get_x(0)
+
+    @property
+    def y(self):
+        return self._y[0]
+
+    # ------------------------------------------------------------------ transforms (plugin point)
+    def ft(self, x):
+        """Stable forward transform along the last dim (abstract_fast_gp.py:197-212), HIP kernels."""
+        raise NotImplementedError
+
+    def ift(self, x):
+        raise NotImplementedError
+
+    # ------------------------------------------------------------------ kernel pieces
+    def _k1parts(self, n):
+        n = int(n)
+        if n not in self._parts:
+            self._ensure_points(n)
+            self._parts[n] = self._compute_parts(self._xb[:n], self._xb[0])
+        return self._parts[n]
+
+    def get_k1parts(self, task0=0, task1=0, n=None):
+        n = self._nint(n)
+        return self._k1parts(n).T[:, None, None, :]
+
+    def _k1(self, n, parts=None):
+        """k1 = scale * prod_j(1 + l_j parts_j)  -> [*param_batch, n] (abstract_fast_gp.py:181-191)."""
+        parts = self._k1parts(n) if parts is None else parts
+        ls = self.lengthscales
+        factors = 1 + ls[..., :, None] * parts          # [*lb, d, n]
+        return self.scale * factors.prod(-2)
+
+    def _nint(self, n):
+        return int(self.n[0]) if n is None else int(torch.as_tensor(n).reshape(-1)[0])
+
+    def get_lam(self, task0=0, task1=0, n=None):
+        n = self._nint(n)
+        return self._cached(("lam", n), lambda: self.ft(self._k1(n)))
+
+    def get_ytilde(self, task=0):
+        n = int(self.n[0])
+
+        def f():
+            y = self._y[0]
+            return self.ft(y) if n > 1 else y.clone().to(self._FTOUTDTYPE)
+        return self._cached(("ytilde", n), f, grad_sensitive=False)
+
+    def _ev(self, n):
+        """sqrt(n) lam + noise (util.py:285,292-298, single task; adaptive nugget: util.py:286-290)."""
+        lam = self.get_lam(0, 0, n)
+        ev = math.sqrt(n) * lam
+        if self.adaptive_nugget:
+            ev = ev + self.noise * (ev.sum(-1, keepdim=True) / ev.sum(-1, keepdim=True)).abs()
+        else:
+            ev = ev + self.noise
+        return ev * self._task_scalar()
+
+    def get_inv_log_det(self, n=None):
+        n = self._nint(n)
+
+        def f():
+            ev = self._ev(n)
+            return (1 / ev)[..., None, None, :], torch.log(torch.abs(ev)).sum(-1)
+        return self._cached(("invlogdet", n), f)
+
+    def _inv(self, n):
+        return self.get_inv_log_det(n)[0][..., 0, 0, :]
+
+    def _solve(self, v, n):
+        """K^-1 v = ift(A ft(v)).real (util.py:338-353)."""
+        return self.ift(self.ft(v) * self._inv(n)).real
+
+    @property
+    def coeffs(self):
+        n = int(self.n[0])
+        return self._cached(("coeffs", n), lambda: self._solve(self._y[0], n))
+
+    # ------------------------------------------------------------------ fit
+    def fit(self, loss_metric="MLL", iterations=5000, lr=None, optimizer=None, stop_crit_improvement_threshold=5e-2,
+            stop_crit_wait_iterations=10, store_hists=False, store_loss_hist=False, store_scale_hist=False,
+            store_lengthscales_hist=False, store_noise_hist=False, store_task_kernel_hist=False, verbose=5,
+            verbose_indent=4, masks=None, cv_weights=1):
+        """Hyper-parameter optimisation with the reference's semantics (abstract_gp.py:152-306)."""
+        assert isinstance(loss_metric, str) and loss_metric.upper() in ["MLL", "GCV", "CV"]
+        assert (self.n > 0).any(), "cannot fit without data"
+        assert isinstance(iterations, int) and iterations >= 0
+        assert (isinstance(verbose, int) or isinstance(verbose, bool)) and verbose >= 0, \
+            "require verbose is a non-negative int"
+        assert isinstance(verbose_indent, int) and verbose_indent >= 0, \
+            "require verbose_indent is a non-negative int"
+        assert np.isscalar(stop_crit_improvement_threshold) and 0 < stop_crit_improvement_threshold, \
+            "require stop_crit_improvement_threshold is a positive float"
+        assert isinstance(stop_crit_wait_iterations, int) and stop_crit_wait_iterations > 0
+        assert masks is None or isinstance(masks, torch.Tensor)
+        loss_metric = loss_metric.upper()
+        hists = dict(loss=store_hists or store_loss_hist,
+                     scale=store_hists or (store_scale_hist and self.raw_scale.requires_grad),
+                     lengthscales=store_hists or (store_lengthscales_hist and self.raw_lengthscales.requires_grad),
+                     noise=store_hists or (store_noise_hist and self.raw_noise.requires_grad),
+                     task_kernel=store_hists or (store_task_kernel_hist and (
+                         self.raw_factor_task_kernel.requires_grad or self.raw_noise_task_kernel.requires_grad)))
+        stop = (np.log(1 + stop_crit_improvement_threshold), stop_crit_wait_iterations)
+        fused = (loss_metric == "MLL" and optimizer is None and masks is None and self._fused_ok())
+        if optimizer is None:
+            optimizer = None if fused else self.get_default_optimizer(lr)
+        else:
+            assert isinstance(optimizer, torch.optim.Optimizer)
+        if fused:
+            return self._fit_fused(iterations, 1e-1 if lr is None else lr, stop, hists, verbose, verbose_indent)
+        return self._fit_generic(loss_metric, iterations, optimizer, stop, hists, verbose, verbose_indent, masks,
+                                 cv_weights)
+
+    def _fused_ok(self):
+        n = int(self.n[0])
+        if n < 16 or self.d > 8 or self.adaptive_nugget:
+            return False
+        if self._tfs["scale"][1] is not _exp or self._tfs["lengthscales"][1] is not _exp or \
+                self._tfs["noise"][1] is not _exp:
+            return False
+        if self.raw_factor_task_kernel.requires_grad or self.raw_noise_task_kernel.requires_grad:
+            return False
+        kt = self.gram_matrix_tasks.detach()
+        if not torch.equal(kt, torch.ones_like(kt)):
+            return False
+        pb = self._problem_batch()
+        return pb is not None
+
+    def _problem_batch(self):
+        """G and the per-problem flags for the fused layout (None when shapes need broadcasting)."""
+        shapes = [self.raw_scale.shape[:-1], self.raw_lengthscales.shape[:-1], self.raw_noise.shape[:-1]]
+        big = max(shapes, key=len)
+        G = int(torch.tensor(big).prod()) if len(big) else 1
+        for s in shapes:
+            cnt = int(torch.tensor(s).prod()) if len(s) else 1
+            if cnt != 1 and s != big:
+                return None
+        return big, G
+
+    def _ysq(self, pb_shape, G):
+        yt = self.get_ytilde(0)
+        ysq = (yt.real ** 2 + yt.imag ** 2) if yt.is_complex() else yt ** 2
+        return ysq.reshape((-1, G, ysq.shape[-1])).sum(0)
+
+    def _log_header(self, verbose, indent):
+        if verbose:
+            s = "%16s | %-10s | %-10s | %-10s" % ("iter of %.1e" % self._iters_for_log, "loss", "term1", "term2")
+            print(" " * indent + s)
+            print(" " * indent + "~" * len(s))
+
+    def _log_row(self, i, loss, t1, t2, indent):
+        print(" " * indent + "%16.2e | %-10.2e | %-10.2e | %-10.2e" % (i, loss, t1, t2))
+
+    def _fit_fused(self, iterations, lr, stop, hists, verbose, indent):
+        logtol, wait_max = stop
+        n = int(self.n[0])
+        pb_shape, G = self._problem_batch()
+        d_out = int(torch.tensor(self.shape_batch).prod())
+        parts = self._k1parts(n)
+        ls_raw = self.raw_lengthscales.detach()
+        ls2 = ls_raw.reshape(-1, ls_raw.shape[-1])
+        eng = FusedMLL(self._FAMILY, parts, self._ysq(pb_shape, G), self.raw_scale.detach().reshape(-1), ls2,
+                       self.raw_noise.detach().reshape(-1), logdet_weight=d_out / G,
+                       mll_const=mll_constant(d_out, n),
+                       requires_grad=(self.raw_scale.requires_grad, self.raw_lengthscales.requires_grad,
+                                      self.raw_noise.requires_grad),
+                       lr=lr, max_iters=min(iterations + 1, 64))
+        self._iters_for_log = iterations
+        self._log_header(verbose, indent)
+        best, save, waited = math.inf, math.inf, 0
+        best_i, i, i0, chunk = 0, 0, 0, 4
+        total = iterations + 1
+        done = False
+        losses = []
+        while not done:
+            k = min(chunk, total - i0)
+            eng.run(i0, k, final_no_update=(i0 + k == total))
+            lh = eng.loss_hist[i0:i0 + k].cpu()
+            for r in range(k):
+                i = i0 + r
+                lv = float(lh[r, 0])
+                losses.append((lv, float(lh[r, 1]), float(lh[r, 2])))
+                if lv < best:
+                    best, best_i = lv, i
+                if (save - lv) > logtol:
+                    waited = 0
+                    save = best
+                else:
+                    waited += 1
+                brk = i == iterations or waited == wait_max
+                if verbose and (i % verbose == 0 or brk):
+                    self._log_row(i, lv, losses[-1][1], losses[-1][2], indent)
+                if brk:
+                    done = True
+                    break
+            i0 += k
+            chunk = min(64, chunk * 2)
+        raw_hist = eng.raw_hist[:i + 1]
+        s_raw, l_raw, nz_raw = eng.split_raw(raw_hist)
+        b_s, b_l, b_n = eng.split_raw(raw_hist[best_i])
+        with torch.no_grad():
+            for name, val in (("raw_scale", b_s), ("raw_lengthscales", b_l), ("raw_noise", b_n)):
+                old = getattr(self, name)
+                setattr(self, name, torch.nn.Parameter(val.reshape(old.shape).clone(), requires_grad=old.requires_grad))
+        self._cache = {}
+        self._snap = None
+        data = {"iterations": i}
+        if hists["loss"]:
+            data["loss_hist"] = torch.tensor([-v[0] for v in losses])
+        if hists["scale"]:
+            data["scale_hist"] = self.tf_scale(s_raw.reshape((-1,) + self.raw_scale.shape)).cpu()
+        if hists["lengthscales"]:
+            data["lengthscales_hist"] = self.tf_lengthscales(l_raw.reshape((-1,) + self.raw_lengthscales.shape)).cpu()
+        if hists["noise"]:
+            data["noise_hist"] = self.tf_noise(nz_raw.reshape((-1,) + self.raw_noise.shape)).cpu()
+        if hists["task_kernel"]:
+            data["task_kernel_hist"] = self.gram_matrix_tasks.detach().cpu()[None].expand(
+                (i + 1,) + self.gram_matrix_tasks.shape).clone()
+        return data
+
+    def _loss_generic(self, loss_metric, masks, cv_weights, d_out):
+        n = int(self.n[0])
+        A, logdet = self.get_inv_log_det(n)
+        A = A[..., 0, 0, :]
+        yt = self.get_ytilde(0)
+        if loss_metric == "MLL":
+            z = yt * A
+            norm = (yt.conj() * z).real.sum(-1, keepdim=True) if yt.is_complex() else (yt * z).sum(-1, keepdim=True)
+            logdet = logdet[..., None]
+            if masks is None:
+                t1 = norm.sum()
+                t2 = d_out / torch.tensor(logdet.shape).prod() * logdet.sum()
+            else:
+                t1 = norm[(..., *masks, 0)].sum()
+                t2 = logdet.expand(list(self.shape_batch) + [1])[(..., *masks, 0)].sum()
+            return 0.5 * (t1 + t2 + d_out * n * np.log(2 * np.pi)), t1, t2, None
+        if loss_metric == "GCV":
+            z = yt * A
+            numer = (z.conj() * z).real.sum(-1, keepdim=True) if z.is_complex() else (z * z).sum(-1, keepdim=True)
+            denom = ((A.real if A.is_complex() else A).sum(-1, keepdim=True) / n) ** 2
+            if masks is None:
+                t1, t2 = numer, denom
+            else:
+                t1 = numer[(..., *masks, slice(None))]
+                t2 = denom.expand(list(self.shape_batch) + [1])[(..., *masks, slice(None))]
+            loss = (t1 / t2).sum()
+            return loss, t1, t2, loss
+        # CV (util.py:381-385 single task; abstract_gp.py:262-273)
+        coeffs = self._solve(self._y[0], n)
+        lam = self.get_lam(0, 0, n)
+        inv_diag = (1 / (lam * np.sqrt(n))).mean(-1, keepdim=True)
+        sq = ((coeffs / inv_diag) ** 2 * cv_weights)
+        sq = (sq.real if sq.is_complex() else sq).sum(-1, keepdim=True)
+        loss = sq.sum() if masks is None else sq[(..., *masks, 0)].sum()
+        nan = torch.nan * torch.ones(1)
+        return loss, nan, nan, loss
+
+    def _fit_generic(self, loss_metric, iterations, optimizer, stop, hists, verbose, indent, masks, cv_weights):
+        logtol, wait_max = stop
+        if masks is not None:
+            masks = torch.atleast_2d(masks)
+            assert masks.ndim == 2 and len(masks) <= len(self.shape_batch)
+            d_out = torch.empty(self.shape_batch)[(..., *masks)].numel()
+        else:
+            d_out = int(torch.tensor(self.shape_batch).prod())
+        self._iters_for_log = iterations
+        self._log_header(verbose, indent)
+        rec = {k: [] for k in ("loss", "scale", "lengthscales", "noise", "task_kernel")}
+        best, save, waited = math.inf, math.inf, 0
+        best_params = None
+        for i in range(iterations + 1):
+            self._cache = {}
+            loss, t1, t2, metric = self._loss_generic(loss_metric, masks, cv_weights, d_out)
+            lv = loss.item()
+            if lv < best:
+                best = lv
+                best_params = {k: p.data.clone() for k, p in self.named_parameters()}
+            if (save - lv) > logtol:
+                waited = 0
+                save = best
+            else:
+                waited += 1
+            brk = i == iterations or waited == wait_max
+            if hists["loss"]:
+                rec["loss"].append(-lv if metric is None else metric.item())
+            if hists["scale"]:
+                rec["scale"].append(self.scale.detach().cpu())
+            if hists["lengthscales"]:
+                rec["lengthscales"].append(self.lengthscales.detach().cpu())
+            if hists["noise"]:
+                rec["noise"].append(self.noise.detach().cpu())
+            if hists["task_kernel"]:
+                rec["task_kernel"].append(self.gram_matrix_tasks.detach().cpu())
+            if verbose and (i % verbose == 0 or brk):
+                self._log_row(i, lv, t1.item() if t1.numel() == 1 else torch.nan,
+                              t2.item() if t2.numel() == 1 else torch.nan, indent)
+            if brk:
+                break
+            loss.backward()
+            optimizer.step()
+            optimizer.zero_grad()
+        for k, v in best_params.items():
+            setattr(self, k, torch.nn.Parameter(v, requires_grad=getattr(self, k).requires_grad))
+        self._cache = {}
+        self._snap = None
+        data = {"iterations": i}
+        if hists["loss"]:
+            data["loss_hist"] = torch.tensor(rec["loss"])
+        for k in ("scale", "lengthscales", "noise", "task_kernel"):
+            if hists[k]:
+                data[k + "_hist"] = torch.stack(rec[k])
+        return data
+
+    # ------------------------------------------------------------------ prediction
+    def _hyp_rows(self, batch_params):
+        """[Gk, 1+d] (scale, lengthscales) rows for the prediction kernels."""
+        s, ls = self.scale.detach(), self.lengthscales.detach()
+        if not batch_params:
+            return torch.cat([s.reshape(1), ls.reshape(-1).expand(self.d)])[None]
+        sb = self.shape_batch
+        s = s.expand(tuple(sb) + (1,)).reshape(-1, 1)
+        ls = ls.expand(tuple(sb) + (self.d,)).reshape(-1, self.d)
+        return torch.cat([s, ls], -1)
+
+    def _has_batch_params(self):
+        return self.raw_scale.dim() > 1 or self.raw_lengthscales.dim() > 1
+
+    def _check_unit(self, x, name="x"):
+        assert ((0 <= x) & (x <= 1)).all(), "%s should have all elements in [0,1]" % name
+
+    def _task_arg(self, task):
+        if task is None:
+            task = self.default_task
+        inttask = isinstance(task, int)
+        if inttask:
+            task = torch.tensor([task], dtype=torch.int64)
+        if isinstance(task, list):
+            task = torch.tensor(task, dtype=torch.int64)
+        assert task.ndim == 1 and (task >= 0).all() and (task < self.num_tasks).all()
+        return inttask
+
+    def _n_arg(self, n):
+        if n is None:
+            n = self.n
+        if isinstance(n, int):
+            n = torch.tensor([n], dtype=torch.int64, device=self.device)
+        assert isinstance(n, torch.Tensor) and (n & (n - 1) == 0).all() and (n >= self.n).all(), \
+            "require n are all power of two greater than or equal to self.n"
+        return int(n.reshape(-1)[0])
+
+    def _cross_rows(self, x, n, batch_params):
+        """rows[g, t, i] = K(x_t, xb_i) for the first n points."""
+        self._ensure_points(n)
+        z = self._xb[:n].T.contiguous()
+        return ops.kernel_rows(self._FAMILY, x, z, self._hyp_rows(batch_params), alphas=self._alphas,
+                               tbits=self._tbits())
+
+    def _kdiag(self, x):
+        """K(x, x) (zero distance parts)."""
+        part0 = self._part_at_zero().to(self.device)
+        return self.scale * (1 + self.lengthscales * part0).prod(-1, keepdim=True)
+
+    def post_mean(self, x, task=None, eval=True):
+        """Posterior mean (abstract_gp.py:352-380) via the matrix-free HIP contraction."""
+        coeffs = self.coeffs
+        if eval:
+            incoming = torch.is_grad_enabled()
+            torch.set_grad_enabled(False)
+        try:
+            assert x.ndim == 2 and x.size(1) == self.d, "x must a torch.Tensor with shape (-1,d)"
+            inttask = self._task_arg(task)
+            x = x.to(device=self.device, dtype=torch.float64)
+            self._check_unit(x)
+            n = int(self.n[0])
+            if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+                kmat = self._kernel_torch(x[:, None, :], self._xb[:n][None, :, :])
+                pm = torch.einsum("...i,...i->...", kmat, coeffs[..., None, :])
+            else:
+                bp = self._has_batch_params()
+                c2 = coeffs.reshape(-1, n)
+                z = self._xb[:n].T.contiguous()
+                pm = ops.post_mean_matfree(self._FAMILY, x, z, self._hyp_rows(bp), c2, alphas=self._alphas,
+                                           tbits=self._tbits())
+                pm = pm.reshape(tuple(coeffs.shape[:-1]) + (x.size(0),))
+        finally:
+            if eval:
+                torch.set_grad_enabled(incoming)
+        return pm if inttask else pm[..., None, :]
+
+    def post_var(self, x, task=None, n=None, eval=True):
+        """Posterior variance (abstract_gp.py:381-416, abstract_fast_gp.py:41-46)."""
+        n = self._n_arg(n)
+        assert x.ndim == 2 and x.size(1) == self.d, "x must a torch.Tensor with shape (-1,d)"
+        if eval:
+            incoming = torch.is_grad_enabled()
+            torch.set_grad_enabled(False)
+        try:
+            inttask = self._task_arg(task)
+            x = x.to(device=self.device, dtype=torch.float64)
+            self._check_unit(x)
+            bp = self._has_batch_params()
+            rows = self._cross_rows(x, n, bp)                      # [Gk, N, n]
+            kmat = rows[0] if not bp else rows.reshape(tuple(self.shape_batch) + rows.shape[1:])
+            t = self._solve(kmat.movedim(-2, 0), n).movedim(0, -2)
+            diag = self._kdiag(x) - (t * kmat).sum(-1)
+            diag[diag < 0] = 0
+        finally:
+            if eval:
+                torch.set_grad_enabled(incoming)
+        return diag if inttask else diag[..., None, :]
+
+    def post_cov(self, x0, x1, task0=None, task1=None, n=None, eval=True):
+        """Posterior covariance (abstract_gp.py:417-474, abstract_fast_gp.py:47-52)."""
+        n_arg = n if n is not None else self.n
+        if isinstance(n_arg, int):
+            n_arg = torch.tensor([n_arg], dtype=torch.int64, device=self.device)
+        assert isinstance(n_arg, torch.Tensor) and (n_arg & (n_arg - 1) == 0).all() and (n_arg >= self.n).all(), \
+            "require n are all power of two"
+        n = int(n_arg.reshape(-1)[0])
+        assert x0.ndim == 2 and x0.size(1) == self.d, "x must a torch.Tensor with shape (-1,d)"
+        assert x1.ndim == 2 and x1.size(1) == self.d, "z must a torch.Tensor with shape (-1,d)"
+        if eval:
+            incoming = torch.is_grad_enabled()
+            torch.set_grad_enabled(False)
+        try:
+            i0 = self._task_arg(task0)
+            i1 = self._task_arg(task1)
+            x0 = x0.to(device=self.device, dtype=torch.float64)
+            x1 = x1.to(device=self.device, dtype=torch.float64)
+            equal = torch.equal(x0, x1)
+            bp = self._has_batch_params()
+            hyp = self._hyp_rows(bp)
+            z1 = (x1 if self._FAMILY == ops.LATTICE else self._to_b(x1)).T.contiguous()
+            knew = ops.kernel_rows(self._FAMILY, x0, z1, hyp, alphas=self._alphas, tbits=self._tbits())
+            k1 = self._cross_rows(x0, n, bp)
+            k2 = k1 if equal else self._cross_rows(x1, n, bp)
+            shp = (lambda r: r[0]) if not bp else (lambda r: r.reshape(tuple(self.shape_batch) + r.shape[1:]))
+            knew, k1, k2 = shp(knew), shp(k1), shp(k2)
+            t = self._solve(k2.movedim(-2, 0), n).movedim(0, -2)    # [..., M, n]
+            cov = knew - torch.einsum("...ni,...mi->...nm", k1, t)
+            if equal:
+                dg = cov.diagonal(dim1=-2, dim2=-1)
+                dg[dg < 0] = 0
+        finally:
+            if eval:
+                torch.set_grad_enabled(incoming)
+        if i0 and i1:
+            return cov
+        if i0:
+            return cov[..., None, :, :]
+        if i1:
+            return cov[..., None, :, :]
+        return cov[..., None, None, :, :]
+
+    def post_error(self, x, task=None, n=None, confidence=0.99, eval=True):
+        assert np.isscalar(confidence) and 0 < confidence < 1, "confidence must be between 0 and 1"
+        q = scipy.stats.norm.ppf(1 - (1 - confidence) / 2)
+        pvar = self.post_var(x, task=task, n=n, eval=eval)
+        return pvar, q, q * torch.sqrt(pvar)
+
+    def post_ci(self, x, task=None, confidence=0.99, eval=True):
+        assert np.isscalar(confidence) and 0 < confidence < 1, "confidence must be between 0 and 1"
+        q = scipy.stats.norm.ppf(1 - (1 - confidence) / 2)
+        pmean = self.post_mean(x, task=task, eval=eval)
+        pvar, q, perror = self.post_error(x, task=task, confidence=confidence)
+        # the reference scales by q twice (abstract_gp.py:497-498,523-525); kept for drop-in parity
+        return pmean, pvar, q, pmean - q * perror, pmean + q * perror
+
+    def post_cubature_mean(self, task=None, eval=True):
+        """abstract_fast_gp.py:65-81 (single task)."""
+        coeffs = self.coeffs
+        if eval:
+            incoming = torch.is_grad_enabled()
+            torch.set_grad_enabled(False)
+        try:
+            inttask = self._task_arg(task)
+            pc = (self.scale * coeffs).sum(-1) * self._task_scalar()
+        finally:
+            if eval:
+                torch.set_grad_enabled(incoming)
+        return pc if inttask else pc[..., None]
+
+    def post_cubature_var(self, task=None, n=None, eval=True):
+        """abstract_fast_gp.py:82-109 (single task: the frequency-0 entry of the inverse)."""
+        n = self._n_arg(n)
+        A = self._inv(n)
+        if eval:
+            incoming = torch.is_grad_enabled()
+            torch.set_grad_enabled(False)
+        try:
+            inttask = self._task_arg(task)
+            term = n * A[..., 0:1]
+            term = term.real if term.is_complex() else term
+            pcvar = self.scale - self.scale ** 2 * term
+            pcvar[pcvar < 0] = 0.
+        finally:
+            if eval:
+                torch.set_grad_enabled(incoming)
+        return pcvar[..., 0] if inttask else pcvar
+
+    def post_cubature_cov(self, task0=None, task1=None, n=None, eval=True):
+        pv = self.post_cubature_var(task=0, n=n, eval=eval)
+        i0 = task0 is None or isinstance(task0, int)
+        i1 = task1 is None or isinstance(task1, int)
+        if i0 and i1:
+            return pv
+        return pv[..., None, None] if not (i0 or i1) else pv[..., None]
+
+    def post_cubature_error(self, task=None, n=None, confidence=0.99, eval=True):
+        assert np.isscalar(confidence) and 0 < confidence < 1, "confidence must be between 0 and 1"
+        q = scipy.stats.norm.ppf(1 - (1 - confidence) / 2)
+        pcvar = self.post_cubature_var(task=task, n=n, eval=eval)
+        return pcvar, q, q * torch.sqrt(pcvar)
+
+    def post_cubature_ci(self, task=None, confidence=0.99, eval=True):
+        assert np.isscalar(confidence) and 0 < confidence < 1, "confidence must be between 0 and 1"
+        q = scipy.stats.norm.ppf(1 - (1 - confidence) / 2)
+        pcmean = self.post_cubature_mean(task=task, eval=eval)
+        pcvar, q, pcerror = self.post_cubature_error(task=task, confidence=confidence, eval=eval)
+        return pcmean, pcvar, q, pcmean - pcerror, pcmean + pcerror
+
+    def kernel(self, x, z, beta0=None, beta1=None, c0=None, c1=None):
+        """K(x, z) with broadcasting (abstract_gp.py:693-706), beta = kappa = 0 only."""
+        assert isinstance(x, torch.Tensor) and x.size(-1) == self.d
+        assert isinstance(z, torch.Tensor) and z.size(-1) == self.d
+        for b in (beta0, beta1):
+            if b is not None and (b != 0).any():
+                raise NotImplementedError("derivative kernels (beta != 0) are not built yet")
+        return self._kernel_torch(x, z)
+
+
+class FastGPLattice(AbstractFastGP):
+    """Fast GP on shifted rank-1 lattices with shift-invariant (Bernoulli) kernels: the Gram matrix
+    is diagonalised by the bit-reversed-input FFT (fastgps/fast_gp_lattice.py:7-273)."""
+
+    _FAMILY = ops.LATTICE
+    _XBDTYPE = torch.float64
+    _FTOUTDTYPE = torch.complex128
+
+    def __init__(self, seqs, num_tasks=None, seed_for_seq=None, alpha=2, scale=1., lengthscales=1., noise=1e-8,
+                 factor_task_kernel=1., rank_factor_task_kernel=None, noise_task_kernel=1., device="cuda",
+                 tfs_scale=_DEFAULT_TFS, tfs_lengthscales=_DEFAULT_TFS, tfs_noise=_DEFAULT_TFS,
+                 tfs_factor_task_kernel=_IDENTITY_TFS, tfs_noise_task_kernel=_DEFAULT_TFS, requires_grad_scale=True,
+                 requires_grad_lengthscales=True, requires_grad_noise=False, requires_grad_factor_task_kernel=None,
+                 requires_grad_noise_task_kernel=None, shape_batch=torch.Size([]), shape_scale=torch.Size([1]),
+                 shape_lengthscales=None, shape_noise=torch.Size([1]), shape_factor_task_kernel=None,
+                 shape_noise_task_kernel=None, derivatives=None, derivatives_coeffs=None, compile_fts=False,
+                 compile_fts_kwargs={}, adaptive_nugget=False):
+        assert isinstance(alpha, int) and alpha in (1, 2, 3, 4), "alpha must be in [1, 2, 3, 4]"
+        super().__init__(seqs, num_tasks, seed_for_seq, alpha, scale, lengthscales, noise, factor_task_kernel,
+                         rank_factor_task_kernel, noise_task_kernel, device, tfs_scale, tfs_lengthscales, tfs_noise,
+                         tfs_factor_task_kernel, tfs_noise_task_kernel, requires_grad_scale,
+                         requires_grad_lengthscales, requires_grad_noise, requires_grad_factor_task_kernel,
+                         requires_grad_noise_task_kernel, shape_batch, shape_scale, shape_lengthscales, shape_noise,
+                         shape_factor_task_kernel, shape_noise_task_kernel, derivatives, derivatives_coeffs,
+                         compile_fts, compile_fts_kwargs, adaptive_nugget)
+
+    def _default_seq(self, d, seed):
+        return _seqs.Lattice(d, seed=seed, randomize="SHIFT")
+
+    def _check_seq(self, s):
+        assert getattr(s, "order", "NATURAL") == "NATURAL", "each seq should be in 'NATURAL' order "
+        assert getattr(s, "replications", 1) == 1, "each seq should have only 1 replication"
+        assert getattr(s, "randomize", "SHIFT") in ["FALSE", "SHIFT"], \
+            "each seq should have randomize in ['FALSE','SHIFT']"
+
+    def _sample(self, n_min, n_max):
+        x = torch.from_numpy(np.asarray(self.seq(n_min=int(n_min), n_max=int(n_max)), dtype=np.float64)).to(self.device)
+        return x, x
+
+    def _tbits(self):
+        return 0
+
+    def get_omega(self, m):
+        return torch.exp(-torch.pi * 1j * torch.arange(2 ** m, device=self.device) / 2 ** m)
+
+    def ft(self, x):
+        return ops.fftbr(x, stable=True)
+
+    def ift(self, x):
+        return ops.ifftbr(x, stable=True)
+
+    def _compute_parts(self, xb, x0):
+        self._check_unit(xb)
+        return ops.lattice_parts(xb, x0, self._alphas)
+
+    def _part_at_zero(self):
+        return torch.tensor([ops.lattice_coefficient(a) * float(_bern(2 * a, 0.0)) for a in self._alphas],
+                            dtype=torch.float64)
+
+    def _kernel_torch(self, x, z):
+        delta = (x - z) % 1
+        parts = torch.stack([ops.lattice_coefficient(a) * _bern_t(2 * a, delta[..., j])
+                             for j, a in enumerate(self._alphas)], -1)
+        ndim = parts.ndim
+        s = self.scale.reshape(self.scale.shape + torch.Size([1] * (ndim - 2)))
+        ls = self.lengthscales.reshape(self.lengthscales.shape[:-1] + torch.Size([1] * (ndim - 1)) +
+                                       self.lengthscales.shape[-1:])
+        return s * (1 + ls * parts).prod(-1)
+
+
+class FastGPDigitalNetB2(AbstractFastGP):
+    """Fast GP on digitally shifted base-2 digital nets with digitally-shift-invariant (Walsh)
+    kernels: the Gram matrix is diagonalised by the FWHT (fastgps/fast_gp_digital_net_b2.py:7-301).
+    Order-1 Walsh kernels (alpha=1) are supported; orders 2-4 need qmcpy.weighted_walsh_funcs,
+    whose values are unpinned offline and raise NotImplementedError."""
+
+    _FAMILY = ops.NET
+    _XBDTYPE = torch.int64
+    _FTOUTDTYPE = torch.float64
+
+    def __init__(self, seqs, num_tasks=None, seed_for_seq=None, alpha=2, scale=1., lengthscales=1., noise=1e-16,
+                 factor_task_kernel=1., rank_factor_task_kernel=None, noise_task_kernel=1., device="cuda",
+                 tfs_scale=_DEFAULT_TFS, tfs_lengthscales=_DEFAULT_TFS, tfs_noise=_DEFAULT_TFS,
+                 tfs_factor_task_kernel=_IDENTITY_TFS, tfs_noise_task_kernel=_DEFAULT_TFS, requires_grad_scale=True,
+                 requires_grad_lengthscales=True, requires_grad_noise=False, requires_grad_factor_task_kernel=None,
+                 requires_grad_noise_task_kernel=None, shape_batch=torch.Size([]), shape_scale=torch.Size([1]),
+                 shape_lengthscales=None, shape_noise=torch.Size([1]), shape_factor_task_kernel=None,
+                 shape_noise_task_kernel=None, derivatives=None, derivatives_coeffs=None, compile_fts=False,
+                 compile_fts_kwargs={}, adaptive_nugget=False):
+        super().__init__(seqs, num_tasks, seed_for_seq, alpha, scale, lengthscales, noise, factor_task_kernel,
+                         rank_factor_task_kernel, noise_task_kernel, device, tfs_scale, tfs_lengthscales, tfs_noise,
+                         tfs_factor_task_kernel, tfs_noise_task_kernel, requires_grad_scale,
+                         requires_grad_lengthscales, requires_grad_noise, requires_grad_factor_task_kernel,
+                         requires_grad_noise_task_kernel, shape_batch, shape_scale, shape_lengthscales, shape_noise,
+                         shape_factor_task_kernel, shape_noise_task_kernel, derivatives, derivatives_coeffs,
+                         compile_fts, compile_fts_kwargs, adaptive_nugget)
+        assert (1 <= self.alpha).all() and (self.alpha <= 4).all()
+        self.t = int(self.seq.t)
+        assert self.t < 64, "each seq must have t<64"
+        if any(a != 1 for a in self._alphas):
+            raise NotImplementedError("digital-net kernels of order alpha>=2 need qmcpy.weighted_walsh_funcs, "
+                                      "which is not available offline (parity unpinned); use alpha=1")
+
+    def _default_seq(self, d, seed):
+        return _seqs.DigitalNetB2(d, seed=seed, randomize="DS")
+
+    def _check_seq(self, s):
+        assert getattr(s, "order", "NATURAL") == "NATURAL", "each seq should be in 'NATURAL' order "
+        assert getattr(s, "replications", 1) == 1, "each seq should have only 1 replication"
+        assert getattr(s, "randomize", "DS") in ['FALSE', 'DS', 'LMS', 'LMS_DS'], \
+            "seq should have randomize in ['FALSE','DS','LMS','LMS_DS']"
+
+    def _sample(self, n_min, n_max):
+        xb = torch.from_numpy(np.asarray(self.seq(n_min=int(n_min), n_max=int(n_max), return_binary=True))
+                              .astype(np.int64)).to(self.device)
+        return self._convert_from_b(xb), xb
+
+    def _tbits(self):
+        return self.t
+
+    def get_omega(self, m):
+        return 1
+
+    def _to_b(self, x):
+        return torch.floor((x % 1) * 2 ** self.t).to(torch.int64)
+
+    _convert_to_b = _to_b
+
+    def _convert_from_b(self, xb):
+        return xb * 2 ** (-self.t)
+
+    def ft(self, x):
+        return ops.fwht(x, stable=True)
+
+    def ift(self, x):
+        return ops.fwht(x, stable=True)
+
+    def _compute_parts(self, xb, x0):
+        return ops.net_parts(xb, x0, self.t)
+
+    def _part_at_zero(self):
+        return torch.ones(self.d, dtype=torch.float64)
+
+    def _kernel_torch(self, x, z):
+        xb = self._to_b(x) if torch.is_floating_point(x) else x
+        zb = self._to_b(z) if torch.is_floating_point(z) else z
+        delta = xb ^ zb
+        parts = 6 * (1 / 6 - 2 ** (torch.log2(delta).floor() - self.t - 1))
+        ndim = parts.ndim
+        s = self.scale.reshape(self.scale.shape + torch.Size([1] * (ndim - 2)))
+        ls = self.lengthscales.reshape(self.lengthscales.shape[:-1] + torch.Size([1] * (ndim - 1)) +
+                                       self.lengthscales.shape[-1:])
+        return s * (1 + ls * parts).prod(-1)
+
+
+_BERN = {
+    2: [1.0, -1.0, 1 / 6], 4: [1.0, -2.0, 1.0, 0.0, -1 / 30], 6: [1.0, -3.0, 5 / 2, 0.0, -1 / 2, 0.0, 1 / 42],
+    8: [1.0, -4.0, 14 / 3, 0.0, -7 / 3, 0.0, 2 / 3, 0.0, -1 / 30],
+}
+
+
+def _bern(order, x):
+    y = 0.0
+    for c in _BERN[order]:
+        y = y * x + c
+    return y
+
+
+def _bern_t(order, x):
+    c = _BERN[order]
+    y = torch.zeros_like(x) + c[0]
+    for ci in c[1:]:
+        y = y * x + ci
+    return y

@@ -1,0 +1,136 @@
+"""Device-resident MLL fit loop (fgp_nll_fwd / fgp_nll_bwd / fgp_fit_step of include/fgp_hip.h).
+
+One `FusedMLL` holds, for G eigen-problems of size n = 2^m:
+  * kernel parts [G?, d, n] (shared when parts_stride = 0),
+  * Y[g, k] = sum over the outputs of problem g of |ytilde[k]|^2 (the only data the MLL needs),
+  * the raw hyper-parameter vector  [raw_scale..., raw_lengthscales..., raw_noise...]  (log scale),
+  * workspaces (dL/dlambda, 2-pass intermediate, per-block partials), Rprop state and histories.
+`run(iter0, k)` enqueues k complete iterations (forward, adjoint, reduction, Rprop) on the current
+stream without any host synchronisation; the caller reads the histories back in chunks to apply
+AbstractGP.fit's early-stopping rule (fastgps/abstract_gp.py:276-284) exactly.
+"""
+import math
+
+import torch
+
+from . import _native as N
+from .ops import log2_exact, require_device
+
+# torch.optim.Rprop defaults (etas=(0.5, 1.2), step_sizes=(1e-6, 50))
+RPROP_ETAS = (0.5, 1.2)
+RPROP_STEPS = (1e-6, 50.0)
+
+
+class FusedMLL(object):
+    def __init__(self, family, parts, ysq, raw_scale, raw_lengthscales, raw_noise, logdet_weight, mll_const,
+                 requires_grad=(True, True, False), lr=0.1, max_iters=1, parts_per_problem=False):
+        """
+        family: 0 lattice (FFT) / 1 net (FWHT)
+        parts:  [d, n] shared, or [G, d, n] when parts_per_problem
+        ysq:    [G, n]
+        raw_scale [S] with S in {1, G}; raw_lengthscales [S_l, D_l] with S_l in {1, G}, D_l in {1, d};
+        raw_noise [S_n] with S_n in {1, G}
+        """
+        require_device(ysq, "FusedMLL")
+        self.device = ysq.device
+        self.family = int(family)
+        G, n = ysq.shape
+        self.G, self.n = int(G), int(n)
+        self.m = log2_exact(n)
+        if self.m < 4:
+            raise ValueError("fused fit needs n >= 16")
+        d = parts.shape[-2]
+        self.d = int(d)
+        if d > 8:
+            raise ValueError("fused fit supports d <= 8")
+        self.parts = parts.contiguous()
+        self.ysq = ysq.contiguous()
+        S = raw_scale.numel()
+        Sl, Dl = raw_lengthscales.shape
+        Sn = raw_noise.numel()
+        for cnt in (S, Sl, Sn):
+            if cnt not in (1, G):
+                raise ValueError("hyper-parameter batch must be 1 or G")
+        if Dl not in (1, d):
+            raise ValueError("lengthscales last dim must be 1 or d")
+        self.layout = dict(scale_off=0, scale_pp=int(S == G and G > 1),
+                           ls_off=S, ls_pp=int(Sl == G and G > 1), ls_pd=int(Dl == d and Dl > 1 or d == 1),
+                           noise_off=S + Sl * Dl, noise_pp=int(Sn == G and G > 1))
+        if d == 1:
+            self.layout["ls_pd"] = 1
+        self.sizes = (S, Sl * Dl, Sn)
+        self.n_params = S + Sl * Dl + Sn
+        self.raw = torch.cat([raw_scale.reshape(-1), raw_lengthscales.reshape(-1), raw_noise.reshape(-1)]).to(
+            device=self.device, dtype=torch.float64).contiguous()
+        cdt = torch.complex128 if self.family == 0 else torch.float64
+        self.grad_lam = torch.empty((G, n), dtype=cdt, device=self.device)
+        self.work = torch.empty((G, n), dtype=cdt, device=self.device) if self.m > 12 else None
+        nb = max(1, n >> 12)
+        self.partials = torch.empty((G * (4 + d) * (nb + 1),), dtype=torch.float64, device=self.device)
+        self.prev = torch.zeros(self.n_params, dtype=torch.float64, device=self.device)
+        self.step = torch.full((self.n_params,), float(lr), dtype=torch.float64, device=self.device)
+        self.grad = torch.zeros(self.n_params, dtype=torch.float64, device=self.device)
+        self.max_iters = 0
+        self.loss_hist = None
+        self.raw_hist = None
+        self.ensure_history(max_iters)
+        self._nll = N.NllDesc(
+            family=self.family, log2n=self.m, d=self.d, G=self.G,
+            parts=self.parts.data_ptr(), parts_stride=(d * n if parts_per_problem else 0),
+            ysq=self.ysq.data_ptr(), ysq_stride=n, raw=self.raw.data_ptr(),
+            logdet_weight=float(logdet_weight),
+            grad_lam=self.grad_lam.data_ptr(), work=(self.work.data_ptr() if self.work is not None else 0),
+            partials=self.partials.data_ptr(), **self.layout)
+        self.requires_grad = tuple(int(bool(r)) for r in requires_grad)
+        self.mll_const = float(mll_const)
+        self._fit = None
+        self._refresh_fit_desc()
+
+    def ensure_history(self, iters):
+        if iters <= self.max_iters:
+            return
+        new_max = max(iters, 2 * self.max_iters, 16)
+        lh = torch.zeros((new_max, 3), dtype=torch.float64, device=self.device)
+        rh = torch.zeros((new_max, self.n_params), dtype=torch.float64, device=self.device)
+        if self.loss_hist is not None:
+            lh[:self.max_iters] = self.loss_hist
+            rh[:self.max_iters] = self.raw_hist
+        self.loss_hist, self.raw_hist, self.max_iters = lh, rh, new_max
+        self._refresh_fit_desc()
+
+    def _refresh_fit_desc(self):
+        if not hasattr(self, "mll_const"):
+            return
+        self._fit = N.FitDesc(
+            n_params=self.n_params, raw=self.raw.data_ptr(), rprop_prev=self.prev.data_ptr(),
+            rprop_step=self.step.data_ptr(), grad_out=self.grad.data_ptr(), loss_hist=self.loss_hist.data_ptr(),
+            raw_hist=self.raw_hist.data_ptr(), scale_rg=self.requires_grad[0], ls_rg=self.requires_grad[1],
+            noise_rg=self.requires_grad[2], mll_const=self.mll_const, eta_minus=RPROP_ETAS[0],
+            eta_plus=RPROP_ETAS[1], step_min=RPROP_STEPS[0], step_max=RPROP_STEPS[1])
+
+    def stream(self):
+        return N.stream_ptr(self.device)
+
+    def run(self, iter0, iters, final_no_update=False):
+        """Enqueue `iters` fit iterations writing history rows iter0 .. iter0+iters-1."""
+        self.ensure_history(iter0 + iters)
+        N.call("fgp_fit_run", self._nll, self._fit, int(iter0), int(iters), int(bool(final_no_update)), self.stream())
+
+    def evaluate(self, slot=0):
+        """Loss terms and gradient at the current raw parameters (no update); synchronises."""
+        self.ensure_history(slot + 1)
+        st = self.stream()
+        N.call("fgp_nll_fwd", self._nll, st)
+        N.call("fgp_nll_bwd", self._nll, st)
+        N.call("fgp_fit_step", self._nll, self._fit, int(slot), 0, st)
+        lh = self.loss_hist[slot].cpu()
+        return float(lh[0]), float(lh[1]), float(lh[2]), self.grad.cpu()
+
+    def split_raw(self, raw_vec):
+        S, L, Nn = self.sizes
+        return raw_vec[..., :S], raw_vec[..., S:S + L], raw_vec[..., S + L:S + L + Nn]
+
+
+def mll_constant(d_out, n):
+    """d_out * n * log(2 pi) (fastgps/abstract_gp.py:235)."""
+    return d_out * n * math.log(2 * math.pi)

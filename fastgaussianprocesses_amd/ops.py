@@ -1,0 +1,240 @@
+"""Torch-facing operators over the C-ABI library (include/fgp_hip.h).
+
+Every operator runs on the input tensors' HIP device, on torch's current stream, and raises if a
+tensor is not on a HIP device: there is no CPU fallback.
+
+Drop-in transforms (the plugin point `ft`/`ift` of AbstractFastGP, fastgps/abstract_fast_gp.py:26-27,
+197-228, filled by qmcpy.fftbr_torch / ifftbr_torch / fwht_torch at fast_gp_lattice.py:224-225 and
+fast_gp_digital_net_b2.py:226):
+    fftbr(x)   = fft(x[..., bitrev], norm="ortho")          (complex128 out)
+    ifftbr(x)  = ifft(x, norm="ortho")[..., bitrev]
+    fwht(x)    = orthonormal Sylvester-order Walsh-Hadamard
+all differentiable (backward = the exact adjoint transform, real part for real inputs).
+With stable=True the mean-centring of AbstractFastGP.ft/ift happens inside the kernels.
+"""
+import math
+
+import torch
+
+from . import _native as N
+
+LATTICE = 0
+NET = 1
+
+
+def require_device(t, what):
+    if not t.is_cuda:
+        raise RuntimeError("%s: tensor on %s; fastgaussianprocesses_amd runs only on a HIP device (MI355X) "
+                           "and has no CPU fallback" % (what, t.device))
+
+
+def log2_exact(n):
+    n = int(n)
+    if n < 1 or (n & (n - 1)) != 0:
+        raise AssertionError("n = %d must be a power of 2" % n)
+    return n.bit_length() - 1
+
+
+def _as_rows(x):
+    """View x[..., n] as [batch, n] with unit inner stride; returns (rows, batch_stride)."""
+    n = x.shape[-1]
+    r = x.reshape(-1, n)
+    if r.stride(-1) != 1 or (r.size(0) > 1 and r.stride(0) < n):
+        r = r.contiguous()
+    return r, (r.stride(0) if r.size(0) > 1 else n)
+
+
+def _stream(t):
+    return N.stream_ptr(t.device)
+
+
+# ------------------------------------------------------------------------------------- transforms
+def fftbr_raw(x, stable=True):
+    require_device(x, "fftbr")
+    if x.is_complex():
+        x = x.to(torch.complex128)
+    else:
+        x = x.to(torch.float64)
+    shape = x.shape
+    n = shape[-1]
+    m = log2_exact(n)
+    rows, bs = _as_rows(x)
+    out = torch.empty(rows.shape, dtype=torch.complex128, device=x.device)
+    N.call("fgp_fftbr", N.ptr(rows), bs, 0 if x.is_complex() else 1, N.ptr(out), rows.size(0), m, int(stable),
+           _stream(x))
+    return out.reshape(shape)
+
+
+def ifftbr_raw(x, stable=True, real_out=False):
+    require_device(x, "ifftbr")
+    x = x.to(torch.complex128)
+    shape = x.shape
+    n = shape[-1]
+    m = log2_exact(n)
+    rows, bs = _as_rows(x)
+    if real_out:
+        out = torch.empty(rows.shape, dtype=torch.float64, device=x.device)
+        work = torch.empty(rows.shape, dtype=torch.complex128, device=x.device) if m > 12 else None
+    else:
+        out = torch.empty(rows.shape, dtype=torch.complex128, device=x.device)
+        work = None
+    N.call("fgp_ifftbr", N.ptr(rows), bs, N.ptr(out), int(real_out), N.ptr(work), rows.size(0), m, int(stable),
+           _stream(x))
+    return out.reshape(shape)
+
+
+def fwht_raw(x, stable=True):
+    require_device(x, "fwht")
+    if x.is_complex():
+        return torch.complex(fwht_raw(x.real, stable), fwht_raw(x.imag, stable))
+    x = x.to(torch.float64)
+    shape = x.shape
+    m = log2_exact(shape[-1])
+    rows, bs = _as_rows(x)
+    out = torch.empty(rows.shape, dtype=torch.float64, device=x.device)
+    N.call("fgp_fwht", N.ptr(rows), bs, N.ptr(out), rows.size(0), m, int(stable), _stream(x))
+    return out.reshape(shape)
+
+
+class _FFTBR(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, stable):
+        ctx.real_in = not x.is_complex()
+        ctx.stable = stable
+        return fftbr_raw(x, stable)
+
+    @staticmethod
+    def backward(ctx, g):
+        # y = A x  =>  dL/dx = A^H g (real part for a real x); A^H = ifftbr
+        return ifftbr_raw(g, ctx.stable, real_out=ctx.real_in), None
+
+
+class _IFFTBR(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, stable):
+        ctx.real_in = not x.is_complex()
+        ctx.stable = stable
+        return ifftbr_raw(x, stable)
+
+    @staticmethod
+    def backward(ctx, g):
+        gx = fftbr_raw(g, ctx.stable)
+        return (gx.real.contiguous() if ctx.real_in else gx), None
+
+
+class _FWHT(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, stable):
+        ctx.stable = stable
+        return fwht_raw(x, stable)
+
+    @staticmethod
+    def backward(ctx, g):
+        return fwht_raw(g, ctx.stable), None
+
+
+def fftbr(x, stable=False):
+    """Drop-in for qmcpy.fftbr_torch (stable=False) or AbstractFastGP.ft on lattices (stable=True)."""
+    return _FFTBR.apply(x, stable)
+
+
+def ifftbr(x, stable=False):
+    """Drop-in for qmcpy.ifftbr_torch (stable=False) or AbstractFastGP.ift on lattices (stable=True)."""
+    return _IFFTBR.apply(x, stable)
+
+
+def fwht(x, stable=False):
+    """Drop-in for qmcpy.fwht_torch (stable=False) or AbstractFastGP.ft/ift on nets (stable=True)."""
+    return _FWHT.apply(x, stable)
+
+
+# ------------------------------------------------------------------------------------- kernel parts
+def lattice_coefficient(alpha):
+    """(-1)^(alpha+1) (2 pi)^(2 alpha) / (2 alpha)!  evaluated exactly as fast_gp_lattice.py:272."""
+    order = torch.tensor(2 * int(alpha), dtype=torch.int64)
+    return ((-1) ** (int(alpha) + 1) * torch.exp(2 * int(alpha) * math.log(2 * math.pi) - torch.lgamma(order + 1.0))).item()
+
+
+def lattice_parts(x, z, alphas):
+    """parts[j, i] = c_j B_{2 alpha_j}((x[i, j] - z[j]) % 1)  -> [d, n] (fast_gp_lattice.py:263-273)."""
+    require_device(x, "lattice_parts")
+    x = x.to(torch.float64)
+    if x.stride(-1) != 1:
+        x = x.contiguous()
+    z = z.to(torch.float64).contiguous()
+    n, d = x.shape
+    out = torch.empty((d, n), dtype=torch.float64, device=x.device)
+    N.call("fgp_lattice_parts", N.ptr(x), x.stride(0), N.ptr(z), n, d, N.int_array([2 * a for a in alphas]),
+           N.double_array([lattice_coefficient(a) for a in alphas]), N.ptr(out), _stream(x))
+    return out
+
+
+def net_parts(xb, z, t):
+    """Order-1 Walsh parts for delta = xb XOR z -> [d, n] (fast_gp_digital_net_b2.py:274-301)."""
+    require_device(xb, "net_parts")
+    xb = xb.to(torch.int64)
+    if xb.stride(-1) != 1:
+        xb = xb.contiguous()
+    z = z.to(torch.int64).contiguous()
+    n, d = xb.shape
+    out = torch.empty((d, n), dtype=torch.float64, device=xb.device)
+    N.call("fgp_net_parts", N.ptr(xb), xb.stride(0), N.ptr(z), n, d, int(t), N.ptr(out), _stream(xb))
+    return out
+
+
+# ------------------------------------------------------------------------------------- prediction
+def _pred_args(family, alphas, d):
+    if family == LATTICE:
+        return N.int_array([2 * a for a in alphas]), N.double_array([lattice_coefficient(a) for a in alphas])
+    return N.int_array([0] * d), N.double_array([0.0] * d)
+
+
+def post_mean_matfree(family, xt, z_dn, hyp, coeffs, alphas=None, tbits=0, chunk=4096):
+    """out[b, t] = sum_i K_{b mod Gk}(xt[t], z[:, i]) coeffs[b, i] -> [B, N] (see fgp_post_mean).
+
+    xt [N, d] float64, z_dn [d, n] (float64 lattice / int64 net), hyp [Gk, 1 + d] (scale, lengthscales),
+    coeffs [B, n]."""
+    require_device(xt, "post_mean")
+    xt = xt.to(torch.float64).contiguous()
+    Nt, d = xt.shape
+    n = z_dn.shape[1]
+    hyp = hyp.to(torch.float64).contiguous()
+    Gk = hyp.shape[0]
+    coeffs = coeffs.to(torch.float64)
+    if coeffs.stride(-1) != 1:
+        coeffs = coeffs.contiguous()
+    B = coeffs.shape[0]
+    out = torch.empty((B, Nt), dtype=torch.float64, device=xt.device)
+    order, coef = _pred_args(family, alphas, d)
+    nchunks = (n + chunk - 1) // chunk
+    for b0 in range(0, B, 4):
+        b1 = min(B, b0 + 4)
+        if Gk > 1:
+            assert b0 % Gk == 0 or Gk % 4 == 0 or B <= 4, "output chunking must respect b mod Gk"
+        hyp_b = hyp if Gk == 1 else hyp[torch.arange(b0, b1, device=hyp.device) % Gk]
+        work = torch.empty((nchunks, b1 - b0, Nt), dtype=torch.float64, device=xt.device)
+        cb = coeffs[b0:b1]
+        N.call("fgp_post_mean", family, N.ptr(xt), Nt, N.ptr(z_dn), n, d, int(tbits), order, coef, N.ptr(hyp_b),
+               hyp_b.shape[0], N.ptr(cb), cb.stride(0) if cb.shape[0] > 1 else n, b1 - b0, N.ptr(out[b0:b1]),
+               Nt, N.ptr(work), chunk, _stream(xt))
+    return out
+
+
+def kernel_rows(family, xt, z_dn, hyp, alphas=None, tbits=0):
+    """rows[g, t, i] = K_g(xt[t], z[:, i]) -> [Gk, N, n]."""
+    require_device(xt, "kernel_rows")
+    xt = xt.to(torch.float64).contiguous()
+    Nt, d = xt.shape
+    n = z_dn.shape[1]
+    hyp = hyp.to(torch.float64).contiguous()
+    Gk = hyp.shape[0]
+    rows = torch.empty((Gk, Nt, n), dtype=torch.float64, device=xt.device)
+    order, coef = _pred_args(family, alphas, d)
+    for t0 in range(0, Nt, 65535):
+        t1 = min(Nt, t0 + 65535)
+        sub = torch.empty((Gk, t1 - t0, n), dtype=torch.float64, device=xt.device) if Nt > 65535 else rows
+        N.call("fgp_kernel_rows", family, N.ptr(xt[t0:t1]), t1 - t0, N.ptr(z_dn), n, d, int(tbits), order, coef,
+               N.ptr(hyp), Gk, N.ptr(sub), _stream(xt))
+        if sub is not rows:
+            rows[:, t0:t1] = sub
+    return rows

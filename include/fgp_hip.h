@@ -1,0 +1,171 @@
+/* fgp_hip.h — C-ABI of the MI355X-native fast-transform GP hot path (libfgp_hip.so).
+ *
+ * Plain pointers, sizes and an opaque hipStream_t (passed as void*): no torch types cross this
+ * boundary.  Every entry point is stream-ordered (no host synchronisation except the one-time
+ * table initialisation), returns 0 on success or a negative FGP_ERR_* code, and records a
+ * message retrievable with fgp_last_error().  All device pointers are HIP device memory.
+ *
+ * Layout conventions: a "[batch, n]" array is batch rows of n contiguous elements, row i starting
+ * at element i*batch_stride.  complex128 = interleaved (re, im) doubles (torch.complex128).
+ *
+ * Reference interfaces replaced (alegresor/FastGaussianProcesses @ /root/reference):
+ *   fgp_fftbr   <- qmcpy.fftbr_torch injected as ft   (fastgps/fast_gp_lattice.py:224,231) and its
+ *                  stabilising wrapper AbstractFastGP.ft (fastgps/abstract_fast_gp.py:197-212)
+ *   fgp_ifftbr  <- qmcpy.ifftbr_torch injected as ift (fastgps/fast_gp_lattice.py:225,231) and
+ *                  AbstractFastGP.ift (fastgps/abstract_fast_gp.py:213-228); `out_real` fuses the
+ *                  `.real` taken by gram_matrix_solve (fastgps/util.py:343)
+ *   fgp_fwht    <- qmcpy.fwht_torch injected as ft = ift (fastgps/fast_gp_digital_net_b2.py:226,231)
+ */
+#ifndef FGP_HIP_H_
+#define FGP_HIP_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FGP_ABI_VERSION 2
+
+#define FGP_OK 0
+#define FGP_ERR_INVALID (-1)     /* bad argument (shape, stride, null pointer) */
+#define FGP_ERR_UNSUPPORTED (-2) /* size outside the supported range (n > 2^24, ...) */
+#define FGP_ERR_HIP (-3)         /* HIP runtime / launch failure */
+
+/* Library identification and error reporting. */
+int fgp_abi_version(void);
+const char* fgp_last_error(void);
+/* Optional eager initialisation of the per-device twiddle tables on `stream` (otherwise done on
+ * first use; call before hipGraph capture). */
+int fgp_init(void* stream);
+
+/* Orthonormal DFT of bit-reversed-order input along the last axis:
+ *   out[b, k] = n^-1/2 * sum_i in[b, brev_m(i)] exp(-2 pi i k i / n),  n = 2^log2n, 0 <= log2n <= 24.
+ * in: [batch, n] float64 (in_is_real=1) or complex128, row stride in_batch_stride (elements).
+ * out: [batch, n] complex128, contiguous, must not alias `in` unless in is complex and contiguous.
+ * stable=1 applies AbstractFastGP.ft's mean-centring (mathematically the identity). */
+int fgp_fftbr(const void* in, int64_t in_batch_stride, int in_is_real, void* out, int64_t batch, int log2n,
+              int stable, void* stream);
+
+/* Adjoint of fgp_fftbr (= ifft(x, norm="ortho")[..., brev_m]):
+ *   out[b, i] = n^-1/2 * sum_k in[b, k] exp(+2 pi i k brev_m(i) / n).
+ * in: [batch, n] complex128 (row stride in_batch_stride).  out: [batch, n] contiguous, complex128,
+ * or float64 holding only the real part when out_real=1 (then, for n > 4096, `work` must be a
+ * complex128 [batch, n] scratch buffer; otherwise work may be NULL). */
+int fgp_ifftbr(const void* in, int64_t in_batch_stride, void* out, int out_real, void* work, int64_t batch,
+               int log2n, int stable, void* stream);
+
+/* Orthonormal Walsh-Hadamard transform in Sylvester (natural) order, self-inverse:
+ *   out[b, k] = n^-1/2 * sum_i in[b, i] (-1)^popcount(i & k).   float64 in/out, in-place allowed
+ * when in_batch_stride == n. */
+int fgp_fwht(const double* in, int64_t in_batch_stride, double* out, int64_t batch, int log2n, int stable,
+             void* stream);
+
+
+/* ---------------------------------------------------------------------------------------------
+ * Kernel parts and the fused negative-log-likelihood / gradient / Rprop fit step.
+ *
+ * Replaces, for the single-task beta=kappa=0 MLL fit driven by AbstractGP.fit
+ * (fastgps/abstract_gp.py:152-306, default Rprop optimizer fastgps/abstract_fast_gp.py:53-57):
+ *   _K1PartsSeq / _kernel_parts            (fastgps/util.py:50-62, abstract_fast_gp.py:173-180)
+ *   _kernel_from_parts                     (fastgps/abstract_fast_gp.py:181-191)
+ *   _LamCaches lam = ft(k1)                (fastgps/util.py:95-112)
+ *   _FastInverseLogDetCache.__call__       (fastgps/util.py:275-300, single-task branch)
+ *   get_norm_term_logdet_term              (fastgps/util.py:354-370)
+ *   MLL assembly + loss.backward()         (fastgps/abstract_gp.py:235,253-261,294)
+ *   torch.optim.Rprop(lr).step()           (fastgps/abstract_fast_gp.py:53-57)
+ * ------------------------------------------------------------------------------------------- */
+
+#define FGP_FAMILY_LATTICE 0 /* shift-invariant kernel on lattice points: bit-reversed FFT */
+#define FGP_FAMILY_NET 1     /* digitally-shift-invariant kernel on digital nets: FWHT */
+#define FGP_MAX_D 8
+
+/* Lattice first-column kernel parts (fastgps/fast_gp_lattice.py:263-273, beta=kappa=0):
+ *   parts[j, i] = coef[j] * B_{order[j]}((x[i, j] - x[0, j]) % 1),   i < n, j < d.
+ * x: [n, d] float64 with row stride x_row_stride; order[j] = 2*alpha_j in {2,4,6,8};
+ * coef[j] = (-1)^(alpha_j+1) (2 pi)^(2 alpha_j) / (2 alpha_j)!  (host arrays of length d).
+ * parts: [d, n] float64 (dimension-major).  z: [d] float64 reference point (x[0] for the first column). */
+int fgp_lattice_parts(const double* x, int64_t x_row_stride, const double* z, int64_t n, int d, const int* order,
+                      const double* coef, double* parts, void* stream);
+
+/* Digital-net first-column kernel parts, order-1 Walsh kernel (fastgps/fast_gp_digital_net_b2.py:274-301):
+ *   delta = xb[i, j] XOR z[j];  parts[j, i] = 6*(1/6 - 2^(floor(log2 delta) - t - 1))  (1 when delta = 0).
+ * xb: [n, d] int64 t-bit integers (row stride xb_row_stride), z: [d] int64 (device). */
+int fgp_net_parts(const int64_t* xb, int64_t xb_row_stride, const int64_t* z, int64_t n, int d, int t, double* parts,
+                  void* stream);
+
+/* One fused MLL problem batch: G independent eigen-problems of size n = 2^log2n (log2n >= 4). */
+typedef struct fgp_nll_desc {
+  int family;                 /* FGP_FAMILY_LATTICE / FGP_FAMILY_NET */
+  int log2n;                  /* 4 .. 24 */
+  int d;                      /* 1 .. FGP_MAX_D */
+  int G;                      /* number of eigen-problems */
+  const double* parts;        /* [G][d][n] kernel parts; parts_stride elements between problems (0 = shared) */
+  int64_t parts_stride;
+  const double* ysq;          /* [G][n] sum over the outputs of problem g of |ytilde|^2 */
+  int64_t ysq_stride;
+  const double* raw;          /* raw (log) hyper-parameters, device; indexed as below */
+  int scale_off, scale_pp;    /* log scale of g    = raw[scale_off + (scale_pp ? g : 0)] */
+  int ls_off, ls_pp, ls_pd;   /* log lengthscale_j = raw[ls_off + (ls_pp ? g : 0) * (ls_pd ? d : 1) + (ls_pd ? j : 0)] */
+  int noise_off, noise_pp;    /* log noise of g    = raw[noise_off + (noise_pp ? g : 0)] */
+  double logdet_weight;       /* d_out / numel(logdet)  (fastgps/abstract_gp.py:256) */
+  void* grad_lam;             /* workspace [G][n]: dL/dlambda (complex128 lattice, float64 net) */
+  void* work;                 /* workspace [G][n] complex128 (lattice) / float64 (net) */
+  double* partials;           /* workspace [G][4 + d][max(1, n / 4096) + 1] */
+} fgp_nll_desc;
+
+/* Forward: k1 from parts, lambda = ft(k1), ev = sqrt(n) lambda + noise; per-problem partial sums of
+ * the norm term sum|ytilde|^2 Re(1/ev), logdet sum log|ev| and dL/dnoise; writes dL/dlambda. */
+int fgp_nll_fwd(const fgp_nll_desc* desc, void* stream);
+/* Backward: g = Re(ft^H(dL/dlambda)), partial sums of dL/draw_scale and dL/draw_lengthscales. */
+int fgp_nll_bwd(const fgp_nll_desc* desc, void* stream);
+
+/* Rprop state and histories for the device-side fit loop. */
+typedef struct fgp_fit_desc {
+  int n_params;               /* length of raw (== total hyper-parameters of the desc) */
+  double* raw;                /* [n_params] updated in place (the desc's raw) */
+  double* rprop_prev;         /* [n_params] previous gradient (init 0) */
+  double* rprop_step;         /* [n_params] step sizes (init lr) */
+  double* grad_out;           /* [n_params] gradient of the last step (diagnostics) */
+  double* loss_hist;          /* [max_iters][3]: loss, term1 (norm), term2 (weighted logdet) */
+  double* raw_hist;           /* [max_iters][n_params]: raw parameters at which the loss was evaluated */
+  int scale_rg, ls_rg, noise_rg; /* requires_grad of each block */
+  double mll_const;           /* d_out * n * log(2 pi) (fastgps/abstract_gp.py:235) */
+  double eta_minus, eta_plus, step_min, step_max; /* torch.optim.Rprop defaults 0.5, 1.2, 1e-6, 50 */
+} fgp_fit_desc;
+
+/* Reduce the partials of fgp_nll_fwd/bwd, assemble loss = 1/2 (term1 + term2 + mll_const), record
+ * loss_hist[iter] and raw_hist[iter], and (if do_update) apply one Rprop step to raw. */
+int fgp_fit_step(const fgp_nll_desc* nll, const fgp_fit_desc* fit, int iter, int do_update, void* stream);
+
+/* Run `iters` complete fit iterations starting at history index iter0 (fwd, bwd, step per iteration;
+ * the last one without update when final_no_update=1). Stream-ordered, no host synchronisation. */
+int fgp_fit_run(const fgp_nll_desc* nll, const fgp_fit_desc* fit, int iter0, int iters, int final_no_update,
+                void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Prediction.
+ * ------------------------------------------------------------------------------------------- */
+
+/* Matrix-free posterior mean (replaces the kmat build + einsum of AbstractGP.post_mean,
+ * fastgps/abstract_gp.py:352-380, with the fast-GP kernel of abstract_fast_gp.py:192-196):
+ *   out[b, t] = sum_i K_g(xt[t], z[:, i]) coeffs[b, i],  g = b mod Gk,
+ *   K_g(x, z) = hyp[g, 0] * prod_j (1 + hyp[g, 1 + j] part_j(x, z))   (hyp holds scale, lengthscales)
+ * lattice: part_j = coef[j] B_{order[j]}((x_j - z_j) % 1), z float64 [d][n];
+ * net:     part_j = walsh1(floor((x_j % 1) 2^tbits) XOR z_j), z int64 [d][n] (order/coef unused).
+ * xt: [N, d] float64 contiguous; coeffs: [B][n] with row stride coeff_stride; 1 <= B <= 4;
+ * out: [B][N] row stride out_stride; work: float64 scratch of ceil(n/chunk) * B * N entries. */
+int fgp_post_mean(int family, const double* xt, int64_t N, const void* z, int64_t n, int d, int tbits, const int* order,
+                  const double* coef, const double* hyp, int Gk, const double* coeffs, int64_t coeff_stride, int B,
+                  double* out, int64_t out_stride, double* work, int64_t chunk, void* stream);
+
+/* Cross-kernel rows rows[g, t, i] = K_g(xt[t], z[:, i]) (same kernel as fgp_post_mean), [Gk][N][n],
+ * N <= 65535: the kmat of AbstractGP.post_var / post_cov (fastgps/abstract_gp.py:407-411,452-457). */
+int fgp_kernel_rows(int family, const double* xt, int64_t N, const void* z, int64_t n, int d, int tbits,
+                    const int* order, const double* coef, const double* hyp, int Gk, double* rows, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FGP_HIP_H_ */

@@ -1,0 +1,126 @@
+"""GPU parity of the HIP transforms (fgp_fftbr / fgp_ifftbr / fgp_fwht) against the CPU oracle.
+
+Tolerance (fp64): max |gpu - oracle| <= 1e-13 * max|oracle| * (1 + m) for the orthonormal
+transforms (both are O(eps log n) backward-stable; measured spread between two CPU FFT libraries
+is ~1e-15 relative).  Bit-reversal / index work is exact by construction and checked through
+permutation inputs (unit vectors map to exact roots of unity).
+"""
+import numpy as np
+import pytest
+import torch
+
+import fastgaussianprocesses_amd as F
+from oracle import fgp_oracle as O
+from tests.golden_util import golden_names, load_golden
+
+pytestmark = pytest.mark.gpu
+torch.set_default_dtype(torch.float64)
+DEV = "cuda"
+
+
+def _tol(m):
+    return 1e-13 * (1 + m)
+
+
+def _close(a, b, m):
+    a = a.detach().cpu()
+    b = b.detach().cpu()
+    scale = float(b.abs().max()) if b.numel() else 1.0
+    err = float((a - b).abs().max()) if b.numel() else 0.0
+    assert err <= _tol(m) * max(scale, 1e-300), "err %.3e scale %.3e (m=%d)" % (err, scale, m)
+
+
+@pytest.mark.parametrize("m", list(range(0, 21)))
+def test_fftbr_matches_oracle(m):
+    n = 2 ** m
+    g = torch.Generator().manual_seed(m)
+    batch = 3 if m <= 16 else 1
+    xr = torch.randn((batch, n), generator=g) + 2.0
+    xc = torch.randn((batch, n), generator=g) + 1j * torch.randn((batch, n), generator=g)
+    _close(F.ops.fftbr_raw(xr.to(DEV), stable=False), O.fftbr(xr), m)
+    _close(F.ops.fftbr_raw(xc.to(DEV), stable=False), O.fftbr(xc), m)
+    _close(F.ops.fftbr_raw(xr.to(DEV), stable=True), O.ft_stable(xr, O.fftbr), m)
+
+
+@pytest.mark.parametrize("m", list(range(0, 21)))
+def test_ifftbr_matches_oracle(m):
+    n = 2 ** m
+    g = torch.Generator().manual_seed(100 + m)
+    batch = 2 if m <= 16 else 1
+    x = torch.randn((batch, n), generator=g) + 1j * torch.randn((batch, n), generator=g) + 0.5
+    _close(F.ops.ifftbr_raw(x.to(DEV), stable=False), O.ifftbr(x), m)
+    _close(F.ops.ifftbr_raw(x.to(DEV), stable=True), O.ft_stable(x, O.ifftbr), m)
+    _close(F.ops.ifftbr_raw(x.to(DEV), stable=True, real_out=True), O.ft_stable(x, O.ifftbr).real, m)
+
+
+@pytest.mark.parametrize("m", list(range(0, 21)))
+def test_fwht_matches_oracle(m):
+    n = 2 ** m
+    g = torch.Generator().manual_seed(200 + m)
+    batch = 3 if m <= 16 else 1
+    x = torch.randn((batch, n), generator=g) + 3.0
+    _close(F.ops.fwht_raw(x.to(DEV), stable=False), O.fwht(x), m)
+    _close(F.ops.fwht_raw(x.to(DEV), stable=True), O.ft_stable(x, O.fwht), m)
+
+
+@pytest.mark.parametrize("m", [0, 3, 4, 12, 13, 16, 20])
+def test_unit_vectors_give_exact_bitreversed_roots(m):
+    """fftbr(e_i)[k] = exp(-2 pi i brev(i) k / n) / sqrt(n): locates the bit-reversal exactly."""
+    n = 2 ** m
+    br = O.bitrev_indices(m)
+    for i in sorted({0, 1, n // 3, n - 1}):
+        e = torch.zeros(n)
+        e[i] = 1.0
+        y = F.ops.fftbr_raw(e.to(DEV)).cpu() * np.sqrt(n)
+        k = torch.arange(n, dtype=torch.float64)
+        ref = torch.exp(-2j * np.pi * ((int(br[i]) * k) % n) / n)
+        assert float((y - ref).abs().max()) < 1e-12 * (1 + m)
+
+
+@pytest.mark.parametrize("m", [4, 12, 13, 18, 20])
+def test_roundtrip_and_parseval(m):
+    n = 2 ** m
+    g = torch.Generator().manual_seed(300 + m)
+    x = (torch.randn((2, n), generator=g) + 1j * torch.randn((2, n), generator=g)).to(DEV)
+    y = F.ops.fftbr_raw(x, stable=True)
+    back = F.ops.ifftbr_raw(y, stable=True)
+    assert float((back - x).abs().max()) < 1e-13 * (1 + m) * float(x.abs().max())
+    assert torch.allclose(y.abs().pow(2).sum(-1), x.abs().pow(2).sum(-1), rtol=1e-13 * (1 + m))
+    w = F.ops.fwht_raw(F.ops.fwht_raw(x.real.contiguous(), stable=True), stable=True)
+    assert float((w - x.real).abs().max()) < 1e-13 * (1 + m) * float(x.real.abs().max())
+
+
+def test_noncontiguous_and_batched_shapes():
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn((4, 3, 64), generator=g)
+    xt = x.to(DEV).transpose(0, 1)  # non-contiguous leading dims
+    _close(F.ops.fftbr_raw(xt), O.fftbr(x.transpose(0, 1)), 6)
+    big = torch.randn((2, 2 ** 14 * 2), generator=g)[:, ::2]  # strided last dim
+    _close(F.ops.fftbr_raw(big.to(DEV)), O.fftbr(big.contiguous()), 14)
+
+
+def test_autograd_adjoints():
+    """backward of each transform is its exact adjoint: <A x, y> = <x, A^H y>."""
+    g = torch.Generator().manual_seed(9)
+    for m in (3, 10, 15):
+        n = 2 ** m
+        x = torch.randn(n, generator=g).to(DEV).requires_grad_(True)
+        w = (torch.randn(n, generator=g) + 1j * torch.randn(n, generator=g)).to(DEV)
+        (F.ops.fftbr(x, stable=True) * w.conj()).real.sum().backward()
+        ref = O.ifftbr(w.cpu()).real
+        assert float((x.grad.cpu() - ref).abs().max()) < 1e-12
+        xw = torch.randn(n, generator=g).to(DEV).requires_grad_(True)
+        v = torch.randn(n, generator=g).to(DEV)
+        (F.ops.fwht(xw) * v).sum().backward()
+        assert float((xw.grad.cpu() - O.fwht(v.cpu())).abs().max()) < 1e-12
+
+
+@pytest.mark.parametrize("name", golden_names())
+def test_golden_stable_transforms(name):
+    g = load_golden(name)
+    m = int(g["m"])
+    fam = str(g["family"])
+    ft = (lambda v: F.ops.fftbr(v, stable=True)) if fam == "lattice" else (lambda v: F.ops.fwht(v, stable=True))
+    ift = (lambda v: F.ops.ifftbr(v, stable=True)) if fam == "lattice" else (lambda v: F.ops.fwht(v, stable=True))
+    _close(ft(torch.from_numpy(g["ft_in"]).to(DEV)), torch.from_numpy(g["ft_out"]), m)
+    _close(ift(torch.from_numpy(g["ift_in"]).to(DEV)), torch.from_numpy(g["ift_out"]), m)
