@@ -1,0 +1,248 @@
+"""Benchmark: GP fit+predict points/sec at n = 2^20, fp64 (BASELINE.json metric) on MI355X.
+
+Workload (BASELINE config C4 "FastGPLattice n=2^20 d=5, 64 random shifts batched
+across 8 MI355X"): every rank owns `--shifts` independent randomly shifted lattice GPs (weak
+scaling: 8 per GPU -> 64 at N=8; seeds 1000 + global shift index).  One step = for every shift:
+  y~ = ft(y), k1 parts, fit (K=50 Rprop iterations, early stopping disabled), coeffs = K^-1 y,
+  post_mean at N=256 test points, post_var at N=8 test points.
+Inputs (points, y = f_ackley(x)) are resident in HBM before the timed region; GP state is reset to the
+initial hyper-parameters and all caches are dropped at the start of every step.
+value = (shifts * n * world_size) / (max-over-ranks seconds per step).
+
+Extra JSON keys: "roofline" for the dominant kernel (HIP-event timing of that kernel on its stream),
+"cpu_baseline" (the oracle = torch-CPU restatement of the reference, rank 0 at N=1, bounded sample),
+"phases_ms" (per-phase breakdown of one GP, HIP events).
+"""
+import argparse
+import json
+import math
+import os
+import time
+
+import numpy as np
+import torch
+
+torch.set_default_dtype(torch.float64)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP64_PEAK_TFS = 78.6           # MI355X FP64 vector/matrix peak (spec)
+
+
+def f_ackley(x, a=20, b=0.2, c=2 * np.pi, scaling=32.768):
+    # the reference's doctest workload (fastgps/fast_gp_lattice.py:14-22)
+    x = 2 * scaling * x - scaling
+    t1 = a * torch.exp(-b * torch.sqrt(torch.mean(x ** 2, 1)))
+    t2 = torch.exp(torch.mean(torch.cos(c * x), 1))
+    return -t1 - t2 + a + np.exp(1)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--log2n", type=int, default=20)
+    p.add_argument("--d", type=int, default=5)
+    p.add_argument("--shifts", type=int, default=8, help="independent GPs per GPU")
+    p.add_argument("--fit-iters", type=int, default=50)
+    p.add_argument("--n-mean", type=int, default=256)
+    p.add_argument("--n-var", type=int, default=8)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--sequential", dest="batched", action="store_false",
+                   help="fit the shifts one by one (default: one fused fit_batched loop over all shifts)")
+    p.add_argument("--cpu-sample-iters", type=int, default=3)
+    return p.parse_args()
+
+
+class Shift(object):
+    """One randomly shifted lattice GP with resident inputs."""
+
+    def __init__(self, F, d, n, seed, device):
+        self.seq = F.Lattice(d, seed=seed, randomize="SHIFT")
+        self.gp = F.FastGPLattice(self.seq, device=device)
+        x = self.gp.get_x_next(n)                        # host point generation: untimed
+        self.y = f_ackley(x).contiguous()
+        self.init = {k: v.detach().clone() for k, v in self.gp.named_parameters()}
+
+    def reset(self):
+        gp = self.gp
+        with torch.no_grad():
+            for k, v in self.init.items():
+                setattr(gp, k, torch.nn.Parameter(v.clone(), requires_grad=getattr(gp, k).requires_grad))
+        gp._y = [torch.empty(0, device=gp.device)]
+        gp.n.zero_()
+        gp._parts = {}
+        gp._cache = {}
+        gp._snap = None
+        gp.add_y_next(self.y)
+
+
+def phase_breakdown(sh, iters, xm, xv):
+    """HIP-event timing of each phase for one GP (on torch's current stream)."""
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+    sh.reset()
+    gp = sh.gp
+    ev[0].record()
+    gp.get_ytilde(0)
+    gp._k1parts(int(gp.n[0]))
+    ev[1].record()
+    gp.fit(iterations=iters, stop_crit_wait_iterations=iters + 1, verbose=0)
+    ev[2].record()
+    _ = gp.coeffs
+    ev[3].record()
+    gp.post_mean(xm)
+    ev[4].record()
+    gp.post_var(xv)
+    ev[5].record()
+    torch.cuda.synchronize()
+    names = ["ytilde+parts", "fit", "coeffs", "post_mean", "post_var"]
+    return {names[i]: ev[i].elapsed_time(ev[i + 1]) for i in range(5)}
+
+
+def roofline_fit_iteration(F, shifts, iters):
+    """Time the fused fit iterations of all shifts (one batched engine, as in the step) with HIP
+    events on the engine's stream; bytes = SURVEY §8(d) B_iter per GP x shifts."""
+    for sh in shifts:
+        sh.reset()
+    gp = shifts[0].gp
+    n = int(gp.n[0])
+    d = gp.d
+    P = len(shifts)
+    parts = torch.stack([sh.gp._k1parts(n) for sh in shifts])
+    ysq = torch.stack([sh.gp._ysq(*sh.gp._problem_batch())[0] for sh in shifts])
+    eng = F.FusedMLL(gp._FAMILY, parts, ysq, torch.zeros(P), torch.zeros(P, d), torch.full((P,), math.log(1e-8)),
+                     logdet_weight=1.0, mll_const=F.fit_engine.mll_constant(1, n), max_iters=iters + 1,
+                     parts_per_problem=True, per_problem=True)
+    eng.run(0, 2)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    eng.run(0, iters)
+    e1.record()
+    torch.cuda.synchronize()
+    t_iter = e0.elapsed_time(e1) / 1e3 / iters
+    # B_iter = 16 n d + 32 n + 32 n B per GP (lattice, B = 1 output)
+    b_iter = (16 * n * d + 32 * n + 32 * n) * P
+    return t_iter, b_iter
+
+
+def cpu_baseline(args, n, d):
+    """Oracle (torch-CPU restatement of the reference) on a bounded sample of one GP, scaled to the
+    per-GP workload of one step."""
+    from oracle import fgp_oracle as O
+    torch.set_num_threads(max(1, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
+    threads = torch.get_num_threads()
+    seq = np.random.default_rng(1000).uniform(size=d)
+    from fastgaussianprocesses_amd.seqs import DEFAULT_LATTICE_Z
+    x = torch.from_numpy(O.lattice_points(DEFAULT_LATTICE_Z[:d], seq, 0, n))
+    y = f_ackley(x)
+    o = O.OracleFastGP("lattice", x, None, y, alpha=2)
+    t0 = time.perf_counter()
+    o.ytilde()
+    o.k1parts()
+    t_setup = time.perf_counter() - t0
+    k = args.cpu_sample_iters
+    t0 = time.perf_counter()
+    o.fit(iterations=k, stop_crit_wait_iterations=k + 1)
+    t_fit_per = (time.perf_counter() - t0) / (k + 1)   # k+1 loss evaluations, k backward+steps
+    t0 = time.perf_counter()
+    o.coeffs()
+    t_coeffs = time.perf_counter() - t0
+    g = torch.Generator().manual_seed(17)
+    nm = 8
+    xm = torch.rand((nm, d), generator=g)
+    t0 = time.perf_counter()
+    o.post_mean(xm, chunk=4)
+    t_pm = (time.perf_counter() - t0) / nm
+    xv = torch.rand((1, d), generator=g)
+    t0 = time.perf_counter()
+    o.post_var(xv)
+    t_pv = time.perf_counter() - t0
+    t_gp = t_setup + (args.fit_iters + 1) * t_fit_per + t_coeffs + args.n_mean * t_pm + args.n_var * t_pv
+    return {"value": n / t_gp, "unit": "points/s", "cores": threads, "kind": "port",
+            "sample": ("oracle (oracle/fgp_oracle.py, torch-CPU restatement of the reference) on one n=2^%d d=%d GP: "
+                       "ytilde+parts, %d fit iterations, coeffs, post_mean of %d points, post_var of 1 point; scaled "
+                       "to %d fit iterations + post_mean N=%d + post_var N=%d per GP" %
+                       (int(math.log2(n)), d, k, nm, args.fit_iters, args.n_mean, args.n_var)),
+            "seconds_per_gp": t_gp}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    import fastgaussianprocesses_amd as F
+    n = 2 ** args.log2n
+    d = args.d
+    shifts = [Shift(F, d, n, 1000 + rank * args.shifts + s, device) for s in range(args.shifts)]
+    g = torch.Generator().manual_seed(17)
+    xm = torch.rand((args.n_mean, d), generator=g).to(device)
+    xv = torch.rand((args.n_var, d), generator=g).to(device)
+
+    def step():
+        for sh in shifts:
+            sh.reset()
+        if args.batched:
+            F.fit_batched([sh.gp for sh in shifts], iterations=args.fit_iters,
+                          stop_crit_wait_iterations=args.fit_iters + 1)
+        else:
+            for sh in shifts:
+                sh.gp.fit(iterations=args.fit_iters, stop_crit_wait_iterations=args.fit_iters + 1, verbose=0)
+        for sh in shifts:
+            sh.gp.post_mean(xm)
+            sh.gp.post_var(xv)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    el = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([el], device=device)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        el = float(t)
+    sec_step = el / args.steps
+    value = args.shifts * n * world / sec_step
+
+    phases = phase_breakdown(shifts[0], args.fit_iters, xm, xv)
+    t_iter, b_iter = roofline_fit_iteration(F, shifts, args.fit_iters)
+    roof = {"bound": "hbm", "kernel": "fit iteration (k_fwd_rows, k_fwd_cols, k_cols<adj>, k_bwd_rows, k_fit_reduce, "
+                                      "k_fit_step)",
+            "achieved": b_iter / t_iter / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": b_iter / t_iter / 1e9 / HBM_PEAK_GBS, "traffic": None,
+            "algorithmic_bytes": b_iter, "avg_us": t_iter * 1e6}
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, n, d)
+    if rank == 0:
+        out = {"metric": "GP fit+predict points/sec at n=2^20 fp64; achieved HBM GB/s vs roofline",
+               "value": value, "unit": "points/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": sec_step * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+               "dtype": "f64", "data": "synthetic (f_ackley on shifted rank-1 lattices)",
+               "config": {"workload": "C4: FastGPLattice n=2^%d d=%d, %d random shifts per GPU, fit %d Rprop iters + "
+                                      "post_mean N=%d + post_var N=%d per shift" %
+                                      (args.log2n, d, args.shifts, args.fit_iters, args.n_mean, args.n_var),
+                          "global_shifts": args.shifts * world, "parallelism": "replicas%d" % world},
+               "roofline": roof, "cpu_baseline": cpu, "phases_ms": phases}
+        print(json.dumps(out))
+    if dist:
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -8,7 +8,8 @@ __version__ = "0.1.0"
 
 from . import ops
 from .fast_gp import AbstractFastGP, FastGPDigitalNetB2, FastGPLattice
+from .batch import fit_batched
 from .fit_engine import FusedMLL
 from .seqs import DigitalNetB2, Lattice
 
-__all__ = ["FastGPLattice", "FastGPDigitalNetB2", "AbstractFastGP", "Lattice", "DigitalNetB2", "FusedMLL", "ops"]
+__all__ = ["FastGPLattice", "FastGPDigitalNetB2", "AbstractFastGP", "Lattice", "DigitalNetB2", "FusedMLL", "fit_batched", "ops"]

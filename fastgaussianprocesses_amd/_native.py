@@ -50,6 +50,7 @@ class FitDesc(ctypes.Structure):
         ("scale_rg", _c_int), ("ls_rg", _c_int), ("noise_rg", _c_int),
         ("mll_const", _c_dbl), ("eta_minus", _c_dbl), ("eta_plus", _c_dbl),
         ("step_min", _c_dbl), ("step_max", _c_dbl),
+        ("per_problem", _c_int),
     ]
 
 

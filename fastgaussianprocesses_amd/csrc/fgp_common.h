@@ -68,8 +68,82 @@ __device__ __forceinline__ void bfly_dif(double& a, double& b, const double2* __
   b = t - b;
 }
 
+// v * exp(-2 pi i J / K) for compile-time J, K (K | 16): +-1 and +-i are free, the eighth roots
+// cost 2 multiplies, the rest a constant complex multiply.  CONJ multiplies by the conjugate root.
+template <int K, int J, bool CONJ>
+__device__ __forceinline__ double2 mul_root(double2 v) {
+  constexpr int j = (J * (16 / K)) & 15;              // exponent in units of 2 pi / 16
+  constexpr double c16[16] = {1.0, 0.92387953251128673848, 0.70710678118654752440, 0.38268343236508978178,
+                              0.0, -0.38268343236508978178, -0.70710678118654752440, -0.92387953251128673848,
+                              -1.0, -0.92387953251128673848, -0.70710678118654752440, -0.38268343236508978178,
+                              0.0, 0.38268343236508978178, 0.70710678118654752440, 0.92387953251128673848};
+  constexpr double cr = c16[j];
+  constexpr double ci = CONJ ? -c16[(j + 4) & 15] : c16[(j + 4) & 15];   // exp(-i t) = (cos t, cos(t + pi/2))
+  if constexpr (j == 0) {
+    return v;
+  } else if constexpr (j == 8) {
+    return make_double2(-v.x, -v.y);
+  } else if constexpr (j == 4) {
+    return CONJ ? make_double2(-v.y, v.x) : make_double2(v.y, -v.x);
+  } else if constexpr (j == 12) {
+    return CONJ ? make_double2(v.y, -v.x) : make_double2(-v.y, v.x);
+  } else {
+    return make_double2(cr * v.x - ci * v.y, cr * v.y + ci * v.x);
+  }
+}
+
+// DIT / DIF butterflies at stage Q2 of a register group for element pair (t, t | 2^Q2), given the
+// group's base twiddle wb = exp(-2 pi i blo / 2^(S+Q2+1)) (unused when S == 0): the full twiddle is
+// wb * exp(-2 pi i (t mod 2^Q2) / 2^(Q2+1)).
+template <int S, int Q2, int T0, bool ADJ>
+__device__ __forceinline__ void group_bfly(double2& a, double2& b, double2 wb) {
+  constexpr int J = T0 & ((1 << Q2) - 1);
+  if constexpr (!ADJ) {
+    double2 bw = mul_root<(2 << Q2), J, false>(b);
+    if constexpr (S > 0) bw = cmul(bw, wb);
+    b = a - bw;
+    a = a + bw;
+  } else {
+    double2 d = a - b;
+    a = a + b;
+    if constexpr (S > 0) d = cmulc(d, wb);
+    b = mul_root<(2 << Q2), J, true>(d);
+  }
+}
+template <int S, int Q2, int T0, bool ADJ>
+__device__ __forceinline__ void group_bfly(double& a, double& b, double2) {
+  const double t = a;
+  a = t + b;
+  b = t - b;
+}
+
+template <int Q2, int T, int RL, int S, bool ADJ, typename E>
+__device__ __forceinline__ void stage_pairs(E* v, double2 wb) {
+  if constexpr (T < (1 << RL)) {
+    if constexpr (!(T & (1 << Q2))) group_bfly<S, Q2, T, ADJ>(v[T], v[T | (1 << Q2)], wb);
+    stage_pairs<Q2, T + 1, RL, S, ADJ>(v, wb);
+  }
+}
+
+template <int Q2, int RL, int S, bool ADJ, typename E>
+__device__ __forceinline__ void stages_dit(E* v, const double2* wb) {
+  if constexpr (Q2 < RL) {
+    stage_pairs<Q2, 0, RL, S, ADJ>(v, wb[Q2]);
+    stages_dit<Q2 + 1, RL, S, ADJ>(v, wb);
+  }
+}
+template <int Q2, int RL, int S, bool ADJ, typename E>
+__device__ __forceinline__ void stages_dif(E* v, const double2* wb) {
+  if constexpr (Q2 >= 0) {
+    stage_pairs<Q2, 0, RL, S, ADJ>(v, wb[Q2]);
+    stages_dif<Q2 - 1, RL, S, ADJ>(v, wb);
+  }
+}
+
 // One radix-2^RL register pass over stages [S, S+RL) of a length-2^P transform held in LDS
 // (padded layout, base pointer s), run by TL = 2^P/16 threads (tt = thread index in the group).
+// Twiddles: exp(-2 pi i pos / 2h) with pos = blo + (t mod 2^q2) 2^S factors into a per-group base
+// tw[blo << (11 - S - q2)] (one table load per stage, none when S = 0) times a compile-time root.
 template <int P, int S, int RL, bool ADJ, typename T>
 __device__ __forceinline__ void lds_pass(T* s, int tt, const double2* __restrict__ tw) {
   constexpr int R = 1 << RL;
@@ -80,30 +154,17 @@ __device__ __forceinline__ void lds_pass(T* s, int tt, const double2* __restrict
     const int q = tt + j * TL;
     const int blo = q & ((1 << S) - 1);
     const int base = blo + ((q >> S) << (S + RL));
+    double2 wb[RL];
+#pragma unroll
+    for (int q2 = 0; q2 < RL; ++q2) {
+      if constexpr (S > 0 && sizeof(T) == 16) wb[q2] = tw[blo << (11 - S - q2)];
+      else wb[q2] = make_double2(1.0, 0.0);
+    }
     T v[R];
 #pragma unroll
     for (int t = 0; t < R; ++t) v[t] = s[padi(base + (t << S))];
-    if constexpr (!ADJ) {
-#pragma unroll
-      for (int q2 = 0; q2 < RL; ++q2) {
-#pragma unroll
-        for (int t = 0; t < R; ++t) {
-          if (t & (1 << q2)) continue;
-          const int pos = blo + ((t & ((1 << q2) - 1)) << S);
-          bfly_dit(v[t], v[t | (1 << q2)], tw, pos << (11 - S - q2));
-        }
-      }
-    } else {
-#pragma unroll
-      for (int q2 = RL - 1; q2 >= 0; --q2) {
-#pragma unroll
-        for (int t = 0; t < R; ++t) {
-          if (t & (1 << q2)) continue;
-          const int pos = blo + ((t & ((1 << q2) - 1)) << S);
-          bfly_dif(v[t], v[t | (1 << q2)], tw, pos << (11 - S - q2));
-        }
-      }
-    }
+    if constexpr (!ADJ) stages_dit<0, RL, S, false>(v, wb);
+    else stages_dif<RL - 1, RL, S, true>(v, wb);
 #pragma unroll
     for (int t = 0; t < R; ++t) s[padi(base + (t << S))] = v[t];
   }
@@ -186,6 +247,30 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
 __device__ __forceinline__ unsigned brev_bits(unsigned u, int bits) {
   return bits == 0 ? 0u : (__builtin_bitreverse32(u) >> (32 - bits));
 }
+
+// Inter-pass twiddle of a length-2^m transform split as N1 = 2^m1 rows of N2 = 2^P2:
+//   w_n^e, e < n, from the two-level table  twm[e mod N2] * tw[(e >> P2) << (12 - m1)]
+__device__ __forceinline__ double2 inter_tw(unsigned e, int P2, int m1, const double2* __restrict__ tw,
+                                            const double2* __restrict__ twm) {
+  return cmul(twm[e & ((1u << P2) - 1)], tw[(e >> P2) << (kTileLog - m1)]);
+}
+
+// Twiddles w_n^{j1 e_k} of the 16 elements e_k = tid + 256 k of a thread whose workgroup holds ONE row
+// (row index u, j1 = brev_m1(u) uniform): base = w^{j1 tid} (one per-lane table pair) times the
+// uniform step w^{j1 256 k} (broadcast table loads); exponents add exactly.
+struct RowTwiddle {
+  double2 base;
+  unsigned j1;
+  __device__ __forceinline__ RowTwiddle(unsigned u, int tid, int P2, int m1, const double2* __restrict__ tw,
+                                        const double2* __restrict__ twm) {
+    j1 = brev_bits(u, m1);
+    base = inter_tw(j1 * (unsigned)tid, P2, m1, tw, twm);
+  }
+  __device__ __forceinline__ double2 at(int k, int P2, int m1, const double2* __restrict__ tw,
+                                        const double2* __restrict__ twm) const {
+    return cmul(base, inter_tw(j1 * 256u * (unsigned)k, P2, m1, tw, twm));
+  }
+};
 
 // ---------------------------------------------------------------- generic element I/O
 template <typename T> __device__ __forceinline__ T load_in(const void* p, int64_t i, int in_real);

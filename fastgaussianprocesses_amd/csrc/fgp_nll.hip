@@ -126,15 +126,26 @@ __device__ __forceinline__ double k1_at(const Nll& a, const Hyp& h, const double
   return h.scale * p;
 }
 
-// gradient terms at element i: acc[0] += g k1, acc[1+j] += g scale l_j p_j prod_{m != j} f_m
-__device__ __forceinline__ void grad_terms(const Nll& a, const Hyp& h, const double* __restrict__ pg, int64_t n,
-                                           int64_t i, double gi, double* acc) {
-  double f[FGP_MAX_D], pj[FGP_MAX_D];
+// k1 at the consecutive elements (i, i+1) from 16-byte loads of each dimension's parts (i even)
+__device__ __forceinline__ double2 k1_pair(const Nll& a, const Hyp& h, const double* __restrict__ pg, int64_t n,
+                                           int64_t i) {
+  double p0 = 1.0, p1 = 1.0;
 #pragma unroll
   for (int j = 0; j < FGP_MAX_D; ++j) {
-    pj[j] = (j < a.d) ? pg[(int64_t)j * n + i] : 0.0;
-    f[j] = 1.0 + h.ls[j] * pj[j];     // padded dims: l = 0 -> f = 1 exactly
+    if (j < a.d) {
+      const double2 pv = *reinterpret_cast<const double2*>(pg + (int64_t)j * n + i);
+      p0 *= 1.0 + h.ls[j] * pv.x;
+      p1 *= 1.0 + h.ls[j] * pv.y;
+    }
   }
+  return make_double2(h.scale * p0, h.scale * p1);
+}
+
+// gradient terms at element i: acc[0] += g k1, acc[1+j] += g scale l_j p_j prod_{m != j} f_m
+__device__ __forceinline__ void grad_terms_p(const Hyp& h, const double* pj, double gi, double* acc) {
+  double f[FGP_MAX_D];
+#pragma unroll
+  for (int j = 0; j < FGP_MAX_D; ++j) f[j] = 1.0 + h.ls[j] * pj[j];     // padded dims: l = 0 -> f = 1 exactly
   double suf[FGP_MAX_D + 1];
   suf[FGP_MAX_D] = 1.0;
 #pragma unroll
@@ -148,14 +159,38 @@ __device__ __forceinline__ void grad_terms(const Nll& a, const Hyp& h, const dou
   }
 }
 
+__device__ __forceinline__ void grad_terms(const Nll& a, const Hyp& h, const double* __restrict__ pg, int64_t n,
+                                           int64_t i, double gi, double* acc) {
+  double pj[FGP_MAX_D];
+#pragma unroll
+  for (int j = 0; j < FGP_MAX_D; ++j) pj[j] = (j < a.d) ? pg[(int64_t)j * n + i] : 0.0;
+  grad_terms_p(h, pj, gi, acc);
+}
+
+// gradient terms at the consecutive elements (i, i+1), 16-byte parts loads (i even)
+__device__ __forceinline__ void grad_terms_pair(const Nll& a, const Hyp& h, const double* __restrict__ pg, int64_t n,
+                                                int64_t i, double g0, double g1, double* acc) {
+  double p0[FGP_MAX_D], p1[FGP_MAX_D];
+#pragma unroll
+  for (int j = 0; j < FGP_MAX_D; ++j) {
+    double2 pv = make_double2(0.0, 0.0);
+    if (j < a.d) pv = *reinterpret_cast<const double2*>(pg + (int64_t)j * n + i);
+    p0[j] = pv.x;
+    p1[j] = pv.y;
+  }
+  grad_terms_p(h, p0, g0, acc);
+  grad_terms_p(h, p1, g1, acc);
+}
+
 // eigenvalue terms for one frequency: returns dL/dlambda, accumulates norm / logdet / dnoise
 __device__ __forceinline__ double2 eig_terms(double2 lam, double rootn, double noise, double Y, double w,
                                              double& norm, double& logdet, double& dnoise) {
   const double ar = rootn * lam.x + noise, ai = rootn * lam.y;    // ev = sqrt(n) lam + noise
   const double den = ar * ar + ai * ai;
-  const double rr = ar / den, ri = -ai / den;                      // 1/ev
+  const double inv = 1.0 / den;
+  const double rr = ar * inv, ri = -ai * inv;                      // 1/ev
   norm += Y * rr;
-  logdet += log(hypot(ar, ai));
+  logdet += 0.5 * log(den);                                        // log|ev|
   // G_e = 1/2 conj(w/ev - Y/ev^2) ; 1/ev^2 = (rr^2 - ri^2, 2 rr ri)
   const double qr = w * rr - Y * (rr * rr - ri * ri);
   const double qi = w * ri - Y * (2.0 * rr * ri);
@@ -259,25 +294,36 @@ __global__ __launch_bounds__(kWG) void k_fwd_rows(Nll a, const double2* __restri
   load_hyp(a, g, h);
   const double* pg = a.parts + (int64_t)g * a.parts_stride;
   const int64_t base = (int64_t)row0 * N2;
+  // k1 for element pairs (2 tid + 512 kk, +1): 16-byte loads of every dimension's parts
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const int e = tid + k * kWG;
-    lds[padi(e)] = real_to_T<T>(k1_at(a, h, pg, n, base + e));
+  for (int kk = 0; kk < 8; ++kk) {
+    const int e = 2 * tid + 512 * kk;
+    const double2 kv = k1_pair(a, h, pg, n, base + e);
+    lds[padi(e)] = real_to_T<T>(kv.x);
+    lds[padi(e + 1)] = real_to_T<T>(kv.y);
   }
   __syncthreads();
   T* s = lds + (tid / TL) * (N2 + N2 / 16);
   center_transform<P2, false>(s, tid % TL, 1, red, tw);
   T* out = static_cast<T*>(a.work) + (int64_t)g * n + base;
+  if constexpr (sizeof(T) == 16 && RPW == 1) {
+    const RowTwiddle rt((unsigned)row0, tid, P2, m1, tw, twm);
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const int e = tid + k * kWG;
-    T v = lds[padi(e)];
-    if constexpr (sizeof(T) == 16) {
-      const unsigned u = (unsigned)(row0 + (e >> P2));
-      const unsigned ex = brev_bits(u, m1) * (unsigned)(e & (N2 - 1));
-      v = tw_mul<T>(v, cmul(twm[ex & (N2 - 1)], tw[(ex >> P2) << (kTileLog - m1)]), false);
+    for (int k = 0; k < 16; ++k) {
+      const int e = tid + k * kWG;
+      out[e] = tw_mul<T>(lds[padi(e)], rt.at(k, P2, m1, tw, twm), false);
     }
-    out[e] = v;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int e = tid + k * kWG;
+      T v = lds[padi(e)];
+      if constexpr (sizeof(T) == 16) {
+        const unsigned ex = brev_bits((unsigned)(row0 + (e >> P2)), m1) * (unsigned)(e & (N2 - 1));
+        v = tw_mul<T>(v, inter_tw(ex, P2, m1, tw, twm), false);
+      }
+      out[e] = v;
+    }
   }
 }
 
@@ -340,28 +386,43 @@ __global__ __launch_bounds__(kWG) void k_fwd_cols(Nll a, const double2* __restri
 
 // ---------------------------------------------------------------- n > 4096: adjoint row pass + gradient terms
 template <int P2, typename T>
-__global__ __launch_bounds__(kWG) void k_bwd_rows(Nll a, const double2* __restrict__ tw) {
-  constexpr int N2 = 1 << P2, TL = N2 / 16;
-  constexpr bool ADJ = sizeof(T) == 16;   // FFT: adjoint network; WHT: self-adjoint
+__global__ __launch_bounds__(kWG) void k_bwd_rows(Nll a, const double2* __restrict__ tw, const double2* __restrict__ twm) {
+  constexpr int N2 = 1 << P2, TL = N2 / 16, RPW = kTile / N2;
+  constexpr bool FFT = sizeof(T) == 16;   // FFT: adjoint network + conj twiddle; WHT: self-adjoint
   __shared__ T lds[kTile + kTile / 16];
   __shared__ T red[kWG / 64];
   __shared__ double redd[kWG / 64];
-  const int m = a.log2n;
+  const int m = a.log2n, m1 = m - P2;
   const int64_t n = (int64_t)1 << m;
   const int64_t tiles = n >> kTileLog;
   const int g = (int)(blockIdx.x / tiles);
   const int blk = (int)(blockIdx.x % tiles);
+  const int row0 = blk * RPW;
   const int64_t base = (int64_t)blk * kTile;
   const int tid = threadIdx.x;
   const T* in = static_cast<const T*>(a.work) + (int64_t)g * n + base;
+  if constexpr (FFT && RPW == 1) {
+    const RowTwiddle rt((unsigned)row0, tid, P2, m1, tw, twm);
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const int e = tid + k * kWG;
-    lds[padi(e)] = in[e];
+    for (int k = 0; k < 16; ++k) {
+      const int e = tid + k * kWG;
+      lds[padi(e)] = tw_mul<T>(in[e], rt.at(k, P2, m1, tw, twm), true);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int e = tid + k * kWG;
+      T v = in[e];
+      if constexpr (FFT) {
+        const unsigned ex = brev_bits((unsigned)(row0 + (e >> P2)), m1) * (unsigned)(e & (N2 - 1));
+        v = tw_mul<T>(v, inter_tw(ex, P2, m1, tw, twm), true);
+      }
+      lds[padi(e)] = v;
+    }
   }
   __syncthreads();
   T* s = lds + (tid / TL) * (N2 + N2 / 16);
-  center_transform<P2, ADJ>(s, tid % TL, 1, red, tw);
+  center_transform<P2, FFT>(s, tid % TL, 1, red, tw);
   Hyp h;
   load_hyp(a, g, h);
   const double* pg = a.parts + (int64_t)g * a.parts_stride;
@@ -369,10 +430,10 @@ __global__ __launch_bounds__(kWG) void k_bwd_rows(Nll a, const double2* __restri
   double acc[1 + FGP_MAX_D];
 #pragma unroll
   for (int q = 0; q < 1 + FGP_MAX_D; ++q) acc[q] = 0.0;
-#pragma unroll 4
-  for (int k = 0; k < 16; ++k) {
-    const int e = tid + k * kWG;
-    grad_terms(a, h, pg, n, base + e, re(lds[padi(e)]) * inv_rootn, acc);
+#pragma unroll 2
+  for (int kk = 0; kk < 8; ++kk) {
+    const int e = 2 * tid + 512 * kk;
+    grad_terms_pair(a, h, pg, n, base + e, re(lds[padi(e)]) * inv_rootn, re(lds[padi(e + 1)]) * inv_rootn, acc);
   }
 #pragma unroll
   for (int q = 0; q < 1 + FGP_MAX_D; ++q) {
@@ -394,7 +455,19 @@ struct Fit {
   double* raw_hist;
   int scale_rg, ls_rg, noise_rg;
   double mll_const, eta_minus, eta_plus, step_min, step_max;
+  int per_problem;
 };
+
+__device__ __forceinline__ void rprop_update(const Fit& f, int p, double gp) {
+  const double prod = gp * f.prev[p];
+  const double sgn = prod > 0.0 ? f.eta_plus : (prod < 0.0 ? f.eta_minus : 1.0);
+  const double st = fmin(fmax(f.step[p] * sgn, f.step_min), f.step_max);
+  f.step[p] = st;
+  const double gg = (sgn == f.eta_minus) ? 0.0 : gp;
+  const double gs = gg > 0.0 ? 1.0 : (gg < 0.0 ? -1.0 : 0.0);
+  f.raw[p] = f.raw[p] + (-1.0) * (gs * st);
+  f.prev[p] = gg;
+}
 
 __device__ __forceinline__ double* red_ptr(const Nll& a, int g, int q) {
   return a.partials + (int64_t)a.G * a.nq * a.nb + (int64_t)g * a.nq + q;
@@ -449,14 +522,56 @@ __global__ __launch_bounds__(kWG) void k_fit_step(Nll a, Fit f, int iter, int do
     else if (p >= a.ls_off && p < a.ls_off + ls_cnt) rg = f.ls_rg;
     else rg = f.noise_rg;
     if (!rg) continue;
-    const double prod = gp * f.prev[p];
-    const double sgn = prod > 0.0 ? f.eta_plus : (prod < 0.0 ? f.eta_minus : 1.0);
-    const double st = fmin(fmax(f.step[p] * sgn, f.step_min), f.step_max);
-    f.step[p] = st;
-    const double gg = (sgn == f.eta_minus) ? 0.0 : gp;
-    const double gs = gg > 0.0 ? 1.0 : (gg < 0.0 ? -1.0 : 0.0);
-    f.raw[p] = f.raw[p] + (-1.0) * (gs * st);
-    f.prev[p] = gg;
+    rprop_update(f, p, gp);
+  }
+}
+
+// Independent problems (per_problem): one workgroup per GP reduces its partials, records its loss
+// and parameters and applies Rprop to the parameters it owns -- no cross-problem dependency.
+__global__ __launch_bounds__(kWG) void k_fit_reduce_step(Nll a, Fit f, int iter, int do_update) {
+  __shared__ double redd[kWG / 64];
+  __shared__ double vals[4 + FGP_MAX_D];
+  const int g = blockIdx.x;
+  for (int q = 0; q < a.nq; ++q) {
+    double v = 0.0;
+    for (int b = threadIdx.x; b < a.nb; b += kWG) v += *part_ptr(a, g, q, b);
+    v = block_sum(v, redd);
+    if (threadIdx.x == 0) vals[q] = v;
+  }
+  __syncthreads();
+  const int dl = a.ls_pd ? a.d : 1;
+  const int k = threadIdx.x;
+  if (k == 0) {
+    const double term2 = a.logdet_weight * vals[1];
+    double* lh = f.loss_hist + ((int64_t)iter * a.G + g) * 3;
+    lh[0] = 0.5 * (vals[0] + term2 + f.mll_const);
+    lh[1] = vals[0];
+    lh[2] = term2;
+  }
+  if (k < 2 + dl) {
+    int p, rg;
+    double gp;
+    if (k == 0) {
+      p = a.scale_off + (a.scale_pp ? g : 0);
+      gp = vals[3];
+      rg = f.scale_rg;
+    } else if (k <= dl) {
+      p = a.ls_off + (a.ls_pp ? g : 0) * dl + (k - 1);
+      if (a.ls_pd) {
+        gp = vals[4 + (k - 1)];
+      } else {
+        gp = 0.0;
+        for (int j = 0; j < a.d; ++j) gp += vals[4 + j];
+      }
+      rg = f.ls_rg;
+    } else {
+      p = a.noise_off + (a.noise_pp ? g : 0);
+      gp = exp(a.raw[p]) * vals[2];
+      rg = f.noise_rg;
+    }
+    f.raw_hist[(int64_t)iter * f.n_params + p] = f.raw[p];
+    f.grad_out[p] = gp;
+    if (do_update && rg) rprop_update(f, p, gp);
   }
 }
 
@@ -532,11 +647,12 @@ template <typename T>
 static int launch_bwd2(const Nll& a, const Tables* tb, hipStream_t st) {
   const int m = a.log2n, m2 = split_m2(m);
   const unsigned grid = (unsigned)((int64_t)a.G << (m - kTileLog));
-  // adjoint column pass: grad_lam -> work (generic column kernel; conj twiddle for the FFT)
+  // adjoint column pass: grad_lam -> work (generic column kernel; the conj twiddle is applied on load
+  // by k_bwd_rows)
   int rc = cols_adjoint_launch(sizeof(T) == 16, m, a.grad_lam, a.work, a.G, tb, st);
   if (rc != kOk) return rc;
   switch (m2) {
-#define FGP_C(PP) case PP: k_bwd_rows<PP, T><<<grid, kWG, 0, st>>>(a, tb->tw4096); break;
+#define FGP_C(PP) case PP: k_bwd_rows<PP, T><<<grid, kWG, 0, st>>>(a, tb->tw4096, tb->twm[m]); break;
     FGP_C(9) FGP_C(10) FGP_C(11) FGP_C(12)
 #undef FGP_C
     default: return set_error(kErrInvalid, "bad m2");
@@ -577,10 +693,21 @@ static int to_fit(const fgp_fit_desc* d, Fit& f) {
   f.eta_plus = d->eta_plus;
   f.step_min = d->step_min;
   f.step_max = d->step_max;
+  f.per_problem = d->per_problem;
+  return kOk;
+}
+
+static int check_per_problem(const Nll& a, const Fit& f) {
+  if (f.per_problem && a.G > 1 && !(a.scale_pp && a.ls_pp && a.noise_pp))
+    return set_error(kErrInvalid, "per_problem fit needs per-problem scale, lengthscales and noise");
   return kOk;
 }
 
 static int fit_step(const Nll& a, const Fit& f, int iter, int do_update, hipStream_t st) {
+  if (f.per_problem) {
+    k_fit_reduce_step<<<a.G, kWG, 0, st>>>(a, f, iter, do_update);
+    return check_launch("k_fit_reduce_step");
+  }
   k_fit_reduce<<<a.G, kWG, 0, st>>>(a);
   int rc = check_launch("k_fit_reduce");
   if (rc != kOk) return rc;
@@ -638,6 +765,7 @@ int fgp_fit_step(const fgp_nll_desc* nll, const fgp_fit_desc* fit, int iter, int
   Fit f;
   int rc = to_nll(nll, a);
   if (rc == kOk) rc = to_fit(fit, f);
+  if (rc == kOk) rc = check_per_problem(a, f);
   if (rc != kOk) return rc;
   return fit_step(a, f, iter, do_update, (hipStream_t)stream);
 }
@@ -648,6 +776,7 @@ int fgp_fit_run(const fgp_nll_desc* nll, const fgp_fit_desc* fit, int iter0, int
   Fit f;
   int rc = to_nll(nll, a);
   if (rc == kOk) rc = to_fit(fit, f);
+  if (rc == kOk) rc = check_per_problem(a, f);
   if (rc != kOk) return rc;
   const bool lat = nll->family == FGP_FAMILY_LATTICE;
   hipStream_t st = (hipStream_t)stream;

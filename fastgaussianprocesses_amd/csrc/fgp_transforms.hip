@@ -96,7 +96,8 @@ __global__ __launch_bounds__(kWG) void k_single(const void* in, int64_t in_bs, i
 // ------------------------------------------------------------------ m > 12: row pass
 // View of one batch item: N1 rows of N2 = 2^P2 contiguous elements.  4096/N2 rows per workgroup.
 // Forward (!ADJ): row transform, then (twiddle) multiply position (u, k2) by w_n^{brev_m1(u) k2}.
-// Adjoint  (ADJ): row transform of the column pass' output (no twiddle here).
+// Adjoint  (ADJ): (twiddle) multiply the column pass' output by conj(w_n^{brev_m1(u) k2}) on load,
+//                 then the row transform.
 template <int P2, typename T, bool ADJ>
 __global__ __launch_bounds__(kWG) void k_rows(const void* in, int64_t in_bs, int in_real, void* out,
                                                int64_t out_bs, int out_real, int m, int stable, double scale,
@@ -113,26 +114,53 @@ __global__ __launch_bounds__(kWG) void k_rows(const void* in, int64_t in_bs, int
   const int row0 = (int)(blockIdx.x % tiles) * RPW;
   const int tid = threadIdx.x;
   const int64_t ibase = b * in_bs + (int64_t)row0 * N2;   // rows are contiguous: the tile is one slab
+  if constexpr (ADJ && sizeof(T) == 16) {
+    if (twiddle) {
+      if constexpr (RPW == 1) {
+        const RowTwiddle rt((unsigned)row0, tid, P2, m1, tw, twm);
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const int e = tid + k * kWG;
-    lds[padi(e)] = load_in<T>(in, ibase + e, in_real);
+        for (int k = 0; k < 16; ++k) {
+          const int e = tid + k * kWG;
+          lds[padi(e)] = tw_mul<T>(load_in<T>(in, ibase + e, in_real), rt.at(k, P2, m1, tw, twm), true);
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const int e = tid + k * kWG;
+          const unsigned ex = brev_bits((unsigned)(row0 + (e >> P2)), m1) * (unsigned)(e & (N2 - 1));
+          lds[padi(e)] = tw_mul<T>(load_in<T>(in, ibase + e, in_real), inter_tw(ex, P2, m1, tw, twm), true);
+        }
+      }
+    }
+  }
+  if (!(ADJ && sizeof(T) == 16 && twiddle)) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int e = tid + k * kWG;
+      lds[padi(e)] = load_in<T>(in, ibase + e, in_real);
+    }
   }
   __syncthreads();
   const int tt = tid % TL;
   T* s = lds + (tid / TL) * (N2 + N2 / 16);
   center_transform<P2, ADJ>(s, tt, stable, red, tw);
   const int64_t obase = b * out_bs + (int64_t)row0 * N2;
+  if (!ADJ && twiddle && RPW == 1) {
+    const RowTwiddle rt((unsigned)row0, tid, P2, m1, tw, twm);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int e = tid + k * kWG;
+      store_out(out, obase + e, tw_mul<T>(lds[padi(e)], rt.at(k, P2, m1, tw, twm), false) * scale, out_real);
+    }
+    return;
+  }
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     const int e = tid + k * kWG;
     T v = lds[padi(e)];
-    if (twiddle) {
-      const unsigned u = (unsigned)(row0 + (e >> P2));
-      const unsigned k2 = (unsigned)(e & (N2 - 1));
-      const unsigned ex = brev_bits(u, m1) * k2;   // < 2^m
-      const double2 w = cmul(twm[ex & (N2 - 1)], tw[(ex >> P2) << (kTileLog - m1)]);
-      v = tw_mul<T>(v, w, false);
+    if (!ADJ && twiddle) {
+      const unsigned ex = brev_bits((unsigned)(row0 + (e >> P2)), m1) * (unsigned)(e & (N2 - 1));   // < 2^m
+      v = tw_mul<T>(v, inter_tw(ex, P2, m1, tw, twm), false);
     }
     store_out(out, obase + e, v * scale, out_real);
   }
@@ -141,8 +169,9 @@ __global__ __launch_bounds__(kWG) void k_rows(const void* in, int64_t in_bs, int
 // ------------------------------------------------------------------ m > 12: column pass
 // C = 4096/N1 adjacent columns (k2 in [c0, c0+C)) of length N1 = 2^P1 per workgroup, staged
 // column-major in LDS with an odd column stride (conflict-free transposing ds_write_b128).
-// Forward (!ADJ): plain column transform (natural-order output rows k1).
-// Adjoint  (ADJ): column transform, then (twiddle) multiply output row u by conj(w_n^{brev(u) k2}).
+// Forward (!ADJ): column transform (natural-order output rows k1); adjoint (ADJ): its transpose-
+// conjugate (output row u in bit-reversed position).  No twiddle here: both directions apply the
+// inter-pass twiddle in the row pass, where a workgroup's row index is uniform.
 // In-place safe (in == out): each workgroup reads its whole tile before writing it.
 template <int P1>
 struct ColLayout {
@@ -181,19 +210,13 @@ __global__ __launch_bounds__(kWG) void k_cols(const void* in, int64_t in_bs, int
   T* s = lds + col * CS;
   center_transform<P1, ADJ>(s, tt, stable, red, tw);
   const int64_t obase = b * out_bs + c0;
-  const int m2 = P2;
+  (void)twiddle;
+  (void)twm;
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     const int e = tid + k * kWG;
     const int c = e % C, r = e / C;
-    T v = lds[c * CS + padi(r)];
-    if (twiddle) {
-      const unsigned k2 = (unsigned)(c0 + c);
-      const unsigned ex = brev_bits((unsigned)r, P1) * k2;
-      const double2 w = cmul(twm[ex & (unsigned)(N2 - 1)], tw[(ex >> m2) << (kTileLog - P1)]);
-      v = tw_mul<T>(v, w, true);
-    }
-    store_out(out, obase + (int64_t)r * N2 + c, v * scale, out_real);
+    store_out(out, obase + (int64_t)r * N2 + c, lds[c * CS + padi(r)] * scale, out_real);
   }
 }
 
@@ -287,7 +310,7 @@ static int validate(const void* in, const void* out, int64_t batch, int log2n, i
 int cols_adjoint_launch(bool fft, int m, const void* in, void* out, int64_t batch, const Tables* tb,
                         hipStream_t st) {
   const int64_t n = (int64_t)1 << m;
-  if (fft) return launch_cols<double2, true>(m, in, n, 0, out, n, 0, batch, 1, 1.0, 1, tb, st);
+  if (fft) return launch_cols<double2, true>(m, in, n, 0, out, n, 0, batch, 1, 1.0, 0, tb, st);
   return launch_cols<double, false>(m, in, n, 0, out, n, 0, batch, 1, 1.0, 0, tb, st);
 }
 
@@ -326,9 +349,9 @@ int fgp_ifftbr(const void* in, int64_t in_batch_stride, void* out, int out_real,
   if (log2n <= 12) return launch_single<double2, true>(log2n, in, in_batch_stride, 0, out, out_real, batch, stable, scale, tb->tw4096, st);
   void* mid = out_real ? work : out;
   if (mid == nullptr) return set_error(kErrInvalid, "fgp_ifftbr: out_real with n > 4096 needs a complex work buffer");
-  rc = launch_cols<double2, true>(log2n, in, in_batch_stride, 0, mid, n, 0, batch, stable, 1.0, 1, tb, st);
+  rc = launch_cols<double2, true>(log2n, in, in_batch_stride, 0, mid, n, 0, batch, stable, 1.0, 0, tb, st);
   if (rc != kOk) return rc;
-  return launch_rows<double2, true>(log2n, mid, n, 0, out, n, out_real, batch, stable, scale, 0, tb, st);
+  return launch_rows<double2, true>(log2n, mid, n, 0, out, n, out_real, batch, stable, scale, 1, tb, st);
 }
 
 int fgp_fwht(const double* in, int64_t in_batch_stride, double* out, int64_t batch, int log2n, int stable,

@@ -52,14 +52,14 @@ class _Hyper(object):
     """Resolves one hyper-parameter's shape exactly as AbstractGP.__init__ (abstract_gp.py:78-139)."""
 
     @staticmethod
-    def make(value, shape, shape_batch, last_ok, name, positive, device):
+    def make(value, shape, shape_batch, last_ok, name, positive, device, core=1):
         assert np.isscalar(value) or isinstance(value, torch.Tensor), "%s must be a scalar or torch.Tensor" % name
         if isinstance(value, torch.Tensor):
             shape = value.shape
         shape = _as_size(shape)
         assert isinstance(shape, torch.Size) and last_ok(shape[-1])
-        if len(shape) > 1:
-            assert shape[:-1] == shape_batch[-(len(shape) - 1):]
+        if len(shape) > core:   # leading dims must be a suffix of shape_batch
+            assert shape[:-core] == shape_batch[-(len(shape) - core):]
         if np.isscalar(value):
             value = value * torch.ones(shape, device=device)
         value = value.to(device=device, dtype=torch.float64)
@@ -120,7 +120,7 @@ class AbstractFastGP(torch.nn.Module):
                 rank_factor_task_kernel = 0
             shape_factor_task_kernel = torch.Size([1, rank_factor_task_kernel])
         factor_task_kernel = _Hyper.make(factor_task_kernel, shape_factor_task_kernel, shape_batch,
-                                         lambda v: 0 <= v <= 1, "factor_task_kernel", None, dev)
+                                         lambda v: 0 <= v <= 1, "factor_task_kernel", None, dev, core=2)
         if shape_noise_task_kernel is None and not isinstance(noise_task_kernel, torch.Tensor):
             shape_noise_task_kernel = torch.Size([1])
         noise_task_kernel = _Hyper.make(noise_task_kernel, shape_noise_task_kernel, shape_batch, lambda v: v == 1,
@@ -310,11 +310,16 @@ class AbstractFastGP(torch.nn.Module):
         raise NotImplementedError
 
     # ------------------------------------------------------------------ kernel pieces
-    def _k1parts(self, n):
+    def _k1parts(self, n, out=None):
+        """[d, n] first-column kernel parts (cached per n; `out` places them in a caller buffer)."""
         n = int(n)
-        if n not in self._parts:
+        if n not in self._parts or (out is not None and self._parts[n].data_ptr() != out.data_ptr()):
             self._ensure_points(n)
-            self._parts[n] = self._compute_parts(self._xb[:n], self._xb[0])
+            if out is not None and n in self._parts:
+                out.copy_(self._parts[n])
+            else:
+                out = self._compute_parts(self._xb[:n], self._xb[0], out)
+            self._parts[n] = out
         return self._parts[n]
 
     def get_k1parts(self, task0=0, task1=0, n=None):
@@ -472,7 +477,7 @@ class AbstractFastGP(torch.nn.Module):
         while not done:
             k = min(chunk, total - i0)
             eng.run(i0, k, final_no_update=(i0 + k == total))
-            lh = eng.loss_hist[i0:i0 + k].cpu()
+            lh = eng.loss_hist[i0:i0 + k, 0].cpu()
             for r in range(k):
                 i = i0 + r
                 lv = float(lh[r, 0])
@@ -877,9 +882,9 @@ class FastGPLattice(AbstractFastGP):
     def ift(self, x):
         return ops.ifftbr(x, stable=True)
 
-    def _compute_parts(self, xb, x0):
+    def _compute_parts(self, xb, x0, out=None):
         self._check_unit(xb)
-        return ops.lattice_parts(xb, x0, self._alphas)
+        return ops.lattice_parts(xb, x0, self._alphas, out=out)
 
     def _part_at_zero(self):
         return torch.tensor([ops.lattice_coefficient(a) * float(_bern(2 * a, 0.0)) for a in self._alphas],
@@ -963,8 +968,8 @@ class FastGPDigitalNetB2(AbstractFastGP):
     def ift(self, x):
         return ops.fwht(x, stable=True)
 
-    def _compute_parts(self, xb, x0):
-        return ops.net_parts(xb, x0, self.t)
+    def _compute_parts(self, xb, x0, out=None):
+        return ops.net_parts(xb, x0, self.t, out=out)
 
     def _part_at_zero(self):
         return torch.ones(self.d, dtype=torch.float64)

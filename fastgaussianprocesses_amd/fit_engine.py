@@ -23,11 +23,13 @@ RPROP_STEPS = (1e-6, 50.0)
 
 class FusedMLL(object):
     def __init__(self, family, parts, ysq, raw_scale, raw_lengthscales, raw_noise, logdet_weight, mll_const,
-                 requires_grad=(True, True, False), lr=0.1, max_iters=1, parts_per_problem=False):
+                 requires_grad=(True, True, False), lr=0.1, max_iters=1, parts_per_problem=False, per_problem=None):
         """
         family: 0 lattice (FFT) / 1 net (FWHT)
         parts:  [d, n] shared, or [G, d, n] when parts_per_problem
         ysq:    [G, n]
+        per_problem: the G problems are independent GPs with their own loss / Rprop (default: G == 1);
+                otherwise one loss sums over the G problems (per-output hyper-parameters of one GP)
         raw_scale [S] with S in {1, G}; raw_lengthscales [S_l, D_l] with S_l in {1, G}, D_l in {1, d};
         raw_noise [S_n] with S_n in {1, G}
         """
@@ -73,7 +75,7 @@ class FusedMLL(object):
         self.max_iters = 0
         self.loss_hist = None
         self.raw_hist = None
-        self.ensure_history(max_iters)
+        self._init_max_iters = max_iters
         self._nll = N.NllDesc(
             family=self.family, log2n=self.m, d=self.d, G=self.G,
             parts=self.parts.data_ptr(), parts_stride=(d * n if parts_per_problem else 0),
@@ -81,16 +83,17 @@ class FusedMLL(object):
             logdet_weight=float(logdet_weight),
             grad_lam=self.grad_lam.data_ptr(), work=(self.work.data_ptr() if self.work is not None else 0),
             partials=self.partials.data_ptr(), **self.layout)
+        self.per_problem = bool(G == 1 if per_problem is None else per_problem)
         self.requires_grad = tuple(int(bool(r)) for r in requires_grad)
         self.mll_const = float(mll_const)
         self._fit = None
-        self._refresh_fit_desc()
+        self.ensure_history(self._init_max_iters)
 
     def ensure_history(self, iters):
         if iters <= self.max_iters:
             return
         new_max = max(iters, 2 * self.max_iters, 16)
-        lh = torch.zeros((new_max, 3), dtype=torch.float64, device=self.device)
+        lh = torch.zeros((new_max, self.G if self.per_problem else 1, 3), dtype=torch.float64, device=self.device)
         rh = torch.zeros((new_max, self.n_params), dtype=torch.float64, device=self.device)
         if self.loss_hist is not None:
             lh[:self.max_iters] = self.loss_hist
@@ -106,7 +109,8 @@ class FusedMLL(object):
             rprop_step=self.step.data_ptr(), grad_out=self.grad.data_ptr(), loss_hist=self.loss_hist.data_ptr(),
             raw_hist=self.raw_hist.data_ptr(), scale_rg=self.requires_grad[0], ls_rg=self.requires_grad[1],
             noise_rg=self.requires_grad[2], mll_const=self.mll_const, eta_minus=RPROP_ETAS[0],
-            eta_plus=RPROP_ETAS[1], step_min=RPROP_STEPS[0], step_max=RPROP_STEPS[1])
+            eta_plus=RPROP_ETAS[1], step_min=RPROP_STEPS[0], step_max=RPROP_STEPS[1],
+            per_problem=int(self.per_problem))
 
     def stream(self):
         return N.stream_ptr(self.device)
@@ -123,7 +127,7 @@ class FusedMLL(object):
         N.call("fgp_nll_fwd", self._nll, st)
         N.call("fgp_nll_bwd", self._nll, st)
         N.call("fgp_fit_step", self._nll, self._fit, int(slot), 0, st)
-        lh = self.loss_hist[slot].cpu()
+        lh = self.loss_hist[slot].sum(0).cpu() if self.per_problem else self.loss_hist[slot, 0].cpu()
         return float(lh[0]), float(lh[1]), float(lh[2]), self.grad.cpu()
 
     def split_raw(self, raw_vec):

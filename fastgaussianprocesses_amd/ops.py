@@ -155,7 +155,7 @@ def lattice_coefficient(alpha):
     return ((-1) ** (int(alpha) + 1) * torch.exp(2 * int(alpha) * math.log(2 * math.pi) - torch.lgamma(order + 1.0))).item()
 
 
-def lattice_parts(x, z, alphas):
+def lattice_parts(x, z, alphas, out=None):
     """parts[j, i] = c_j B_{2 alpha_j}((x[i, j] - z[j]) % 1)  -> [d, n] (fast_gp_lattice.py:263-273)."""
     require_device(x, "lattice_parts")
     x = x.to(torch.float64)
@@ -163,13 +163,15 @@ def lattice_parts(x, z, alphas):
         x = x.contiguous()
     z = z.to(torch.float64).contiguous()
     n, d = x.shape
-    out = torch.empty((d, n), dtype=torch.float64, device=x.device)
+    if out is None:
+        out = torch.empty((d, n), dtype=torch.float64, device=x.device)
+    assert out.shape == (d, n) and out.is_contiguous() and out.dtype == torch.float64
     N.call("fgp_lattice_parts", N.ptr(x), x.stride(0), N.ptr(z), n, d, N.int_array([2 * a for a in alphas]),
            N.double_array([lattice_coefficient(a) for a in alphas]), N.ptr(out), _stream(x))
     return out
 
 
-def net_parts(xb, z, t):
+def net_parts(xb, z, t, out=None):
     """Order-1 Walsh parts for delta = xb XOR z -> [d, n] (fast_gp_digital_net_b2.py:274-301)."""
     require_device(xb, "net_parts")
     xb = xb.to(torch.int64)
@@ -177,7 +179,9 @@ def net_parts(xb, z, t):
         xb = xb.contiguous()
     z = z.to(torch.int64).contiguous()
     n, d = xb.shape
-    out = torch.empty((d, n), dtype=torch.float64, device=xb.device)
+    if out is None:
+        out = torch.empty((d, n), dtype=torch.float64, device=xb.device)
+    assert out.shape == (d, n) and out.is_contiguous() and out.dtype == torch.float64
     N.call("fgp_net_parts", N.ptr(xb), xb.stride(0), N.ptr(z), n, d, int(t), N.ptr(out), _stream(xb))
     return out
 
@@ -189,7 +193,7 @@ def _pred_args(family, alphas, d):
     return N.int_array([0] * d), N.double_array([0.0] * d)
 
 
-def post_mean_matfree(family, xt, z_dn, hyp, coeffs, alphas=None, tbits=0, chunk=4096):
+def post_mean_matfree(family, xt, z_dn, hyp, coeffs, alphas=None, tbits=0, chunk=1024):
     """out[b, t] = sum_i K_{b mod Gk}(xt[t], z[:, i]) coeffs[b, i] -> [B, N] (see fgp_post_mean).
 
     xt [N, d] float64, z_dn [d, n] (float64 lattice / int64 net), hyp [Gk, 1 + d] (scale, lengthscales),
@@ -209,8 +213,6 @@ def post_mean_matfree(family, xt, z_dn, hyp, coeffs, alphas=None, tbits=0, chunk
     nchunks = (n + chunk - 1) // chunk
     for b0 in range(0, B, 4):
         b1 = min(B, b0 + 4)
-        if Gk > 1:
-            assert b0 % Gk == 0 or Gk % 4 == 0 or B <= 4, "output chunking must respect b mod Gk"
         hyp_b = hyp if Gk == 1 else hyp[torch.arange(b0, b1, device=hyp.device) % Gk]
         work = torch.empty((nchunks, b1 - b0, Nt), dtype=torch.float64, device=xt.device)
         cb = coeffs[b0:b1]

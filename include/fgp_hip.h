@@ -127,11 +127,14 @@ typedef struct fgp_fit_desc {
   double* rprop_prev;         /* [n_params] previous gradient (init 0) */
   double* rprop_step;         /* [n_params] step sizes (init lr) */
   double* grad_out;           /* [n_params] gradient of the last step (diagnostics) */
-  double* loss_hist;          /* [max_iters][3]: loss, term1 (norm), term2 (weighted logdet) */
+  double* loss_hist;          /* [max_iters][3] (or [max_iters][G][3] when per_problem): loss, term1 (norm),
+                                 term2 (weighted logdet) */
   double* raw_hist;           /* [max_iters][n_params]: raw parameters at which the loss was evaluated */
   int scale_rg, ls_rg, noise_rg; /* requires_grad of each block */
   double mll_const;           /* d_out * n * log(2 pi) (fastgps/abstract_gp.py:235) */
   double eta_minus, eta_plus, step_min, step_max; /* torch.optim.Rprop defaults 0.5, 1.2, 1e-6, 50 */
+  int per_problem;            /* 1: the G problems are independent GPs (each owns its parameters, loss, Rprop
+                                 state; every *_pp flag must be set when G > 1), one fused reduce+step kernel */
 } fgp_fit_desc;
 
 /* Reduce the partials of fgp_nll_fwd/bwd, assemble loss = 1/2 (term1 + term2 + mll_const), record

@@ -68,7 +68,7 @@ def test_unit_vectors_give_exact_bitreversed_roots(m):
     """fftbr(e_i)[k] = exp(-2 pi i brev(i) k / n) / sqrt(n): locates the bit-reversal exactly."""
     n = 2 ** m
     br = O.bitrev_indices(m)
-    for i in sorted({0, 1, n // 3, n - 1}):
+    for i in sorted({0, 1, n // 3, n - 1} & set(range(n))):
         e = torch.zeros(n)
         e[i] = 1.0
         y = F.ops.fftbr_raw(e.to(DEV)).cpu() * np.sqrt(n)

@@ -46,7 +46,7 @@ def test_struct_layouts_match_header():
     # fgp_nll_desc: 4 ints, ptr, i64, ptr, i64, ptr, 7 ints, double, 3 ptrs
     assert ctypes.sizeof(N.NllDesc) == 120
     assert N.NllDesc.logdet_weight.offset == 88
-    assert ctypes.sizeof(N.FitDesc) == 112
+    assert ctypes.sizeof(N.FitDesc) == 120
 
 
 def test_ops_refuse_cpu_tensors():
