@@ -54,6 +54,22 @@ def parse():
     return p.parse_args()
 
 
+def shard_seeds(rank, world, per_rank, base=1000):
+    """Replica sharding of the C4 shifts: rank r owns global shifts r*per_rank ... (weak scaling);
+    no data-path collective (independent GPs)."""
+    return [base + rank * per_rank + s for s in range(per_rank)]
+
+
+def max_over_ranks(seconds, device):
+    """Max of the per-rank elapsed time (the only collective: timing, not data)."""
+    import torch.distributed as tdist
+    if not (tdist.is_available() and tdist.is_initialized()) or tdist.get_world_size() == 1:
+        return seconds
+    t = torch.tensor([seconds], dtype=torch.float64, device=device)
+    tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+    return float(t)
+
+
 class Shift(object):
     """One randomly shifted lattice GP with resident inputs."""
 
@@ -182,7 +198,7 @@ def main():
     import fastgaussianprocesses_amd as F
     n = 2 ** args.log2n
     d = args.d
-    shifts = [Shift(F, d, n, 1000 + rank * args.shifts + s, device) for s in range(args.shifts)]
+    shifts = [Shift(F, d, n, seed, device) for seed in shard_seeds(rank, world, args.shifts)]
     g = torch.Generator().manual_seed(17)
     xm = torch.rand((args.n_mean, d), generator=g).to(device)
     xv = torch.rand((args.n_var, d), generator=g).to(device)
@@ -211,11 +227,7 @@ def main():
     torch.cuda.synchronize()
     if dist:
         tdist.barrier()
-    el = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([el], device=device)
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        el = float(t)
+    el = max_over_ranks(time.perf_counter() - t0, device)
     sec_step = el / args.steps
     value = args.shifts * n * world / sec_step
 

@@ -67,6 +67,9 @@ _SIGNATURES = {
     "fgp_net_parts": [_c_vp, _c_i64, _c_vp, _c_i64, _c_int, _c_int, _c_vp, _c_vp],
     "fgp_nll_fwd": [_P_NLL, _c_vp],
     "fgp_nll_bwd": [_P_NLL, _c_vp],
+    "fgp_nll_lam": [_P_NLL, _c_vp],
+    "fgp_post_var_qf": [_c_int, _c_vp, _c_i64, _c_vp, _c_int, _c_int, _c_int, _c_pi, _c_pd, _c_vp, _c_vp, _c_vp,
+                        _c_vp, _c_vp, _c_vp],
     "fgp_fit_step": [_P_NLL, _P_FIT, _c_int, _c_int, _c_vp],
     "fgp_fit_run": [_P_NLL, _P_FIT, _c_int, _c_int, _c_int, _c_vp],
     "fgp_post_mean": [_c_int, _c_vp, _c_i64, _c_vp, _c_i64, _c_int, _c_int, _c_pi, _c_pd, _c_vp, _c_int, _c_vp,

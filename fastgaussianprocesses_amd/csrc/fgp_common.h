@@ -317,4 +317,53 @@ __device__ __forceinline__ void center_transform(T* s, int tt, int stable, T* re
   __syncthreads();
 }
 
+// ---------------------------------------------------------------- centring folded into the load
+// Whole-workgroup sum of a T (result in every thread).
+template <typename T>
+__device__ __forceinline__ T block_sum_t(T v, T* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += shfl_xor_d(v, o);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  T tot = red[0];
+#pragma unroll
+  for (int i = 1; i < kWG / 64; ++i) tot += red[i];
+  __syncthreads();
+  return tot;
+}
+
+// Column sums of a column tile (C columns of a 4096-element tile; the thread with index tid staged
+// elements of column tid mod C).  column_partials() stores per-wave partials in `part` ((C < 64 ?
+// 4 C : kWG) entries) and synchronises; column_total(c) then returns the sum of column c.
+template <int C, typename T>
+__device__ __forceinline__ void column_partials(T v, T* part) {
+  if constexpr (C < 64) {
+#pragma unroll
+    for (int o = C; o < 64; o <<= 1) v += shfl_xor_d(v, o);
+    if ((threadIdx.x & 63) < C) part[(threadIdx.x >> 6) * C + (threadIdx.x & 63)] = v;
+  } else {
+    part[threadIdx.x] = v;
+  }
+  __syncthreads();
+}
+template <int C, typename T>
+__device__ __forceinline__ T column_total(int c, const T* part) {
+  constexpr int K = C < 64 ? kWG / 64 : kWG / C;
+  constexpr int STRIDE = C;
+  T tot = part[c];
+#pragma unroll
+  for (int i = 1; i < K; ++i) tot += part[c + i * STRIDE];
+  return tot;
+}
+template <int C> struct ColPart { static constexpr int size = C < 64 ? 4 * C : kWG; };
+
+// Transform of data staged in LDS with its mean already removed; adds mean * L back to bin 0.
+template <int P, bool ADJ, typename T>
+__device__ __forceinline__ void transform_add_mean(T* s, int tt, T mean, const double2* __restrict__ tw) {
+  lds_transform<P, ADJ>(s, tt, tw);
+  if (tt == 0) s[0] += mean * (double)(1 << P);
+  __syncthreads();
+}
+
 }  // namespace fgp

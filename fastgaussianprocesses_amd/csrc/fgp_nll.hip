@@ -220,7 +220,7 @@ __device__ __forceinline__ double* part_ptr(const Nll& a, int g, int q, int blk)
 }
 
 // ---------------------------------------------------------------- n <= 4096: one kernel
-template <int P, typename T>
+template <int P, typename T, bool EMIT>
 __global__ __launch_bounds__(kWG) void k_iter_single(Nll a, const double2* __restrict__ tw) {
   constexpr int L = 1 << P, TL = L / 16, TPW = kTile / L;
   __shared__ T lds[kTile + kTile / 16];
@@ -244,6 +244,14 @@ __global__ __launch_bounds__(kWG) void k_iter_single(Nll a, const double2* __res
   __syncthreads();
   center_transform<P, false>(s, tt, 1, red, tw);
   const double rootn = sqrt((double)L), inv_rootn = 1.0 / rootn;
+  if constexpr (EMIT) {
+    if (live) {
+      T* gl = static_cast<T*>(a.grad_lam) + (int64_t)g * L;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) gl[tt + j * TL] = s[padi(tt + j * TL)] * inv_rootn;
+    }
+    return;
+  }
   const double* yg = a.ysq + (int64_t)g * a.ysq_stride;
   double norm = 0.0, logdet = 0.0, dnoise = 0.0;
 #pragma unroll
@@ -295,16 +303,35 @@ __global__ __launch_bounds__(kWG) void k_fwd_rows(Nll a, const double2* __restri
   const double* pg = a.parts + (int64_t)g * a.parts_stride;
   const int64_t base = (int64_t)row0 * N2;
   // k1 for element pairs (2 tid + 512 kk, +1): 16-byte loads of every dimension's parts
+  if constexpr (RPW == 1) {
+    double2 kv[8];
+    double sum = 0.0;
 #pragma unroll
-  for (int kk = 0; kk < 8; ++kk) {
-    const int e = 2 * tid + 512 * kk;
-    const double2 kv = k1_pair(a, h, pg, n, base + e);
-    lds[padi(e)] = real_to_T<T>(kv.x);
-    lds[padi(e + 1)] = real_to_T<T>(kv.y);
+    for (int kk = 0; kk < 8; ++kk) {
+      kv[kk] = k1_pair(a, h, pg, n, base + 2 * tid + 512 * kk);
+      sum += kv[kk].x + kv[kk].y;
+    }
+    const double mean = block_sum(sum, (double*)red) * (1.0 / N2);
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      const int e = 2 * tid + 512 * kk;
+      lds[padi(e)] = real_to_T<T>(kv[kk].x - mean);
+      lds[padi(e + 1)] = real_to_T<T>(kv[kk].y - mean);
+    }
+    __syncthreads();
+    transform_add_mean<P2, false>(lds, tid, real_to_T<T>(mean), tw);
+  } else {
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      const int e = 2 * tid + 512 * kk;
+      const double2 kv = k1_pair(a, h, pg, n, base + e);
+      lds[padi(e)] = real_to_T<T>(kv.x);
+      lds[padi(e + 1)] = real_to_T<T>(kv.y);
+    }
+    __syncthreads();
+    T* s = lds + (tid / TL) * (N2 + N2 / 16);
+    center_transform<P2, false>(s, tid % TL, 1, red, tw);
   }
-  __syncthreads();
-  T* s = lds + (tid / TL) * (N2 + N2 / 16);
-  center_transform<P2, false>(s, tid % TL, 1, red, tw);
   T* out = static_cast<T*>(a.work) + (int64_t)g * n + base;
   if constexpr (sizeof(T) == 16 && RPW == 1) {
     const RowTwiddle rt((unsigned)row0, tid, P2, m1, tw, twm);
@@ -336,12 +363,12 @@ struct ColLay {
   static constexpr int CS = (PADLEN % 2 == 0) ? PADLEN + 1 : PADLEN;
 };
 
-template <int P1, typename T>
+template <int P1, typename T, bool EMIT>
 __global__ __launch_bounds__(kWG) void k_fwd_cols(Nll a, const double2* __restrict__ tw) {
   using Lay = ColLay<P1, T>;
   constexpr int N1 = Lay::N1, C = Lay::C, CS = Lay::CS, TL = N1 / 16;
   __shared__ T lds[kLds];
-  __shared__ T red[kWG / 64];
+  __shared__ T part[ColPart<C>::size];
   __shared__ double redd[kWG / 64];
   const int m = a.log2n;
   const int64_t n = (int64_t)1 << m, N2 = n >> P1;
@@ -351,20 +378,35 @@ __global__ __launch_bounds__(kWG) void k_fwd_cols(Nll a, const double2* __restri
   const int64_t c0 = (int64_t)blk * C;
   const int tid = threadIdx.x;
   const T* in = static_cast<const T*>(a.work) + (int64_t)g * n + c0;
+  const int cl = tid % C, col = tid / TL;
+  T v[16];
+  T sum = zero_v<T>();
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
-    const int e = tid + k * kWG;
-    const int c = e % C, u = e / C;
-    lds[c * CS + padi(u)] = in[(int64_t)u * N2 + c];
+    v[k] = in[(int64_t)((tid + k * kWG) / C) * N2 + cl];
+    sum += v[k];
   }
+  column_partials<C>(sum, part);
+  const T mean_l = column_total<C>(cl, part) * (1.0 / N1);
+  const T mean_t = column_total<C>(col, part) * (1.0 / N1);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) lds[cl * CS + padi((tid + k * kWG) / C)] = v[k] - mean_l;
   __syncthreads();
-  T* s = lds + (tid / TL) * CS;
-  center_transform<P1, false>(s, tid % TL, 1, red, tw);
+  transform_add_mean<P1, false>(lds + col * CS, tid % TL, mean_t, tw);
+  const double rootn = sqrt((double)n), inv_rootn = 1.0 / rootn;
+  T* gl = static_cast<T*>(a.grad_lam) + (int64_t)g * n + c0;
+  if constexpr (EMIT) {   // lambda = ft(k1) (fgp_nll_lam)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int e = tid + k * kWG;
+      const int c = e % C, r = e / C;
+      gl[(int64_t)r * N2 + c] = lds[c * CS + padi(r)] * inv_rootn;
+    }
+    return;
+  }
   Hyp h;
   load_hyp(a, g, h);
-  const double rootn = sqrt((double)n), inv_rootn = 1.0 / rootn;
   const double* yg = a.ysq + (int64_t)g * a.ysq_stride + c0;
-  T* gl = static_cast<T*>(a.grad_lam) + (int64_t)g * n + c0;
   double norm = 0.0, logdet = 0.0, dnoise = 0.0;
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
@@ -401,13 +443,28 @@ __global__ __launch_bounds__(kWG) void k_bwd_rows(Nll a, const double2* __restri
   const int64_t base = (int64_t)blk * kTile;
   const int tid = threadIdx.x;
   const T* in = static_cast<const T*>(a.work) + (int64_t)g * n + base;
-  if constexpr (FFT && RPW == 1) {
-    const RowTwiddle rt((unsigned)row0, tid, P2, m1, tw, twm);
+  if constexpr (RPW == 1) {
+    T v[16];
+    T sum = zero_v<T>();
+    if constexpr (FFT) {
+      const RowTwiddle rt((unsigned)row0, tid, P2, m1, tw, twm);
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int e = tid + k * kWG;
-      lds[padi(e)] = tw_mul<T>(in[e], rt.at(k, P2, m1, tw, twm), true);
+      for (int k = 0; k < 16; ++k) {
+        v[k] = tw_mul<T>(in[tid + k * kWG], rt.at(k, P2, m1, tw, twm), true);
+        sum += v[k];
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        v[k] = in[tid + k * kWG];
+        sum += v[k];
+      }
     }
+    const T mean = block_sum_t(sum, red) * (1.0 / N2);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) lds[padi(tid + k * kWG)] = v[k] - mean;
+    __syncthreads();
+    transform_add_mean<P2, FFT>(lds, tid, mean, tw);
   } else {
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
@@ -419,10 +476,10 @@ __global__ __launch_bounds__(kWG) void k_bwd_rows(Nll a, const double2* __restri
       }
       lds[padi(e)] = v;
     }
+    __syncthreads();
+    T* s = lds + (tid / TL) * (N2 + N2 / 16);
+    center_transform<P2, FFT>(s, tid % TL, 1, red, tw);
   }
-  __syncthreads();
-  T* s = lds + (tid / TL) * (N2 + N2 / 16);
-  center_transform<P2, FFT>(s, tid % TL, 1, red, tw);
   Hyp h;
   load_hyp(a, g, h);
   const double* pg = a.parts + (int64_t)g * a.parts_stride;
@@ -610,11 +667,15 @@ static int to_nll(const fgp_nll_desc* d, Nll& a) {
 }
 
 template <typename T>
-static int launch_iter_single(const Nll& a, const Tables* tb, hipStream_t st) {
+static int launch_iter_single(const Nll& a, const Tables* tb, hipStream_t st, bool emit = false) {
   const int P = a.log2n;
   const unsigned grid = (unsigned)((a.G + (kTile >> P) - 1) / (kTile >> P));
   switch (P) {
-#define FGP_C(PP) case PP: k_iter_single<PP, T><<<grid, kWG, 0, st>>>(a, tb->tw4096); break;
+#define FGP_C(PP)                                                                   \
+  case PP:                                                                          \
+    if (emit) k_iter_single<PP, T, true><<<grid, kWG, 0, st>>>(a, tb->tw4096);      \
+    else k_iter_single<PP, T, false><<<grid, kWG, 0, st>>>(a, tb->tw4096);          \
+    break;
     FGP_C(4) FGP_C(5) FGP_C(6) FGP_C(7) FGP_C(8) FGP_C(9) FGP_C(10) FGP_C(11) FGP_C(12)
 #undef FGP_C
     default: return set_error(kErrInvalid, "bad log2n");
@@ -623,7 +684,7 @@ static int launch_iter_single(const Nll& a, const Tables* tb, hipStream_t st) {
 }
 
 template <typename T>
-static int launch_fwd2(const Nll& a, const Tables* tb, hipStream_t st) {
+static int launch_fwd2(const Nll& a, const Tables* tb, hipStream_t st, bool emit) {
   const int m = a.log2n, m2 = split_m2(m), m1 = m - m2;
   const unsigned grid = (unsigned)((int64_t)a.G << (m - kTileLog));
   switch (m2) {
@@ -635,7 +696,11 @@ static int launch_fwd2(const Nll& a, const Tables* tb, hipStream_t st) {
   int rc = check_launch("k_fwd_rows");
   if (rc != kOk) return rc;
   switch (m1) {
-#define FGP_C(PP) case PP: k_fwd_cols<PP, T><<<grid, kWG, 0, st>>>(a, tb->tw4096); break;
+#define FGP_C(PP)                                                           \
+  case PP:                                                                  \
+    if (emit) k_fwd_cols<PP, T, true><<<grid, kWG, 0, st>>>(a, tb->tw4096); \
+    else k_fwd_cols<PP, T, false><<<grid, kWG, 0, st>>>(a, tb->tw4096);     \
+    break;
     FGP_C(4) FGP_C(5) FGP_C(6) FGP_C(7) FGP_C(8) FGP_C(9) FGP_C(10) FGP_C(11) FGP_C(12)
 #undef FGP_C
     default: return set_error(kErrInvalid, "bad m1");
@@ -664,7 +729,7 @@ static int nll_fwd(const Nll& a, hipStream_t st, bool lattice) {
   const Tables* tb = get_tables(st);
   if (!tb) return set_error(kErrHip, "twiddle table initialisation failed");
   if (a.log2n <= 12) return lattice ? launch_iter_single<double2>(a, tb, st) : launch_iter_single<double>(a, tb, st);
-  return lattice ? launch_fwd2<double2>(a, tb, st) : launch_fwd2<double>(a, tb, st);
+  return lattice ? launch_fwd2<double2>(a, tb, st, false) : launch_fwd2<double>(a, tb, st, false);
 }
 
 static int nll_bwd(const Nll& a, hipStream_t st, bool lattice) {
@@ -751,6 +816,18 @@ int fgp_nll_fwd(const fgp_nll_desc* desc, void* stream) {
   int rc = to_nll(desc, a);
   if (rc != kOk) return rc;
   return nll_fwd(a, (hipStream_t)stream, desc->family == FGP_FAMILY_LATTICE);
+}
+
+int fgp_nll_lam(const fgp_nll_desc* desc, void* stream) {
+  Nll a;
+  int rc = to_nll(desc, a);
+  if (rc != kOk) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  const Tables* tb = get_tables(st);
+  if (!tb) return set_error(kErrHip, "twiddle table initialisation failed");
+  const bool lat = desc->family == FGP_FAMILY_LATTICE;
+  if (a.log2n <= 12) return lat ? launch_iter_single<double2>(a, tb, st, true) : launch_iter_single<double>(a, tb, st, true);
+  return lat ? launch_fwd2<double2>(a, tb, st, true) : launch_fwd2<double>(a, tb, st, true);
 }
 
 int fgp_nll_bwd(const fgp_nll_desc* desc, void* stream) {

@@ -197,6 +197,178 @@ __global__ __launch_bounds__(kWG) void k_kernel_rows(const double* __restrict__ 
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Posterior variance by Parseval (n > 4096):  with r_t[i] = K(x_t, z_i) and A = 1/ev,
+//   sum_i r_t[i] (K^-1 r_t)[i] = Re <r_t, ift(A ft(r_t))> = sum_k Re(A_k) |ft(r_t)_k|^2,
+// which equals the reference's sum(t * kmat) with t = ift(A ft(kmat)).real (abstract_gp.py:408-412,
+// util.py:338-353) for real r.  One forward transform per test point instead of two, and the kernel
+// rows are generated inside the row pass instead of being materialised.
+struct QfArgs {
+  int log2n, d, tbits, N;
+  const double* xt;          // [N][d]
+  const void* z;             // [d][n] float64 (lattice) / int64 (net)
+  PredSpec spec;
+  const double* hyp;         // device [1 + d]: scale, lengthscales
+  const double* wa;          // [n] Re(A)
+  void* work;                // [N][n]
+  double* partial;           // [N][n / 4096]
+};
+
+template <int P2, typename T>
+__global__ __launch_bounds__(kWG) void k_qf_rows(QfArgs q, const double2* __restrict__ tw, const double2* __restrict__ twm) {
+  constexpr int N2 = 1 << P2, TL = N2 / 16, RPW = kTile / N2;
+  constexpr int FAM = sizeof(T) == 16 ? 0 : 1;
+  __shared__ T lds[kTile + kTile / 16];
+  __shared__ T red[kWG / 64];
+  const int m = q.log2n, m1 = m - P2;
+  const int64_t n = (int64_t)1 << m;
+  const int64_t tiles = n >> kTileLog;
+  const int t = (int)(blockIdx.x / tiles);
+  const int row0 = (int)(blockIdx.x % tiles) * RPW;
+  const int tid = threadIdx.x;
+  double xv[FGP_MAX_D], fa[FGP_MAX_D], fc[FGP_MAX_D];
+  unsigned long long xb[FGP_MAX_D];
+  const double scale = q.hyp[0];
+#pragma unroll
+  for (int j = 0; j < FGP_MAX_D; ++j) {
+    xv[j] = j < q.d ? q.xt[(int64_t)t * q.d + j] : 0.0;
+    const double l = j < q.d ? q.hyp[1 + j] : 0.0;
+    if constexpr (FAM == 0) {
+      fa[j] = l * q.spec.coef[j];
+      fc[j] = fac_const(q.spec.order[j], fa[j]);
+    } else {
+      xb[j] = to_bits(xv[j], q.tbits);
+      fa[j] = 1.0 + l;
+      fc[j] = 3.0 * l;
+    }
+  }
+  const int64_t base = (int64_t)row0 * N2;
+  double kv0[8], kv1[8];
+  double sum = 0.0;
+#pragma unroll 2
+  for (int kk = 0; kk < 8; ++kk) {
+    const int e = 2 * tid + 512 * kk;
+    double p0 = scale, p1 = scale;
+#pragma unroll
+    for (int j = 0; j < FGP_MAX_D; ++j) {
+      if (j < q.d) {
+        if constexpr (FAM == 0) {
+          const double2 zv = *reinterpret_cast<const double2*>(static_cast<const double*>(q.z) + (int64_t)j * n + base + e);
+          p0 *= lat_factor(q.spec.order[j], fabs(xv[j] - zv.x), fa[j], fc[j]);
+          p1 *= lat_factor(q.spec.order[j], fabs(xv[j] - zv.y), fa[j], fc[j]);
+        } else {
+          const longlong2 zv = *reinterpret_cast<const longlong2*>(static_cast<const long long*>(q.z) + (int64_t)j * n + base + e);
+          p0 *= net_factor(xb[j] ^ (unsigned long long)zv.x, q.tbits, fa[j], fc[j]);
+          p1 *= net_factor(xb[j] ^ (unsigned long long)zv.y, q.tbits, fa[j], fc[j]);
+        }
+      }
+    }
+    kv0[kk] = p0;
+    kv1[kk] = p1;
+    sum += p0 + p1;
+  }
+  if constexpr (RPW == 1) {
+    const double mean = block_sum(sum, (double*)red) * (1.0 / N2);
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      const int e = 2 * tid + 512 * kk;
+      if constexpr (FAM == 0) {
+        lds[padi(e)] = make_double2(kv0[kk] - mean, 0.0);
+        lds[padi(e + 1)] = make_double2(kv1[kk] - mean, 0.0);
+      } else {
+        lds[padi(e)] = kv0[kk] - mean;
+        lds[padi(e + 1)] = kv1[kk] - mean;
+      }
+    }
+    __syncthreads();
+    T mt;
+    if constexpr (FAM == 0) mt = make_double2(mean, 0.0);
+    else mt = mean;
+    transform_add_mean<P2, false>(lds, tid, mt, tw);
+  } else {
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      const int e = 2 * tid + 512 * kk;
+      if constexpr (FAM == 0) {
+        lds[padi(e)] = make_double2(kv0[kk], 0.0);
+        lds[padi(e + 1)] = make_double2(kv1[kk], 0.0);
+      } else {
+        lds[padi(e)] = kv0[kk];
+        lds[padi(e + 1)] = kv1[kk];
+      }
+    }
+    __syncthreads();
+    T* s = lds + (tid / TL) * (N2 + N2 / 16);
+    center_transform<P2, false>(s, tid % TL, 1, red, tw);
+  }
+  T* out = static_cast<T*>(q.work) + (int64_t)t * n + base;
+  if constexpr (FAM == 0 && RPW == 1) {
+    const RowTwiddle rt((unsigned)row0, tid, P2, m1, tw, twm);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int e = tid + k * kWG;
+      out[e] = cmul(lds[padi(e)], rt.at(k, P2, m1, tw, twm));
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int e = tid + k * kWG;
+      T v = lds[padi(e)];
+      if constexpr (FAM == 0) {
+        const unsigned ex = brev_bits((unsigned)(row0 + (e >> P2)), m1) * (unsigned)(e & (N2 - 1));
+        v = cmul(v, inter_tw(ex, P2, m1, tw, twm));
+      }
+      out[e] = v;
+    }
+  }
+}
+
+__device__ __forceinline__ double sqabs(double2 v) { return v.x * v.x + v.y * v.y; }
+__device__ __forceinline__ double sqabs(double v) { return v * v; }
+
+template <int P1, typename T>
+__global__ __launch_bounds__(kWG) void k_qf_cols(QfArgs q, const double2* __restrict__ tw) {
+  constexpr int N1 = 1 << P1, C = kTile / N1, TL = N1 / 16;
+  constexpr int PADLEN = N1 + N1 / 16;
+  constexpr int CS = (PADLEN % 2 == 0) ? PADLEN + 1 : PADLEN;
+  __shared__ T lds[kLds];
+  __shared__ T part[ColPart<C>::size];
+  __shared__ double redd[kWG / 64];
+  const int m = q.log2n;
+  const int64_t n = (int64_t)1 << m, N2 = n >> P1;
+  const int64_t tiles = n >> kTileLog;
+  const int t = (int)(blockIdx.x / tiles);
+  const int blk = (int)(blockIdx.x % tiles);
+  const int64_t c0 = (int64_t)blk * C;
+  const int tid = threadIdx.x;
+  const T* in = static_cast<const T*>(q.work) + (int64_t)t * n + c0;
+  const int cl = tid % C, col = tid / TL;
+  T v[16];
+  T sum = zero_v<T>();
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    v[k] = in[(int64_t)((tid + k * kWG) / C) * N2 + cl];
+    sum += v[k];
+  }
+  column_partials<C>(sum, part);
+  const T mean_l = column_total<C>(cl, part) * (1.0 / N1);
+  const T mean_t = column_total<C>(col, part) * (1.0 / N1);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) lds[cl * CS + padi((tid + k * kWG) / C)] = v[k] - mean_l;
+  __syncthreads();
+  transform_add_mean<P1, false>(lds + col * CS, tid % TL, mean_t, tw);
+  const double inv_n = 1.0 / (double)n;
+  double acc = 0.0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int e = tid + k * kWG;
+    const int c = e % C, r = e / C;
+    acc += sqabs(lds[c * CS + padi(r)]) * inv_n * q.wa[(int64_t)r * N2 + c0 + c];
+  }
+  acc = block_sum(acc, redd);
+  if (tid == 0) q.partial[(int64_t)t * tiles + blk] = acc;
+}
+
 template <int FAM, int D>
 static void post_mean_d(dim3 grid, hipStream_t st, bool uniform4, int B, const double* xt, int64_t N, const void* z,
                         int64_t n, const PredSpec& spec, int tbits, const double* hyp, int Gk, const double* coeffs,
@@ -280,6 +452,66 @@ int fgp_post_mean(int family, const double* xt, int64_t N, const void* z, int64_
   if (family == FGP_FAMILY_LATTICE)
     return launch_post_mean<0>(d, xt, N, z, n, spec, tbits, hyp, Gk, coeffs, coeff_stride, B, out, out_stride, work, st);
   return launch_post_mean<1>(d, xt, N, z, n, spec, tbits, hyp, Gk, coeffs, coeff_stride, B, out, out_stride, work, st);
+}
+
+int fgp_post_var_qf(int family, const double* xt, int64_t N, const void* z, int log2n, int d, int tbits,
+                    const int* order, const double* coef, const double* hyp, const double* wa, void* work,
+                    double* partial, double* out, void* stream) {
+  if (N < 0 || d < 1 || d > FGP_MAX_D || log2n < 13 || log2n > kMaxLog2N)
+    return set_error(kErrInvalid, "fgp_post_var_qf: needs 13 <= log2n <= 24 and 1 <= d <= %d", FGP_MAX_D);
+  if (N == 0) return kOk;
+  if (!xt || !z || !hyp || !wa || !work || !partial || !out) return set_error(kErrInvalid, "fgp_post_var_qf: null pointer");
+  if ((N << (log2n - kTileLog)) >= ((int64_t)1 << 31)) return set_error(kErrUnsupported, "fgp_post_var_qf: N too large");
+  hipStream_t st = (hipStream_t)stream;
+  const Tables* tb = get_tables(st);
+  if (!tb) return set_error(kErrHip, "twiddle table initialisation failed");
+  QfArgs q;
+  q.log2n = log2n;
+  q.d = d;
+  q.tbits = tbits;
+  q.N = (int)N;
+  q.xt = xt;
+  q.z = z;
+  int rc = make_spec(family, d, order, coef, q.spec);
+  if (rc != kOk) return rc;
+  q.hyp = hyp;
+  q.wa = wa;
+  q.work = work;
+  q.partial = partial;
+  const int m2 = split_m2(log2n), m1 = log2n - m2;
+  const dim3 grid((unsigned)(N << (log2n - kTileLog)));
+  const double2* tw = tb->tw4096;
+  const double2* twm = tb->twm[log2n];
+  if (family == FGP_FAMILY_LATTICE) {
+    switch (m2) {
+#define FGP_C(PP) case PP: k_qf_rows<PP, double2><<<grid, kWG, 0, st>>>(q, tw, twm); break;
+      FGP_C(9) FGP_C(10) FGP_C(11) FGP_C(12)
+#undef FGP_C
+    }
+  } else {
+    switch (m2) {
+#define FGP_C(PP) case PP: k_qf_rows<PP, double><<<grid, kWG, 0, st>>>(q, tw, twm); break;
+      FGP_C(9) FGP_C(10) FGP_C(11) FGP_C(12)
+#undef FGP_C
+    }
+  }
+  if ((rc = check_launch("k_qf_rows")) != kOk) return rc;
+  if (family == FGP_FAMILY_LATTICE) {
+    switch (m1) {
+#define FGP_C(PP) case PP: k_qf_cols<PP, double2><<<grid, kWG, 0, st>>>(q, tw); break;
+      FGP_C(4) FGP_C(5) FGP_C(6) FGP_C(7) FGP_C(8) FGP_C(9) FGP_C(10) FGP_C(11) FGP_C(12)
+#undef FGP_C
+    }
+  } else {
+    switch (m1) {
+#define FGP_C(PP) case PP: k_qf_cols<PP, double><<<grid, kWG, 0, st>>>(q, tw); break;
+      FGP_C(4) FGP_C(5) FGP_C(6) FGP_C(7) FGP_C(8) FGP_C(9) FGP_C(10) FGP_C(11) FGP_C(12)
+#undef FGP_C
+    }
+  }
+  if ((rc = check_launch("k_qf_cols")) != kOk) return rc;
+  k_sum_chunks<<<(unsigned)N, kWG, 0, st>>>(partial, (int64_t)1 << (log2n - kTileLog), out, N, N);
+  return check_launch("k_sum_chunks");
 }
 
 int fgp_kernel_rows(int family, const double* xt, int64_t N, const void* z, int64_t n, int d, int tbits,

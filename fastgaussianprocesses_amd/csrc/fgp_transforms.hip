@@ -106,6 +106,7 @@ __global__ __launch_bounds__(kWG) void k_rows(const void* in, int64_t in_bs, int
   constexpr int N2 = 1 << P2;
   constexpr int TL = N2 / 16;
   constexpr int RPW = kTile / N2;
+  constexpr bool FFT = sizeof(T) == 16;
   __shared__ T lds[kTile + kTile / 16];
   __shared__ T red[kWG / 64];
   const int m1 = m - P2;
@@ -114,51 +115,50 @@ __global__ __launch_bounds__(kWG) void k_rows(const void* in, int64_t in_bs, int
   const int row0 = (int)(blockIdx.x % tiles) * RPW;
   const int tid = threadIdx.x;
   const int64_t ibase = b * in_bs + (int64_t)row0 * N2;   // rows are contiguous: the tile is one slab
-  if constexpr (ADJ && sizeof(T) == 16) {
-    if (twiddle) {
-      if constexpr (RPW == 1) {
-        const RowTwiddle rt((unsigned)row0, tid, P2, m1, tw, twm);
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          const int e = tid + k * kWG;
-          lds[padi(e)] = tw_mul<T>(load_in<T>(in, ibase + e, in_real), rt.at(k, P2, m1, tw, twm), true);
-        }
-      } else {
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          const int e = tid + k * kWG;
-          const unsigned ex = brev_bits((unsigned)(row0 + (e >> P2)), m1) * (unsigned)(e & (N2 - 1));
-          lds[padi(e)] = tw_mul<T>(load_in<T>(in, ibase + e, in_real), inter_tw(ex, P2, m1, tw, twm), true);
-        }
-      }
-    }
-  }
-  if (!(ADJ && sizeof(T) == 16 && twiddle)) {
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int e = tid + k * kWG;
-      lds[padi(e)] = load_in<T>(in, ibase + e, in_real);
-    }
-  }
-  __syncthreads();
-  const int tt = tid % TL;
-  T* s = lds + (tid / TL) * (N2 + N2 / 16);
-  center_transform<P2, ADJ>(s, tt, stable, red, tw);
   const int64_t obase = b * out_bs + (int64_t)row0 * N2;
-  if (!ADJ && twiddle && RPW == 1) {
+  if constexpr (RPW == 1) {
+    // one row per workgroup: uniform twiddle row, mean folded into the staging store
     const RowTwiddle rt((unsigned)row0, tid, P2, m1, tw, twm);
+    T v[16];
+    T sum = zero_v<T>();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      v[k] = load_in<T>(in, ibase + tid + k * kWG, in_real);
+      if (ADJ && FFT && twiddle) v[k] = tw_mul<T>(v[k], rt.at(k, P2, m1, tw, twm), true);
+      sum += v[k];
+    }
+    const T mean = stable ? block_sum_t(sum, red) * (1.0 / N2) : zero_v<T>();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) lds[padi(tid + k * kWG)] = v[k] - mean;
+    __syncthreads();
+    transform_add_mean<P2, ADJ>(lds, tid, mean, tw);
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const int e = tid + k * kWG;
-      store_out(out, obase + e, tw_mul<T>(lds[padi(e)], rt.at(k, P2, m1, tw, twm), false) * scale, out_real);
+      T r = lds[padi(e)];
+      if (!ADJ && FFT && twiddle) r = tw_mul<T>(r, rt.at(k, P2, m1, tw, twm), false);
+      store_out(out, obase + e, r * scale, out_real);
     }
     return;
   }
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     const int e = tid + k * kWG;
+    T v = load_in<T>(in, ibase + e, in_real);
+    if (ADJ && FFT && twiddle) {
+      const unsigned ex = brev_bits((unsigned)(row0 + (e >> P2)), m1) * (unsigned)(e & (N2 - 1));
+      v = tw_mul<T>(v, inter_tw(ex, P2, m1, tw, twm), true);
+    }
+    lds[padi(e)] = v;
+  }
+  __syncthreads();
+  T* s = lds + (tid / TL) * (N2 + N2 / 16);
+  center_transform<P2, ADJ>(s, tid % TL, stable, red, tw);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int e = tid + k * kWG;
     T v = lds[padi(e)];
-    if (!ADJ && twiddle) {
+    if (!ADJ && FFT && twiddle) {
       const unsigned ex = brev_bits((unsigned)(row0 + (e >> P2)), m1) * (unsigned)(e & (N2 - 1));   // < 2^m
       v = tw_mul<T>(v, inter_tw(ex, P2, m1, tw, twm), false);
     }
@@ -190,7 +190,9 @@ __global__ __launch_bounds__(kWG) void k_cols(const void* in, int64_t in_bs, int
   using Lay = ColLayout<P1>;
   constexpr int N1 = Lay::N1, C = Lay::C, CS = Lay::CS, TL = N1 / 16;
   __shared__ T lds[kLds];
-  __shared__ T red[kWG / 64];
+  __shared__ T part[ColPart<C>::size];
+  (void)twiddle;
+  (void)twm;
   const int P2 = m - P1;
   const int64_t N2 = (int64_t)1 << P2;
   const int64_t tiles = (int64_t)1 << (m - kTileLog);
@@ -198,25 +200,32 @@ __global__ __launch_bounds__(kWG) void k_cols(const void* in, int64_t in_bs, int
   const int64_t c0 = (blockIdx.x % tiles) * C;
   const int tid = threadIdx.x;
   const int64_t ibase = b * in_bs + c0;
+  const int cl = tid % C;         // column this thread stages (e = tid + 256 k keeps e mod C fixed)
+  T v[16];
+  T sum = zero_v<T>();
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     const int e = tid + k * kWG;
-    const int c = e % C, u = e / C;
-    lds[c * CS + padi(u)] = load_in<T>(in, ibase + (int64_t)u * N2 + c, in_real);
+    v[k] = load_in<T>(in, ibase + (int64_t)(e / C) * N2 + cl, in_real);
+    sum += v[k];
   }
+  T mean_l = zero_v<T>(), mean_t = zero_v<T>();
+  const int col = tid / TL;       // column this thread transforms
+  if (stable) {
+    column_partials<C>(sum, part);
+    mean_l = column_total<C>(cl, part) * (1.0 / N1);
+    mean_t = column_total<C>(col, part) * (1.0 / N1);
+  }
+#pragma unroll
+  for (int k = 0; k < 16; ++k) lds[cl * CS + padi((tid + k * kWG) / C)] = v[k] - mean_l;
   __syncthreads();
-  const int tt = tid % TL;
-  const int col = tid / TL;
-  T* s = lds + col * CS;
-  center_transform<P1, ADJ>(s, tt, stable, red, tw);
+  transform_add_mean<P1, ADJ>(lds + col * CS, tid % TL, mean_t, tw);
   const int64_t obase = b * out_bs + c0;
-  (void)twiddle;
-  (void)twm;
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     const int e = tid + k * kWG;
-    const int c = e % C, r = e / C;
-    store_out(out, obase + (int64_t)r * N2 + c, lds[c * CS + padi(r)] * scale, out_real);
+    const int r = e / C;
+    store_out(out, obase + (int64_t)r * N2 + cl, lds[cl * CS + padi(r)] * scale, out_real);
   }
 }
 

@@ -151,6 +151,7 @@ class AbstractFastGP(torch.nn.Module):
         # data
         self.n = torch.zeros(1, dtype=torch.int64, device=dev)
         self.m = -torch.ones(1, dtype=torch.int64, device=dev)
+        self._nh = 0           # host mirror of self.n[0] (no device syncs on the hot path)
         self._y = [torch.empty(0, device=dev)]
         self._pts_n = 0
         self._x = torch.empty((0, self.d), device=dev)
@@ -210,33 +211,47 @@ class AbstractFastGP(torch.nn.Module):
     def get_default_optimizer(self, lr):
         return torch.optim.Rprop(self.parameters(), lr=1e-1 if lr is None else lr)
 
-    def _snapshot(self):
-        return tuple(p.detach().clone() for p in (self.raw_scale, self.raw_lengthscales, self.raw_noise,
-                                                   self.raw_factor_task_kernel, self.raw_noise_task_kernel))
+    def _param_key(self):
+        # identity + version counter of every raw hyper-parameter: in-place updates (optimizer steps)
+        # bump the version, reassignment changes the identity -- no device synchronisation needed
+        return tuple((id(p), p._version, p.data_ptr()) for p in (
+            self.raw_scale, self.raw_lengthscales, self.raw_noise, self.raw_factor_task_kernel,
+            self.raw_noise_task_kernel))
 
     def _params_changed(self):
-        cur = (self.raw_scale, self.raw_lengthscales, self.raw_noise, self.raw_factor_task_kernel,
-               self.raw_noise_task_kernel)
-        if self._snap is None or any(a.shape != b.shape or not torch.equal(a.detach(), b) for a, b in zip(cur, self._snap)):
-            self._snap = self._snapshot()
+        key = self._param_key()
+        if self._snap != key:
+            self._snap = key
             return True
         return False
 
+    def _hparams(self):
+        return (self.raw_scale, self.raw_lengthscales, self.raw_noise, self.raw_factor_task_kernel,
+                self.raw_noise_task_kernel)
+
+    def _gradmode(self):
+        """True when results must carry an autograd graph w.r.t. the hyper-parameters."""
+        return torch.is_grad_enabled() and any(p.requires_grad for p in self._hparams())
+
     def _cached(self, key, fn, grad_sensitive=True):
         """Cache a derived quantity until n or the hyper-parameters change (the reference's
-        _frozen_equal / FASTGP_FORCE_RECOMPILE invalidation, util.py:81-94,185-205)."""
+        _frozen_equal / FASTGP_FORCE_RECOMPILE invalidation, util.py:81-94,185-205).  Values computed
+        with and without an autograd graph are cached separately; graph-free ones come from the
+        fused HIP paths."""
         if self._params_changed():
             self._cache = {k: v for k, v in self._cache.items() if not k[2]}
-        k = (key[0], key[1], grad_sensitive)
+        k = (key[0], key[1], grad_sensitive, grad_sensitive and self._gradmode())
         if k not in self._cache:
             self._cache[k] = fn()
         return self._cache[k]
 
     def _task_scalar(self):
-        kt = self.gram_matrix_tasks
-        if not torch.equal(kt.detach(), torch.ones_like(kt)):
-            raise NotImplementedError("single-task GPs with a non-unit task kernel are not supported")
-        return 1.0
+        def check():
+            kt = self.gram_matrix_tasks
+            if not torch.equal(kt.detach(), torch.ones_like(kt)):
+                raise NotImplementedError("single-task GPs with a non-unit task kernel are not supported")
+            return 1.0
+        return self._cached(("task_unit", 0), check)
 
     # ------------------------------------------------------------------ points and data
     def _ensure_points(self, n):
@@ -252,14 +267,14 @@ class AbstractFastGP(torch.nn.Module):
 
     def get_x(self, task=0, n=None):
         assert task == 0
-        n = int(self.n[0]) if n is None else int(n)
+        n = self._nh if n is None else int(n)
         assert n >= 0
         self._ensure_points(n)
         return self._x[:n]
 
     def get_xb(self, task=0, n=None):
         assert task == 0
-        n = int(self.n[0]) if n is None else int(n)
+        n = self._nh if n is None else int(n)
         assert n >= 0
         self._ensure_points(n)
         return self._xb[:n]
@@ -276,9 +291,9 @@ class AbstractFastGP(torch.nn.Module):
             task = self.default_task
         inttask = isinstance(task, int)
         ns = n.tolist()
-        assert all(v >= int(self.n[0]) for v in ns), \
+        assert all(v >= self._nh for v in ns), \
             "maximum sequence index must be greater than the current number of samples"
-        out = [self.get_x(0, v)[int(self.n[0]):v] for v in ns]
+        out = [self.get_x(0, v)[self._nh:v] for v in ns]
         return out[0] if inttask else out
 
     def add_y_next(self, y_next, task=None):
@@ -288,10 +303,11 @@ class AbstractFastGP(torch.nn.Module):
         assert all(y.shape[:-1] == self.shape_batch for y in y_next)
         y = y_next[0].to(device=self.device, dtype=torch.float64)
         self._y[0] = torch.cat([self._y[0], y], -1)
-        self.n = torch.tensor([self._y[0].size(-1)], dtype=torch.int64, device=self.device)
-        self.m = torch.where(self.n == 0, -1, torch.log2(self.n.double())).to(torch.int64)
+        self._nh = int(self._y[0].size(-1))
+        self.n = torch.tensor([self._nh], dtype=torch.int64, device=self.device)
+        self.m = torch.tensor([self._nh.bit_length() - 1 if self._nh > 0 else -1], dtype=torch.int64, device=self.device)
         self._cache = {}
-        assert torch.logical_or(self.n == 0, (self.n & (self.n - 1) == 0)).all(), "total samples must be power of 2"
+        assert self._nh == 0 or (self._nh & (self._nh - 1)) == 0, "total samples must be power of 2"
 
     @property
     def x(self):
@@ -334,14 +350,32 @@ class AbstractFastGP(torch.nn.Module):
         return self.scale * factors.prod(-2)
 
     def _nint(self, n):
-        return int(self.n[0]) if n is None else int(torch.as_tensor(n).reshape(-1)[0])
+        return self._nh if n is None else int(torch.as_tensor(n).reshape(-1)[0])
 
     def get_lam(self, task0=0, task1=0, n=None):
         n = self._nint(n)
-        return self._cached(("lam", n), lambda: self.ft(self._k1(n)))
+
+        def f():
+            if not self._gradmode() and self._lam_fusable(n):
+                return self._lam_fused(n)
+            return self.ft(self._k1(n))
+        return self._cached(("lam", n), f)
+
+    def _lam_fusable(self, n):
+        return (n >= 16 and self.d <= 8 and self._tfs["scale"][1] is _exp and self._tfs["lengthscales"][1] is _exp
+                and self._tfs["noise"][1] is _exp and self._problem_batch() is not None)
+
+    def _lam_fused(self, n):
+        """lambda = ft(k1) by fgp_nll_lam (k1 formed on the fly from the cached parts)."""
+        from .fit_engine import fused_lam
+        pb, G = self._problem_batch()
+        lam = fused_lam(self._FAMILY, self._k1parts(n), self.raw_scale.detach().reshape(-1),
+                        self.raw_lengthscales.detach().reshape(-1, self.raw_lengthscales.shape[-1]),
+                        self.raw_noise.detach().reshape(-1), G)
+        return lam.reshape(tuple(pb) + (n,))
 
     def get_ytilde(self, task=0):
-        n = int(self.n[0])
+        n = self._nh
 
         def f():
             y = self._y[0]
@@ -373,10 +407,19 @@ class AbstractFastGP(torch.nn.Module):
         """K^-1 v = ift(A ft(v)).real (util.py:338-353)."""
         return self.ift(self.ft(v) * self._inv(n)).real
 
+    def _coeffs_now(self):
+        n = self._nh
+        if self._gradmode() or n < 2:
+            return self._solve(self._y[0], n)
+        # graph-free: reuse the cached ytilde = ft(y); real part fused into the inverse transform
+        yt = self.get_ytilde(0) * self._inv(n)
+        if self._FAMILY == ops.LATTICE:
+            return ops.ifftbr_raw(yt, stable=True, real_out=True)
+        return ops.fwht_raw(yt, stable=True)
+
     @property
     def coeffs(self):
-        n = int(self.n[0])
-        return self._cached(("coeffs", n), lambda: self._solve(self._y[0], n))
+        return self._cached(("coeffs", self._nh), self._coeffs_now)
 
     # ------------------------------------------------------------------ fit
     def fit(self, loss_metric="MLL", iterations=5000, lr=None, optimizer=None, stop_crit_improvement_threshold=5e-2,
@@ -414,7 +457,7 @@ class AbstractFastGP(torch.nn.Module):
                                  cv_weights)
 
     def _fused_ok(self):
-        n = int(self.n[0])
+        n = self._nh
         if n < 16 or self.d > 8 or self.adaptive_nugget:
             return False
         if self._tfs["scale"][1] is not _exp or self._tfs["lengthscales"][1] is not _exp or \
@@ -455,7 +498,7 @@ class AbstractFastGP(torch.nn.Module):
 
     def _fit_fused(self, iterations, lr, stop, hists, verbose, indent):
         logtol, wait_max = stop
-        n = int(self.n[0])
+        n = self._nh
         pb_shape, G = self._problem_batch()
         d_out = int(torch.tensor(self.shape_batch).prod())
         parts = self._k1parts(n)
@@ -521,7 +564,7 @@ class AbstractFastGP(torch.nn.Module):
         return data
 
     def _loss_generic(self, loss_metric, masks, cv_weights, d_out):
-        n = int(self.n[0])
+        n = self._nh
         A, logdet = self.get_inv_log_det(n)
         A = A[..., 0, 0, :]
         yt = self.get_ytilde(0)
@@ -630,6 +673,20 @@ class AbstractFastGP(torch.nn.Module):
     def _check_unit(self, x, name="x"):
         assert ((0 <= x) & (x <= 1)).all(), "%s should have all elements in [0,1]" % name
 
+    def _defer_unit(self, x, name="x"):
+        """Enqueue the [0, 1] range check of x (fast_gp_lattice.py:264-265) without synchronising;
+        _raise_deferred() reads all pending flags back once, after the dependent work is enqueued."""
+        flag = ((0 <= x) & (x <= 1)).all()
+        self._pending_checks = getattr(self, "_pending_checks", []) + [(flag, name)]
+
+    def _raise_deferred(self):
+        pend = getattr(self, "_pending_checks", [])
+        self._pending_checks = []
+        if pend:
+            ok = torch.stack([f for f, _ in pend]).cpu()
+            for good, (_, name) in zip(ok.tolist(), pend):
+                assert good, "%s should have all elements in [0,1]" % name
+
     def _task_arg(self, task):
         if task is None:
             task = self.default_task
@@ -657,6 +714,20 @@ class AbstractFastGP(torch.nn.Module):
         return ops.kernel_rows(self._FAMILY, x, z, self._hyp_rows(batch_params), alphas=self._alphas,
                                tbits=self._tbits())
 
+    def _post_var_qf(self, x, n, chunk=16):
+        """sum_k Re(A_k) |ft(K(x_t, .))_k|^2 for every test point (fgp_post_var_qf)."""
+        self._ensure_points(n)
+        z = self._xb[:n].T.contiguous()
+        wa = self._inv(n)
+        wa = (wa.real if wa.is_complex() else wa).contiguous()
+        hyp = self._hyp_rows(False)[0].contiguous()
+        out = torch.empty(x.size(0), dtype=torch.float64, device=self.device)
+        for t0 in range(0, x.size(0), chunk):
+            xs = x[t0:t0 + chunk].contiguous()
+            out[t0:t0 + xs.size(0)] = ops.post_var_quadform(self._FAMILY, xs, z, hyp, wa, alphas=self._alphas,
+                                                            tbits=self._tbits())
+        return out
+
     def _kdiag(self, x):
         """K(x, x) (zero distance parts)."""
         part0 = self._part_at_zero().to(self.device)
@@ -664,7 +735,11 @@ class AbstractFastGP(torch.nn.Module):
 
     def post_mean(self, x, task=None, eval=True):
         """Posterior mean (abstract_gp.py:352-380) via the matrix-free HIP contraction."""
-        coeffs = self.coeffs
+        if eval:
+            with torch.no_grad():
+                coeffs = self.coeffs
+        else:
+            coeffs = self.coeffs
         if eval:
             incoming = torch.is_grad_enabled()
             torch.set_grad_enabled(False)
@@ -672,8 +747,8 @@ class AbstractFastGP(torch.nn.Module):
             assert x.ndim == 2 and x.size(1) == self.d, "x must a torch.Tensor with shape (-1,d)"
             inttask = self._task_arg(task)
             x = x.to(device=self.device, dtype=torch.float64)
-            self._check_unit(x)
-            n = int(self.n[0])
+            self._defer_unit(x)
+            n = self._nh
             if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
                 kmat = self._kernel_torch(x[:, None, :], self._xb[:n][None, :, :])
                 pm = torch.einsum("...i,...i->...", kmat, coeffs[..., None, :])
@@ -684,6 +759,7 @@ class AbstractFastGP(torch.nn.Module):
                 pm = ops.post_mean_matfree(self._FAMILY, x, z, self._hyp_rows(bp), c2, alphas=self._alphas,
                                            tbits=self._tbits())
                 pm = pm.reshape(tuple(coeffs.shape[:-1]) + (x.size(0),))
+            self._raise_deferred()
         finally:
             if eval:
                 torch.set_grad_enabled(incoming)
@@ -699,13 +775,17 @@ class AbstractFastGP(torch.nn.Module):
         try:
             inttask = self._task_arg(task)
             x = x.to(device=self.device, dtype=torch.float64)
-            self._check_unit(x)
+            self._defer_unit(x)
             bp = self._has_batch_params()
-            rows = self._cross_rows(x, n, bp)                      # [Gk, N, n]
-            kmat = rows[0] if not bp else rows.reshape(tuple(self.shape_batch) + rows.shape[1:])
-            t = self._solve(kmat.movedim(-2, 0), n).movedim(0, -2)
-            diag = self._kdiag(x) - (t * kmat).sum(-1)
+            if not self._gradmode() and not bp and n > 4096 and self.d <= 8 and self._lam_fusable(n):
+                diag = self._kdiag(x) - self._post_var_qf(x, n)
+            else:
+                rows = self._cross_rows(x, n, bp)                      # [Gk, N, n]
+                kmat = rows[0] if not bp else rows.reshape(tuple(self.shape_batch) + rows.shape[1:])
+                t = self._solve(kmat.movedim(-2, 0), n).movedim(0, -2)
+                diag = self._kdiag(x) - (t * kmat).sum(-1)
             diag[diag < 0] = 0
+            self._raise_deferred()
         finally:
             if eval:
                 torch.set_grad_enabled(incoming)
@@ -883,8 +963,10 @@ class FastGPLattice(AbstractFastGP):
         return ops.ifftbr(x, stable=True)
 
     def _compute_parts(self, xb, x0, out=None):
-        self._check_unit(xb)
-        return ops.lattice_parts(xb, x0, self._alphas, out=out)
+        self._defer_unit(xb)
+        parts = ops.lattice_parts(xb, x0, self._alphas, out=out)
+        self._raise_deferred()
+        return parts
 
     def _part_at_zero(self):
         return torch.tensor([ops.lattice_coefficient(a) * float(_bern(2 * a, 0.0)) for a in self._alphas],

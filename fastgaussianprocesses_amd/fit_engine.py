@@ -138,3 +138,26 @@ class FusedMLL(object):
 def mll_constant(d_out, n):
     """d_out * n * log(2 pi) (fastgps/abstract_gp.py:235)."""
     return d_out * n * math.log(2 * math.pi)
+
+
+def fused_lam(family, parts, raw_scale, raw_lengthscales, raw_noise, G):
+    """lambda = ft(k1) for G eigen-problems sharing `parts` ([d, n]) via fgp_nll_lam -> [G, n]."""
+    require_device(parts, "fused_lam")
+    d, n = parts.shape
+    m = log2_exact(n)
+    dev = parts.device
+    S, (Sl, Dl), Sn = raw_scale.numel(), raw_lengthscales.shape, raw_noise.numel()
+    raw = torch.cat([raw_scale.reshape(-1), raw_lengthscales.reshape(-1), raw_noise.reshape(-1)]).to(
+        device=dev, dtype=torch.float64).contiguous()
+    cdt = torch.complex128 if family == 0 else torch.float64
+    out = torch.empty((G, n), dtype=cdt, device=dev)
+    work = torch.empty((G, n), dtype=cdt, device=dev) if m > 12 else None
+    parts = parts.contiguous()
+    desc = N.NllDesc(family=family, log2n=m, d=d, G=G, parts=parts.data_ptr(), parts_stride=0,
+                     ysq=out.data_ptr(), ysq_stride=0, raw=raw.data_ptr(),
+                     scale_off=0, scale_pp=int(S == G and G > 1), ls_off=S, ls_pp=int(Sl == G and G > 1),
+                     ls_pd=int(Dl == d), noise_off=S + Sl * Dl, noise_pp=int(Sn == G and G > 1), logdet_weight=1.0,
+                     grad_lam=out.data_ptr(), work=(work.data_ptr() if work is not None else 0),
+                     partials=out.data_ptr())
+    N.call("fgp_nll_lam", desc, N.stream_ptr(dev))
+    return out

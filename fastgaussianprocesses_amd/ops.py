@@ -240,3 +240,19 @@ def kernel_rows(family, xt, z_dn, hyp, alphas=None, tbits=0):
         if sub is not rows:
             rows[:, t0:t1] = sub
     return rows
+
+
+def post_var_quadform(family, xt, z_dn, hyp, wa, alphas=None, tbits=0):
+    """q[t] = sum_k wa[k] |ft(K(xt[t], z))_k|^2 (fgp_post_var_qf); hyp: device [1 + d] (scale, l_1..l_d)."""
+    require_device(xt, "post_var_quadform")
+    Nt, d = xt.shape
+    n = z_dn.shape[1]
+    m = log2_exact(n)
+    cdt = torch.complex128 if family == LATTICE else torch.float64
+    work = torch.empty((Nt, n), dtype=cdt, device=xt.device)
+    partial = torch.empty((Nt, n >> 12), dtype=torch.float64, device=xt.device)
+    out = torch.empty(Nt, dtype=torch.float64, device=xt.device)
+    order, coef = _pred_args(family, alphas, d)
+    N.call("fgp_post_var_qf", family, N.ptr(xt), Nt, N.ptr(z_dn), m, d, int(tbits), order, coef,
+           N.ptr(hyp.to(torch.float64).contiguous()), N.ptr(wa), N.ptr(work), N.ptr(partial), N.ptr(out), _stream(xt))
+    return out

@@ -117,6 +117,9 @@ typedef struct fgp_nll_desc {
 /* Forward: k1 from parts, lambda = ft(k1), ev = sqrt(n) lambda + noise; per-problem partial sums of
  * the norm term sum|ytilde|^2 Re(1/ev), logdet sum log|ev| and dL/dnoise; writes dL/dlambda. */
 int fgp_nll_fwd(const fgp_nll_desc* desc, void* stream);
+/* Eigenvalues only: lambda = ft(k1) (stable) written to desc->grad_lam ([G][n], complex128 lattice /
+ * float64 net); ysq and partials are not used (replaces _LamCaches, fastgps/util.py:95-112). */
+int fgp_nll_lam(const fgp_nll_desc* desc, void* stream);
 /* Backward: g = Re(ft^H(dL/dlambda)), partial sums of dL/draw_scale and dL/draw_lengthscales. */
 int fgp_nll_bwd(const fgp_nll_desc* desc, void* stream);
 
@@ -161,6 +164,15 @@ int fgp_fit_run(const fgp_nll_desc* nll, const fgp_fit_desc* fit, int iter0, int
 int fgp_post_mean(int family, const double* xt, int64_t N, const void* z, int64_t n, int d, int tbits, const int* order,
                   const double* coef, const double* hyp, int Gk, const double* coeffs, int64_t coeff_stride, int B,
                   double* out, int64_t out_stride, double* work, int64_t chunk, void* stream);
+
+/* Posterior-variance quadratic form by Parseval, 13 <= log2n <= 24:
+ *   out[t] = sum_i r_t[i] (K^-1 r_t)[i] = sum_k wa[k] |ft(r_t)[k]|^2,  r_t[i] = K(xt[t], z[:, i])
+ * with wa = Re(1 / ev) (fastgps/abstract_gp.py:408-412 + util.py:338-353 for real kernel rows).
+ * hyp: device [1 + d] (scale, lengthscales).  work: device scratch [N][n] (complex128 lattice,
+ * float64 net); partial: device [N][n / 4096]; out: device [N]. */
+int fgp_post_var_qf(int family, const double* xt, int64_t N, const void* z, int log2n, int d, int tbits,
+                    const int* order, const double* coef, const double* hyp, const double* wa, void* work,
+                    double* partial, double* out, void* stream);
 
 /* Cross-kernel rows rows[g, t, i] = K_g(xt[t], z[:, i]) (same kernel as fgp_post_mean), [Gk][N][n],
  * N <= 65535: the kmat of AbstractGP.post_var / post_cov (fastgps/abstract_gp.py:407-411,452-457). */

@@ -174,3 +174,37 @@ def test_fit_batched_equals_individual_fits(family, m):
         assert torch.equal(a["loss_hist"], b["loss_hist"])
         assert torch.equal(ga.raw_lengthscales, gb.raw_lengthscales)
         assert torch.equal(ga.raw_scale, gb.raw_scale)
+
+
+@pytest.mark.parametrize("family,m", [("lattice", 6), ("lattice", 13), ("lattice", 16), ("net", 12), ("net", 15)])
+def test_fused_paths_equal_autograd_paths(family, m):
+    """Graph-free fused kernels (fgp_nll_lam, fgp_post_var_qf, fused coeffs) agree with the
+    differentiable torch+HIP-transform paths at fp64 precision."""
+    from oracle.fgp_oracle import f_ackley
+    d, n = 3, 2 ** m
+    if family == "lattice":
+        gp = F.FastGPLattice(F.Lattice(d, seed=3), lengthscales=torch.tensor([0.7, 1.3, 2.0]), device=DEV)
+    else:
+        gp = F.FastGPDigitalNetB2(F.DigitalNetB2(d, seed=3), alpha=1, lengthscales=torch.tensor([0.7, 1.3, 2.0]),
+                                  device=DEV)
+    gp.add_y_next(f_ackley(gp.get_x_next(n)))
+    xt = torch.rand((9, d), generator=torch.Generator().manual_seed(5)).to(DEV)
+    with torch.no_grad():
+        lam_f = gp.get_lam(0, 0).clone()
+        coeffs_f = gp.coeffs.clone()
+        pvar_f = gp.post_var(xt)
+    lam_t = gp.get_lam(0, 0).detach()          # grad mode: torch k1 + HIP transform
+    coeffs_t = gp.coeffs.detach()
+    assert rel_err(lam_f, lam_t.cpu().numpy()) <= 1e-13
+    # coeffs = K^-1 y with cond(K) ~ n / noise ~ 1e12: a 1e-15 relative change of lambda (different
+    # summation order of k1) moves coeffs by up to ~1e-6 relative; post_mean is insensitive to it
+    assert rel_err(coeffs_f, coeffs_t.cpu().numpy()) <= 1e-5
+    pm_f = gp.post_mean(xt)
+    kmat = gp._kernel_torch(xt[:, None, :], gp._xb[:n][None, :, :]).detach()
+    assert rel_err(pm_f, (kmat * coeffs_t).sum(-1).cpu().numpy()) <= 1e-8
+    rows = gp._cross_rows(xt, n, False)[0]
+    t = gp._solve(rows, n).detach()
+    pvar_t = gp._kdiag(xt).detach() - (t * rows).sum(-1)
+    pvar_t[pvar_t < 0] = 0
+    kxx = float(gp._kdiag(xt).detach().abs().max())
+    assert abs_err(pvar_f, pvar_t.cpu().numpy()) <= 1e-10 * kxx

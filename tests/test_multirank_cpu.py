@@ -1,0 +1,55 @@
+"""N > 1 path of bench.py on CPU with gloo (world_size 2): replica sharding of the shifts and the
+max-over-ranks timing reduction (the only collective; the data path has none)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    seeds = bench.shard_seeds(rank, world, 8)
+    el = bench.max_over_ranks(1.0 + rank, "cpu")
+    gathered = [None] * world
+    dist.all_gather_object(gathered, seeds)
+    q.put((rank, seeds, el, gathered))
+    dist.destroy_process_group()
+
+
+def test_two_rank_sharding_and_timing():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort()
+    all_seeds = sorted(s for _, seeds, _, _ in res for s in seeds)
+    assert all_seeds == list(range(1000, 1016))           # 64 at N=8; here 2 x 8, disjoint, complete
+    assert all(el == 2.0 for _, _, el, _ in res)           # max over ranks
+    assert res[0][3] == res[1][3]
+
+
+def test_single_rank_helpers_without_process_group():
+    import bench
+    assert bench.shard_seeds(0, 1, 8) == list(range(1000, 1008))
+    assert bench.max_over_ranks(3.5, "cpu") == 3.5
