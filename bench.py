@@ -115,31 +115,43 @@ def phase_breakdown(sh, iters, xm, xv):
     return {names[i]: ev[i].elapsed_time(ev[i + 1]) for i in range(5)}
 
 
-def roofline_fit_iteration(F, shifts, iters):
-    """Time the fused fit iterations of all shifts (one batched engine, as in the step) with HIP
-    events on the engine's stream; bytes = SURVEY §8(d) B_iter per GP x shifts."""
+STAGES = ("k_fwd_rows", "k_fwd_cols", "k_bwd_rows")
+
+
+def stage_bytes(n, d, P, parts_array):
+    """Algorithmic HBM bytes of one launch of each fit-iteration kernel over P lattice problems
+    (complex128 intermediate `work`, float64 Y; DESIGN.md 'Kernels'):
+      k_fwd_rows: write work 16n (+ read parts 8nd when not regenerated)
+      k_fwd_cols: read work 16n + read Y 8n + write work 16n
+      k_bwd_rows: read work 16n (+ read parts 8nd)"""
+    pb = 8 * n * d if parts_array else 0
+    return {"k_fwd_rows": (16 * n + pb) * P, "k_fwd_cols": 40 * n * P, "k_bwd_rows": (16 * n + pb) * P}
+
+
+def roofline_fit_kernels(F, shifts, iters):
+    """HIP-event timing (torch's current stream = the stream the kernels are launched on) of every
+    kernel of the batched fit iteration, as launched in the step (same engine, same grid)."""
     for sh in shifts:
         sh.reset()
-    gp = shifts[0].gp
-    n = int(gp.n[0])
-    d = gp.d
-    P = len(shifts)
-    parts = torch.stack([sh.gp._k1parts(n) for sh in shifts])
-    ysq = torch.stack([sh.gp._ysq(*sh.gp._problem_batch())[0] for sh in shifts])
-    eng = F.FusedMLL(gp._FAMILY, parts, ysq, torch.zeros(P), torch.zeros(P, d), torch.full((P,), math.log(1e-8)),
-                     logdet_weight=1.0, mll_const=F.fit_engine.mll_constant(1, n), max_iters=iters + 1,
-                     parts_per_problem=True, per_problem=True)
+    gps = [sh.gp for sh in shifts]
+    n = int(gps[0].n[0])
+    eng = F.batch.batched_engine(gps, iters)
     eng.run(0, 2)
     torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    eng.run(0, iters)
-    e1.record()
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(iters)]
+    for it in range(iters):
+        e = ev[it]
+        e[0].record()
+        for k in range(3):
+            eng.stage(k)
+            e[k + 1].record()
+        eng.step(it)
+        e[4].record()
     torch.cuda.synchronize()
-    t_iter = e0.elapsed_time(e1) / 1e3 / iters
-    # SURVEY §8(d): B_iter = 16 n d + 32 n + 32 n B per GP (lattice, B = 1 output)
-    b_iter = (16 * n * d + 32 * n + 32 * n) * P
-    return t_iter, b_iter
+    us = {name: 1e3 * sum(e[k].elapsed_time(e[k + 1]) for e in ev) / iters for k, name in enumerate(STAGES)}
+    us["k_fit_reduce_step"] = 1e3 * sum(e[3].elapsed_time(e[4]) for e in ev) / iters
+    t_iter = sum(us.values()) / 1e6
+    return n, eng.gen is None, us, t_iter
 
 
 def cpu_baseline(args, n, d):
@@ -232,12 +244,21 @@ def main():
     value = args.shifts * n * world / sec_step
 
     phases = phase_breakdown(shifts[0], args.fit_iters, xm, xv)
-    t_iter, b_iter = roofline_fit_iteration(F, shifts, args.fit_iters)
-    roof = {"bound": "hbm", "kernel": "fit iteration (k_fwd_rows, k_fwd_cols, k_cols<adj>, k_bwd_rows, k_fit_reduce, "
-                                      "k_fit_step)",
-            "achieved": b_iter / t_iter / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": b_iter / t_iter / 1e9 / HBM_PEAK_GBS, "traffic": None,
-            "algorithmic_bytes": b_iter, "avg_us": t_iter * 1e6}
+    n_, parts_array, us, t_iter = roofline_fit_kernels(F, shifts, args.fit_iters)
+    P = len(shifts)
+    sb = stage_bytes(n, d, P, parts_array)
+    dom = max(STAGES, key=lambda k: us[k])
+    ach = sb[dom] / (us[dom] * 1e-6) / 1e9
+    # SURVEY §8(d) reference-dataflow bytes of one fit iteration: 16nd + 32n + 32nB per GP (B = 1)
+    b_iter = (16 * n * d + 32 * n + 32 * n) * P
+    roof = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": ach / HBM_PEAK_GBS, "traffic": None, "algorithmic_bytes": sb[dom], "avg_us": us[dom],
+            "launch": "%d problems x n=2^%d (grid %d workgroups)" % (P, args.log2n, P * n // 4096),
+            "kernels": {k: {"avg_us": us[k], "bytes": sb.get(k),
+                            "GB/s": (sb[k] / (us[k] * 1e-6) / 1e9) if k in sb else None} for k in us},
+            "parts": "array" if parts_array else "regenerated (FGP_PARTS_LATTICE)",
+            "iteration": {"avg_us": t_iter * 1e6, "survey_bytes": b_iter,
+                          "survey_equiv_GB/s": b_iter / t_iter / 1e9}}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, n, d)

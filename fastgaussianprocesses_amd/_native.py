@@ -12,7 +12,10 @@ import torch
 
 _LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
 LIB_PATH = os.path.join(_LIB_DIR, "libfgp_hip.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
+MAX_D = 8
+PARTS_ARRAY = 0
+PARTS_LATTICE = 1
 
 _lock = threading.Lock()
 _lib = None
@@ -38,6 +41,8 @@ class NllDesc(ctypes.Structure):
         ("noise_off", _c_int), ("noise_pp", _c_int),
         ("logdet_weight", _c_dbl),
         ("grad_lam", _c_vp), ("work", _c_vp), ("partials", _c_vp),
+        ("parts_gen", _c_int), ("gen_order", _c_int * 8), ("gen_coef", _c_dbl * 8), ("gen_z", _c_i64 * 8),
+        ("gen_shift", _c_vp), ("gen_shift_stride", _c_i64),
     ]
 
 
@@ -68,6 +73,7 @@ _SIGNATURES = {
     "fgp_nll_fwd": [_P_NLL, _c_vp],
     "fgp_nll_bwd": [_P_NLL, _c_vp],
     "fgp_nll_lam": [_P_NLL, _c_vp],
+    "fgp_nll_stage": [_P_NLL, _c_int, _c_vp],
     "fgp_post_var_qf": [_c_int, _c_vp, _c_i64, _c_vp, _c_int, _c_int, _c_int, _c_pi, _c_pd, _c_vp, _c_vp, _c_vp,
                         _c_vp, _c_vp, _c_vp],
     "fgp_fit_step": [_P_NLL, _P_FIT, _c_int, _c_int, _c_vp],

@@ -12,7 +12,7 @@ import math
 
 import torch
 
-from .fit_engine import FusedMLL, mll_constant
+from .fit_engine import FusedMLL, LatticePartsGen, mll_constant
 
 
 def fit_batched(gps, iterations=5000, lr=None, stop_crit_improvement_threshold=5e-2, stop_crit_wait_iterations=10,
@@ -31,24 +31,9 @@ def fit_batched(gps, iterations=5000, lr=None, stop_crit_improvement_threshold=5
         assert gp.raw_lengthscales.shape == g0.raw_lengthscales.shape
         assert (gp.raw_scale.requires_grad, gp.raw_lengthscales.requires_grad, gp.raw_noise.requires_grad) == \
                (g0.raw_scale.requires_grad, g0.raw_lengthscales.requires_grad, g0.raw_noise.requires_grad)
-    P = len(gps)
-    d = g0.d
+    eng = batched_engine(gps, iterations, lr)
     dev = g0.device
-    parts = torch.empty((P, d, n), dtype=torch.float64, device=dev)
-    for p, gp in enumerate(gps):
-        gp._k1parts(n, out=parts[p])
-    ysq = torch.stack([gp._ysq(*gp._problem_batch())[0] for gp in gps])
-    d_out = int(torch.tensor(g0.shape_batch).prod())
     dl = g0.raw_lengthscales.shape[-1]
-    eng = FusedMLL(g0._FAMILY, parts, ysq,
-                   torch.stack([gp.raw_scale.detach().reshape(-1)[0] for gp in gps]),
-                   torch.stack([gp.raw_lengthscales.detach().reshape(dl) for gp in gps]),
-                   torch.stack([gp.raw_noise.detach().reshape(-1)[0] for gp in gps]),
-                   logdet_weight=float(d_out), mll_const=mll_constant(d_out, n),
-                   requires_grad=(g0.raw_scale.requires_grad, g0.raw_lengthscales.requires_grad,
-                                  g0.raw_noise.requires_grad),
-                   lr=1e-1 if lr is None else lr, max_iters=min(iterations + 1, 64), parts_per_problem=True,
-                   per_problem=True)
     logtol = math.log(1 + stop_crit_improvement_threshold)
     state = [dict(best=math.inf, save=math.inf, waited=0, best_i=0, stop=None, losses=[]) for _ in gps]
     total = iterations + 1
@@ -94,3 +79,36 @@ def fit_batched(gps, iterations=5000, lr=None, stop_crit_improvement_threshold=5
             data["loss_hist"] = torch.tensor([-v for v in s["losses"]])
         out.append(data)
     return out
+
+
+def batched_engine(gps, iterations, lr=None):
+    """The FusedMLL (per_problem mode) over the GPs' stacked problems: Y = |ytilde|^2 rows and raw
+    parameters stacked, the kernel parts regenerated in the kernels for lattice GPs sharing one
+    generating vector (otherwise a stacked [P, d, n] parts array)."""
+    g0 = gps[0]
+    n = int(g0.n[0])
+    P = len(gps)
+    d = g0.d
+    dev = g0.device
+    gens = [gp._parts_gen(n) for gp in gps]
+    gen = None
+    if all(g is not None for g in gens) and all(g.z == gens[0].z for g in gens):
+        # lattice points regenerated in the kernels; only the P shifts (= x[0] rows) are stacked
+        gen = LatticePartsGen(gens[0].z, gens[0].alphas, torch.cat([g.shift for g in gens], 0))
+        parts = None
+    else:
+        parts = torch.empty((P, d, n), dtype=torch.float64, device=dev)
+        for p, gp in enumerate(gps):
+            gp._k1parts(n, out=parts[p])
+    ysq = torch.stack([gp._ysq(*gp._problem_batch())[0] for gp in gps])
+    d_out = int(torch.tensor(g0.shape_batch).prod())
+    dl = g0.raw_lengthscales.shape[-1]
+    return FusedMLL(g0._FAMILY, parts, ysq,
+                    torch.stack([gp.raw_scale.detach().reshape(-1)[0] for gp in gps]),
+                    torch.stack([gp.raw_lengthscales.detach().reshape(dl) for gp in gps]),
+                    torch.stack([gp.raw_noise.detach().reshape(-1)[0] for gp in gps]),
+                    logdet_weight=float(d_out), mll_const=mll_constant(d_out, n),
+                    requires_grad=(g0.raw_scale.requires_grad, g0.raw_lengthscales.requires_grad,
+                                   g0.raw_noise.requires_grad),
+                    lr=1e-1 if lr is None else lr, max_iters=min(iterations + 1, 64), parts_per_problem=True,
+                    per_problem=True, gen=gen)

@@ -18,9 +18,11 @@
 //
 // Launch structure per iteration:
 //   n <= 4096 : k_iter_single  (forward + eigen terms + adjoint + gradient in ONE kernel, in LDS)
-//   n >  4096 : k_fwd_rows (k1 load + row transform + twiddle) -> k_fwd_cols (column transform +
-//               eigen terms) -> k_cols<ADJ> / k_rows (adjoint column pass) -> k_bwd_rows (adjoint
-//               row transform + gradient terms)
+//   n >  4096 : k_fwd_rows (k1 + row transform + twiddle -> work) -> k_fwd_cols (column transform,
+//               eigen terms, adjoint column transform of dL/dlambda, in place in work) -> k_bwd_rows
+//               (twiddle + adjoint row transform + gradient terms).  HBM traffic per iteration:
+//               16n write + (16n + 8n) read + 16n write + 16n read; the parts are read twice (8nd
+//               each) or, with the lattice generator (FGP_PARTS_LATTICE), regenerated in registers.
 //   then k_fit_step (one workgroup: deterministic reduction of the per-block partials, loss
 //   assembly, histories, Rprop update).
 #include <cmath>
@@ -101,6 +103,13 @@ struct Nll {
   void* grad_lam;
   void* work;
   double* partials;
+  // lattice parts generator (FGP_PARTS_LATTICE)
+  int pgen;
+  int gorder[FGP_MAX_D];
+  double gcoef[FGP_MAX_D];
+  unsigned gz[FGP_MAX_D];        // z_j mod n
+  const double* gshift;
+  int64_t gshift_stride;
 };
 
 struct Hyp {
@@ -116,29 +125,86 @@ __device__ __forceinline__ void load_hyp(const Nll& a, int g, Hyp& h) {
   for (int j = 0; j < FGP_MAX_D; ++j) h.ls[j] = (j < a.d) ? exp(a.raw[lb + (a.ls_pd ? j : 0)]) : 0.0;
 }
 
-// k1_i = scale * prod_j (1 + l_j p_ij)   (product in j order, as torch.prod)
-// (loops fully unrolled to FGP_MAX_D with predicates so every per-dimension array stays in registers)
-__device__ __forceinline__ double k1_at(const Nll& a, const Hyp& h, const double* __restrict__ pg, int64_t n, int64_t i) {
-  double p = 1.0;
+// ------------------------------------------------------------------ parts source (array / generated)
+// Per-problem source of the kernel parts: the parts array, or (FGP_PARTS_LATTICE) the lattice point
+// x_0 = shift from which the parts of element i are regenerated with fgp_lattice_parts' arithmetic.
+struct PSrc {
+  const double* pg;
+  double sh[FGP_MAX_D];
+};
+
+__device__ __forceinline__ void psrc_init(const Nll& a, int g, PSrc& s) {
+  s.pg = a.parts + (int64_t)g * a.parts_stride;
 #pragma unroll
   for (int j = 0; j < FGP_MAX_D; ++j)
-    if (j < a.d) p *= 1.0 + h.ls[j] * pg[(int64_t)j * n + i];
-  return h.scale * p;
+    s.sh[j] = (a.pgen && j < a.d) ? a.gshift[(int64_t)g * a.gshift_stride + j] : 0.0;
 }
 
-// k1 at the consecutive elements (i, i+1) from 16-byte loads of each dimension's parts (i even)
-__device__ __forceinline__ double2 k1_pair(const Nll& a, const Hyp& h, const double* __restrict__ pg, int64_t n,
-                                           int64_t i) {
-  double p0 = 1.0, p1 = 1.0;
+// Lattice part of dimension j at the point with bit-reversed index br:
+//   x = ((br z_j mod n) / n + shift) % 1  (the host generator's exact value and rounding, seqs.Lattice),
+//   delta = torch.remainder(x - x_0, 1),  part = coef B_order(delta)  (k_lattice_parts).
+__device__ __forceinline__ double gen_part(const Nll& a, const PSrc& s, int j, unsigned br, unsigned mask,
+                                           double inv_n) {
+  double x = (double)((br * a.gz[j]) & mask) * inv_n;   // exact: (v(i) z_j) % 1
+  x = x + s.sh[j];
+  if (x >= 1.0) x -= 1.0;                               // numpy remainder on [0, 2): exact
+  double dl = x - s.sh[j];
+  if (dl < 0.0) dl += 1.0;                              // torch.remainder on (-1, 1)
+  return a.gcoef[j] * bernoulli(a.gorder[j], dl);
+}
+
+// parts of element i (p[j], zero-padded to FGP_MAX_D)
+__device__ __forceinline__ void parts_one(const Nll& a, const PSrc& s, int64_t n, int64_t i, double* p) {
+  if (a.pgen) {
+    const int m = a.log2n;
+    const unsigned br = brev_bits((unsigned)i, m), mask = (unsigned)(n - 1);
+    const double inv_n = ldexp(1.0, -m);
 #pragma unroll
-  for (int j = 0; j < FGP_MAX_D; ++j) {
-    if (j < a.d) {
-      const double2 pv = *reinterpret_cast<const double2*>(pg + (int64_t)j * n + i);
-      p0 *= 1.0 + h.ls[j] * pv.x;
-      p1 *= 1.0 + h.ls[j] * pv.y;
+    for (int j = 0; j < FGP_MAX_D; ++j) p[j] = (j < a.d) ? gen_part(a, s, j, br, mask, inv_n) : 0.0;
+  } else {
+#pragma unroll
+    for (int j = 0; j < FGP_MAX_D; ++j) p[j] = (j < a.d) ? s.pg[(int64_t)j * n + i] : 0.0;
+  }
+}
+
+// parts of the consecutive elements (i, i+1), i even: 16-byte loads, or generated (brev_m(i + 1) =
+// brev_m(i) + n/2)
+__device__ __forceinline__ void parts_pair(const Nll& a, const PSrc& s, int64_t n, int64_t i, double* p0,
+                                           double* p1) {
+  if (a.pgen) {
+    const int m = a.log2n;
+    const unsigned br = brev_bits((unsigned)i, m), mask = (unsigned)(n - 1);
+    const unsigned br1 = br + (unsigned)(n >> 1);
+    const double inv_n = ldexp(1.0, -m);
+#pragma unroll
+    for (int j = 0; j < FGP_MAX_D; ++j) {
+      p0[j] = (j < a.d) ? gen_part(a, s, j, br, mask, inv_n) : 0.0;
+      p1[j] = (j < a.d) ? gen_part(a, s, j, br1, mask, inv_n) : 0.0;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < FGP_MAX_D; ++j) {
+      double2 pv = make_double2(0.0, 0.0);
+      if (j < a.d) pv = *reinterpret_cast<const double2*>(s.pg + (int64_t)j * n + i);
+      p0[j] = pv.x;
+      p1[j] = pv.y;
     }
   }
-  return make_double2(h.scale * p0, h.scale * p1);
+}
+
+__device__ __forceinline__ double k1_from(const Nll& a, const Hyp& h, const double* p) {
+  double r = 1.0;
+#pragma unroll
+  for (int j = 0; j < FGP_MAX_D; ++j)
+    if (j < a.d) r *= 1.0 + h.ls[j] * p[j];
+  return h.scale * r;
+}
+
+// k1 at the consecutive elements (i, i+1), i even
+__device__ __forceinline__ double2 k1_pair(const Nll& a, const Hyp& h, const PSrc& s, int64_t n, int64_t i) {
+  double p0[FGP_MAX_D], p1[FGP_MAX_D];
+  parts_pair(a, s, n, i, p0, p1);
+  return make_double2(k1_from(a, h, p0), k1_from(a, h, p1));
 }
 
 // gradient terms at element i: acc[0] += g k1, acc[1+j] += g scale l_j p_j prod_{m != j} f_m
@@ -157,29 +223,6 @@ __device__ __forceinline__ void grad_terms_p(const Hyp& h, const double* pj, dou
     acc[1 + j] += gi * (h.scale * h.ls[j] * pj[j] * (pre * suf[j + 1]));
     pre *= f[j];
   }
-}
-
-__device__ __forceinline__ void grad_terms(const Nll& a, const Hyp& h, const double* __restrict__ pg, int64_t n,
-                                           int64_t i, double gi, double* acc) {
-  double pj[FGP_MAX_D];
-#pragma unroll
-  for (int j = 0; j < FGP_MAX_D; ++j) pj[j] = (j < a.d) ? pg[(int64_t)j * n + i] : 0.0;
-  grad_terms_p(h, pj, gi, acc);
-}
-
-// gradient terms at the consecutive elements (i, i+1), 16-byte parts loads (i even)
-__device__ __forceinline__ void grad_terms_pair(const Nll& a, const Hyp& h, const double* __restrict__ pg, int64_t n,
-                                                int64_t i, double g0, double g1, double* acc) {
-  double p0[FGP_MAX_D], p1[FGP_MAX_D];
-#pragma unroll
-  for (int j = 0; j < FGP_MAX_D; ++j) {
-    double2 pv = make_double2(0.0, 0.0);
-    if (j < a.d) pv = *reinterpret_cast<const double2*>(pg + (int64_t)j * n + i);
-    p0[j] = pv.x;
-    p1[j] = pv.y;
-  }
-  grad_terms_p(h, p0, g0, acc);
-  grad_terms_p(h, p1, g1, acc);
 }
 
 // eigenvalue terms for one frequency: returns dL/dlambda, accumulates norm / logdet / dnoise
@@ -233,13 +276,16 @@ __global__ __launch_bounds__(kWG) void k_iter_single(Nll a, const double2* __res
   const int g = live ? gq : a.G - 1;
   Hyp h;
   load_hyp(a, g, h);
-  const double* pg = a.parts + (int64_t)g * a.parts_stride;
+  PSrc src;
+  psrc_init(a, g, src);
   T* s = lds + tr * (L + L / 16);
   // k1 into LDS (each thread its own 16 strided elements of its transform)
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
     const int i = tt + j * TL;
-    s[padi(i)] = real_to_T<T>(k1_at(a, h, pg, L, i));
+    double p[FGP_MAX_D];
+    parts_one(a, src, L, i, p);
+    s[padi(i)] = real_to_T<T>(k1_from(a, h, p));
   }
   __syncthreads();
   center_transform<P, false>(s, tt, 1, red, tw);
@@ -271,7 +317,9 @@ __global__ __launch_bounds__(kWG) void k_iter_single(Nll a, const double2* __res
 #pragma unroll 4
   for (int j = 0; j < 16; ++j) {
     const int i = tt + j * TL;
-    grad_terms(a, h, pg, L, i, re(s[padi(i)]) * inv_rootn, acc);
+    double p[FGP_MAX_D];
+    parts_one(a, src, L, i, p);
+    grad_terms_p(h, p, re(s[padi(i)]) * inv_rootn, acc);
   }
 #pragma unroll
   for (int q = 0; q < 1 + FGP_MAX_D; ++q)
@@ -300,7 +348,8 @@ __global__ __launch_bounds__(kWG) void k_fwd_rows(Nll a, const double2* __restri
   const int tid = threadIdx.x;
   Hyp h;
   load_hyp(a, g, h);
-  const double* pg = a.parts + (int64_t)g * a.parts_stride;
+  PSrc src;
+  psrc_init(a, g, src);
   const int64_t base = (int64_t)row0 * N2;
   // k1 for element pairs (2 tid + 512 kk, +1): 16-byte loads of every dimension's parts
   if constexpr (RPW == 1) {
@@ -308,7 +357,7 @@ __global__ __launch_bounds__(kWG) void k_fwd_rows(Nll a, const double2* __restri
     double sum = 0.0;
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) {
-      kv[kk] = k1_pair(a, h, pg, n, base + 2 * tid + 512 * kk);
+      kv[kk] = k1_pair(a, h, src, n, base + 2 * tid + 512 * kk);
       sum += kv[kk].x + kv[kk].y;
     }
     const double mean = block_sum(sum, (double*)red) * (1.0 / N2);
@@ -324,7 +373,7 @@ __global__ __launch_bounds__(kWG) void k_fwd_rows(Nll a, const double2* __restri
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) {
       const int e = 2 * tid + 512 * kk;
-      const double2 kv = k1_pair(a, h, pg, n, base + e);
+      const double2 kv = k1_pair(a, h, src, n, base + e);
       lds[padi(e)] = real_to_T<T>(kv.x);
       lds[padi(e + 1)] = real_to_T<T>(kv.y);
     }
@@ -363,10 +412,15 @@ struct ColLay {
   static constexpr int CS = (PADLEN % 2 == 0) ? PADLEN + 1 : PADLEN;
 };
 
+// Column pass of the forward transform.  EMIT (fgp_nll_lam): write lambda.  Otherwise (the fit):
+// eigen terms -> dL/dlambda kept in LDS -> the adjoint column transform of it, written back in place
+// over the column tile of `work` this workgroup read (k_bwd_rows finishes the adjoint).  Per
+// iteration the forward column output therefore never leaves the workgroup.
 template <int P1, typename T, bool EMIT>
 __global__ __launch_bounds__(kWG) void k_fwd_cols(Nll a, const double2* __restrict__ tw) {
   using Lay = ColLay<P1, T>;
   constexpr int N1 = Lay::N1, C = Lay::C, CS = Lay::CS, TL = N1 / 16;
+  constexpr bool FFT = sizeof(T) == 16;
   __shared__ T lds[kLds];
   __shared__ T part[ColPart<C>::size];
   __shared__ double redd[kWG / 64];
@@ -377,25 +431,25 @@ __global__ __launch_bounds__(kWG) void k_fwd_cols(Nll a, const double2* __restri
   const int blk = (int)(blockIdx.x % tiles);
   const int64_t c0 = (int64_t)blk * C;
   const int tid = threadIdx.x;
-  const T* in = static_cast<const T*>(a.work) + (int64_t)g * n + c0;
+  T* wk = static_cast<T*>(a.work) + (int64_t)g * n + c0;
   const int cl = tid % C, col = tid / TL;
   T v[16];
   T sum = zero_v<T>();
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
-    v[k] = in[(int64_t)((tid + k * kWG) / C) * N2 + cl];
+    v[k] = wk[(int64_t)((tid + k * kWG) / C) * N2 + cl];
     sum += v[k];
   }
   column_partials<C>(sum, part);
-  const T mean_l = column_total<C>(cl, part) * (1.0 / N1);
-  const T mean_t = column_total<C>(col, part) * (1.0 / N1);
+  T mean_l = column_total<C>(cl, part) * (1.0 / N1);
+  T mean_t = column_total<C>(col, part) * (1.0 / N1);
 #pragma unroll
   for (int k = 0; k < 16; ++k) lds[cl * CS + padi((tid + k * kWG) / C)] = v[k] - mean_l;
   __syncthreads();
   transform_add_mean<P1, false>(lds + col * CS, tid % TL, mean_t, tw);
   const double rootn = sqrt((double)n), inv_rootn = 1.0 / rootn;
-  T* gl = static_cast<T*>(a.grad_lam) + (int64_t)g * n + c0;
   if constexpr (EMIT) {   // lambda = ft(k1) (fgp_nll_lam)
+    T* gl = static_cast<T*>(a.grad_lam) + (int64_t)g * n + c0;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const int e = tid + k * kWG;
@@ -408,13 +462,26 @@ __global__ __launch_bounds__(kWG) void k_fwd_cols(Nll a, const double2* __restri
   load_hyp(a, g, h);
   const double* yg = a.ysq + (int64_t)g * a.ysq_stride + c0;
   double norm = 0.0, logdet = 0.0, dnoise = 0.0;
+  // element e = tid + 256 k lies in column e mod C = cl for every k: the thread's 16 values share a column
+  sum = zero_v<T>();
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
-    const int e = tid + k * kWG;
-    const int c = e % C, r = e / C;
-    const int64_t off = (int64_t)r * N2 + c;
-    const T lam = lds[c * CS + padi(r)] * inv_rootn;
-    gl[off] = eig_terms(lam, rootn, h.noise, yg[off], a.logdet_weight, norm, logdet, dnoise);
+    const int r = (tid + k * kWG) / C;
+    const T lam = lds[cl * CS + padi(r)] * inv_rootn;
+    v[k] = eig_terms(lam, rootn, h.noise, yg[(int64_t)r * N2 + cl], a.logdet_weight, norm, logdet, dnoise);
+    sum += v[k];
+  }
+  column_partials<C>(sum, part);   // (synchronises: every forward value has been read)
+  mean_l = column_total<C>(cl, part) * (1.0 / N1);
+  mean_t = column_total<C>(col, part) * (1.0 / N1);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) lds[cl * CS + padi((tid + k * kWG) / C)] = v[k] - mean_l;
+  __syncthreads();
+  transform_add_mean<P1, FFT>(lds + col * CS, tid % TL, mean_t, tw);   // adjoint (WHT: self-adjoint)
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int r = (tid + k * kWG) / C;
+    wk[(int64_t)r * N2 + cl] = lds[cl * CS + padi(r)];
   }
   norm = block_sum(norm, redd);
   logdet = block_sum(logdet, redd);
@@ -482,7 +549,8 @@ __global__ __launch_bounds__(kWG) void k_bwd_rows(Nll a, const double2* __restri
   }
   Hyp h;
   load_hyp(a, g, h);
-  const double* pg = a.parts + (int64_t)g * a.parts_stride;
+  PSrc src;
+  psrc_init(a, g, src);
   const double inv_rootn = 1.0 / sqrt((double)n);
   double acc[1 + FGP_MAX_D];
 #pragma unroll
@@ -490,7 +558,10 @@ __global__ __launch_bounds__(kWG) void k_bwd_rows(Nll a, const double2* __restri
 #pragma unroll 2
   for (int kk = 0; kk < 8; ++kk) {
     const int e = 2 * tid + 512 * kk;
-    grad_terms_pair(a, h, pg, n, base + e, re(lds[padi(e)]) * inv_rootn, re(lds[padi(e + 1)]) * inv_rootn, acc);
+    double p0[FGP_MAX_D], p1[FGP_MAX_D];
+    parts_pair(a, src, n, base + e, p0, p1);
+    grad_terms_p(h, p0, re(lds[padi(e)]) * inv_rootn, acc);
+    grad_terms_p(h, p1, re(lds[padi(e + 1)]) * inv_rootn, acc);
   }
 #pragma unroll
   for (int q = 0; q < 1 + FGP_MAX_D; ++q) {
@@ -640,8 +711,23 @@ static int to_nll(const fgp_nll_desc* d, Nll& a) {
   if (d->log2n < 4 || d->log2n > kMaxLog2N) return set_error(kErrUnsupported, "fused fit needs 4 <= log2n <= 24");
   if (d->d < 1 || d->d > FGP_MAX_D) return set_error(kErrUnsupported, "d=%d outside [1, %d]", d->d, FGP_MAX_D);
   if (d->G < 1) return set_error(kErrInvalid, "G < 1");
-  if (!d->parts || !d->ysq || !d->raw || !d->grad_lam || !d->partials || (d->log2n > 12 && !d->work))
+  if (!d->ysq || !d->raw || !d->partials || (d->log2n > 12 && !d->work))
     return set_error(kErrInvalid, "null pointer in nll desc");
+  if (d->parts_gen == FGP_PARTS_ARRAY) {
+    if (!d->parts) return set_error(kErrInvalid, "null parts in nll desc");
+  } else if (d->parts_gen == FGP_PARTS_LATTICE) {
+    if (d->family != FGP_FAMILY_LATTICE) return set_error(kErrInvalid, "lattice parts generator needs the lattice family");
+    if (!d->gen_shift) return set_error(kErrInvalid, "null gen_shift in nll desc");
+    for (int j = 0; j < d->d; ++j) {
+      const int o = d->gen_order[j];
+      if (o < 2 || o > 8 || (o & 1)) return set_error(kErrUnsupported, "Bernoulli order %d unsupported", o);
+      if (d->gen_z[j] <= 0 || (d->log2n < 53 && d->gen_z[j] >= ((int64_t)1 << (53 - d->log2n))))
+        return set_error(kErrUnsupported, "generating vector entry %lld outside (0, 2^(53-log2n))",
+                         (long long)d->gen_z[j]);
+    }
+  } else {
+    return set_error(kErrInvalid, "bad parts_gen %d", d->parts_gen);
+  }
   a.log2n = d->log2n;
   a.d = d->d;
   a.G = d->G;
@@ -663,6 +749,16 @@ static int to_nll(const fgp_nll_desc* d, Nll& a) {
   a.grad_lam = d->grad_lam;
   a.work = d->work;
   a.partials = d->partials;
+  a.pgen = d->parts_gen == FGP_PARTS_LATTICE;
+  const uint64_t zmask = ((uint64_t)1 << d->log2n) - 1;
+  for (int j = 0; j < FGP_MAX_D; ++j) {
+    const bool on = a.pgen && j < d->d;
+    a.gorder[j] = on ? d->gen_order[j] : 0;
+    a.gcoef[j] = on ? d->gen_coef[j] : 0.0;
+    a.gz[j] = on ? (unsigned)((uint64_t)d->gen_z[j] & zmask) : 0u;
+  }
+  a.gshift = d->gen_shift;
+  a.gshift_stride = d->gen_shift_stride;
   return kOk;
 }
 
@@ -684,8 +780,8 @@ static int launch_iter_single(const Nll& a, const Tables* tb, hipStream_t st, bo
 }
 
 template <typename T>
-static int launch_fwd2(const Nll& a, const Tables* tb, hipStream_t st, bool emit) {
-  const int m = a.log2n, m2 = split_m2(m), m1 = m - m2;
+static int launch_rows_fwd(const Nll& a, const Tables* tb, hipStream_t st) {
+  const int m = a.log2n, m2 = split_m2(m);
   const unsigned grid = (unsigned)((int64_t)a.G << (m - kTileLog));
   switch (m2) {
 #define FGP_C(PP) case PP: k_fwd_rows<PP, T><<<grid, kWG, 0, st>>>(a, tb->tw4096, tb->twm[m]); break;
@@ -693,8 +789,13 @@ static int launch_fwd2(const Nll& a, const Tables* tb, hipStream_t st, bool emit
 #undef FGP_C
     default: return set_error(kErrInvalid, "bad m2");
   }
-  int rc = check_launch("k_fwd_rows");
-  if (rc != kOk) return rc;
+  return check_launch("k_fwd_rows");
+}
+
+template <typename T>
+static int launch_cols_fwd(const Nll& a, const Tables* tb, hipStream_t st, bool emit) {
+  const int m = a.log2n, m1 = m - split_m2(m);
+  const unsigned grid = (unsigned)((int64_t)a.G << (m - kTileLog));
   switch (m1) {
 #define FGP_C(PP)                                                           \
   case PP:                                                                  \
@@ -709,13 +810,9 @@ static int launch_fwd2(const Nll& a, const Tables* tb, hipStream_t st, bool emit
 }
 
 template <typename T>
-static int launch_bwd2(const Nll& a, const Tables* tb, hipStream_t st) {
+static int launch_rows_bwd(const Nll& a, const Tables* tb, hipStream_t st) {
   const int m = a.log2n, m2 = split_m2(m);
   const unsigned grid = (unsigned)((int64_t)a.G << (m - kTileLog));
-  // adjoint column pass: grad_lam -> work (generic column kernel; the conj twiddle is applied on load
-  // by k_bwd_rows)
-  int rc = cols_adjoint_launch(sizeof(T) == 16, m, a.grad_lam, a.work, a.G, tb, st);
-  if (rc != kOk) return rc;
   switch (m2) {
 #define FGP_C(PP) case PP: k_bwd_rows<PP, T><<<grid, kWG, 0, st>>>(a, tb->tw4096, tb->twm[m]); break;
     FGP_C(9) FGP_C(10) FGP_C(11) FGP_C(12)
@@ -725,19 +822,31 @@ static int launch_bwd2(const Nll& a, const Tables* tb, hipStream_t st) {
   return check_launch("k_bwd_rows");
 }
 
-static int nll_fwd(const Nll& a, hipStream_t st, bool lattice) {
-  const Tables* tb = get_tables(st);
-  if (!tb) return set_error(kErrHip, "twiddle table initialisation failed");
-  if (a.log2n <= 12) return lattice ? launch_iter_single<double2>(a, tb, st) : launch_iter_single<double>(a, tb, st);
-  return lattice ? launch_fwd2<double2>(a, tb, st, false) : launch_fwd2<double>(a, tb, st, false);
+// one kernel of the pipeline: 0 = forward rows (n <= 4096: the single-kernel iteration), 1 = eigen
+// terms + adjoint columns, 2 = adjoint rows + gradient terms
+template <typename T>
+static int nll_stage_t(const Nll& a, int stage, const Tables* tb, hipStream_t st) {
+  if (a.log2n <= 12) return stage == 0 ? launch_iter_single<T>(a, tb, st) : kOk;
+  switch (stage) {
+    case 0: return launch_rows_fwd<T>(a, tb, st);
+    case 1: return launch_cols_fwd<T>(a, tb, st, false);
+    case 2: return launch_rows_bwd<T>(a, tb, st);
+    default: return set_error(kErrInvalid, "bad stage %d", stage);
+  }
 }
 
-static int nll_bwd(const Nll& a, hipStream_t st, bool lattice) {
-  if (a.log2n <= 12) return kOk;   // fused into the forward kernel
+static int nll_stage(const Nll& a, int stage, hipStream_t st, bool lattice) {
   const Tables* tb = get_tables(st);
   if (!tb) return set_error(kErrHip, "twiddle table initialisation failed");
-  return lattice ? launch_bwd2<double2>(a, tb, st) : launch_bwd2<double>(a, tb, st);
+  return lattice ? nll_stage_t<double2>(a, stage, tb, st) : nll_stage_t<double>(a, stage, tb, st);
 }
+
+static int nll_fwd(const Nll& a, hipStream_t st, bool lattice) {
+  int rc = nll_stage(a, 0, st, lattice);
+  return rc != kOk ? rc : nll_stage(a, 1, st, lattice);
+}
+
+static int nll_bwd(const Nll& a, hipStream_t st, bool lattice) { return nll_stage(a, 2, st, lattice); }
 
 static int to_fit(const fgp_fit_desc* d, Fit& f) {
   if (!d || !d->raw || !d->rprop_prev || !d->rprop_step || !d->grad_out || !d->loss_hist || !d->raw_hist)
@@ -822,12 +931,25 @@ int fgp_nll_lam(const fgp_nll_desc* desc, void* stream) {
   Nll a;
   int rc = to_nll(desc, a);
   if (rc != kOk) return rc;
+  if (!desc->grad_lam) return set_error(kErrInvalid, "fgp_nll_lam: null grad_lam (the output)");
   hipStream_t st = (hipStream_t)stream;
   const Tables* tb = get_tables(st);
   if (!tb) return set_error(kErrHip, "twiddle table initialisation failed");
   const bool lat = desc->family == FGP_FAMILY_LATTICE;
   if (a.log2n <= 12) return lat ? launch_iter_single<double2>(a, tb, st, true) : launch_iter_single<double>(a, tb, st, true);
-  return lat ? launch_fwd2<double2>(a, tb, st, true) : launch_fwd2<double>(a, tb, st, true);
+  if (lat) {
+    rc = launch_rows_fwd<double2>(a, tb, st);
+    return rc != kOk ? rc : launch_cols_fwd<double2>(a, tb, st, true);
+  }
+  rc = launch_rows_fwd<double>(a, tb, st);
+  return rc != kOk ? rc : launch_cols_fwd<double>(a, tb, st, true);
+}
+
+int fgp_nll_stage(const fgp_nll_desc* desc, int stage, void* stream) {
+  Nll a;
+  int rc = to_nll(desc, a);
+  if (rc != kOk) return rc;
+  return nll_stage(a, stage, (hipStream_t)stream, desc->family == FGP_FAMILY_LATTICE);
 }
 
 int fgp_nll_bwd(const fgp_nll_desc* desc, void* stream) {

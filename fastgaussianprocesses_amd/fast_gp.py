@@ -27,7 +27,7 @@ import torch
 
 from . import ops
 from . import seqs as _seqs
-from .fit_engine import FusedMLL, mll_constant
+from .fit_engine import FusedMLL, LatticePartsGen, mll_constant
 
 
 def _log(x):
@@ -338,6 +338,10 @@ class AbstractFastGP(torch.nn.Module):
             self._parts[n] = out
         return self._parts[n]
 
+    def _parts_gen(self, n):
+        """Parts generator for the fused kernels (None: read the cached parts array)."""
+        return None
+
     def get_k1parts(self, task0=0, task1=0, n=None):
         n = self._nint(n)
         return self._k1parts(n).T[:, None, None, :]
@@ -369,9 +373,10 @@ class AbstractFastGP(torch.nn.Module):
         """lambda = ft(k1) by fgp_nll_lam (k1 formed on the fly from the cached parts)."""
         from .fit_engine import fused_lam
         pb, G = self._problem_batch()
-        lam = fused_lam(self._FAMILY, self._k1parts(n), self.raw_scale.detach().reshape(-1),
+        gen = self._parts_gen(n)
+        lam = fused_lam(self._FAMILY, self._k1parts(n) if gen is None else None, self.raw_scale.detach().reshape(-1),
                         self.raw_lengthscales.detach().reshape(-1, self.raw_lengthscales.shape[-1]),
-                        self.raw_noise.detach().reshape(-1), G)
+                        self.raw_noise.detach().reshape(-1), G, gen=gen, n=n)
         return lam.reshape(tuple(pb) + (n,))
 
     def get_ytilde(self, task=0):
@@ -501,7 +506,8 @@ class AbstractFastGP(torch.nn.Module):
         n = self._nh
         pb_shape, G = self._problem_batch()
         d_out = int(torch.tensor(self.shape_batch).prod())
-        parts = self._k1parts(n)
+        gen = self._parts_gen(n)
+        parts = self._k1parts(n) if gen is None else None
         ls_raw = self.raw_lengthscales.detach()
         ls2 = ls_raw.reshape(-1, ls_raw.shape[-1])
         eng = FusedMLL(self._FAMILY, parts, self._ysq(pb_shape, G), self.raw_scale.detach().reshape(-1), ls2,
@@ -509,7 +515,7 @@ class AbstractFastGP(torch.nn.Module):
                        mll_const=mll_constant(d_out, n),
                        requires_grad=(self.raw_scale.requires_grad, self.raw_lengthscales.requires_grad,
                                       self.raw_noise.requires_grad),
-                       lr=lr, max_iters=min(iterations + 1, 64))
+                       lr=lr, max_iters=min(iterations + 1, 64), gen=gen)
         self._iters_for_log = iterations
         self._log_header(verbose, indent)
         best, save, waited = math.inf, math.inf, 0
@@ -967,6 +973,21 @@ class FastGPLattice(AbstractFastGP):
         parts = ops.lattice_parts(xb, x0, self._alphas, out=out)
         self._raise_deferred()
         return parts
+
+    def _parts_gen(self, n):
+        """Regenerate the parts in the fused kernels (FGP_PARTS_LATTICE) when the points are this
+        package's natural-order Lattice: bit-identical to the parts array, without its 2 x 8nd bytes of
+        HBM reads per fit iteration.  FGP_PARTS_GEN=0 disables it."""
+        if os.environ.get("FGP_PARTS_GEN", "1") == "0" or not isinstance(self.seq, _seqs.Lattice):
+            return None
+        m = int(n).bit_length() - 1
+        z = [int(v) for v in self.seq.z[:self.d]]
+        if len(z) != self.d or not all(0 < v < 2 ** (53 - m) for v in z):
+            return None
+        if not np.all((self.seq.shift >= 0) & (self.seq.shift < 1)):
+            return None
+        self._ensure_points(1)
+        return LatticePartsGen(z, self._alphas, self._x[0:1])
 
     def _part_at_zero(self):
         return torch.tensor([ops.lattice_coefficient(a) * float(_bern(2 * a, 0.0)) for a in self._alphas],

@@ -14,19 +14,48 @@ import math
 import torch
 
 from . import _native as N
-from .ops import log2_exact, require_device
+from .ops import lattice_coefficient, log2_exact, require_device
 
 # torch.optim.Rprop defaults (etas=(0.5, 1.2), step_sizes=(1e-6, 50))
 RPROP_ETAS = (0.5, 1.2)
 RPROP_STEPS = (1e-6, 50.0)
 
 
+class LatticePartsGen(object):
+    """FGP_PARTS_LATTICE parts source (include/fgp_hip.h): the kernels regenerate the lattice parts of
+    the natural-order points x_i = ((v(i) z) % 1 + shift) % 1 (seqs.Lattice) instead of reading a
+    [d, n] parts array, bit-identically to fgp_lattice_parts on those points.
+
+    z: generating vector [d] (ints); alphas: [d] smoothness; shift: device [S, d] float64 (S = 1 shared
+    or one row per problem) holding x[0] (= the shift) of each problem."""
+
+    def __init__(self, z, alphas, shift):
+        self.z = [int(v) for v in z]
+        self.alphas = [int(a) for a in alphas]
+        self.shift = shift.to(torch.float64).reshape(-1, len(self.z)).contiguous()
+
+    def apply(self, desc, n):
+        d = len(self.z)
+        m = log2_exact(n)
+        for j in range(d):
+            if not (0 < self.z[j] < 2 ** (53 - m)):
+                raise ValueError("generating vector entry outside (0, 2^(53-m))")
+        desc.parts_gen = N.PARTS_LATTICE
+        for j in range(d):
+            desc.gen_order[j] = 2 * self.alphas[j]
+            desc.gen_coef[j] = lattice_coefficient(self.alphas[j])
+            desc.gen_z[j] = self.z[j]
+        desc.gen_shift = self.shift.data_ptr()
+        desc.gen_shift_stride = d if self.shift.shape[0] > 1 else 0
+
+
 class FusedMLL(object):
     def __init__(self, family, parts, ysq, raw_scale, raw_lengthscales, raw_noise, logdet_weight, mll_const,
-                 requires_grad=(True, True, False), lr=0.1, max_iters=1, parts_per_problem=False, per_problem=None):
+                 requires_grad=(True, True, False), lr=0.1, max_iters=1, parts_per_problem=False, per_problem=None,
+                 gen=None):
         """
         family: 0 lattice (FFT) / 1 net (FWHT)
-        parts:  [d, n] shared, or [G, d, n] when parts_per_problem
+        parts:  [d, n] shared, or [G, d, n] when parts_per_problem; None with `gen` (LatticePartsGen)
         ysq:    [G, n]
         per_problem: the G problems are independent GPs with their own loss / Rprop (default: G == 1);
                 otherwise one loss sums over the G problems (per-output hyper-parameters of one GP)
@@ -41,11 +70,14 @@ class FusedMLL(object):
         self.m = log2_exact(n)
         if self.m < 4:
             raise ValueError("fused fit needs n >= 16")
-        d = parts.shape[-2]
+        d = parts.shape[-2] if parts is not None else len(gen.z)
         self.d = int(d)
         if d > 8:
             raise ValueError("fused fit supports d <= 8")
-        self.parts = parts.contiguous()
+        self.gen = gen
+        self.parts = parts.contiguous() if parts is not None else None
+        if gen is not None and gen.shift.shape[0] not in (1, G):
+            raise ValueError("generator shift rows must be 1 or G")
         self.ysq = ysq.contiguous()
         S = raw_scale.numel()
         Sl, Dl = raw_lengthscales.shape
@@ -65,7 +97,6 @@ class FusedMLL(object):
         self.raw = torch.cat([raw_scale.reshape(-1), raw_lengthscales.reshape(-1), raw_noise.reshape(-1)]).to(
             device=self.device, dtype=torch.float64).contiguous()
         cdt = torch.complex128 if self.family == 0 else torch.float64
-        self.grad_lam = torch.empty((G, n), dtype=cdt, device=self.device)
         self.work = torch.empty((G, n), dtype=cdt, device=self.device) if self.m > 12 else None
         nb = max(1, n >> 12)
         self.partials = torch.empty((G * (4 + d) * (nb + 1),), dtype=torch.float64, device=self.device)
@@ -78,11 +109,14 @@ class FusedMLL(object):
         self._init_max_iters = max_iters
         self._nll = N.NllDesc(
             family=self.family, log2n=self.m, d=self.d, G=self.G,
-            parts=self.parts.data_ptr(), parts_stride=(d * n if parts_per_problem else 0),
+            parts=(self.parts.data_ptr() if self.parts is not None else 0),
+            parts_stride=(d * n if parts_per_problem else 0),
             ysq=self.ysq.data_ptr(), ysq_stride=n, raw=self.raw.data_ptr(),
             logdet_weight=float(logdet_weight),
-            grad_lam=self.grad_lam.data_ptr(), work=(self.work.data_ptr() if self.work is not None else 0),
+            grad_lam=0, work=(self.work.data_ptr() if self.work is not None else 0),
             partials=self.partials.data_ptr(), **self.layout)
+        if gen is not None:
+            gen.apply(self._nll, n)
         self.per_problem = bool(G == 1 if per_problem is None else per_problem)
         self.requires_grad = tuple(int(bool(r)) for r in requires_grad)
         self.mll_const = float(mll_const)
@@ -130,6 +164,15 @@ class FusedMLL(object):
         lh = self.loss_hist[slot].sum(0).cpu() if self.per_problem else self.loss_hist[slot, 0].cpu()
         return float(lh[0]), float(lh[1]), float(lh[2]), self.grad.cpu()
 
+    def step(self, slot, update=True):
+        """Enqueue the reduction + Rprop step of history slot `slot` (fgp_fit_step)."""
+        self.ensure_history(slot + 1)
+        N.call("fgp_fit_step", self._nll, self._fit, int(slot), int(bool(update)), self.stream())
+
+    def stage(self, k):
+        """Enqueue one kernel of the fwd/bwd pipeline (fgp_nll_stage; per-kernel timing)."""
+        N.call("fgp_nll_stage", self._nll, int(k), self.stream())
+
     def split_raw(self, raw_vec):
         S, L, Nn = self.sizes
         return raw_vec[..., :S], raw_vec[..., S:S + L], raw_vec[..., S + L:S + L + Nn]
@@ -140,24 +183,32 @@ def mll_constant(d_out, n):
     return d_out * n * math.log(2 * math.pi)
 
 
-def fused_lam(family, parts, raw_scale, raw_lengthscales, raw_noise, G):
-    """lambda = ft(k1) for G eigen-problems sharing `parts` ([d, n]) via fgp_nll_lam -> [G, n]."""
-    require_device(parts, "fused_lam")
-    d, n = parts.shape
+def fused_lam(family, parts, raw_scale, raw_lengthscales, raw_noise, G, gen=None, n=None):
+    """lambda = ft(k1) for G eigen-problems sharing `parts` ([d, n]; or the generator `gen` with size n)
+    via fgp_nll_lam -> [G, n]."""
+    if parts is not None:
+        require_device(parts, "fused_lam")
+        d, n = parts.shape
+        dev = parts.device
+        parts = parts.contiguous()
+    else:
+        require_device(gen.shift, "fused_lam")
+        d, dev = len(gen.z), gen.shift.device
     m = log2_exact(n)
-    dev = parts.device
     S, (Sl, Dl), Sn = raw_scale.numel(), raw_lengthscales.shape, raw_noise.numel()
     raw = torch.cat([raw_scale.reshape(-1), raw_lengthscales.reshape(-1), raw_noise.reshape(-1)]).to(
         device=dev, dtype=torch.float64).contiguous()
     cdt = torch.complex128 if family == 0 else torch.float64
     out = torch.empty((G, n), dtype=cdt, device=dev)
     work = torch.empty((G, n), dtype=cdt, device=dev) if m > 12 else None
-    parts = parts.contiguous()
-    desc = N.NllDesc(family=family, log2n=m, d=d, G=G, parts=parts.data_ptr(), parts_stride=0,
+    desc = N.NllDesc(family=family, log2n=m, d=d, G=G, parts=(parts.data_ptr() if parts is not None else 0),
+                     parts_stride=0,
                      ysq=out.data_ptr(), ysq_stride=0, raw=raw.data_ptr(),
                      scale_off=0, scale_pp=int(S == G and G > 1), ls_off=S, ls_pp=int(Sl == G and G > 1),
                      ls_pd=int(Dl == d), noise_off=S + Sl * Dl, noise_pp=int(Sn == G and G > 1), logdet_weight=1.0,
                      grad_lam=out.data_ptr(), work=(work.data_ptr() if work is not None else 0),
                      partials=out.data_ptr())
+    if gen is not None:
+        gen.apply(desc, n)
     N.call("fgp_nll_lam", desc, N.stream_ptr(dev))
     return out

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define FGP_ABI_VERSION 2
+#define FGP_ABI_VERSION 3
 
 #define FGP_OK 0
 #define FGP_ERR_INVALID (-1)     /* bad argument (shape, stride, null pointer) */
@@ -109,19 +109,42 @@ typedef struct fgp_nll_desc {
   int ls_off, ls_pp, ls_pd;   /* log lengthscale_j = raw[ls_off + (ls_pp ? g : 0) * (ls_pd ? d : 1) + (ls_pd ? j : 0)] */
   int noise_off, noise_pp;    /* log noise of g    = raw[noise_off + (noise_pp ? g : 0)] */
   double logdet_weight;       /* d_out / numel(logdet)  (fastgps/abstract_gp.py:256) */
-  void* grad_lam;             /* workspace [G][n]: dL/dlambda (complex128 lattice, float64 net) */
-  void* work;                 /* workspace [G][n] complex128 (lattice) / float64 (net) */
+  void* grad_lam;             /* output [G][n] of fgp_nll_lam (lambda; complex128 lattice, float64 net);
+                                 unused (may be NULL) by fgp_nll_fwd / fgp_nll_bwd */
+  void* work;                 /* workspace [G][n] complex128 (lattice) / float64 (net), n > 4096 */
   double* partials;           /* workspace [G][4 + d][max(1, n / 4096) + 1] */
+  /* Parts source.  parts_gen = FGP_PARTS_ARRAY: `parts` above.  parts_gen = FGP_PARTS_LATTICE: the
+   * lattice parts are regenerated inside the kernels (no parts array is read) from the natural-order
+   * rank-1 lattice x[i, j] = ((brev_m(i) z_j mod n) / n + shift_j) % 1, i < n, with exactly the
+   * floating-point operations of fgp_lattice_parts applied to those points and x[0] = shift, so the
+   * result is bit-identical to the FGP_PARTS_ARRAY path on the same points.  Requires
+   * 0 < gen_z[j] < 2^(53 - log2n) (the host point generator is then exact) and 0 <= shift < 1. */
+  int parts_gen;
+  int gen_order[FGP_MAX_D];   /* 2 alpha_j in {2, 4, 6, 8} */
+  double gen_coef[FGP_MAX_D]; /* (-1)^(alpha_j+1) (2 pi)^(2 alpha_j) / (2 alpha_j)! */
+  int64_t gen_z[FGP_MAX_D];   /* generating vector */
+  const double* gen_shift;    /* device [G][d] (row stride gen_shift_stride; 0 = shared): x[0] = shift */
+  int64_t gen_shift_stride;
 } fgp_nll_desc;
 
-/* Forward: k1 from parts, lambda = ft(k1), ev = sqrt(n) lambda + noise; per-problem partial sums of
- * the norm term sum|ytilde|^2 Re(1/ev), logdet sum log|ev| and dL/dnoise; writes dL/dlambda. */
+#define FGP_PARTS_ARRAY 0
+#define FGP_PARTS_LATTICE 1
+
+/* Forward: k1 from the parts, lambda = ft(k1), ev = sqrt(n) lambda + noise; per-problem partial sums
+ * of the norm term sum|ytilde|^2 Re(1/ev), logdet sum log|ev| and dL/dnoise.  The eigen-terms kernel
+ * also runs the first (column) pass of the adjoint transform of dL/dlambda in place, so for
+ * n > 4096 `work` holds that intermediate afterwards (consumed by fgp_nll_bwd). */
 int fgp_nll_fwd(const fgp_nll_desc* desc, void* stream);
 /* Eigenvalues only: lambda = ft(k1) (stable) written to desc->grad_lam ([G][n], complex128 lattice /
  * float64 net); ysq and partials are not used (replaces _LamCaches, fastgps/util.py:95-112). */
 int fgp_nll_lam(const fgp_nll_desc* desc, void* stream);
-/* Backward: g = Re(ft^H(dL/dlambda)), partial sums of dL/draw_scale and dL/draw_lengthscales. */
+/* Backward (after fgp_nll_fwd): g = Re(ft^H(dL/dlambda)), partial sums of dL/draw_scale and
+ * dL/draw_lengthscales. */
 int fgp_nll_bwd(const fgp_nll_desc* desc, void* stream);
+/* One kernel of the fwd/bwd pipeline, for per-kernel timing (bench.py): stage 0 = forward row pass
+ * (n <= 4096: the whole single-kernel iteration), 1 = column pass (eigen terms + adjoint columns),
+ * 2 = adjoint row pass + gradient terms.  Stages 1-2 are no-ops for n <= 4096. */
+int fgp_nll_stage(const fgp_nll_desc* desc, int stage, void* stream);
 
 /* Rprop state and histories for the device-side fit loop. */
 typedef struct fgp_fit_desc {

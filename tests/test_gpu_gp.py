@@ -208,3 +208,56 @@ def test_fused_paths_equal_autograd_paths(family, m):
     pvar_t[pvar_t < 0] = 0
     kxx = float(gp._kdiag(xt).detach().abs().max())
     assert abs_err(pvar_f, pvar_t.cpu().numpy()) <= 1e-10 * kxx
+
+
+@pytest.mark.parametrize("m,d,alpha", [(6, 2, 1), (12, 3, 2), (14, 5, 2), (17, 4, 3), (20, 5, 2)])
+def test_lattice_parts_generator_bit_identical(monkeypatch, m, d, alpha):
+    """FGP_PARTS_LATTICE (parts regenerated inside the fused kernels) reproduces the parts-array path
+    bit for bit: same eigenvalues, same fit trajectory, same fitted parameters."""
+    from oracle.fgp_oracle import f_ackley
+    n = 2 ** m
+
+    def make():
+        gp = F.FastGPLattice(F.Lattice(d, seed=11), alpha=alpha, device=DEV)
+        gp.add_y_next(f_ackley(gp.get_x_next(n)))
+        return gp
+
+    res = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("FGP_PARTS_GEN", mode)
+        gp = make()
+        assert (gp._parts_gen(n) is not None) == (mode == "1")
+        with torch.no_grad():
+            lam = gp.get_lam().clone()      # graph-free: fgp_nll_lam
+        data = gp.fit(iterations=12, verbose=0, store_loss_hist=True, stop_crit_wait_iterations=20)
+        res[mode] = (lam, data["loss_hist"], gp.raw_lengthscales.detach().clone(), gp.raw_scale.detach().clone())
+    for a, b in zip(res["1"], res["0"]):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("family,m", [("lattice", 10), ("lattice", 16), ("net", 15)])
+def test_stage_launches_equal_fit_run(family, m):
+    """fgp_nll_stage 0/1/2 + fgp_fit_step (the per-kernel timing path of bench.py) is the same
+    computation as fgp_fit_run."""
+    from oracle.fgp_oracle import f_ackley
+    d, n = 3, 2 ** m
+
+    def make(seed):
+        if family == "lattice":
+            gp = F.FastGPLattice(F.Lattice(d, seed=seed), device=DEV)
+        else:
+            gp = F.FastGPDigitalNetB2(F.DigitalNetB2(d, seed=seed), alpha=1, device=DEV)
+        gp.add_y_next(f_ackley(gp.get_x_next(n)))
+        return gp
+
+    gps = [make(s) for s in range(2)]
+    e1 = F.batch.batched_engine(gps, 8)
+    e1.run(0, 6)
+    e2 = F.batch.batched_engine(gps, 8)
+    for it in range(6):
+        for k in range(3):
+            e2.stage(k)
+        e2.step(it)
+    torch.cuda.synchronize()
+    assert torch.equal(e1.loss_hist[:6], e2.loss_hist[:6])
+    assert torch.equal(e1.raw, e2.raw)

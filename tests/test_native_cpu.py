@@ -42,11 +42,28 @@ def test_abi_version_and_error_reporting():
     assert rc == -1
 
 
-def test_struct_layouts_match_header():
-    # fgp_nll_desc: 4 ints, ptr, i64, ptr, i64, ptr, 7 ints, double, 3 ptrs
-    assert ctypes.sizeof(N.NllDesc) == 120
-    assert N.NllDesc.logdet_weight.offset == 88
-    assert ctypes.sizeof(N.FitDesc) == 120
+def test_struct_layouts_match_header(tmp_path):
+    """Compile a probe against include/fgp_hip.h with gcc and compare sizeof/offsetof of every field
+    with the ctypes mirrors in _native.py."""
+    import shutil
+    import subprocess
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "fgp_hip.h"', "int main(void) {"]
+    expect = []
+    for cname, cls in (("fgp_nll_desc", N.NllDesc), ("fgp_fit_desc", N.FitDesc)):
+        lines.append('printf("%%zu\\n", sizeof(%s));' % cname)
+        expect.append(ctypes.sizeof(cls))
+        for fname, _ in cls._fields_:
+            lines.append('printf("%%zu\\n", offsetof(%s, %s));' % (cname, fname))
+            expect.append(getattr(cls, fname).offset)
+    lines.append("return 0; }")
+    src = tmp_path / "probe.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "probe"
+    subprocess.check_call(["gcc", "-std=c99", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
+    got = [int(v) for v in subprocess.check_output([str(exe)]).split()]
+    assert got == expect
 
 
 def test_ops_refuse_cpu_tensors():
