@@ -26,6 +26,7 @@
 //   then k_fit_step (one workgroup: deterministic reduction of the per-block partials, loss
 //   assembly, histories, Rprop update).
 #include <cmath>
+#include <type_traits>
 
 #include "fgp_common.h"
 #include "fgp_runtime.h"
@@ -58,6 +59,11 @@ __device__ __forceinline__ double bernoulli(int order, double x) {
              1.0 / 30.0;
     default: return __builtin_nan("");
   }
+}
+
+template <int ORD>
+__device__ __forceinline__ double bernoulli_t(double x) {
+  return bernoulli(ORD, x);   // constant-folded switch: the same expressions as the runtime form
 }
 
 // Order-1 Walsh part for an XOR distance (fast_gp_digital_net_b2.py:297-298).
@@ -103,8 +109,8 @@ struct Nll {
   void* grad_lam;
   void* work;
   double* partials;
-  // lattice parts generator (FGP_PARTS_LATTICE)
-  int pgen;
+  // lattice parts generator (FGP_PARTS_LATTICE); pg = its Bernoulli order (0: parts array)
+  int pgen, pg;
   int gorder[FGP_MAX_D];
   double gcoef[FGP_MAX_D];
   unsigned gz[FGP_MAX_D];        // z_j mod n
@@ -137,12 +143,13 @@ __device__ __forceinline__ void psrc_init(const Nll& a, int g, PSrc& s) {
   s.pg = a.parts + (int64_t)g * a.parts_stride;
 #pragma unroll
   for (int j = 0; j < FGP_MAX_D; ++j)
-    s.sh[j] = (a.pgen && j < a.d) ? a.gshift[(int64_t)g * a.gshift_stride + j] : 0.0;
+    s.sh[j] = (a.pgen && j < a.d) ? a.gshift[(int64_t)g * a.gshift_stride + j] : 0.0;   // (x_0 = shift)
 }
 
 // Lattice part of dimension j at the point with bit-reversed index br:
 //   x = ((br z_j mod n) / n + shift) % 1  (the host generator's exact value and rounding, seqs.Lattice),
-//   delta = torch.remainder(x - x_0, 1),  part = coef B_order(delta)  (k_lattice_parts).
+//   delta = torch.remainder(x - x_0, 1),  part = coef B_ORD(delta)  (k_lattice_parts).
+template <int ORD>
 __device__ __forceinline__ double gen_part(const Nll& a, const PSrc& s, int j, unsigned br, unsigned mask,
                                            double inv_n) {
   double x = (double)((br * a.gz[j]) & mask) * inv_n;   // exact: (v(i) z_j) % 1
@@ -150,17 +157,20 @@ __device__ __forceinline__ double gen_part(const Nll& a, const PSrc& s, int j, u
   if (x >= 1.0) x -= 1.0;                               // numpy remainder on [0, 2): exact
   double dl = x - s.sh[j];
   if (dl < 0.0) dl += 1.0;                              // torch.remainder on (-1, 1)
-  return a.gcoef[j] * bernoulli(a.gorder[j], dl);
+  return a.gcoef[j] * bernoulli_t<ORD>(dl);
 }
 
+// Parts source as a compile-time choice: PG = 0 reads the parts array, PG = 2/4/6/8 regenerates the
+// lattice parts with Bernoulli order PG (FGP_PARTS_LATTICE, one order for every dimension).
 // parts of element i (p[j], zero-padded to FGP_MAX_D)
+template <int PG>
 __device__ __forceinline__ void parts_one(const Nll& a, const PSrc& s, int64_t n, int64_t i, double* p) {
-  if (a.pgen) {
+  if constexpr (PG != 0) {
     const int m = a.log2n;
     const unsigned br = brev_bits((unsigned)i, m), mask = (unsigned)(n - 1);
     const double inv_n = ldexp(1.0, -m);
 #pragma unroll
-    for (int j = 0; j < FGP_MAX_D; ++j) p[j] = (j < a.d) ? gen_part(a, s, j, br, mask, inv_n) : 0.0;
+    for (int j = 0; j < FGP_MAX_D; ++j) p[j] = (j < a.d) ? gen_part<PG>(a, s, j, br, mask, inv_n) : 0.0;
   } else {
 #pragma unroll
     for (int j = 0; j < FGP_MAX_D; ++j) p[j] = (j < a.d) ? s.pg[(int64_t)j * n + i] : 0.0;
@@ -169,17 +179,18 @@ __device__ __forceinline__ void parts_one(const Nll& a, const PSrc& s, int64_t n
 
 // parts of the consecutive elements (i, i+1), i even: 16-byte loads, or generated (brev_m(i + 1) =
 // brev_m(i) + n/2)
+template <int PG>
 __device__ __forceinline__ void parts_pair(const Nll& a, const PSrc& s, int64_t n, int64_t i, double* p0,
                                            double* p1) {
-  if (a.pgen) {
+  if constexpr (PG != 0) {
     const int m = a.log2n;
     const unsigned br = brev_bits((unsigned)i, m), mask = (unsigned)(n - 1);
     const unsigned br1 = br + (unsigned)(n >> 1);
     const double inv_n = ldexp(1.0, -m);
 #pragma unroll
     for (int j = 0; j < FGP_MAX_D; ++j) {
-      p0[j] = (j < a.d) ? gen_part(a, s, j, br, mask, inv_n) : 0.0;
-      p1[j] = (j < a.d) ? gen_part(a, s, j, br1, mask, inv_n) : 0.0;
+      p0[j] = (j < a.d) ? gen_part<PG>(a, s, j, br, mask, inv_n) : 0.0;
+      p1[j] = (j < a.d) ? gen_part<PG>(a, s, j, br1, mask, inv_n) : 0.0;
     }
   } else {
 #pragma unroll
@@ -201,10 +212,24 @@ __device__ __forceinline__ double k1_from(const Nll& a, const Hyp& h, const doub
 }
 
 // k1 at the consecutive elements (i, i+1), i even
+template <int PG>
 __device__ __forceinline__ double2 k1_pair(const Nll& a, const Hyp& h, const PSrc& s, int64_t n, int64_t i) {
-  double p0[FGP_MAX_D], p1[FGP_MAX_D];
-  parts_pair(a, s, n, i, p0, p1);
-  return make_double2(k1_from(a, h, p0), k1_from(a, h, p1));
+  if constexpr (PG == 0) {   // product accumulated as each dimension's 16-byte load arrives
+    double r0 = 1.0, r1 = 1.0;
+#pragma unroll
+    for (int j = 0; j < FGP_MAX_D; ++j) {
+      if (j < a.d) {
+        const double2 pv = *reinterpret_cast<const double2*>(s.pg + (int64_t)j * n + i);
+        r0 *= 1.0 + h.ls[j] * pv.x;
+        r1 *= 1.0 + h.ls[j] * pv.y;
+      }
+    }
+    return make_double2(h.scale * r0, h.scale * r1);
+  } else {
+    double p0[FGP_MAX_D], p1[FGP_MAX_D];
+    parts_pair<PG>(a, s, n, i, p0, p1);
+    return make_double2(k1_from(a, h, p0), k1_from(a, h, p1));
+  }
 }
 
 // gradient terms at element i: acc[0] += g k1, acc[1+j] += g scale l_j p_j prod_{m != j} f_m
@@ -263,7 +288,7 @@ __device__ __forceinline__ double* part_ptr(const Nll& a, int g, int q, int blk)
 }
 
 // ---------------------------------------------------------------- n <= 4096: one kernel
-template <int P, typename T, bool EMIT>
+template <int P, typename T, bool EMIT, int PG>
 __global__ __launch_bounds__(kWG) void k_iter_single(Nll a, const double2* __restrict__ tw) {
   constexpr int L = 1 << P, TL = L / 16, TPW = kTile / L;
   __shared__ T lds[kTile + kTile / 16];
@@ -284,7 +309,7 @@ __global__ __launch_bounds__(kWG) void k_iter_single(Nll a, const double2* __res
   for (int j = 0; j < 16; ++j) {
     const int i = tt + j * TL;
     double p[FGP_MAX_D];
-    parts_one(a, src, L, i, p);
+    parts_one<PG>(a, src, L, i, p);
     s[padi(i)] = real_to_T<T>(k1_from(a, h, p));
   }
   __syncthreads();
@@ -300,7 +325,7 @@ __global__ __launch_bounds__(kWG) void k_iter_single(Nll a, const double2* __res
   }
   const double* yg = a.ysq + (int64_t)g * a.ysq_stride;
   double norm = 0.0, logdet = 0.0, dnoise = 0.0;
-#pragma unroll
+#pragma unroll 4
   for (int j = 0; j < 16; ++j) {
     const int k = tt + j * TL;
     const T lam = s[padi(k)] * inv_rootn;
@@ -318,7 +343,7 @@ __global__ __launch_bounds__(kWG) void k_iter_single(Nll a, const double2* __res
   for (int j = 0; j < 16; ++j) {
     const int i = tt + j * TL;
     double p[FGP_MAX_D];
-    parts_one(a, src, L, i, p);
+    parts_one<PG>(a, src, L, i, p);
     grad_terms_p(h, p, re(s[padi(i)]) * inv_rootn, acc);
   }
 #pragma unroll
@@ -335,7 +360,7 @@ __global__ __launch_bounds__(kWG) void k_iter_single(Nll a, const double2* __res
 }
 
 // ---------------------------------------------------------------- n > 4096: forward row pass
-template <int P2, typename T>
+template <int P2, typename T, int PG>
 __global__ __launch_bounds__(kWG) void k_fwd_rows(Nll a, const double2* __restrict__ tw, const double2* __restrict__ twm) {
   constexpr int N2 = 1 << P2, TL = N2 / 16, RPW = kTile / N2;
   __shared__ T lds[kTile + kTile / 16];
@@ -351,13 +376,13 @@ __global__ __launch_bounds__(kWG) void k_fwd_rows(Nll a, const double2* __restri
   PSrc src;
   psrc_init(a, g, src);
   const int64_t base = (int64_t)row0 * N2;
-  // k1 for element pairs (2 tid + 512 kk, +1): 16-byte loads of every dimension's parts
-  if constexpr (RPW == 1) {
-    double2 kv[8];
+  // k1 for element pairs (2 tid + 512 kk, +1): 16-byte loads of every dimension's parts, or generated
+  if constexpr (RPW == 1 && PG == 0) {
+    double2 kv[8];   // all loads in flight first
     double sum = 0.0;
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) {
-      kv[kk] = k1_pair(a, h, src, n, base + 2 * tid + 512 * kk);
+      kv[kk] = k1_pair<PG>(a, h, src, n, base + 2 * tid + 512 * kk);
       sum += kv[kk].x + kv[kk].y;
     }
     const double mean = block_sum(sum, (double*)red) * (1.0 / N2);
@@ -369,11 +394,32 @@ __global__ __launch_bounds__(kWG) void k_fwd_rows(Nll a, const double2* __restri
     }
     __syncthreads();
     transform_add_mean<P2, false>(lds, tid, real_to_T<T>(mean), tw);
+  } else if constexpr (RPW == 1) {
+    // generated parts: pure ALU, written straight to the thread's own LDS slots (bounded registers),
+    // centred in a second sweep over the same slots once the block mean is known
+    double sum = 0.0;
+#pragma unroll 2
+    for (int kk = 0; kk < 8; ++kk) {
+      const int e = 2 * tid + 512 * kk;
+      const double2 kv = k1_pair<PG>(a, h, src, n, base + e);
+      sum += kv.x + kv.y;
+      lds[padi(e)] = real_to_T<T>(kv.x);
+      lds[padi(e + 1)] = real_to_T<T>(kv.y);
+    }
+    const double mean = block_sum(sum, (double*)red) * (1.0 / N2);
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      const int e = 2 * tid + 512 * kk;
+      lds[padi(e)] -= real_to_T<T>(mean);
+      lds[padi(e + 1)] -= real_to_T<T>(mean);
+    }
+    __syncthreads();
+    transform_add_mean<P2, false>(lds, tid, real_to_T<T>(mean), tw);
   } else {
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) {
       const int e = 2 * tid + 512 * kk;
-      const double2 kv = k1_pair(a, h, src, n, base + e);
+      const double2 kv = k1_pair<PG>(a, h, src, n, base + e);
       lds[padi(e)] = real_to_T<T>(kv.x);
       lds[padi(e + 1)] = real_to_T<T>(kv.y);
     }
@@ -462,20 +508,36 @@ __global__ __launch_bounds__(kWG) void k_fwd_cols(Nll a, const double2* __restri
   load_hyp(a, g, h);
   const double* yg = a.ysq + (int64_t)g * a.ysq_stride + c0;
   double norm = 0.0, logdet = 0.0, dnoise = 0.0;
-  // element e = tid + 256 k lies in column e mod C = cl for every k: the thread's 16 values share a column
+  // element e = tid + 256 k lies in column e mod C = cl for every k: the thread's 16 values share a
+  // column.  dL/dlambda overwrites lambda in the thread's own LDS slots, then a second sweep centres
+  // them by their column mean.
+  // Y is read in groups of 4 with the next group's loads in flight (software pipelined); a fully
+  // unrolled 16-wide divide/log sequence would spill past the 2-waves/SIMD register budget.
   sum = zero_v<T>();
+  double y4[4], yn[4];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const int r = (tid + k * kWG) / C;
-    const T lam = lds[cl * CS + padi(r)] * inv_rootn;
-    v[k] = eig_terms(lam, rootn, h.noise, yg[(int64_t)r * N2 + cl], a.logdet_weight, norm, logdet, dnoise);
-    sum += v[k];
+  for (int j = 0; j < 4; ++j) y4[j] = yg[(int64_t)((tid + j * kWG) / C) * N2 + cl];
+#pragma unroll 1
+  for (int k0 = 0; k0 < 16; k0 += 4) {
+    if (k0 + 4 < 16) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) yn[j] = yg[(int64_t)((tid + (k0 + 4 + j) * kWG) / C) * N2 + cl];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      T* slot = lds + cl * CS + padi((tid + (k0 + j) * kWG) / C);
+      const T gv = eig_terms(*slot * inv_rootn, rootn, h.noise, y4[j], a.logdet_weight, norm, logdet, dnoise);
+      *slot = gv;
+      sum += gv;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) y4[j] = yn[j];
   }
-  column_partials<C>(sum, part);   // (synchronises: every forward value has been read)
+  column_partials<C>(sum, part);
   mean_l = column_total<C>(cl, part) * (1.0 / N1);
   mean_t = column_total<C>(col, part) * (1.0 / N1);
 #pragma unroll
-  for (int k = 0; k < 16; ++k) lds[cl * CS + padi((tid + k * kWG) / C)] = v[k] - mean_l;
+  for (int k = 0; k < 16; ++k) lds[cl * CS + padi((tid + k * kWG) / C)] -= mean_l;
   __syncthreads();
   transform_add_mean<P1, FFT>(lds + col * CS, tid % TL, mean_t, tw);   // adjoint (WHT: self-adjoint)
 #pragma unroll
@@ -494,7 +556,7 @@ __global__ __launch_bounds__(kWG) void k_fwd_cols(Nll a, const double2* __restri
 }
 
 // ---------------------------------------------------------------- n > 4096: adjoint row pass + gradient terms
-template <int P2, typename T>
+template <int P2, typename T, int PG>
 __global__ __launch_bounds__(kWG) void k_bwd_rows(Nll a, const double2* __restrict__ tw, const double2* __restrict__ twm) {
   constexpr int N2 = 1 << P2, TL = N2 / 16, RPW = kTile / N2;
   constexpr bool FFT = sizeof(T) == 16;   // FFT: adjoint network + conj twiddle; WHT: self-adjoint
@@ -559,7 +621,7 @@ __global__ __launch_bounds__(kWG) void k_bwd_rows(Nll a, const double2* __restri
   for (int kk = 0; kk < 8; ++kk) {
     const int e = 2 * tid + 512 * kk;
     double p0[FGP_MAX_D], p1[FGP_MAX_D];
-    parts_pair(a, src, n, base + e, p0, p1);
+    parts_pair<PG>(a, src, n, base + e, p0, p1);
     grad_terms_p(h, p0, re(lds[padi(e)]) * inv_rootn, acc);
     grad_terms_p(h, p1, re(lds[padi(e + 1)]) * inv_rootn, acc);
   }
@@ -721,6 +783,8 @@ static int to_nll(const fgp_nll_desc* d, Nll& a) {
     for (int j = 0; j < d->d; ++j) {
       const int o = d->gen_order[j];
       if (o < 2 || o > 8 || (o & 1)) return set_error(kErrUnsupported, "Bernoulli order %d unsupported", o);
+      if (o != d->gen_order[0])
+        return set_error(kErrUnsupported, "lattice parts generator needs one Bernoulli order for every dimension");
       if (d->gen_z[j] <= 0 || (d->log2n < 53 && d->gen_z[j] >= ((int64_t)1 << (53 - d->log2n))))
         return set_error(kErrUnsupported, "generating vector entry %lld outside (0, 2^(53-log2n))",
                          (long long)d->gen_z[j]);
@@ -750,6 +814,7 @@ static int to_nll(const fgp_nll_desc* d, Nll& a) {
   a.work = d->work;
   a.partials = d->partials;
   a.pgen = d->parts_gen == FGP_PARTS_LATTICE;
+  a.pg = a.pgen ? d->gen_order[0] : 0;
   const uint64_t zmask = ((uint64_t)1 << d->log2n) - 1;
   for (int j = 0; j < FGP_MAX_D; ++j) {
     const bool on = a.pgen && j < d->d;
@@ -762,34 +827,56 @@ static int to_nll(const fgp_nll_desc* d, Nll& a) {
   return kOk;
 }
 
+// Calls fn(std::integral_constant<int, PG>) with the parts source of `a` as a compile-time value
+// (generated lattice parts exist only for the complex / lattice instantiations).
+template <typename T, typename Fn>
+static int with_pg(const Nll& a, Fn&& fn) {
+  if constexpr (sizeof(T) == 16) {
+    switch (a.pg) {
+      case 2: return fn(std::integral_constant<int, 2>{});
+      case 4: return fn(std::integral_constant<int, 4>{});
+      case 6: return fn(std::integral_constant<int, 6>{});
+      case 8: return fn(std::integral_constant<int, 8>{});
+      default: break;
+    }
+  }
+  return fn(std::integral_constant<int, 0>{});
+}
+
 template <typename T>
 static int launch_iter_single(const Nll& a, const Tables* tb, hipStream_t st, bool emit = false) {
   const int P = a.log2n;
   const unsigned grid = (unsigned)((a.G + (kTile >> P) - 1) / (kTile >> P));
-  switch (P) {
-#define FGP_C(PP)                                                                   \
-  case PP:                                                                          \
-    if (emit) k_iter_single<PP, T, true><<<grid, kWG, 0, st>>>(a, tb->tw4096);      \
-    else k_iter_single<PP, T, false><<<grid, kWG, 0, st>>>(a, tb->tw4096);          \
+  return with_pg<T>(a, [&](auto pgc) {
+    constexpr int PG = decltype(pgc)::value;
+    switch (P) {
+#define FGP_C(PP)                                                                     \
+  case PP:                                                                            \
+    if (emit) k_iter_single<PP, T, true, PG><<<grid, kWG, 0, st>>>(a, tb->tw4096);    \
+    else k_iter_single<PP, T, false, PG><<<grid, kWG, 0, st>>>(a, tb->tw4096);        \
     break;
-    FGP_C(4) FGP_C(5) FGP_C(6) FGP_C(7) FGP_C(8) FGP_C(9) FGP_C(10) FGP_C(11) FGP_C(12)
+      FGP_C(4) FGP_C(5) FGP_C(6) FGP_C(7) FGP_C(8) FGP_C(9) FGP_C(10) FGP_C(11) FGP_C(12)
 #undef FGP_C
-    default: return set_error(kErrInvalid, "bad log2n");
-  }
-  return check_launch("k_iter_single");
+      default: return set_error(kErrInvalid, "bad log2n");
+    }
+    return check_launch("k_iter_single");
+  });
 }
 
 template <typename T>
 static int launch_rows_fwd(const Nll& a, const Tables* tb, hipStream_t st) {
   const int m = a.log2n, m2 = split_m2(m);
   const unsigned grid = (unsigned)((int64_t)a.G << (m - kTileLog));
-  switch (m2) {
-#define FGP_C(PP) case PP: k_fwd_rows<PP, T><<<grid, kWG, 0, st>>>(a, tb->tw4096, tb->twm[m]); break;
-    FGP_C(9) FGP_C(10) FGP_C(11) FGP_C(12)
+  return with_pg<T>(a, [&](auto pgc) {
+    constexpr int PG = decltype(pgc)::value;
+    switch (m2) {
+#define FGP_C(PP) case PP: k_fwd_rows<PP, T, PG><<<grid, kWG, 0, st>>>(a, tb->tw4096, tb->twm[m]); break;
+      FGP_C(9) FGP_C(10) FGP_C(11) FGP_C(12)
 #undef FGP_C
-    default: return set_error(kErrInvalid, "bad m2");
-  }
-  return check_launch("k_fwd_rows");
+      default: return set_error(kErrInvalid, "bad m2");
+    }
+    return check_launch("k_fwd_rows");
+  });
 }
 
 template <typename T>
@@ -813,13 +900,16 @@ template <typename T>
 static int launch_rows_bwd(const Nll& a, const Tables* tb, hipStream_t st) {
   const int m = a.log2n, m2 = split_m2(m);
   const unsigned grid = (unsigned)((int64_t)a.G << (m - kTileLog));
-  switch (m2) {
-#define FGP_C(PP) case PP: k_bwd_rows<PP, T><<<grid, kWG, 0, st>>>(a, tb->tw4096, tb->twm[m]); break;
-    FGP_C(9) FGP_C(10) FGP_C(11) FGP_C(12)
+  return with_pg<T>(a, [&](auto pgc) {
+    constexpr int PG = decltype(pgc)::value;
+    switch (m2) {
+#define FGP_C(PP) case PP: k_bwd_rows<PP, T, PG><<<grid, kWG, 0, st>>>(a, tb->tw4096, tb->twm[m]); break;
+      FGP_C(9) FGP_C(10) FGP_C(11) FGP_C(12)
 #undef FGP_C
-    default: return set_error(kErrInvalid, "bad m2");
-  }
-  return check_launch("k_bwd_rows");
+      default: return set_error(kErrInvalid, "bad m2");
+    }
+    return check_launch("k_bwd_rows");
+  });
 }
 
 // one kernel of the pipeline: 0 = forward rows (n <= 4096: the single-kernel iteration), 1 = eigen
