@@ -982,7 +982,7 @@ class FastGPLattice(AbstractFastGP):
             return None
         m = int(n).bit_length() - 1
         z = [int(v) for v in self.seq.z[:self.d]]
-        if len(z) != self.d or not all(0 < v < 2 ** (53 - m) for v in z):
+        if len(z) != self.d or not all(0 < v < 2 ** (53 - m) for v in z) or len(set(self._alphas)) != 1:
             return None
         if not np.all((self.seq.shift >= 0) & (self.seq.shift < 1)):
             return None
