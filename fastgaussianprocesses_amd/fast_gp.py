@@ -501,16 +501,20 @@ class AbstractFastGP(torch.nn.Module):
     def _log_row(self, i, loss, t1, t2, indent):
         print(" " * indent + "%16.2e | %-10.2e | %-10.2e | %-10.2e" % (i, loss, t1, t2))
 
-    def _fit_fused(self, iterations, lr, stop, hists, verbose, indent):
+    def _fit_fused(self, iterations, lr, stop, hists, verbose, indent, ysq=None, d_out=None):
+        """Device-resident MLL fit.  `ysq` / `d_out` override Y = sum_b |ytilde_b|^2 and the output
+        count (distributed.fit_sharded: Y all-reduced over the ranks' output shards)."""
         logtol, wait_max = stop
         n = self._nh
         pb_shape, G = self._problem_batch()
-        d_out = int(torch.tensor(self.shape_batch).prod())
+        if d_out is None:
+            d_out = int(torch.tensor(self.shape_batch).prod())
         gen = self._parts_gen(n)
         parts = self._k1parts(n) if gen is None else None
         ls_raw = self.raw_lengthscales.detach()
         ls2 = ls_raw.reshape(-1, ls_raw.shape[-1])
-        eng = FusedMLL(self._FAMILY, parts, self._ysq(pb_shape, G), self.raw_scale.detach().reshape(-1), ls2,
+        eng = FusedMLL(self._FAMILY, parts, self._ysq(pb_shape, G) if ysq is None else ysq,
+                       self.raw_scale.detach().reshape(-1), ls2,
                        self.raw_noise.detach().reshape(-1), logdet_weight=d_out / G,
                        mll_const=mll_constant(d_out, n),
                        requires_grad=(self.raw_scale.requires_grad, self.raw_lengthscales.requires_grad,

@@ -261,3 +261,37 @@ def test_stage_launches_equal_fit_run(family, m):
     torch.cuda.synchronize()
     assert torch.equal(e1.loss_hist[:6], e2.loss_hist[:6])
     assert torch.equal(e1.raw, e2.raw)
+
+
+def test_sharded_multi_output_fit_matches_unsharded():
+    """C5 layout (distributed.fit_sharded) on one device: two output shards, their partial Y summed
+    (what the RCCL all-reduce does), give the fit of the unsharded multi-output GP."""
+    from oracle.fgp_oracle import f_ackley
+    d, n, B = 3, 2 ** 14, 6
+    seq = F.Lattice(d, seed=3)
+    full = F.FastGPLattice(seq, shape_batch=[B], device=DEV)
+    x = full.get_x_next(n)
+    y = torch.stack([f_ackley(x) * (1 + 0.1 * b) + 0.01 * torch.sin(7 * b * x[:, 0]) for b in range(B)])
+    full.add_y_next(y)
+    ref = full.fit(iterations=15, verbose=0, store_loss_hist=True, stop_crit_wait_iterations=30)
+    shards = []
+    for a, b in [(0, 4), (4, 6)]:
+        gp = F.FastGPLattice(F.Lattice(d, seed=3), shape_batch=[b - a], device=DEV)
+        gp.get_x_next(n)
+        gp.add_y_next(y[a:b])
+        shards.append(gp)
+    ysq = sum(gp._ysq(*gp._problem_batch()) for gp in shards)
+    outs = []
+    for gp in shards:
+        stop = (np.log(1 + 5e-2), 30)
+        hists = dict(loss=True, scale=False, lengthscales=False, noise=False, task_kernel=False)
+        outs.append(gp._fit_fused(15, 0.1, stop, hists, 0, 4, ysq=ysq.clone(), d_out=B))
+    for o in outs:
+        assert o["iterations"] == ref["iterations"]
+        assert rel_err(o["loss_hist"], ref["loss_hist"]) < 1e-10     # Y summed in another order
+    assert torch.equal(shards[0].raw_lengthscales, shards[1].raw_lengthscales)
+    assert rel_err(shards[0].raw_lengthscales, full.raw_lengthscales) < 1e-10
+    # the shard's posterior mean of its outputs equals the unsharded one
+    xt = torch.rand((16, d), generator=torch.Generator().manual_seed(17)).to(DEV)
+    pm_full = full.post_mean(xt)
+    assert rel_err(shards[1].post_mean(xt), pm_full[4:6]) < 1e-6     # coeffs: cond(K) ~ n / noise
