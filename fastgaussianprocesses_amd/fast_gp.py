@@ -265,6 +265,15 @@ class AbstractFastGP(torch.nn.Module):
             self._xb = self._x
         self._pts_n = n
 
+    def _points_T(self, n):
+        """[d, n] dimension-major copy of the first n points (cached: points only ever grow)."""
+        n = int(n)
+        self._ensure_points(n)
+        pt = getattr(self, "_pts_T", None)
+        if pt is None or pt[0] != n:
+            self._pts_T = (n, self._xb[:n].T.contiguous())
+        return self._pts_T[1]
+
     def get_x(self, task=0, n=None):
         assert task == 0
         n = self._nh if n is None else int(n)
@@ -668,7 +677,10 @@ class AbstractFastGP(torch.nn.Module):
 
     # ------------------------------------------------------------------ prediction
     def _hyp_rows(self, batch_params):
-        """[Gk, 1+d] (scale, lengthscales) rows for the prediction kernels."""
+        """[Gk, 1+d] (scale, lengthscales) rows for the prediction kernels (cached per parameters)."""
+        return self._cached(("hyp_rows", bool(batch_params)), lambda: self._hyp_rows_now(batch_params))
+
+    def _hyp_rows_now(self, batch_params):
         s, ls = self.scale.detach(), self.lengthscales.detach()
         if not batch_params:
             return torch.cat([s.reshape(1), ls.reshape(-1).expand(self.d)])[None]
@@ -685,17 +697,24 @@ class AbstractFastGP(torch.nn.Module):
 
     def _defer_unit(self, x, name="x"):
         """Enqueue the [0, 1] range check of x (fast_gp_lattice.py:264-265) without synchronising;
-        _raise_deferred() reads all pending flags back once, after the dependent work is enqueued."""
+        _raise_deferred() reads all pending flags back once, after the dependent work is enqueued.
+        A tensor already checked (same storage, version counter, shape and strides) is not re-checked."""
+        key = (x.data_ptr(), x._version, tuple(x.shape), tuple(x.stride()), x.device)
+        if any(k == key for k, _ in getattr(self, "_unit_ok", ())):
+            return
         flag = ((0 <= x) & (x <= 1)).all()
-        self._pending_checks = getattr(self, "_pending_checks", []) + [(flag, name)]
+        self._pending_checks = getattr(self, "_pending_checks", []) + [(flag, name, (key, x))]
 
     def _raise_deferred(self):
         pend = getattr(self, "_pending_checks", [])
         self._pending_checks = []
         if pend:
-            ok = torch.stack([f for f, _ in pend]).cpu()
-            for good, (_, name) in zip(ok.tolist(), pend):
+            ok = torch.stack([f for f, _, _ in pend]).cpu()
+            for good, (_, name, _) in zip(ok.tolist(), pend):
                 assert good, "%s should have all elements in [0,1]" % name
+            # (the checked tensors are held, so their storage cannot be reused under the same key)
+            seen = getattr(self, "_unit_ok", [])
+            self._unit_ok = (seen + [kx for _, _, kx in pend])[-8:]
 
     def _task_arg(self, task):
         if task is None:
@@ -710,7 +729,12 @@ class AbstractFastGP(torch.nn.Module):
 
     def _n_arg(self, n):
         if n is None:
-            n = self.n
+            return self._nh       # host mirror of self.n: no device round trip
+        if isinstance(n, (int, np.integer)):
+            n = int(n)
+            assert n > 0 and (n & (n - 1)) == 0 and n >= self._nh, \
+                "require n are all power of two greater than or equal to self.n"
+            return n
         if isinstance(n, int):
             n = torch.tensor([n], dtype=torch.int64, device=self.device)
         assert isinstance(n, torch.Tensor) and (n & (n - 1) == 0).all() and (n >= self.n).all(), \
@@ -719,17 +743,18 @@ class AbstractFastGP(torch.nn.Module):
 
     def _cross_rows(self, x, n, batch_params):
         """rows[g, t, i] = K(x_t, xb_i) for the first n points."""
-        self._ensure_points(n)
-        z = self._xb[:n].T.contiguous()
+        z = self._points_T(n)
         return ops.kernel_rows(self._FAMILY, x, z, self._hyp_rows(batch_params), alphas=self._alphas,
                                tbits=self._tbits())
 
     def _post_var_qf(self, x, n, chunk=16):
         """sum_k Re(A_k) |ft(K(x_t, .))_k|^2 for every test point (fgp_post_var_qf)."""
-        self._ensure_points(n)
-        z = self._xb[:n].T.contiguous()
-        wa = self._inv(n)
-        wa = (wa.real if wa.is_complex() else wa).contiguous()
+        z = self._points_T(n)
+
+        def real_inv():
+            wa = self._inv(n)
+            return (wa.real if wa.is_complex() else wa).contiguous()
+        wa = self._cached(("inv_real", n), real_inv)
         hyp = self._hyp_rows(False)[0].contiguous()
         out = torch.empty(x.size(0), dtype=torch.float64, device=self.device)
         for t0 in range(0, x.size(0), chunk):
@@ -740,7 +765,9 @@ class AbstractFastGP(torch.nn.Module):
 
     def _kdiag(self, x):
         """K(x, x) (zero distance parts)."""
-        part0 = self._part_at_zero().to(self.device)
+        part0 = getattr(self, "_part0_dev", None)
+        if part0 is None:
+            part0 = self._part0_dev = self._part_at_zero().to(self.device)
         return self.scale * (1 + self.lengthscales * part0).prod(-1, keepdim=True)
 
     def post_mean(self, x, task=None, eval=True):
@@ -765,7 +792,7 @@ class AbstractFastGP(torch.nn.Module):
             else:
                 bp = self._has_batch_params()
                 c2 = coeffs.reshape(-1, n)
-                z = self._xb[:n].T.contiguous()
+                z = self._points_T(n)
                 pm = ops.post_mean_matfree(self._FAMILY, x, z, self._hyp_rows(bp), c2, alphas=self._alphas,
                                            tbits=self._tbits())
                 pm = pm.reshape(tuple(coeffs.shape[:-1]) + (x.size(0),))
@@ -794,7 +821,7 @@ class AbstractFastGP(torch.nn.Module):
                 kmat = rows[0] if not bp else rows.reshape(tuple(self.shape_batch) + rows.shape[1:])
                 t = self._solve(kmat.movedim(-2, 0), n).movedim(0, -2)
                 diag = self._kdiag(x) - (t * kmat).sum(-1)
-            diag[diag < 0] = 0
+            diag = diag.clamp_(min=0)          # (diag[diag < 0] = 0 without a host sync)
             self._raise_deferred()
         finally:
             if eval:
