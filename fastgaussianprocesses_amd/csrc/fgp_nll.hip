@@ -48,15 +48,26 @@ __device__ __forceinline__ double mod1(double v) {
   return r;
 }
 
-// Bernoulli polynomial B_order(x), Horner form with the standard rational coefficients.
+// Bernoulli polynomial B_order(x), Horner form with the standard rational coefficients.  Every
+// multiply-add is an explicit fma (zero coefficients as plain multiplies), so the value does not
+// depend on the compiler's contraction choices in the inlining context: the parts array
+// (k_lattice_parts) and the parts regenerated inside the fit kernels are bit-identical.
 __device__ __forceinline__ double bernoulli(int order, double x) {
+  double t;
   switch (order) {
-    case 2: return (x - 1.0) * x + 1.0 / 6.0;
-    case 4: return (((x - 2.0) * x + 1.0) * x + 0.0) * x - 1.0 / 30.0;
-    case 6: return (((((x - 3.0) * x + 5.0 / 2.0) * x + 0.0) * x - 1.0 / 2.0) * x + 0.0) * x + 1.0 / 42.0;
+    case 2: return __builtin_fma(x - 1.0, x, 1.0 / 6.0);
+    case 4:
+      t = __builtin_fma(x - 2.0, x, 1.0) * x;
+      return __builtin_fma(t, x, -1.0 / 30.0);
+    case 6:
+      t = __builtin_fma(x - 3.0, x, 5.0 / 2.0) * x;
+      t = __builtin_fma(t, x, -1.0 / 2.0) * x;
+      return __builtin_fma(t, x, 1.0 / 42.0);
     case 8:
-      return (((((((x - 4.0) * x + 14.0 / 3.0) * x + 0.0) * x - 7.0 / 3.0) * x + 0.0) * x + 2.0 / 3.0) * x + 0.0) * x -
-             1.0 / 30.0;
+      t = __builtin_fma(x - 4.0, x, 14.0 / 3.0) * x;
+      t = __builtin_fma(t, x, -7.0 / 3.0) * x;
+      t = __builtin_fma(t, x, 2.0 / 3.0) * x;
+      return __builtin_fma(t, x, -1.0 / 30.0);
     default: return __builtin_nan("");
   }
 }
@@ -153,7 +164,7 @@ template <int ORD>
 __device__ __forceinline__ double gen_part(const Nll& a, const PSrc& s, int j, unsigned br, unsigned mask,
                                            double inv_n) {
   double x = (double)((br * a.gz[j]) & mask) * inv_n;   // exact: (v(i) z_j) % 1
-  x = x + s.sh[j];
+  x = x + s.sh[j];                                      // (an fma here would round identically)
   if (x >= 1.0) x -= 1.0;                               // numpy remainder on [0, 2): exact
   double dl = x - s.sh[j];
   if (dl < 0.0) dl += 1.0;                              // torch.remainder on (-1, 1)
@@ -207,7 +218,7 @@ __device__ __forceinline__ double k1_from(const Nll& a, const Hyp& h, const doub
   double r = 1.0;
 #pragma unroll
   for (int j = 0; j < FGP_MAX_D; ++j)
-    if (j < a.d) r *= 1.0 + h.ls[j] * p[j];
+    if (j < a.d) r *= __builtin_fma(h.ls[j], p[j], 1.0);
   return h.scale * r;
 }
 
@@ -220,8 +231,8 @@ __device__ __forceinline__ double2 k1_pair(const Nll& a, const Hyp& h, const PSr
     for (int j = 0; j < FGP_MAX_D; ++j) {
       if (j < a.d) {
         const double2 pv = *reinterpret_cast<const double2*>(s.pg + (int64_t)j * n + i);
-        r0 *= 1.0 + h.ls[j] * pv.x;
-        r1 *= 1.0 + h.ls[j] * pv.y;
+        r0 *= __builtin_fma(h.ls[j], pv.x, 1.0);
+        r1 *= __builtin_fma(h.ls[j], pv.y, 1.0);
       }
     }
     return make_double2(h.scale * r0, h.scale * r1);
@@ -236,16 +247,16 @@ __device__ __forceinline__ double2 k1_pair(const Nll& a, const Hyp& h, const PSr
 __device__ __forceinline__ void grad_terms_p(const Hyp& h, const double* pj, double gi, double* acc) {
   double f[FGP_MAX_D];
 #pragma unroll
-  for (int j = 0; j < FGP_MAX_D; ++j) f[j] = 1.0 + h.ls[j] * pj[j];     // padded dims: l = 0 -> f = 1 exactly
+  for (int j = 0; j < FGP_MAX_D; ++j) f[j] = __builtin_fma(h.ls[j], pj[j], 1.0);   // padded dims: l = 0 -> f = 1
   double suf[FGP_MAX_D + 1];
   suf[FGP_MAX_D] = 1.0;
 #pragma unroll
   for (int j = FGP_MAX_D - 1; j >= 0; --j) suf[j] = suf[j + 1] * f[j];
-  acc[0] += gi * (h.scale * suf[0]);
+  acc[0] = __builtin_fma(gi, h.scale * suf[0], acc[0]);
   double pre = 1.0;
 #pragma unroll
   for (int j = 0; j < FGP_MAX_D; ++j) {
-    acc[1 + j] += gi * (h.scale * h.ls[j] * pj[j] * (pre * suf[j + 1]));
+    acc[1 + j] = __builtin_fma(gi, h.scale * h.ls[j] * pj[j] * (pre * suf[j + 1]), acc[1 + j]);
     pre *= f[j];
   }
 }

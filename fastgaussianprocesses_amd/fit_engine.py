@@ -164,7 +164,7 @@ class FusedMLL(object):
         lh = self.loss_hist[slot].sum(0).cpu() if self.per_problem else self.loss_hist[slot, 0].cpu()
         return float(lh[0]), float(lh[1]), float(lh[2]), self.grad.cpu()
 
-    def step(self, slot, update=True):
+    def fit_step(self, slot, update=True):
         """Enqueue the reduction + Rprop step of history slot `slot` (fgp_fit_step)."""
         self.ensure_history(slot + 1)
         N.call("fgp_fit_step", self._nll, self._fit, int(slot), int(bool(update)), self.stream())

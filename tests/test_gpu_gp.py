@@ -257,7 +257,7 @@ def test_stage_launches_equal_fit_run(family, m):
     for it in range(6):
         for k in range(3):
             e2.stage(k)
-        e2.step(it)
+        e2.fit_step(it)
     torch.cuda.synchronize()
     assert torch.equal(e1.loss_hist[:6], e2.loss_hist[:6])
     assert torch.equal(e1.raw, e2.raw)

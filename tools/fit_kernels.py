@@ -38,7 +38,7 @@ def main():
     for it in range(a.iters):
         for k in range(3):
             eng.stage(k)
-        eng.step(it)
+        eng.fit_step(it)
     torch.cuda.synchronize()
     print("ran %d fit iterations over %d problems, n=2^%d, d=%d, parts=%s" %
           (a.iters, a.shifts, a.log2n, a.d, "array" if eng.gen is None else "regenerated"))
