@@ -27,6 +27,7 @@ _c_vp = ctypes.c_void_p
 
 _c_pi = ctypes.POINTER(ctypes.c_int)
 _c_pd = ctypes.POINTER(ctypes.c_double)
+_c_pl = ctypes.POINTER(ctypes.c_int64)
 
 
 class NllDesc(ctypes.Structure):
@@ -69,6 +70,8 @@ _SIGNATURES = {
     "fgp_ifftbr": [_c_vp, _c_i64, _c_vp, _c_int, _c_vp, _c_i64, _c_int, _c_int, _c_vp],
     "fgp_fwht": [_c_vp, _c_i64, _c_vp, _c_i64, _c_int, _c_int, _c_vp],
     "fgp_lattice_parts": [_c_vp, _c_i64, _c_vp, _c_i64, _c_int, _c_pi, _c_pd, _c_vp, _c_vp],
+    "fgp_lattice_points": [_c_pl, _c_vp, _c_i64, _c_i64, _c_int, _c_vp, _c_vp],
+    "fgp_lattice_parts_gen": [_c_pl, _c_vp, _c_int, _c_int, _c_int, _c_pd, _c_vp, _c_vp],
     "fgp_net_parts": [_c_vp, _c_i64, _c_vp, _c_i64, _c_int, _c_int, _c_vp, _c_vp],
     "fgp_nll_fwd": [_P_NLL, _c_vp],
     "fgp_nll_bwd": [_P_NLL, _c_vp],
@@ -87,6 +90,10 @@ _SIGNATURES = {
 
 def int_array(vals):
     return (ctypes.c_int * max(1, len(vals)))(*[int(v) for v in vals])
+
+
+def int64_array(vals):
+    return (ctypes.c_int64 * max(1, len(vals)))(*[int(v) for v in vals])
 
 
 def double_array(vals):

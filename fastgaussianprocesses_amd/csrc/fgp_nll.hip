@@ -72,11 +72,6 @@ __device__ __forceinline__ double bernoulli(int order, double x) {
   }
 }
 
-template <int ORD>
-__device__ __forceinline__ double bernoulli_t(double x) {
-  return bernoulli(ORD, x);   // constant-folded switch: the same expressions as the runtime form
-}
-
 // Order-1 Walsh part for an XOR distance (fast_gp_digital_net_b2.py:297-298).
 __device__ __forceinline__ double walsh1(unsigned long long delta, int t) {
   if (delta == 0ull) return 6.0 * (1.0 / 6.0 - 0.0);
@@ -157,18 +152,25 @@ __device__ __forceinline__ void psrc_init(const Nll& a, int g, PSrc& s) {
     s.sh[j] = (a.pgen && j < a.d) ? a.gshift[(int64_t)g * a.gshift_stride + j] : 0.0;   // (x_0 = shift)
 }
 
-// Lattice part of dimension j at the point with bit-reversed index br:
-//   x = ((br z_j mod n) / n + shift) % 1  (the host generator's exact value and rounding, seqs.Lattice),
+// Lattice part at the natural-order point with bit-reversed index br (dimension with generating
+// vector entry zj mod n, coefficient coef, shift sh = x_0):
+//   x = ((br zj mod n) / n + sh) % 1  (the host generator's exact value and rounding, seqs.Lattice),
 //   delta = torch.remainder(x - x_0, 1),  part = coef B_ORD(delta)  (k_lattice_parts).
+template <int ORD>
+__device__ __forceinline__ double lattice_gen_part(unsigned zj, double coef, double sh, unsigned br, unsigned mask,
+                                                   double inv_n) {
+  double x = (double)((br * zj) & mask) * inv_n;        // exact: (v(i) z_j) % 1
+  x = x + sh;
+  if (x >= 1.0) x -= 1.0;                               // numpy remainder on [0, 2): exact
+  double dl = x - sh;
+  if (dl < 0.0) dl += 1.0;                              // torch.remainder on (-1, 1)
+  return coef * bernoulli(ORD, dl);
+}
+
 template <int ORD>
 __device__ __forceinline__ double gen_part(const Nll& a, const PSrc& s, int j, unsigned br, unsigned mask,
                                            double inv_n) {
-  double x = (double)((br * a.gz[j]) & mask) * inv_n;   // exact: (v(i) z_j) % 1
-  x = x + s.sh[j];                                      // (an fma here would round identically)
-  if (x >= 1.0) x -= 1.0;                               // numpy remainder on [0, 2): exact
-  double dl = x - s.sh[j];
-  if (dl < 0.0) dl += 1.0;                              // torch.remainder on (-1, 1)
-  return a.gcoef[j] * bernoulli_t<ORD>(dl);
+  return lattice_gen_part<ORD>(a.gz[j], a.gcoef[j], s.sh[j], br, mask, inv_n);
 }
 
 // Parts source as a compile-time choice: PG = 0 reads the parts array, PG = 2/4/6/8 regenerates the
@@ -777,6 +779,40 @@ __global__ __launch_bounds__(kWG) void k_fit_reduce_step(Nll a, Fit f, int iter,
 }
 
 // ------------------------------------------------------------------------------------------------
+// on-device lattice points and generated parts (the arithmetic of the FGP_PARTS_LATTICE fit path)
+struct GenSpec {
+  unsigned z[FGP_MAX_D];       // z_j mod 2^bits
+  double coef[FGP_MAX_D];
+  int order;
+};
+
+// x[i - n0, j] = ((brev_bits(i) z_j mod 2^bits) / 2^bits + shift_j) % 1,  i in [n0, n1)
+__global__ __launch_bounds__(kWG) void k_lattice_points(GenSpec g, const double* __restrict__ shift, int64_t n0,
+                                                        int64_t n1, int d, int bits, double* __restrict__ x) {
+  const int64_t i = n0 + (int64_t)blockIdx.x * kWG + threadIdx.x;
+  if (i >= n1) return;
+  const unsigned br = brev_bits((unsigned)i, bits), mask = bits >= 32 ? 0xffffffffu : (1u << bits) - 1u;
+  const double inv = ldexp(1.0, -bits);
+  for (int j = 0; j < d; ++j) {
+    double v = (double)((br * g.z[j]) & mask) * inv;
+    v = v + shift[j];
+    if (v >= 1.0) v -= 1.0;
+    x[(i - n0) * d + j] = v;
+  }
+}
+
+template <int ORD>
+__global__ __launch_bounds__(kWG) void k_lattice_parts_gen(GenSpec g, const double* __restrict__ shift, int m, int d,
+                                                           double* __restrict__ parts) {
+  const int64_t n = (int64_t)1 << m;
+  const int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x;
+  if (i >= n) return;
+  const unsigned br = brev_bits((unsigned)i, m), mask = (unsigned)(n - 1);
+  const double inv_n = ldexp(1.0, -m);
+  for (int j = 0; j < d; ++j) parts[(int64_t)j * n + i] = lattice_gen_part<ORD>(g.z[j], g.coef[j], shift[j], br, mask, inv_n);
+}
+
+// ------------------------------------------------------------------------------------------------
 // host-side launch logic
 static int to_nll(const fgp_nll_desc* d, Nll& a) {
   if (!d) return set_error(kErrInvalid, "null nll desc");
@@ -1019,6 +1055,51 @@ int fgp_net_parts(const int64_t* xb, int64_t xb_row_stride, const int64_t* z, in
   if (!xb || !z || !parts) return set_error(kErrInvalid, "fgp_net_parts: null pointer");
   k_net_parts<<<(unsigned)((n + kWG - 1) / kWG), kWG, 0, (hipStream_t)stream>>>(xb, xb_row_stride, z, n, d, t, parts);
   return check_launch("k_net_parts");
+}
+
+int fgp_lattice_points(const int64_t* z, const double* shift, int64_t n_min, int64_t n_max, int d, double* x,
+                       void* stream) {
+  if (d < 1 || d > FGP_MAX_D || n_min < 0 || n_max < n_min || n_max > ((int64_t)1 << 30))
+    return set_error(kErrInvalid, "fgp_lattice_points: bad n_min/n_max/d");
+  if (n_max == n_min) return kOk;
+  if (!z || !shift || !x) return set_error(kErrInvalid, "fgp_lattice_points: null pointer");
+  int bits = 0;
+  while (((int64_t)1 << bits) < n_max) ++bits;
+  GenSpec g{};
+  for (int j = 0; j < d; ++j) {
+    if (z[j] <= 0 || (bits < 53 && z[j] >= ((int64_t)1 << (53 - bits))))
+      return set_error(kErrUnsupported, "fgp_lattice_points: z[%d] outside (0, 2^(53-bits))", j);
+    g.z[j] = (unsigned)((uint64_t)z[j] & (bits >= 32 ? 0xffffffffull : ((1ull << bits) - 1)));
+  }
+  const int64_t cnt = n_max - n_min;
+  k_lattice_points<<<(unsigned)((cnt + kWG - 1) / kWG), kWG, 0, (hipStream_t)stream>>>(g, shift, n_min, n_max, d,
+                                                                                       bits, x);
+  return check_launch("k_lattice_points");
+}
+
+int fgp_lattice_parts_gen(const int64_t* z, const double* shift, int log2n, int d, int order, const double* coef,
+                          double* parts, void* stream) {
+  if (d < 1 || d > FGP_MAX_D || log2n < 0 || log2n > kMaxLog2N) return set_error(kErrInvalid, "fgp_lattice_parts_gen: bad d/log2n");
+  if (!z || !shift || !coef || !parts) return set_error(kErrInvalid, "fgp_lattice_parts_gen: null pointer");
+  GenSpec g{};
+  const uint64_t zmask = ((uint64_t)1 << log2n) - 1;
+  for (int j = 0; j < d; ++j) {
+    if (z[j] <= 0 || (log2n < 53 && z[j] >= ((int64_t)1 << (53 - log2n))))
+      return set_error(kErrUnsupported, "fgp_lattice_parts_gen: z[%d] outside (0, 2^(53-log2n))", j);
+    g.z[j] = (unsigned)((uint64_t)z[j] & zmask);
+    g.coef[j] = coef[j];
+  }
+  const int64_t n = (int64_t)1 << log2n;
+  const dim3 grid((unsigned)((n + kWG - 1) / kWG));
+  hipStream_t st = (hipStream_t)stream;
+  switch (order) {
+    case 2: k_lattice_parts_gen<2><<<grid, kWG, 0, st>>>(g, shift, log2n, d, parts); break;
+    case 4: k_lattice_parts_gen<4><<<grid, kWG, 0, st>>>(g, shift, log2n, d, parts); break;
+    case 6: k_lattice_parts_gen<6><<<grid, kWG, 0, st>>>(g, shift, log2n, d, parts); break;
+    case 8: k_lattice_parts_gen<8><<<grid, kWG, 0, st>>>(g, shift, log2n, d, parts); break;
+    default: return set_error(kErrUnsupported, "Bernoulli order %d unsupported", order);
+  }
+  return check_launch("k_lattice_parts_gen");
 }
 
 int fgp_nll_fwd(const fgp_nll_desc* desc, void* stream) {

@@ -171,6 +171,31 @@ def lattice_parts(x, z, alphas, out=None):
     return out
 
 
+def lattice_points(z, shift, n_min, n_max, device=None):
+    """Natural-order rank-1 lattice points [n_max - n_min, d] generated on the device (fgp_lattice_points),
+    bit-identical to seqs.Lattice(n_min, n_max).  z: [d] ints; shift: [d] floats in [0, 1)."""
+    shift = torch.as_tensor(shift, dtype=torch.float64, device=device)
+    require_device(shift, "lattice_points")
+    shift = shift.contiguous()
+    d = shift.numel()
+    x = torch.empty((n_max - n_min, d), dtype=torch.float64, device=shift.device)
+    N.call("fgp_lattice_points", N.int64_array(z), N.ptr(shift), int(n_min), int(n_max), d, N.ptr(x), _stream(shift))
+    return x
+
+
+def lattice_parts_gen(z, shift, alphas, n):
+    """The lattice parts [d, n] exactly as the FGP_PARTS_LATTICE fit kernels regenerate them
+    (fgp_lattice_parts_gen); shift: device [d] (= x[0])."""
+    require_device(shift, "lattice_parts_gen")
+    shift = shift.to(torch.float64).reshape(-1).contiguous()
+    d = shift.numel()
+    assert len(set(int(a) for a in alphas)) == 1, "one smoothness for every dimension"
+    parts = torch.empty((d, n), dtype=torch.float64, device=shift.device)
+    N.call("fgp_lattice_parts_gen", N.int64_array(z), N.ptr(shift), log2_exact(n), d, 2 * int(alphas[0]),
+           N.double_array([lattice_coefficient(a) for a in alphas]), N.ptr(parts), _stream(shift))
+    return parts
+
+
 def net_parts(xb, z, t, out=None):
     """Order-1 Walsh parts for delta = xb XOR z -> [d, n] (fast_gp_digital_net_b2.py:274-301)."""
     require_device(xb, "net_parts")

@@ -94,6 +94,22 @@ int fgp_lattice_parts(const double* x, int64_t x_row_stride, const double* z, in
 int fgp_net_parts(const int64_t* xb, int64_t xb_row_stride, const int64_t* z, int64_t n, int d, int t, double* parts,
                   void* stream);
 
+/* On-device natural-order rank-1 lattice points (seqs.Lattice / qmcpy Lattice, the point generation
+ * of AbstractGP.get_x_next, fastgps/abstract_gp.py:307-309 -> util.py:17-48), bit-identical to the host
+ * generator: with bits = ceil(log2(n_max)),
+ *   x[i - n_min, j] = ((brev_bits(i) z[j] mod 2^bits) / 2^bits + shift[j]) % 1,   n_min <= i < n_max.
+ * z: host [d] int64 with 0 < z[j] < 2^(53 - bits); shift: device [d] float64 in [0, 1);
+ * x: device [n_max - n_min, d] float64 row-major. */
+int fgp_lattice_points(const int64_t* z, const double* shift, int64_t n_min, int64_t n_max, int d, double* x,
+                       void* stream);
+
+/* The lattice parts as the FGP_PARTS_LATTICE fit kernels regenerate them (equal to fgp_lattice_parts
+ * on the fgp_lattice_points points of size n = 2^log2n with x_0 = shift):
+ *   parts[j, i] = coef[j] * B_order(((brev_m(i) z_j mod n) / n + shift_j) % 1 - shift_j) % 1).
+ * z, coef: host [d]; shift: device [d]; order in {2, 4, 6, 8}; parts: device [d][n]. */
+int fgp_lattice_parts_gen(const int64_t* z, const double* shift, int log2n, int d, int order, const double* coef,
+                          double* parts, void* stream);
+
 /* One fused MLL problem batch: G independent eigen-problems of size n = 2^log2n (log2n >= 4). */
 typedef struct fgp_nll_desc {
   int family;                 /* FGP_FAMILY_LATTICE / FGP_FAMILY_NET */
