@@ -139,6 +139,9 @@ def roofline_fit_kernels(F, shifts, iters):
     eng.run(0, 2)
     torch.cuda.synchronize()
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(iters)]
+    # hold the stream with a spin kernel while the host enqueues every launch and event, so the
+    # events time back-to-back kernels (no host launch gaps) -- the durations rocprofv3 reports
+    torch.cuda._sleep(int(2.4e9 * 4e-4 * iters))
     for it in range(iters):
         e = ev[it]
         e[0].record()
@@ -152,6 +155,24 @@ def roofline_fit_kernels(F, shifts, iters):
     us["k_fit_reduce_step"] = 1e3 * sum(e[3].elapsed_time(e[4]) for e in ev) / iters
     t_iter = sum(us.values()) / 1e6
     return n, eng.gen is None, us, t_iter
+
+
+PMC_SUMMARY = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_pmc_fit_kernels.json")
+
+
+def pmc_traffic(kernel, grid):
+    """HBM bytes per launch of `kernel` at `grid` threads from the committed rocprofv3 PMC summary
+    (tools/pmc_summary.py over FETCH_SIZE / WRITE_SIZE passes of tools/fit_kernels.py, same kernels
+    and grid; FETCH_SIZE x2 gfx950 correction), or None when absent."""
+    try:
+        summ = json.load(open(PMC_SUMMARY))
+    except (OSError, ValueError):
+        return None
+    for k, v in summ.items():
+        name, _, g = k.partition("|grid=")
+        if name.split("<")[0].endswith(kernel) and g == str(grid) and "traffic_bytes" in v:
+            return v["traffic_bytes"]
+    return None
 
 
 def cpu_baseline(args, n, d):
@@ -253,7 +274,8 @@ def main():
     # SURVEY §8(d) reference-dataflow bytes of one fit iteration: 16nd + 32n + 32nB per GP (B = 1)
     b_iter = (16 * n * d + 32 * n + 32 * n) * P
     roof = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": ach / HBM_PEAK_GBS, "traffic": None, "algorithmic_bytes": sb[dom], "avg_us": us[dom],
+            "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic(dom, P * n // 16),
+            "traffic_source": os.path.relpath(PMC_SUMMARY, os.path.dirname(os.path.abspath(__file__))), "algorithmic_bytes": sb[dom], "avg_us": us[dom],
             "launch": "%d problems x n=2^%d (grid %d workgroups)" % (P, args.log2n, P * n // 4096),
             "kernels": {k: {"avg_us": us[k], "bytes": sb.get(k),
                             "GB/s": (sb[k] / (us[k] * 1e-6) / 1e9) if k in sb else None} for k in us},

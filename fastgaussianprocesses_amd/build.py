@@ -39,7 +39,7 @@ def build(force=False, verbose=True):
     procs = []
     for src in SOURCES:
         obj = os.path.join(LIB_DIR, src.replace(".hip", ".o"))
-        cmd = [HIPCC, "-O3", "-std=c++17", "--offload-arch=" + ARCH, "-fPIC", "-c", os.path.join(CSRC, src), "-o", obj]
+        cmd = [HIPCC, "-O3", "-std=c++17", "-ffp-contract=off", "--offload-arch=" + ARCH, "-fPIC", "-c", os.path.join(CSRC, src), "-o", obj]
         procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
         objs.append(obj)
     for cmd, p in procs:

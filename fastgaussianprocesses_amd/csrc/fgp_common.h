@@ -33,11 +33,13 @@ __device__ __forceinline__ double2 operator-(double2 a, double2 b) { return make
 __device__ __forceinline__ double2 operator*(double2 a, double s) { return make_double2(a.x * s, a.y * s); }
 __device__ __forceinline__ double2& operator+=(double2& a, double2 b) { a.x += b.x; a.y += b.y; return a; }
 __device__ __forceinline__ double2& operator-=(double2& a, double2 b) { a.x -= b.x; a.y -= b.y; return a; }
+// Complex products with explicit fma (the library is compiled with -ffp-contract=off, so rounding
+// never depends on the compiler's contraction choices in a particular kernel).
 __device__ __forceinline__ double2 cmul(double2 a, double2 b) {
-  return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+  return make_double2(__builtin_fma(a.x, b.x, -(a.y * b.y)), __builtin_fma(a.x, b.y, a.y * b.x));
 }
 __device__ __forceinline__ double2 cmulc(double2 a, double2 w) {  // a * conj(w)
-  return make_double2(a.x * w.x + a.y * w.y, a.y * w.x - a.x * w.y);
+  return make_double2(__builtin_fma(a.x, w.x, a.y * w.y), __builtin_fma(a.y, w.x, -(a.x * w.y)));
 }
 
 template <typename T> __device__ __forceinline__ T zero_v();
@@ -88,7 +90,7 @@ __device__ __forceinline__ double2 mul_root(double2 v) {
   } else if constexpr (j == 12) {
     return CONJ ? make_double2(v.y, -v.x) : make_double2(-v.y, v.x);
   } else {
-    return make_double2(cr * v.x - ci * v.y, cr * v.y + ci * v.x);
+    return make_double2(__builtin_fma(cr, v.x, -(ci * v.y)), __builtin_fma(cr, v.y, ci * v.x));
   }
 }
 

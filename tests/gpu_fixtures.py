@@ -33,7 +33,7 @@ def product_gp(g, **kw):
 
 def rel_err(a, b):
     a = torch.as_tensor(a).detach().cpu().reshape(-1)
-    b = torch.as_tensor(np.asarray(b)).reshape(-1)
+    b = (b.detach().cpu() if torch.is_tensor(b) else torch.as_tensor(np.asarray(b))).reshape(-1)
     if b.numel() == 0:
         return 0.0
     return float((a - b).abs().max()) / max(float(b.abs().max()), 1e-300)
@@ -41,5 +41,5 @@ def rel_err(a, b):
 
 def abs_err(a, b):
     a = torch.as_tensor(a).detach().cpu().reshape(-1)
-    b = torch.as_tensor(np.asarray(b)).reshape(-1)
+    b = (b.detach().cpu() if torch.is_tensor(b) else torch.as_tensor(np.asarray(b))).reshape(-1)
     return float((a - b).abs().max()) if b.numel() else 0.0
