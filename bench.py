@@ -11,7 +11,7 @@ value = (shifts * n * world_size) / (max-over-ranks seconds per step).
 
 Extra JSON keys: "roofline" for the dominant kernel (HIP-event timing of that kernel on its stream),
 "cpu_baseline" (the oracle = torch-CPU restatement of the reference, rank 0 at N=1, bounded sample),
-"phases_ms" (per-phase breakdown of one GP, HIP events).
+"phases_ms" (per-phase breakdown of one batched step, HIP events).
 """
 import argparse
 import json
@@ -49,7 +49,7 @@ def parse():
     p.add_argument("--n-var", type=int, default=8)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--sequential", dest="batched", action="store_false",
-                   help="fit the shifts one by one (default: one fused fit_batched loop over all shifts)")
+                   help="fit and predict the shifts one by one (default: one GPBatch over all shifts)")
     p.add_argument("--cpu-sample-iters", type=int, default=3)
     return p.parse_args()
 
@@ -70,48 +70,65 @@ def max_over_ranks(seconds, device):
     return float(t)
 
 
-class Shift(object):
-    """One randomly shifted lattice GP with resident inputs."""
+class Shifts(object):
+    """The rank's randomly shifted lattice GPs with resident inputs: points (generated once, untimed),
+    observations y [P, n] and the initial raw hyper-parameters [P, 2 + d] in HBM."""
 
-    def __init__(self, F, d, n, seed, device):
-        self.seq = F.Lattice(d, seed=seed, randomize="SHIFT")
-        self.gp = F.FastGPLattice(self.seq, device=device)
-        x = self.gp.get_x_next(n)                        # host point generation: untimed
-        self.y = f_ackley(x).contiguous()
-        self.init = {k: v.detach().clone() for k, v in self.gp.named_parameters()}
+    def __init__(self, F, d, n, seeds, device):
+        self.gps, ys = [], []
+        for seed in seeds:
+            gp = F.FastGPLattice(F.Lattice(d, seed=seed, randomize="SHIFT"), device=device)
+            x = gp.get_x_next(n)                         # host point generation: untimed
+            y = f_ackley(x).contiguous()
+            gp.add_y_next(y)
+            self.gps.append(gp)
+            ys.append(y)
+        self.y = torch.stack(ys)
+        self.batch = F.GPBatch(self.gps)
+        self.raw0 = self.batch.raw().clone()
+        self.n = n
 
     def reset(self):
-        gp = self.gp
-        with torch.no_grad():
-            for k, v in self.init.items():
-                setattr(gp, k, torch.nn.Parameter(v.clone(), requires_grad=getattr(gp, k).requires_grad))
-        gp._y = [torch.empty(0, device=gp.device)]
-        gp.n.zero_()
-        gp._parts = {}
-        gp._cache = {}
-        gp._snap = None
-        gp.add_y_next(self.y)
+        """Fresh start of a step: initial hyper-parameters, the observations re-ingested, every cache
+        (ytilde, parts, coefficients) dropped."""
+        self.batch.set_data(self.y)
+        self.batch.set_raw(self.raw0.clone())
+
+
+def step_batched(sh, args, xm, xv):
+    sh.reset()
+    sh.batch.fit(iterations=args.fit_iters, stop_crit_wait_iterations=args.fit_iters + 1)
+    sh.batch.post_mean(xm)
+    sh.batch.post_var(xv)
+
+
+def step_sequential(sh, args, xm, xv):
+    sh.reset()
+    for gp in sh.gps:
+        gp.fit(iterations=args.fit_iters, stop_crit_wait_iterations=args.fit_iters + 1, verbose=0)
+        gp.post_mean(xm)
+        gp.post_var(xv)
 
 
 def phase_breakdown(sh, iters, xm, xv):
-    """HIP-event timing of each phase for one GP (on torch's current stream)."""
+    """HIP-event timing of each phase of one batched step over the rank's shifts (torch's current
+    stream)."""
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
     sh.reset()
-    gp = sh.gp
+    b = sh.batch
     ev[0].record()
-    gp.get_ytilde(0)
-    gp._k1parts(int(gp.n[0]))
+    b.ysq()
     ev[1].record()
-    gp.fit(iterations=iters, stop_crit_wait_iterations=iters + 1, verbose=0)
+    b.fit(iterations=iters, stop_crit_wait_iterations=iters + 1)
     ev[2].record()
-    _ = gp.coeffs
+    b.coeffs()
     ev[3].record()
-    gp.post_mean(xm)
+    b.post_mean(xm)
     ev[4].record()
-    gp.post_var(xv)
+    b.post_var(xv)
     ev[5].record()
     torch.cuda.synchronize()
-    names = ["ytilde+parts", "fit", "coeffs", "post_mean", "post_var"]
+    names = ["ytilde", "fit", "coeffs", "post_mean", "post_var"]
     return {names[i]: ev[i].elapsed_time(ev[i + 1]) for i in range(5)}
 
 
@@ -131,10 +148,9 @@ def stage_bytes(n, d, P, parts_array):
 def roofline_fit_kernels(F, shifts, iters):
     """HIP-event timing (torch's current stream = the stream the kernels are launched on) of every
     kernel of the batched fit iteration, as launched in the step (same engine, same grid)."""
-    for sh in shifts:
-        sh.reset()
-    gps = [sh.gp for sh in shifts]
-    n = int(gps[0].n[0])
+    shifts.reset()
+    gps = shifts.gps
+    n = shifts.n
     eng = F.batch.batched_engine(gps, iters)
     eng.run(0, 2)
     torch.cuda.synchronize()
@@ -231,23 +247,13 @@ def main():
     import fastgaussianprocesses_amd as F
     n = 2 ** args.log2n
     d = args.d
-    shifts = [Shift(F, d, n, seed, device) for seed in shard_seeds(rank, world, args.shifts)]
+    shifts = Shifts(F, d, n, shard_seeds(rank, world, args.shifts), device)
     g = torch.Generator().manual_seed(17)
     xm = torch.rand((args.n_mean, d), generator=g).to(device)
     xv = torch.rand((args.n_var, d), generator=g).to(device)
 
     def step():
-        for sh in shifts:
-            sh.reset()
-        if args.batched:
-            F.fit_batched([sh.gp for sh in shifts], iterations=args.fit_iters,
-                          stop_crit_wait_iterations=args.fit_iters + 1)
-        else:
-            for sh in shifts:
-                sh.gp.fit(iterations=args.fit_iters, stop_crit_wait_iterations=args.fit_iters + 1, verbose=0)
-        for sh in shifts:
-            sh.gp.post_mean(xm)
-            sh.gp.post_var(xv)
+        (step_batched if args.batched else step_sequential)(shifts, args, xm, xv)
 
     for _ in range(args.warmup):
         step()
@@ -264,10 +270,9 @@ def main():
     sec_step = el / args.steps
     value = args.shifts * n * world / sec_step
 
-    phase_breakdown(shifts[0], args.fit_iters, xm, xv)          # first pass absorbs one-off allocations
-    phases = phase_breakdown(shifts[0], args.fit_iters, xm, xv)
+    phases = phase_breakdown(shifts, args.fit_iters, xm, xv)
     n_, parts_array, us, t_iter = roofline_fit_kernels(F, shifts, args.fit_iters)
-    P = len(shifts)
+    P = len(shifts.gps)
     sb = stage_bytes(n, d, P, parts_array)
     dom = max(STAGES, key=lambda k: us[k])
     ach = sb[dom] / (us[dom] * 1e-6) / 1e9

@@ -8,11 +8,11 @@ __version__ = "0.1.0"
 
 from . import ops
 from .fast_gp import AbstractFastGP, FastGPDigitalNetB2, FastGPLattice
-from .batch import fit_batched
+from .batch import GPBatch, fit_batched
 from . import distributed
 from .distributed import fit_sharded
 from .fit_engine import FusedMLL
 from .seqs import DigitalNetB2, Lattice
 
-__all__ = ["FastGPLattice", "FastGPDigitalNetB2", "AbstractFastGP", "Lattice", "DigitalNetB2", "FusedMLL", "fit_batched", "fit_sharded",
+__all__ = ["FastGPLattice", "FastGPDigitalNetB2", "AbstractFastGP", "Lattice", "DigitalNetB2", "FusedMLL", "GPBatch", "fit_batched", "fit_sharded",
            "distributed", "ops"]

@@ -12,7 +12,7 @@ import torch
 
 _LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
 LIB_PATH = os.path.join(_LIB_DIR, "libfgp_hip.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 MAX_D = 8
 PARTS_ARRAY = 0
 PARTS_LATTICE = 1
@@ -60,8 +60,19 @@ class FitDesc(ctypes.Structure):
     ]
 
 
+class PredDesc(ctypes.Structure):
+    """Mirror of fgp_pred_desc (include/fgp_hip.h)."""
+    _fields_ = [
+        ("family", _c_int), ("d", _c_int), ("tbits", _c_int), ("P", _c_int), ("n", _c_i64),
+        ("order", _c_int * 8), ("coef", _c_dbl * 8),
+        ("z", _c_vp), ("z_stride", _c_i64), ("hyp", _c_vp), ("hyp_stride", _c_i64),
+        ("coeffs", _c_vp), ("coeff_stride", _c_i64), ("wa", _c_vp), ("wa_stride", _c_i64),
+    ]
+
+
 _P_NLL = ctypes.POINTER(NllDesc)
 _P_FIT = ctypes.POINTER(FitDesc)
+_P_PRED = ctypes.POINTER(PredDesc)
 
 # name -> argtypes (all return int status); must match include/fgp_hip.h
 _SIGNATURES = {
@@ -85,6 +96,9 @@ _SIGNATURES = {
                       _c_i64, _c_int, _c_vp, _c_i64, _c_vp, _c_i64, _c_vp],
     "fgp_kernel_rows": [_c_int, _c_vp, _c_i64, _c_vp, _c_i64, _c_int, _c_int, _c_pi, _c_pd, _c_vp, _c_int, _c_vp,
                         _c_vp],
+    "fgp_post_mean_batched": [_P_PRED, _c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp],
+    "fgp_post_var_batched": [_P_PRED, _c_vp, _c_i64, _c_i64, _c_pd, _c_vp, _c_vp, _c_vp, _c_vp],
+    "fgp_inv_eig": [_c_int, _c_vp, _c_vp, _c_i64, _c_vp, _c_i64, _c_i64, _c_int, _c_vp, _c_vp, _c_vp],
 }
 
 

@@ -1,53 +1,85 @@
-"""Batched hyper-parameter fits of independent fast GPs (e.g. the randomly shifted replicas of one
-lattice GP, BASELINE config C4) in ONE device-resident loop.
+"""Batches of independent fast GPs (e.g. the randomly shifted replicas of one lattice GP, BASELINE
+config C4) fitted and predicted in ONE device-resident launch sequence.
 
-fastgps fits each GP on its own (AbstractGP.fit, fastgps/abstract_gp.py:152-306).  On MI355X a single
-n = 2^20 GP fills only 256 workgroups per pass, so independent GPs of the same family / n / d are
-stacked into one fgp_fit_run with G problems (per_problem mode: every GP keeps its own loss, its own
-Rprop state and its own early-stopping decision).  The result for each GP is exactly what its own
-`gp.fit(...)` returns: the stopping rule is applied per GP on its own loss history, and each GP's
-best parameters are restored (extra iterations run for GPs that stopped earlier are discarded).
+fastgps fits and predicts each GP on its own (AbstractGP.fit / post_mean / post_var,
+fastgps/abstract_gp.py:152-416).  On MI355X a single n = 2^20 GP fills only 256 workgroups per
+transform pass, and a per-GP predict is a chain of small launches, so independent GPs of the same
+family / n / d / smoothness are stacked: one fgp_fit_run with P problems (per_problem mode: every GP
+keeps its own loss, Rprop state and early-stopping decision), one batched coefficient solve, one
+posterior-mean and one posterior-variance launch for all P GPs.  The result for each GP is what its
+own methods return: the stopping rule is applied per GP on its own loss history, each GP's best
+parameters are restored, and the GP objects hold the fitted parameters and data afterwards.
 """
+import collections
 import math
 
 import torch
 
-from .fit_engine import FusedMLL, LatticePartsGen, mll_constant
+from . import _native as N
+from . import ops
+from .fit_engine import FusedMLL, LatticePartsGen, fused_lam, mll_constant
 
 
-def fit_batched(gps, iterations=5000, lr=None, stop_crit_improvement_threshold=5e-2, stop_crit_wait_iterations=10,
-                store_hists=False, store_loss_hist=False):
-    """Fit independent single-problem GPs (same class, n, d, alpha, shapes) with the fused MLL loop.
+class _LossReader(object):
+    """Pipelined read-back of the loss history: each enqueued chunk of fit iterations is copied to
+    pinned host memory on a side stream once an event recorded after it fires, so reading chunk k
+    never waits for the chunks enqueued after it (the device loop keeps running)."""
 
-    Returns the list of per-GP `data` dicts that `gp.fit(iterations=..., verbose=0, ...)` would return."""
-    assert len(gps) > 0
-    g0 = gps[0]
-    n = int(g0.n[0])
-    for gp in gps:
-        assert type(gp) is type(g0), "fit_batched needs GPs of one family"
-        assert int(gp.n[0]) == n and gp.d == g0.d and gp._alphas == g0._alphas
-        assert gp._fused_ok(), "every GP must qualify for the fused MLL path"
-        assert gp._problem_batch()[1] == 1, "per-output hyper-parameters: fit those GPs individually"
-        assert gp.raw_lengthscales.shape == g0.raw_lengthscales.shape
-        assert (gp.raw_scale.requires_grad, gp.raw_lengthscales.requires_grad, gp.raw_noise.requires_grad) == \
-               (g0.raw_scale.requires_grad, g0.raw_lengthscales.requires_grad, g0.raw_noise.requires_grad)
-    eng = batched_engine(gps, iterations, lr)
-    dev = g0.device
-    dl = g0.raw_lengthscales.shape[-1]
+    def __init__(self, device):
+        self.side = torch.cuda.Stream(device)
+
+    def submit(self, src):
+        ev = torch.cuda.Event()
+        ev.record()
+        host = torch.empty(src.shape, dtype=src.dtype, pin_memory=True)
+        with torch.cuda.stream(self.side):
+            self.side.wait_event(ev)
+            host.copy_(src, non_blocking=True)
+            done = torch.cuda.Event()
+            done.record(self.side)
+        return host, done
+
+    @staticmethod
+    def get(item):
+        host, done = item
+        done.synchronize()
+        return host
+
+
+def _fit_loop(eng, iterations, stop_crit_improvement_threshold, stop_crit_wait_iterations):
+    """AbstractGP.fit's iteration / early-stopping rule (fastgps/abstract_gp.py:241-289) applied per
+    problem of a per_problem FusedMLL.  Chunks of iterations are enqueued ahead while no problem can
+    have stopped before them (a problem that has waited w iterations stops at the earliest after
+    wait - w more), so the host reads losses without draining the device queue; iterations a problem
+    runs after its stop are discarded (its parameters are restored from the history)."""
     logtol = math.log(1 + stop_crit_improvement_threshold)
-    state = [dict(best=math.inf, save=math.inf, waited=0, best_i=0, stop=None, losses=[]) for _ in gps]
+    wait_max = stop_crit_wait_iterations
+    P = eng.G
     total = iterations + 1
-    i0, chunk = 0, 4
-    while any(s["stop"] is None for s in state) and i0 < total:
-        k = min(chunk, total - i0)
-        eng.run(i0, k, final_no_update=(i0 + k == total))
-        lh = eng.loss_hist[i0:i0 + k, :, 0].cpu()
+    eng.ensure_history(total)
+    reader = _LossReader(eng.device)
+    state = [dict(best=math.inf, save=math.inf, waited=0, best_i=0, stop=None, losses=[]) for _ in range(P)]
+    pending = collections.deque()
+    enq = read = 0
+    chunk = 4
+    while True:
+        active = [s for s in state if s["stop"] is None]
+        if not active:
+            break
+        while enq < total and (enq == read or all(wait_max - s["waited"] > enq - read for s in active)):
+            k = min(chunk, total - enq)
+            eng.run(enq, k, final_no_update=(enq + k == total))
+            pending.append((enq, k, reader.submit(eng.loss_hist[enq:enq + k])))
+            enq += k
+            chunk = min(64, chunk * 2)
+        i0, k, item = pending.popleft()
+        lh = _LossReader.get(item)
         for p, s in enumerate(state):
             if s["stop"] is not None:
                 continue
             for r in range(k):
                 i = i0 + r
-                lv = float(lh[r, p])
+                lv = float(lh[r, p, 0])
                 s["losses"].append(lv)
                 if lv < s["best"]:
                     s["best"], s["best_i"] = lv, i
@@ -56,53 +88,73 @@ def fit_batched(gps, iterations=5000, lr=None, stop_crit_improvement_threshold=5
                     s["save"] = s["best"]
                 else:
                     s["waited"] += 1
-                if i == iterations or s["waited"] == stop_crit_wait_iterations:
+                if i == iterations or s["waited"] == wait_max:
                     s["stop"] = i
                     break
-        i0 += k
-        chunk = min(64, chunk * 2)
+        read = i0 + k
+    for _, _, item in pending:          # drain speculative chunks' copies
+        _LossReader.get(item)
+    return state
+
+
+def _best_raw(eng, state, dl):
+    """[P, 2 + dl] = (raw scale, raw lengthscales, raw noise) of every problem at its best iteration
+    (one gather from the per-iteration parameter history)."""
+    P = eng.G
     S, L, _ = eng.sizes
-    out = []
-    best_rows = eng.raw_hist[torch.tensor([s["best_i"] for s in state], device=dev)]
-    for p, (gp, s) in enumerate(zip(gps, state)):
-        row = best_rows[p]
-        with torch.no_grad():
-            vals = {"raw_scale": row[p:p + 1], "raw_lengthscales": row[S + p * dl:S + (p + 1) * dl],
-                    "raw_noise": row[S + L + p:S + L + p + 1]}
-            for name, v in vals.items():
-                old = getattr(gp, name)
-                setattr(gp, name, torch.nn.Parameter(v.reshape(old.shape).clone(), requires_grad=old.requires_grad))
+    rows, cols = [], []
+    for p, s in enumerate(state):
+        c = [p] + [S + p * dl + j for j in range(dl)] + [S + L + p]
+        rows += [s["best_i"]] * len(c)
+        cols += c
+    idx_r = torch.tensor(rows, dtype=torch.int64).to(eng.device, non_blocking=True)
+    idx_c = torch.tensor(cols, dtype=torch.int64).to(eng.device, non_blocking=True)
+    return eng.raw_hist[idx_r, idx_c].reshape(P, 2 + dl)
+
+
+def _check_batch(gps):
+    assert len(gps) > 0
+    g0 = gps[0]
+    n = g0._nh
+    for gp in gps:
+        assert type(gp) is type(g0), "a GP batch needs GPs of one family"
+        assert gp._nh == n and gp.d == g0.d and gp._alphas == g0._alphas and gp.device == g0.device
+        assert gp._fused_ok(), "every GP must qualify for the fused MLL path"
+        assert gp._problem_batch()[1] == 1, "per-output hyper-parameters: fit those GPs individually"
+        assert gp.raw_lengthscales.shape == g0.raw_lengthscales.shape
+        assert (gp.raw_scale.requires_grad, gp.raw_lengthscales.requires_grad, gp.raw_noise.requires_grad) == \
+               (g0.raw_scale.requires_grad, g0.raw_lengthscales.requires_grad, g0.raw_noise.requires_grad)
+    return g0, n
+
+
+def _parts_source(gps, n):
+    """Lattice GPs sharing one generating vector regenerate their parts in the kernels (only the P
+    shifts are stacked); otherwise a stacked [P, d, n] parts array."""
+    gens = [gp._parts_gen(n) for gp in gps]
+    if all(g is not None for g in gens) and all(g.z == gens[0].z for g in gens):
+        return None, LatticePartsGen(gens[0].z, gens[0].alphas, torch.cat([g.shift for g in gens], 0))
+    g0 = gps[0]
+    parts = torch.empty((len(gps), g0.d, n), dtype=torch.float64, device=g0.device)
+    for p, gp in enumerate(gps):
+        gp._k1parts(n, out=parts[p])
+    return parts, None
+
+
+def _set_raw(gps, raw, dl):
+    """Install raw[p] = (scale, lengthscales, noise) as GP p's raw parameters (views: no copies)."""
+    for p, gp in enumerate(gps):
+        vals = {"raw_scale": raw[p, 0:1], "raw_lengthscales": raw[p, 1:1 + dl], "raw_noise": raw[p, 1 + dl:2 + dl]}
+        for name, v in vals.items():
+            old = getattr(gp, name)
+            setattr(gp, name, torch.nn.Parameter(v.reshape(old.shape), requires_grad=old.requires_grad))
         gp._cache = {}
         gp._snap = None
-        data = {"iterations": s["stop"]}
-        if store_hists or store_loss_hist:
-            data["loss_hist"] = torch.tensor([-v for v in s["losses"]])
-        out.append(data)
-    return out
 
 
-def batched_engine(gps, iterations, lr=None):
-    """The FusedMLL (per_problem mode) over the GPs' stacked problems: Y = |ytilde|^2 rows and raw
-    parameters stacked, the kernel parts regenerated in the kernels for lattice GPs sharing one
-    generating vector (otherwise a stacked [P, d, n] parts array)."""
+def _engine(gps, n, ysq, parts, gen, lr, iterations):
     g0 = gps[0]
-    n = int(g0.n[0])
-    P = len(gps)
-    d = g0.d
-    dev = g0.device
-    gens = [gp._parts_gen(n) for gp in gps]
-    gen = None
-    if all(g is not None for g in gens) and all(g.z == gens[0].z for g in gens):
-        # lattice points regenerated in the kernels; only the P shifts (= x[0] rows) are stacked
-        gen = LatticePartsGen(gens[0].z, gens[0].alphas, torch.cat([g.shift for g in gens], 0))
-        parts = None
-    else:
-        parts = torch.empty((P, d, n), dtype=torch.float64, device=dev)
-        for p, gp in enumerate(gps):
-            gp._k1parts(n, out=parts[p])
-    ysq = torch.stack([gp._ysq(*gp._problem_batch())[0] for gp in gps])
-    d_out = int(torch.tensor(g0.shape_batch).prod())
     dl = g0.raw_lengthscales.shape[-1]
+    d_out = int(torch.tensor(g0.shape_batch).prod())
     return FusedMLL(g0._FAMILY, parts, ysq,
                     torch.stack([gp.raw_scale.detach().reshape(-1)[0] for gp in gps]),
                     torch.stack([gp.raw_lengthscales.detach().reshape(dl) for gp in gps]),
@@ -110,5 +162,225 @@ def batched_engine(gps, iterations, lr=None):
                     logdet_weight=float(d_out), mll_const=mll_constant(d_out, n),
                     requires_grad=(g0.raw_scale.requires_grad, g0.raw_lengthscales.requires_grad,
                                    g0.raw_noise.requires_grad),
-                    lr=1e-1 if lr is None else lr, max_iters=min(iterations + 1, 64), parts_per_problem=True,
+                    lr=1e-1 if lr is None else lr, max_iters=iterations + 1, parts_per_problem=True,
                     per_problem=True, gen=gen)
+
+
+def _fit_data(state, store):
+    out = []
+    for s in state:
+        data = {"iterations": s["stop"]}
+        if store:
+            data["loss_hist"] = torch.tensor([-v for v in s["losses"]])
+        out.append(data)
+    return out
+
+
+def fit_batched(gps, iterations=5000, lr=None, stop_crit_improvement_threshold=5e-2, stop_crit_wait_iterations=10,
+                store_hists=False, store_loss_hist=False):
+    """Fit independent single-problem GPs (same class, n, d, alpha, shapes) with the fused MLL loop.
+
+    Returns the list of per-GP `data` dicts that `gp.fit(iterations=..., verbose=0, ...)` would return."""
+    g0, n = _check_batch(gps)
+    eng = batched_engine(gps, iterations, lr)
+    state = _fit_loop(eng, iterations, stop_crit_improvement_threshold, stop_crit_wait_iterations)
+    _set_raw(gps, _best_raw(eng, state, g0.raw_lengthscales.shape[-1]).clone(), g0.raw_lengthscales.shape[-1])
+    return _fit_data(state, store_hists or store_loss_hist)
+
+
+def batched_engine(gps, iterations, lr=None):
+    """The FusedMLL (per_problem mode) over the GPs' stacked problems: Y = |ytilde|^2 rows and raw
+    parameters stacked, the kernel parts regenerated in the kernels for lattice GPs sharing one
+    generating vector (otherwise a stacked [P, d, n] parts array)."""
+    n = gps[0]._nh
+    parts, gen = _parts_source(gps, n)
+    ysq = torch.stack([gp._ysq(*gp._problem_batch())[0] for gp in gps])
+    return _engine(gps, n, ysq, parts, gen, lr, iterations)
+
+
+class GPBatch(object):
+    """P independent single-output fast GPs of one family, n, d and smoothness held in stacked device
+    buffers: ytilde [P, n], Y = |ytilde|^2, training points [P, d, n] (each GP's cached dimension-major
+    points become views of it), fitted raw parameters [P, 2 + dl], coefficients [P, n] and the
+    eigenvalue weights Re(1/ev) [P, n].  Methods mirror the per-GP API and return [P, ...] stacks."""
+
+    def __init__(self, gps):
+        gps = list(gps)
+        g0, n = _check_batch(gps)
+        for gp in gps:
+            assert gp.shape_batch == torch.Size([]), "GPBatch holds single-output GPs"
+        self.gps = gps
+        self.P = len(gps)
+        self.n = n
+        self.m = ops.log2_exact(n)
+        self.d = g0.d
+        self.family = g0._FAMILY
+        self.device = g0.device
+        self.dl = g0.raw_lengthscales.shape[-1]
+        self.z = torch.empty((self.P, self.d, n), dtype=g0._XBDTYPE, device=self.device)
+        for p, gp in enumerate(gps):
+            self.z[p].copy_(gp._points_T(n))
+            gp._pts_T = (n, self.z[p])
+        self.part0 = [float(v) for v in g0._part_at_zero()]
+        self.tbits = g0._tbits()
+        self._n_t = torch.tensor([n], dtype=torch.int64, device=self.device)
+        self._m_t = torch.tensor([self.m], dtype=torch.int64, device=self.device)
+        self._y = None
+        self._st = {}
+        self._src = None
+
+    # ---------------------------------------------------------------------------- data / parameters
+    def set_data(self, y):
+        """Give GP p the observations y[p] at its n points ([P, n]): AbstractGP.add_y_next
+        (fastgps/abstract_gp.py:331-351) on GPs without data, for all P at once."""
+        y = y.to(device=self.device, dtype=torch.float64)
+        assert y.shape == (self.P, self.n)
+        for p, gp in enumerate(self.gps):
+            gp._y[0] = y[p]
+            gp._nh = self.n
+            gp.n, gp.m = self._n_t, self._m_t
+            gp._cache = {}
+        self._y = y
+        self._st = {}
+
+    def set_raw(self, raw):
+        """Set every GP's raw (log) hyper-parameters from raw [P, 2 + dl] = (scale, lengthscales, noise)."""
+        assert raw.shape == (self.P, 2 + self.dl)
+        _set_raw(self.gps, raw, self.dl)
+        for k in ("raw", "coeffs", "wa", "hyp"):
+            self._st.pop(k, None)
+        self._put_ytilde()
+
+    def raw(self):
+        if "raw" not in self._st:
+            self._st["raw"] = torch.stack([torch.cat([gp.raw_scale.detach().reshape(1),
+                                                      gp.raw_lengthscales.detach().reshape(self.dl),
+                                                      gp.raw_noise.detach().reshape(1)]) for gp in self.gps])
+        return self._st["raw"]
+
+    def _source(self):
+        if self._src is None:
+            self._src = _parts_source(self.gps, self.n)
+        return self._src
+
+    def _put_ytilde(self):
+        yt = self._st.get("yt")
+        if yt is not None:
+            for p, gp in enumerate(self.gps):
+                gp._cache[("ytilde", self.n, False, False)] = yt[p]
+
+    def ytilde(self):
+        """[P, n] ytilde = ft(y) of every GP (AbstractFastGP.get_ytilde / _YtildeCache, util.py:164-183),
+        one batched transform; also installed in each GP's cache."""
+        if "yt" not in self._st:
+            y = self._y if self._y is not None else torch.stack([gp._y[0] for gp in self.gps])
+            if self.family == ops.LATTICE:
+                yt = ops.fftbr_raw(y, stable=True)
+            else:
+                yt = ops.fwht_raw(y, stable=True)
+            self._st["yt"] = yt
+            self._put_ytilde()
+        return self._st["yt"]
+
+    def ysq(self):
+        if "ysq" not in self._st:
+            yt = self.ytilde()
+            self._st["ysq"] = (yt.real ** 2 + yt.imag ** 2) if yt.is_complex() else yt ** 2
+        return self._st["ysq"]
+
+    # ---------------------------------------------------------------------------- fit
+    def fit(self, iterations=5000, lr=None, stop_crit_improvement_threshold=5e-2, stop_crit_wait_iterations=10,
+            store_hists=False, store_loss_hist=False):
+        """Every GP's AbstractGP.fit(loss_metric="MLL", verbose=0) in one device loop; returns the list of
+        per-GP data dicts."""
+        parts, gen = self._source()
+        eng = _engine(self.gps, self.n, self.ysq(), parts, gen, lr, iterations)
+        state = _fit_loop(eng, iterations, stop_crit_improvement_threshold, stop_crit_wait_iterations)
+        best = _best_raw(eng, state, self.dl)
+        self.set_raw(best)
+        self._st["raw"] = best
+        return _fit_data(state, store_hists or store_loss_hist)
+
+    # ---------------------------------------------------------------------------- predict
+    def coeffs(self):
+        """[P, n] K^-1 y of every GP (_CoeffsCache, util.py:396-425): lambda by fgp_nll_lam, A = 1/ev and
+        ytilde * A by fgp_inv_eig, one batched inverse transform."""
+        if "coeffs" not in self._st:
+            raw = self.raw()
+            parts, gen = self._source()
+            dl = self.dl
+            lam = fused_lam(self.family, parts, raw[:, 0], raw[:, 1:1 + dl], raw[:, 1 + dl], self.P, gen=gen, n=self.n)
+            yt = self.ytilde()
+            ya = torch.empty_like(lam)
+            wa = torch.empty((self.P, self.n), dtype=torch.float64, device=self.device)
+            noise = raw[:, 1 + dl:]
+            N.call("fgp_inv_eig", self.family, N.ptr(lam), N.ptr(yt), yt.stride(0), N.ptr(noise), raw.stride(0),
+                   self.P, self.m, N.ptr(ya), N.ptr(wa), N.stream_ptr(self.device))
+            if self.family == ops.LATTICE:
+                self._st["coeffs"] = ops.ifftbr_raw(ya, stable=True, real_out=True)
+            else:
+                self._st["coeffs"] = ops.fwht_raw(ya, stable=True)
+            self._st["wa"] = wa
+        return self._st["coeffs"]
+
+    def _hyp(self):
+        if "hyp" not in self._st:
+            h = torch.exp(self.raw()[:, :1 + self.dl])
+            if self.dl != self.d:
+                h = torch.cat([h[:, :1], h[:, 1:2].expand(self.P, self.d)], 1)
+            self._st["hyp"] = h.contiguous()
+        return self._st["hyp"]
+
+    def _desc(self):
+        order, coef = ops._pred_args(self.family, self.gps[0]._alphas, self.d)
+        hyp = self._hyp()
+        coeffs = self._st["coeffs"]
+        wa = self._st["wa"]
+        desc = N.PredDesc(family=self.family, d=self.d, tbits=int(self.tbits), P=self.P, n=self.n,
+                          z=self.z.data_ptr(), z_stride=self.d * self.n, hyp=hyp.data_ptr(), hyp_stride=hyp.stride(0),
+                          coeffs=coeffs.data_ptr(), coeff_stride=coeffs.stride(0), wa=wa.data_ptr(),
+                          wa_stride=wa.stride(0))
+        for j in range(self.d):
+            desc.order[j] = order[j]
+            desc.coef[j] = coef[j]
+        return desc
+
+    def _points(self, x):
+        x = x.to(device=self.device, dtype=torch.float64)
+        assert (x.ndim == 2 and x.size(1) == self.d) or (x.ndim == 3 and x.shape[0] == self.P and x.size(2) == self.d), \
+            "x must have shape (N, d) (shared) or (P, N, d)"
+        assert bool(((0 <= x) & (x <= 1)).all()), "x should have all elements in [0,1]"
+        x = x.contiguous()
+        return x, (0 if x.ndim == 2 else x.stride(0)), x.shape[-2]
+
+    def post_mean(self, x):
+        """[P, N] posterior means (AbstractGP.post_mean of every GP, abstract_gp.py:352-380)."""
+        self.coeffs()
+        x, xs, Nt = self._points(x)
+        nchunks = (self.n + 1023) // 1024
+        work = torch.empty(nchunks * self.P * Nt, dtype=torch.float64, device=self.device)
+        out = torch.empty((self.P, Nt), dtype=torch.float64, device=self.device)
+        N.call("fgp_post_mean_batched", self._desc(), N.ptr(x), xs, Nt, N.ptr(out), N.ptr(work),
+               N.stream_ptr(self.device))
+        return out
+
+    def post_var(self, x, chunk=16):
+        """[P, N] posterior variances at the GPs' current n (AbstractGP.post_var, abstract_gp.py:381-416)."""
+        if self.m < 13:
+            return torch.stack([gp.post_var(x) for gp in self.gps])
+        self.coeffs()
+        x, xs, Nt = self._points(x)
+        out = torch.empty((self.P, Nt), dtype=torch.float64, device=self.device)
+        cdt = torch.complex128 if self.family == ops.LATTICE else torch.float64
+        desc = self._desc()
+        part0 = N.double_array(self.part0)
+        for t0 in range(0, Nt, chunk):
+            t1 = min(Nt, t0 + chunk)
+            xc = x[..., t0:t1, :].contiguous()
+            work = torch.empty((self.P, t1 - t0, self.n), dtype=cdt, device=self.device)
+            partial = torch.empty((self.P, t1 - t0, self.n >> 12), dtype=torch.float64, device=self.device)
+            oc = torch.empty((self.P, t1 - t0), dtype=torch.float64, device=self.device)
+            N.call("fgp_post_var_batched", desc, N.ptr(xc), (0 if xc.ndim == 2 else xc.stride(0)), t1 - t0, part0,
+                   N.ptr(oc), N.ptr(work), N.ptr(partial), N.stream_ptr(self.device))
+            out[:, t0:t1] = oc
+        return out

@@ -28,6 +28,13 @@ struct PredSpec {
   double coef[FGP_MAX_D];
 };
 
+// Element strides between consecutive problems of a batch of independent GPs (all 0: one problem):
+// test points x, training points z ([d][n] per problem), hyper-parameter rows h, coefficients /
+// eigenvalue weights c.
+struct ProbStrides {
+  int64_t x, z, h, c;
+};
+
 // ------------------------------------------------------------------------------------------------
 // Per-factor arithmetic.  Lattice: even Bernoulli polynomials are polynomials in u = t(t - 1), and
 // B_{2a}((x - z) % 1) = B_{2a}(|x - z|) exactly for x, z in [0, 1] (B_{2a}(1 - t) = B_{2a}(t)), so
@@ -75,12 +82,19 @@ __global__ __launch_bounds__(kWG) void k_post_mean(const double* __restrict__ xt
                                                     int64_t n, PredSpec spec, int tbits,
                                                     const double* __restrict__ hyp, int Gk,
                                                     const double* __restrict__ coeffs, int64_t coeff_stride, int B,
-                                                    double* __restrict__ partial, int64_t nchunks) {
+                                                    double* __restrict__ partial, int64_t nchunks, ProbStrides ps) {
   __shared__ double zs[D][kSlab];
   __shared__ double cs[NB][kSlab];
   const int tid = threadIdx.x;
   const int64_t t = (int64_t)blockIdx.y * kWG + tid;
   const bool live = t < N;
+  // problem p of a batch of independent GPs (fgp_post_mean_batched); p = 0 otherwise
+  const int64_t p = blockIdx.z;
+  xt += p * ps.x;
+  z = static_cast<const char*>(z) + p * ps.z * 8;
+  hyp += p * ps.h;
+  coeffs += p * ps.c;
+  partial += p * (int64_t)B * N * nchunks;
   double xv[D];
   unsigned long long xbv[D];
 #pragma unroll
@@ -210,8 +224,9 @@ struct QfArgs {
   PredSpec spec;
   const double* hyp;         // device [1 + d]: scale, lengthscales
   const double* wa;          // [n] Re(A)
-  void* work;                // [N][n]
-  double* partial;           // [N][n / 4096]
+  void* work;                // [P][N][n]
+  double* partial;           // [P][N][n / 4096]
+  ProbStrides ps;            // per-problem strides of xt, z, hyp, wa (batched GPs; 0 for one problem)
 };
 
 template <int P2, typename T>
@@ -223,16 +238,20 @@ __global__ __launch_bounds__(kWG) void k_qf_rows(QfArgs q, const double2* __rest
   const int m = q.log2n, m1 = m - P2;
   const int64_t n = (int64_t)1 << m;
   const int64_t tiles = n >> kTileLog;
-  const int t = (int)(blockIdx.x / tiles);
+  const int tg = (int)(blockIdx.x / tiles);           // (problem, test point) row of work
+  const int pb = tg / q.N, t = tg % q.N;
   const int row0 = (int)(blockIdx.x % tiles) * RPW;
   const int tid = threadIdx.x;
+  const double* xt = q.xt + pb * q.ps.x;
+  const double* hyp = q.hyp + pb * q.ps.h;
+  const void* zp = static_cast<const char*>(q.z) + pb * q.ps.z * 8;
   double xv[FGP_MAX_D], fa[FGP_MAX_D], fc[FGP_MAX_D];
   unsigned long long xb[FGP_MAX_D];
-  const double scale = q.hyp[0];
+  const double scale = hyp[0];
 #pragma unroll
   for (int j = 0; j < FGP_MAX_D; ++j) {
-    xv[j] = j < q.d ? q.xt[(int64_t)t * q.d + j] : 0.0;
-    const double l = j < q.d ? q.hyp[1 + j] : 0.0;
+    xv[j] = j < q.d ? xt[(int64_t)t * q.d + j] : 0.0;
+    const double l = j < q.d ? hyp[1 + j] : 0.0;
     if constexpr (FAM == 0) {
       fa[j] = l * q.spec.coef[j];
       fc[j] = fac_const(q.spec.order[j], fa[j]);
@@ -253,11 +272,11 @@ __global__ __launch_bounds__(kWG) void k_qf_rows(QfArgs q, const double2* __rest
     for (int j = 0; j < FGP_MAX_D; ++j) {
       if (j < q.d) {
         if constexpr (FAM == 0) {
-          const double2 zv = *reinterpret_cast<const double2*>(static_cast<const double*>(q.z) + (int64_t)j * n + base + e);
+          const double2 zv = *reinterpret_cast<const double2*>(static_cast<const double*>(zp) + (int64_t)j * n + base + e);
           p0 *= lat_factor(q.spec.order[j], fabs(xv[j] - zv.x), fa[j], fc[j]);
           p1 *= lat_factor(q.spec.order[j], fabs(xv[j] - zv.y), fa[j], fc[j]);
         } else {
-          const longlong2 zv = *reinterpret_cast<const longlong2*>(static_cast<const long long*>(q.z) + (int64_t)j * n + base + e);
+          const longlong2 zv = *reinterpret_cast<const longlong2*>(static_cast<const long long*>(zp) + (int64_t)j * n + base + e);
           p0 *= net_factor(xb[j] ^ (unsigned long long)zv.x, q.tbits, fa[j], fc[j]);
           p1 *= net_factor(xb[j] ^ (unsigned long long)zv.y, q.tbits, fa[j], fc[j]);
         }
@@ -301,7 +320,7 @@ __global__ __launch_bounds__(kWG) void k_qf_rows(QfArgs q, const double2* __rest
     T* s = lds + (tid / TL) * (N2 + N2 / 16);
     center_transform<P2, false>(s, tid % TL, 1, red, tw);
   }
-  T* out = static_cast<T*>(q.work) + (int64_t)t * n + base;
+  T* out = static_cast<T*>(q.work) + (int64_t)tg * n + base;
   if constexpr (FAM == 0 && RPW == 1) {
     const RowTwiddle rt((unsigned)row0, tid, P2, m1, tw, twm);
 #pragma unroll
@@ -337,11 +356,12 @@ __global__ __launch_bounds__(kWG) void k_qf_cols(QfArgs q, const double2* __rest
   const int m = q.log2n;
   const int64_t n = (int64_t)1 << m, N2 = n >> P1;
   const int64_t tiles = n >> kTileLog;
-  const int t = (int)(blockIdx.x / tiles);
+  const int tg = (int)(blockIdx.x / tiles);
   const int blk = (int)(blockIdx.x % tiles);
   const int64_t c0 = (int64_t)blk * C;
   const int tid = threadIdx.x;
-  const T* in = static_cast<const T*>(q.work) + (int64_t)t * n + c0;
+  const T* in = static_cast<const T*>(q.work) + (int64_t)tg * n + c0;
+  const double* wa = q.wa + (tg / q.N) * q.ps.c;
   const int cl = tid % C, col = tid / TL;
   T v[16];
   T sum = zero_v<T>();
@@ -363,47 +383,94 @@ __global__ __launch_bounds__(kWG) void k_qf_cols(QfArgs q, const double2* __rest
   for (int k = 0; k < 16; ++k) {
     const int e = tid + k * kWG;
     const int c = e % C, r = e / C;
-    acc += sqabs(lds[c * CS + padi(r)]) * inv_n * q.wa[(int64_t)r * N2 + c0 + c];
+    acc += sqabs(lds[c * CS + padi(r)]) * inv_n * wa[(int64_t)r * N2 + c0 + c];
   }
   acc = block_sum(acc, redd);
-  if (tid == 0) q.partial[(int64_t)t * tiles + blk] = acc;
+  if (tid == 0) q.partial[(int64_t)tg * tiles + blk] = acc;
+}
+
+// Posterior variance of (problem p, test point t) from its quadratic-form partials:
+//   out = K(x, x) - sum_c partial[c], negative values set to 0 (abstract_gp.py:407-413), with
+//   K(x, x) = scale * prod_j (1 + l_j part0_j), AbstractFastGP._kernel at zero distance.
+__global__ __launch_bounds__(kWG) void k_qf_finish(const double* __restrict__ partial, int64_t nchunks,
+                                                    const double* __restrict__ hyp, int64_t hps, PredSpec part0,
+                                                    int d, int64_t N, double* __restrict__ out) {
+  __shared__ double red[kWG / 64];
+  const int64_t e = blockIdx.x;
+  double s = 0.0;
+  for (int64_t c = threadIdx.x; c < nchunks; c += kWG) s += partial[e * nchunks + c];
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) {
+    const double* h = hyp + (e / N) * hps;
+    double pr = 1.0;
+    for (int j = 0; j < d; ++j) pr *= 1.0 + h[1 + j] * part0.coef[j];
+    const double v = h[0] * pr - s;
+    out[e] = v < 0.0 ? 0.0 : v;
+  }
+}
+
+// A = 1 / ev, ev = sqrt(n) lam + noise (util.py:285,292-300), and the coefficient-solve input
+// ya = ytilde * A (util.py:341-342 with the cached ytilde); wa = Re(A), the post_var weights.
+template <typename T>
+__global__ __launch_bounds__(kWG) void k_inv_eig(const T* __restrict__ lam, const T* __restrict__ yt, int64_t yts,
+                                                  const double* __restrict__ raw_noise, int64_t nzs, double rootn,
+                                                  int log2n, int64_t total, T* __restrict__ ya,
+                                                  double* __restrict__ wa) {
+  const int64_t e = (int64_t)blockIdx.x * kWG + threadIdx.x;
+  if (e >= total) return;
+  const int64_t p = e >> log2n, i = e & (((int64_t)1 << log2n) - 1);
+  const double noise = exp(raw_noise[p * nzs]);
+  const T l = lam[e];
+  const T y = yt[p * yts + i];
+  if constexpr (sizeof(T) == 16) {
+    const double ar = rootn * l.x + noise, ai = rootn * l.y;
+    const double inv = 1.0 / (ar * ar + ai * ai);
+    const double rr = ar * inv, ri = -ai * inv;
+    ya[e] = make_double2(y.x * rr - y.y * ri, y.x * ri + y.y * rr);
+    if (wa) wa[e] = rr;
+  } else {
+    const double a = 1.0 / (rootn * l + noise);
+    ya[e] = y * a;
+    if (wa) wa[e] = a;
+  }
 }
 
 template <int FAM, int D>
 static void post_mean_d(dim3 grid, hipStream_t st, bool uniform4, int B, const double* xt, int64_t N, const void* z,
                         int64_t n, const PredSpec& spec, int tbits, const double* hyp, int Gk, const double* coeffs,
-                        int64_t cstride, double* work, int64_t nchunks) {
+                        int64_t cstride, double* work, int64_t nchunks, const ProbStrides& ps) {
   if (B == 1) {
     if (FAM == 1 || uniform4)
-      k_post_mean<FAM, D, 1, 4><<<grid, kWG, 0, st>>>(xt, N, z, n, spec, tbits, hyp, Gk, coeffs, cstride, B, work, nchunks);
+      k_post_mean<FAM, D, 1, 4><<<grid, kWG, 0, st>>>(xt, N, z, n, spec, tbits, hyp, Gk, coeffs, cstride, B, work, nchunks, ps);
     else
-      k_post_mean<FAM, D, 1, 0><<<grid, kWG, 0, st>>>(xt, N, z, n, spec, tbits, hyp, Gk, coeffs, cstride, B, work, nchunks);
+      k_post_mean<FAM, D, 1, 0><<<grid, kWG, 0, st>>>(xt, N, z, n, spec, tbits, hyp, Gk, coeffs, cstride, B, work, nchunks, ps);
   } else {
     if (FAM == 1 || uniform4)
-      k_post_mean<FAM, D, kPmB, 4><<<grid, kWG, 0, st>>>(xt, N, z, n, spec, tbits, hyp, Gk, coeffs, cstride, B, work, nchunks);
+      k_post_mean<FAM, D, kPmB, 4><<<grid, kWG, 0, st>>>(xt, N, z, n, spec, tbits, hyp, Gk, coeffs, cstride, B, work, nchunks, ps);
     else
-      k_post_mean<FAM, D, kPmB, 0><<<grid, kWG, 0, st>>>(xt, N, z, n, spec, tbits, hyp, Gk, coeffs, cstride, B, work, nchunks);
+      k_post_mean<FAM, D, kPmB, 0><<<grid, kWG, 0, st>>>(xt, N, z, n, spec, tbits, hyp, Gk, coeffs, cstride, B, work, nchunks, ps);
   }
 }
 
 template <int FAM>
 static int launch_post_mean(int d, const double* xt, int64_t N, const void* z, int64_t n, const PredSpec& spec, int tbits,
                             const double* hyp, int Gk, const double* coeffs, int64_t cstride, int B, double* out,
-                            int64_t out_stride, double* work, hipStream_t st) {
+                            int64_t out_stride, double* work, hipStream_t st, int P = 1,
+                            ProbStrides ps = ProbStrides{0, 0, 0, 0}) {
   const int64_t nchunks = (n + kChunk - 1) / kChunk;
-  const dim3 grid((unsigned)nchunks, (unsigned)((N + kWG - 1) / kWG));
+  const dim3 grid((unsigned)nchunks, (unsigned)((N + kWG - 1) / kWG), (unsigned)P);
   bool uniform4 = true;
   for (int j = 0; j < d; ++j) uniform4 = uniform4 && spec.order[j] == 4;
   switch (d) {
 #define FGP_C(DD) \
-  case DD: post_mean_d<FAM, DD>(grid, st, uniform4, B, xt, N, z, n, spec, tbits, hyp, Gk, coeffs, cstride, work, nchunks); break;
+  case DD: post_mean_d<FAM, DD>(grid, st, uniform4, B, xt, N, z, n, spec, tbits, hyp, Gk, coeffs, cstride, work, nchunks, ps); break;
     FGP_C(1) FGP_C(2) FGP_C(3) FGP_C(4) FGP_C(5) FGP_C(6) FGP_C(7) FGP_C(8)
 #undef FGP_C
     default: return set_error(kErrUnsupported, "post_mean: d=%d unsupported", d);
   }
   int rc = check_launch("k_post_mean");
   if (rc != kOk) return rc;
-  k_sum_chunks<<<(unsigned)((int64_t)B * N), kWG, 0, st>>>(work, nchunks, out, out_stride, N);
+  k_sum_chunks<<<(unsigned)((int64_t)P * B * N), kWG, 0, st>>>(work, nchunks, out, out_stride, N);
   return check_launch("k_sum_chunks");
 }
 
@@ -454,15 +521,13 @@ int fgp_post_mean(int family, const double* xt, int64_t N, const void* z, int64_
   return launch_post_mean<1>(d, xt, N, z, n, spec, tbits, hyp, Gk, coeffs, coeff_stride, B, out, out_stride, work, st);
 }
 
-int fgp_post_var_qf(int family, const double* xt, int64_t N, const void* z, int log2n, int d, int tbits,
-                    const int* order, const double* coef, const double* hyp, const double* wa, void* work,
-                    double* partial, double* out, void* stream) {
-  if (N < 0 || d < 1 || d > FGP_MAX_D || log2n < 13 || log2n > kMaxLog2N)
-    return set_error(kErrInvalid, "fgp_post_var_qf: needs 13 <= log2n <= 24 and 1 <= d <= %d", FGP_MAX_D);
-  if (N == 0) return kOk;
-  if (!xt || !z || !hyp || !wa || !work || !partial || !out) return set_error(kErrInvalid, "fgp_post_var_qf: null pointer");
-  if ((N << (log2n - kTileLog)) >= ((int64_t)1 << 31)) return set_error(kErrUnsupported, "fgp_post_var_qf: N too large");
-  hipStream_t st = (hipStream_t)stream;
+}  // extern "C"
+
+namespace fgp {
+// quadratic-form partials of P problems x N test points (k_qf_rows + k_qf_cols)
+static int launch_qf(int family, const double* xt, int64_t N, const void* z, int log2n, int d, int tbits,
+                     const PredSpec& spec, const double* hyp, const double* wa, void* work, double* partial, int64_t P,
+                     const ProbStrides& ps, hipStream_t st) {
   const Tables* tb = get_tables(st);
   if (!tb) return set_error(kErrHip, "twiddle table initialisation failed");
   QfArgs q;
@@ -472,14 +537,15 @@ int fgp_post_var_qf(int family, const double* xt, int64_t N, const void* z, int 
   q.N = (int)N;
   q.xt = xt;
   q.z = z;
-  int rc = make_spec(family, d, order, coef, q.spec);
-  if (rc != kOk) return rc;
+  q.spec = spec;
   q.hyp = hyp;
   q.wa = wa;
   q.work = work;
   q.partial = partial;
+  q.ps = ps;
+  int rc;
   const int m2 = split_m2(log2n), m1 = log2n - m2;
-  const dim3 grid((unsigned)(N << (log2n - kTileLog)));
+  const dim3 grid((unsigned)((P * N) << (log2n - kTileLog)));
   const double2* tw = tb->tw4096;
   const double2* twm = tb->twm[log2n];
   if (family == FGP_FAMILY_LATTICE) {
@@ -509,9 +575,98 @@ int fgp_post_var_qf(int family, const double* xt, int64_t N, const void* z, int 
 #undef FGP_C
     }
   }
-  if ((rc = check_launch("k_qf_cols")) != kOk) return rc;
+  return check_launch("k_qf_cols");
+}
+}  // namespace fgp
+
+extern "C" {
+
+int fgp_post_var_qf(int family, const double* xt, int64_t N, const void* z, int log2n, int d, int tbits,
+                    const int* order, const double* coef, const double* hyp, const double* wa, void* work,
+                    double* partial, double* out, void* stream) {
+  if (N < 0 || d < 1 || d > FGP_MAX_D || log2n < 13 || log2n > kMaxLog2N)
+    return set_error(kErrInvalid, "fgp_post_var_qf: needs 13 <= log2n <= 24 and 1 <= d <= %d", FGP_MAX_D);
+  if (N == 0) return kOk;
+  if (!xt || !z || !hyp || !wa || !work || !partial || !out) return set_error(kErrInvalid, "fgp_post_var_qf: null pointer");
+  if ((N << (log2n - kTileLog)) >= ((int64_t)1 << 31)) return set_error(kErrUnsupported, "fgp_post_var_qf: N too large");
+  PredSpec spec;
+  int rc = make_spec(family, d, order, coef, spec);
+  if (rc != kOk) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  rc = launch_qf(family, xt, N, z, log2n, d, tbits, spec, hyp, wa, work, partial, 1, ProbStrides{0, 0, 0, 0}, st);
+  if (rc != kOk) return rc;
   k_sum_chunks<<<(unsigned)N, kWG, 0, st>>>(partial, (int64_t)1 << (log2n - kTileLog), out, N, N);
   return check_launch("k_sum_chunks");
+}
+
+int fgp_post_mean_batched(const fgp_pred_desc* pd, const double* xt, int64_t xt_stride, int64_t N, double* out,
+                          double* work, void* stream) {
+  if (!pd) return set_error(kErrInvalid, "fgp_post_mean_batched: null desc");
+  const int d = pd->d;
+  if (N < 0 || pd->n < 1 || d < 1 || d > FGP_MAX_D || pd->P < 1 || pd->P > 65535)
+    return set_error(kErrInvalid, "fgp_post_mean_batched: bad sizes");
+  if (N == 0) return kOk;
+  if (!xt || !pd->z || !pd->hyp || !pd->coeffs || !out || !work)
+    return set_error(kErrInvalid, "fgp_post_mean_batched: null pointer");
+  PredSpec spec;
+  int rc = make_spec(pd->family, d, pd->order, pd->coef, spec);
+  if (rc != kOk) return rc;
+  const ProbStrides ps{xt_stride, pd->z_stride, pd->hyp_stride, pd->coeff_stride};
+  hipStream_t st = (hipStream_t)stream;
+  if (pd->family == FGP_FAMILY_LATTICE)
+    return launch_post_mean<0>(d, xt, N, pd->z, pd->n, spec, pd->tbits, pd->hyp, 1, pd->coeffs, pd->n, 1, out, N, work,
+                               st, pd->P, ps);
+  return launch_post_mean<1>(d, xt, N, pd->z, pd->n, spec, pd->tbits, pd->hyp, 1, pd->coeffs, pd->n, 1, out, N, work, st,
+                             pd->P, ps);
+}
+
+int fgp_post_var_batched(const fgp_pred_desc* pd, const double* xt, int64_t xt_stride, int64_t N, const double* part0,
+                         double* out, void* work, double* partial, void* stream) {
+  if (!pd) return set_error(kErrInvalid, "fgp_post_var_batched: null desc");
+  const int d = pd->d;
+  int log2n = 0;
+  while (((int64_t)1 << log2n) < pd->n) ++log2n;
+  if (((int64_t)1 << log2n) != pd->n || N < 0 || d < 1 || d > FGP_MAX_D || log2n < 13 || log2n > kMaxLog2N ||
+      pd->P < 1)
+    return set_error(kErrInvalid, "fgp_post_var_batched: needs n = 2^m, 13 <= m <= 24, 1 <= d <= %d", FGP_MAX_D);
+  if (N == 0) return kOk;
+  if (!xt || !pd->z || !pd->hyp || !pd->wa || !part0 || !out || !work || !partial)
+    return set_error(kErrInvalid, "fgp_post_var_batched: null pointer");
+  if (((int64_t)pd->P * N << (log2n - kTileLog)) >= ((int64_t)1 << 31))
+    return set_error(kErrUnsupported, "fgp_post_var_batched: P * N too large");
+  PredSpec spec, p0;
+  int rc = make_spec(pd->family, d, pd->order, pd->coef, spec);
+  if (rc != kOk) return rc;
+  for (int j = 0; j < FGP_MAX_D; ++j) {
+    p0.order[j] = 0;
+    p0.coef[j] = j < d ? part0[j] : 0.0;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  rc = launch_qf(pd->family, xt, N, pd->z, log2n, d, pd->tbits, spec, pd->hyp, pd->wa, work, partial, pd->P,
+                 ProbStrides{xt_stride, pd->z_stride, pd->hyp_stride, pd->wa_stride}, st);
+  if (rc != kOk) return rc;
+  k_qf_finish<<<(unsigned)((int64_t)pd->P * N), kWG, 0, st>>>(partial, (int64_t)1 << (log2n - kTileLog), pd->hyp,
+                                                               pd->hyp_stride, p0, d, N, out);
+  return check_launch("k_qf_finish");
+}
+
+int fgp_inv_eig(int family, const void* lam, const void* ytilde, int64_t yt_stride, const double* raw_noise,
+                int64_t noise_stride, int64_t P, int log2n, void* ya, double* wa, void* stream) {
+  if (P < 1 || log2n < 0 || log2n > kMaxLog2N) return set_error(kErrInvalid, "fgp_inv_eig: bad sizes");
+  if (!lam || !ytilde || !raw_noise || !ya) return set_error(kErrInvalid, "fgp_inv_eig: null pointer");
+  const int64_t total = P << log2n;
+  const double rootn = sqrt((double)((int64_t)1 << log2n));
+  hipStream_t st = (hipStream_t)stream;
+  const unsigned grid = (unsigned)((total + kWG - 1) / kWG);
+  if (family == FGP_FAMILY_LATTICE)
+    k_inv_eig<double2><<<grid, kWG, 0, st>>>(static_cast<const double2*>(lam), static_cast<const double2*>(ytilde),
+                                              yt_stride, raw_noise, noise_stride, rootn, log2n, total,
+                                              static_cast<double2*>(ya), wa);
+  else
+    k_inv_eig<double><<<grid, kWG, 0, st>>>(static_cast<const double*>(lam), static_cast<const double*>(ytilde),
+                                             yt_stride, raw_noise, noise_stride, rootn, log2n, total,
+                                             static_cast<double*>(ya), wa);
+  return check_launch("k_inv_eig");
 }
 
 int fgp_kernel_rows(int family, const double* xt, int64_t N, const void* z, int64_t n, int d, int tbits,

@@ -184,13 +184,17 @@ def mll_constant(d_out, n):
 
 
 def fused_lam(family, parts, raw_scale, raw_lengthscales, raw_noise, G, gen=None, n=None):
-    """lambda = ft(k1) for G eigen-problems sharing `parts` ([d, n]; or the generator `gen` with size n)
-    via fgp_nll_lam -> [G, n]."""
+    """lambda = ft(k1) for G eigen-problems sharing `parts` ([d, n]), with parts of their own
+    ([G, d, n]), or with the generator `gen` (size n), via fgp_nll_lam -> [G, n]."""
+    parts_stride = 0
     if parts is not None:
         require_device(parts, "fused_lam")
-        d, n = parts.shape
+        d, n = parts.shape[-2:]
         dev = parts.device
         parts = parts.contiguous()
+        if parts.dim() == 3:
+            assert parts.shape[0] == G
+            parts_stride = d * n
     else:
         require_device(gen.shift, "fused_lam")
         d, dev = len(gen.z), gen.shift.device
@@ -202,7 +206,7 @@ def fused_lam(family, parts, raw_scale, raw_lengthscales, raw_noise, G, gen=None
     out = torch.empty((G, n), dtype=cdt, device=dev)
     work = torch.empty((G, n), dtype=cdt, device=dev) if m > 12 else None
     desc = N.NllDesc(family=family, log2n=m, d=d, G=G, parts=(parts.data_ptr() if parts is not None else 0),
-                     parts_stride=0,
+                     parts_stride=parts_stride,
                      ysq=out.data_ptr(), ysq_stride=0, raw=raw.data_ptr(),
                      scale_off=0, scale_pp=int(S == G and G > 1), ls_off=S, ls_pp=int(Sl == G and G > 1),
                      ls_pd=int(Dl == d), noise_off=S + Sl * Dl, noise_pp=int(Sn == G and G > 1), logdet_weight=1.0,

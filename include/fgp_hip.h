@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define FGP_ABI_VERSION 3
+#define FGP_ABI_VERSION 4
 
 #define FGP_OK 0
 #define FGP_ERR_INVALID (-1)     /* bad argument (shape, stride, null pointer) */
@@ -212,6 +212,49 @@ int fgp_post_mean(int family, const double* xt, int64_t N, const void* z, int64_
 int fgp_post_var_qf(int family, const double* xt, int64_t N, const void* z, int log2n, int d, int tbits,
                     const int* order, const double* coef, const double* hyp, const double* wa, void* work,
                     double* partial, double* out, void* stream);
+
+/* Batched prediction over P independent GPs of one family / n / d (e.g. the randomly shifted
+ * replicas of BASELINE config C4; each replaces one GP's AbstractGP.post_mean / post_var,
+ * fastgps/abstract_gp.py:352-416).  Problem p owns training points z + p*z_stride ([d][n], float64
+ * lattice / int64 net), hyper-parameter row hyp + p*hyp_stride ([1 + d]: scale, lengthscales),
+ * coefficients coeffs + p*coeff_stride ([n], K^-1 y) and eigenvalue weights wa + p*wa_stride ([n],
+ * Re(1/ev), post_var only).  order/coef as fgp_post_mean (lattice); tbits (net). */
+typedef struct fgp_pred_desc {
+  int family;
+  int d;
+  int tbits;
+  int P;
+  int64_t n;
+  int order[FGP_MAX_D];
+  double coef[FGP_MAX_D];
+  const void* z;
+  int64_t z_stride;
+  const double* hyp;
+  int64_t hyp_stride;
+  const double* coeffs;
+  int64_t coeff_stride;
+  const double* wa;
+  int64_t wa_stride;
+} fgp_pred_desc;
+
+/* out[p, t] = sum_i K_p(xt_p[t], z_p[:, i]) coeffs_p[i]; xt_p = xt + p*xt_stride ([N, d]; stride 0 =
+ * shared test points); out [P][N]; work: float64 scratch of ceil(n/1024) * P * N entries. */
+int fgp_post_mean_batched(const fgp_pred_desc* desc, const double* xt, int64_t xt_stride, int64_t N, double* out,
+                          double* work, void* stream);
+
+/* Posterior variance, 13 <= log2(n) <= 24 (AbstractGP.post_var, abstract_gp.py:381-416, n = the GP's n):
+ *   out[p, t] = max(K_p(x, x) - sum_k wa_p[k] |ft(K_p(x_t, z_p))_k|^2, 0)  (negatives set to 0, :413)
+ * with K_p(x, x) = scale_p prod_j (1 + l_pj part0[j]), part0 = the zero-distance kernel parts (host [d]).
+ * work: device scratch [P][N][n] (complex128 lattice / float64 net); partial: [P][N][n / 4096]. */
+int fgp_post_var_batched(const fgp_pred_desc* desc, const double* xt, int64_t xt_stride, int64_t N, const double* part0,
+                         double* out, void* work, double* partial, void* stream);
+
+/* A = 1/ev, ev = sqrt(n) lam + exp(raw_noise) (fastgps/util.py:285,292-300), for P problems:
+ *   ya[p, k] = ytilde[p, k] * A[p, k]  (the tilde-domain solve of util.py:341-342), wa[p, k] = Re(A[p, k])
+ * lam, ya: [P][n] contiguous (complex128 lattice / float64 net); ytilde row stride yt_stride; raw_noise
+ * device, problem p at raw_noise[p * noise_stride]; wa may be NULL. */
+int fgp_inv_eig(int family, const void* lam, const void* ytilde, int64_t yt_stride, const double* raw_noise,
+                int64_t noise_stride, int64_t P, int log2n, void* ya, double* wa, void* stream);
 
 /* Cross-kernel rows rows[g, t, i] = K_g(xt[t], z[:, i]) (same kernel as fgp_post_mean), [Gk][N][n],
  * N <= 65535: the kmat of AbstractGP.post_var / post_cov (fastgps/abstract_gp.py:407-411,452-457). */

@@ -176,6 +176,62 @@ def test_fit_batched_equals_individual_fits(family, m):
         assert torch.equal(ga.raw_scale, gb.raw_scale)
 
 
+@pytest.mark.parametrize("family,m,d", [("lattice", 10, 3), ("lattice", 14, 5), ("net", 13, 2), ("net", 15, 3)])
+def test_gpbatch_equals_individual_gps(family, m, d):
+    """GPBatch (stacked ytilde, one fit loop, one coefficient solve, one post_mean / post_var launch for
+    all GPs) reproduces every GP's own fit / coeffs / post_mean / post_var.  Fit: bit-identical.  The
+    batch forms A = 1/ev in one kernel (fgp_inv_eig) where the per-GP path uses torch's complex
+    reciprocal, an ulp-level difference amplified by cond(K) in coeffs (1e-6) and not in the
+    posteriors (post_mean 1e-9 relative, post_var 1e-10 K(x,x) absolute)."""
+    from oracle.fgp_oracle import f_ackley
+    n = 2 ** m
+
+    def make(seed):
+        if family == "lattice":
+            gp = F.FastGPLattice(F.Lattice(d, seed=seed), device=DEV)
+        else:
+            gp = F.FastGPDigitalNetB2(F.DigitalNetB2(d, seed=seed), alpha=1, device=DEV)
+        gp.add_y_next(f_ackley(gp.get_x_next(n)) * (1 + 0.1 * seed))
+        return gp
+
+    seeds = [11, 12, 13]
+    solo = [make(s) for s in seeds]
+    datas = [gp.fit(iterations=40, verbose=0, store_loss_hist=True) for gp in solo]
+    gps = [make(s) for s in seeds]
+    b = F.GPBatch(gps)
+    bdatas = b.fit(iterations=40, store_loss_hist=True)
+    xt = torch.rand((37, d), generator=torch.Generator().manual_seed(3)).to(DEV)
+    pm = b.post_mean(xt)
+    pv = b.post_var(xt[:11])
+    assert pm.shape == (3, 37) and pv.shape == (3, 11)
+    for p, (a, bd, ga, gb) in enumerate(zip(datas, bdatas, solo, gps)):
+        assert a["iterations"] == bd["iterations"]
+        assert torch.equal(a["loss_hist"], bd["loss_hist"])
+        assert torch.equal(ga.raw_lengthscales, gb.raw_lengthscales)
+        assert torch.equal(ga.raw_scale, gb.raw_scale)
+        with torch.no_grad():
+            assert rel_err(b.coeffs()[p], ga.coeffs) <= 1e-6
+            assert rel_err(pm[p], ga.post_mean(xt)) <= 1e-9
+            kxx = float(ga._kdiag(xt).abs().max())
+            assert abs_err(pv[p], ga.post_var(xt[:11])) <= 1e-10 * kxx
+            # the GP objects hold the fitted state: their own methods agree with the batch
+            assert rel_err(gb.post_mean(xt), ga.post_mean(xt)) <= 1e-9
+    # per-GP test points ([P, N, d])
+    xs = torch.rand((3, 5, d), generator=torch.Generator().manual_seed(4)).to(DEV)
+    pm3 = b.post_mean(xs)
+    for p in range(3):
+        assert rel_err(pm3[p], b.post_mean(xs[p])[p]) <= 1e-15
+    # re-ingesting the data and resetting the parameters reproduces the fit
+    raw0 = torch.stack([torch.cat([g.raw_scale.detach().reshape(1) * 0, g.raw_lengthscales.detach().reshape(-1) * 0,
+                                   torch.log(torch.tensor([1e-8 if family == "lattice" else 1e-16], device=DEV))])
+                        for g in gps])
+    b.set_data(torch.stack([g.y for g in gps]).clone())
+    b.set_raw(raw0)
+    again = b.fit(iterations=40, store_loss_hist=True)
+    for a, bd in zip(datas, again):
+        assert torch.equal(a["loss_hist"], bd["loss_hist"])
+
+
 @pytest.mark.parametrize("family,m", [("lattice", 6), ("lattice", 13), ("lattice", 16), ("net", 12), ("net", 15)])
 def test_fused_paths_equal_autograd_paths(family, m):
     """Graph-free fused kernels (fgp_nll_lam, fgp_post_var_qf, fused coeffs) agree with the
