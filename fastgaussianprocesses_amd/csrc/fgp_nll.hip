@@ -137,6 +137,29 @@ __device__ __forceinline__ void load_hyp(const Nll& a, int g, Hyp& h) {
   for (int j = 0; j < FGP_MAX_D; ++j) h.ls[j] = (j < a.d) ? exp(a.raw[lb + (a.ls_pd ? j : 0)]) : 0.0;
 }
 
+__device__ __forceinline__ double read_lane(double v, int lane) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+  return __hiloint2double(hi, lo);
+}
+
+// load_hyp for a problem index g that is uniform over the wave: one exp per parameter, evaluated
+// lane-parallel (lane 0 scale, 1 noise, 2 + j lengthscale j) and broadcast, instead of 2 + d
+// exps in every lane.  Same libm exp, so the same values as load_hyp.
+__device__ __forceinline__ void load_hyp_wave(const Nll& a, int g, Hyp& h) {
+  const int lane = threadIdx.x & 63;
+  const int lb = a.ls_off + (a.ls_pp ? g : 0) * (a.ls_pd ? a.d : 1);
+  int idx = -1;
+  if (lane == 0) idx = a.scale_off + (a.scale_pp ? g : 0);
+  else if (lane == 1) idx = a.noise_off + (a.noise_pp ? g : 0);
+  else if (lane < 2 + a.d) idx = lb + (a.ls_pd ? lane - 2 : 0);
+  const double e = exp(idx >= 0 ? a.raw[idx] : 0.0);
+  h.scale = read_lane(e, 0);
+  h.noise = read_lane(e, 1);
+#pragma unroll
+  for (int j = 0; j < FGP_MAX_D; ++j) h.ls[j] = (j < a.d) ? read_lane(e, 2 + j) : 0.0;
+}
+
 // ------------------------------------------------------------------ parts source (array / generated)
 // Per-problem source of the kernel parts: the parts array, or (FGP_PARTS_LATTICE) the lattice point
 // x_0 = shift from which the parts of element i are regenerated with fgp_lattice_parts' arithmetic.
@@ -156,15 +179,30 @@ __device__ __forceinline__ void psrc_init(const Nll& a, int g, PSrc& s) {
 // vector entry zj mod n, coefficient coef, shift sh = x_0):
 //   x = ((br zj mod n) / n + sh) % 1  (the host generator's exact value and rounding, seqs.Lattice),
 //   delta = torch.remainder(x - x_0, 1),  part = coef B_ORD(delta)  (k_lattice_parts).
+// low 32 bits of a 24 x 24-bit product (full-rate v_mul_u32_u24; v_mul_lo_u32 is quarter rate):
+// brev_m(i) and z_j mod n are < 2^24, and only the low m <= 24 bits of the product are used
+__device__ __forceinline__ unsigned mul_u24(unsigned a, unsigned b) {
+  unsigned r;
+  asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+// Lattice part from k = (brev(i) z_j) mod n:
+//   x = (k / n + sh) % 1     one rounding (k / n exact); v_fract on [0, 2) is exact
+//   delta = (x - sh) % 1     v_fract on (-1, 1): x - sh, or RN(x - sh + 1) -- torch.remainder's value
+//                            (never rounds up to 1: the wrapped case has |x - sh| >= 1/n - ulp)
+// the same values as the host generator + fgp_lattice_parts' mod1 (bit-identity tested on the GPU).
+template <int ORD>
+__device__ __forceinline__ double lattice_gen_part_k(unsigned k, double coef, double sh, double inv_n) {
+  const double x = __builtin_amdgcn_fract(__builtin_fma((double)k, inv_n, sh));
+  const double dl = __builtin_amdgcn_fract(x - sh);
+  return coef * bernoulli(ORD, dl);
+}
+
 template <int ORD>
 __device__ __forceinline__ double lattice_gen_part(unsigned zj, double coef, double sh, unsigned br, unsigned mask,
                                                    double inv_n) {
-  double x = (double)((br * zj) & mask) * inv_n;        // exact: (v(i) z_j) % 1
-  x = x + sh;
-  if (x >= 1.0) x -= 1.0;                               // numpy remainder on [0, 2): exact
-  double dl = x - sh;
-  if (dl < 0.0) dl += 1.0;                              // torch.remainder on (-1, 1)
-  return coef * bernoulli(ORD, dl);
+  return lattice_gen_part_k<ORD>(mul_u24(br, zj) & mask, coef, sh, inv_n);
 }
 
 template <int ORD>
@@ -173,26 +211,31 @@ __device__ __forceinline__ double gen_part(const Nll& a, const PSrc& s, int j, u
   return lattice_gen_part<ORD>(a.gz[j], a.gcoef[j], s.sh[j], br, mask, inv_n);
 }
 
+// Dimension count as a compile-time constant (D = 1..8), or D = 0: runtime d, loops run over
+// FGP_MAX_D zero-padded dimensions (part 0 and lengthscale 0, so a padded factor 1 + l p is exactly 1).
+template <int D> struct Dims { static constexpr int N = D ? D : FGP_MAX_D; };
+template <int D> __device__ __forceinline__ bool dim_on(const Nll& a, int j) { return D ? true : j < a.d; }
+
 // Parts source as a compile-time choice: PG = 0 reads the parts array, PG = 2/4/6/8 regenerates the
 // lattice parts with Bernoulli order PG (FGP_PARTS_LATTICE, one order for every dimension).
-// parts of element i (p[j], zero-padded to FGP_MAX_D)
-template <int PG>
+// parts of element i (p[j], zero-padded)
+template <int PG, int D>
 __device__ __forceinline__ void parts_one(const Nll& a, const PSrc& s, int64_t n, int64_t i, double* p) {
   if constexpr (PG != 0) {
     const int m = a.log2n;
     const unsigned br = brev_bits((unsigned)i, m), mask = (unsigned)(n - 1);
     const double inv_n = ldexp(1.0, -m);
 #pragma unroll
-    for (int j = 0; j < FGP_MAX_D; ++j) p[j] = (j < a.d) ? gen_part<PG>(a, s, j, br, mask, inv_n) : 0.0;
+    for (int j = 0; j < Dims<D>::N; ++j) p[j] = dim_on<D>(a, j) ? gen_part<PG>(a, s, j, br, mask, inv_n) : 0.0;
   } else {
 #pragma unroll
-    for (int j = 0; j < FGP_MAX_D; ++j) p[j] = (j < a.d) ? s.pg[(int64_t)j * n + i] : 0.0;
+    for (int j = 0; j < Dims<D>::N; ++j) p[j] = dim_on<D>(a, j) ? s.pg[(int64_t)j * n + i] : 0.0;
   }
 }
 
 // parts of the consecutive elements (i, i+1), i even: 16-byte loads, or generated (brev_m(i + 1) =
 // brev_m(i) + n/2)
-template <int PG>
+template <int PG, int D>
 __device__ __forceinline__ void parts_pair(const Nll& a, const PSrc& s, int64_t n, int64_t i, double* p0,
                                            double* p1) {
   if constexpr (PG != 0) {
@@ -201,37 +244,38 @@ __device__ __forceinline__ void parts_pair(const Nll& a, const PSrc& s, int64_t 
     const unsigned br1 = br + (unsigned)(n >> 1);
     const double inv_n = ldexp(1.0, -m);
 #pragma unroll
-    for (int j = 0; j < FGP_MAX_D; ++j) {
-      p0[j] = (j < a.d) ? gen_part<PG>(a, s, j, br, mask, inv_n) : 0.0;
-      p1[j] = (j < a.d) ? gen_part<PG>(a, s, j, br1, mask, inv_n) : 0.0;
+    for (int j = 0; j < Dims<D>::N; ++j) {
+      p0[j] = dim_on<D>(a, j) ? gen_part<PG>(a, s, j, br, mask, inv_n) : 0.0;
+      p1[j] = dim_on<D>(a, j) ? gen_part<PG>(a, s, j, br1, mask, inv_n) : 0.0;
     }
   } else {
 #pragma unroll
-    for (int j = 0; j < FGP_MAX_D; ++j) {
+    for (int j = 0; j < Dims<D>::N; ++j) {
       double2 pv = make_double2(0.0, 0.0);
-      if (j < a.d) pv = *reinterpret_cast<const double2*>(s.pg + (int64_t)j * n + i);
+      if (dim_on<D>(a, j)) pv = *reinterpret_cast<const double2*>(s.pg + (int64_t)j * n + i);
       p0[j] = pv.x;
       p1[j] = pv.y;
     }
   }
 }
 
-__device__ __forceinline__ double k1_from(const Nll& a, const Hyp& h, const double* p) {
+// k1 = scale prod_j (1 + l_j p_j); padded dimensions multiply by exactly 1
+template <int D>
+__device__ __forceinline__ double k1_from(const Hyp& h, const double* p) {
   double r = 1.0;
 #pragma unroll
-  for (int j = 0; j < FGP_MAX_D; ++j)
-    if (j < a.d) r *= __builtin_fma(h.ls[j], p[j], 1.0);
+  for (int j = 0; j < Dims<D>::N; ++j) r *= __builtin_fma(h.ls[j], p[j], 1.0);
   return h.scale * r;
 }
 
 // k1 at the consecutive elements (i, i+1), i even
-template <int PG>
+template <int PG, int D>
 __device__ __forceinline__ double2 k1_pair(const Nll& a, const Hyp& h, const PSrc& s, int64_t n, int64_t i) {
   if constexpr (PG == 0) {   // product accumulated as each dimension's 16-byte load arrives
     double r0 = 1.0, r1 = 1.0;
 #pragma unroll
-    for (int j = 0; j < FGP_MAX_D; ++j) {
-      if (j < a.d) {
+    for (int j = 0; j < Dims<D>::N; ++j) {
+      if (dim_on<D>(a, j)) {
         const double2 pv = *reinterpret_cast<const double2*>(s.pg + (int64_t)j * n + i);
         r0 *= __builtin_fma(h.ls[j], pv.x, 1.0);
         r1 *= __builtin_fma(h.ls[j], pv.y, 1.0);
@@ -239,28 +283,38 @@ __device__ __forceinline__ double2 k1_pair(const Nll& a, const Hyp& h, const PSr
     }
     return make_double2(h.scale * r0, h.scale * r1);
   } else {
-    double p0[FGP_MAX_D], p1[FGP_MAX_D];
-    parts_pair<PG>(a, s, n, i, p0, p1);
-    return make_double2(k1_from(a, h, p0), k1_from(a, h, p1));
+    double p0[Dims<D>::N], p1[Dims<D>::N];
+    parts_pair<PG, D>(a, s, n, i, p0, p1);
+    return make_double2(k1_from<D>(h, p0), k1_from<D>(h, p1));
   }
 }
 
-// gradient terms at element i: acc[0] += g k1, acc[1+j] += g scale l_j p_j prod_{m != j} f_m
+// Gradient terms at element i with dL/dk1_i = g:
+//   acc[0]   += g prod_m f_m                      (x scale after the reduction  = dL/draw_scale)
+//   acc[1+j] += (g p_j) prod_{m != j} f_m        (x scale l_j after the reduction = dL/draw_l_j)
+// f_m = 1 + l_m p_m (prefix / suffix products; padded dimensions contribute f = 1, p = 0).
+template <int D>
 __device__ __forceinline__ void grad_terms_p(const Hyp& h, const double* pj, double gi, double* acc) {
-  double f[FGP_MAX_D];
+  constexpr int ND = Dims<D>::N;
+  double f[ND];
 #pragma unroll
-  for (int j = 0; j < FGP_MAX_D; ++j) f[j] = __builtin_fma(h.ls[j], pj[j], 1.0);   // padded dims: l = 0 -> f = 1
-  double suf[FGP_MAX_D + 1];
-  suf[FGP_MAX_D] = 1.0;
+  for (int j = 0; j < ND; ++j) f[j] = __builtin_fma(h.ls[j], pj[j], 1.0);
+  double suf[ND + 1];
+  suf[ND] = 1.0;
 #pragma unroll
-  for (int j = FGP_MAX_D - 1; j >= 0; --j) suf[j] = suf[j + 1] * f[j];
-  acc[0] = __builtin_fma(gi, h.scale * suf[0], acc[0]);
+  for (int j = ND - 1; j >= 0; --j) suf[j] = suf[j + 1] * f[j];
+  acc[0] = __builtin_fma(gi, suf[0], acc[0]);
   double pre = 1.0;
 #pragma unroll
-  for (int j = 0; j < FGP_MAX_D; ++j) {
-    acc[1 + j] = __builtin_fma(gi, h.scale * h.ls[j] * pj[j] * (pre * suf[j + 1]), acc[1 + j]);
+  for (int j = 0; j < ND; ++j) {
+    acc[1 + j] = __builtin_fma(gi * pj[j], pre * suf[j + 1], acc[1 + j]);
     pre *= f[j];
   }
+}
+
+// factor applied to the reduced gradient partial q (0: scale, 1 + j: scale l_j)
+__device__ __forceinline__ double grad_factor(const Hyp& h, int q) {
+  return q == 0 ? h.scale : h.scale * h.ls[q - 1];
 }
 
 // eigenvalue terms for one frequency: returns dL/dlambda, accumulates norm / logdet / dnoise
@@ -322,8 +376,8 @@ __global__ __launch_bounds__(kWG) void k_iter_single(Nll a, const double2* __res
   for (int j = 0; j < 16; ++j) {
     const int i = tt + j * TL;
     double p[FGP_MAX_D];
-    parts_one<PG>(a, src, L, i, p);
-    s[padi(i)] = real_to_T<T>(k1_from(a, h, p));
+    parts_one<PG, 0>(a, src, L, i, p);
+    s[padi(i)] = real_to_T<T>(k1_from<0>(h, p));
   }
   __syncthreads();
   center_transform<P, false>(s, tt, 1, red, tw);
@@ -356,12 +410,12 @@ __global__ __launch_bounds__(kWG) void k_iter_single(Nll a, const double2* __res
   for (int j = 0; j < 16; ++j) {
     const int i = tt + j * TL;
     double p[FGP_MAX_D];
-    parts_one<PG>(a, src, L, i, p);
-    grad_terms_p(h, p, re(s[padi(i)]) * inv_rootn, acc);
+    parts_one<PG, 0>(a, src, L, i, p);
+    grad_terms_p<0>(h, p, re(s[padi(i)]) * inv_rootn, acc);
   }
 #pragma unroll
   for (int q = 0; q < 1 + FGP_MAX_D; ++q)
-    if (q <= a.d) acc[q] = group_sum<TL>(acc[q], redd);
+    if (q <= a.d) acc[q] = group_sum<TL>(acc[q], redd) * grad_factor(h, q);
   if (live && tt == 0) {
     *part_ptr(a, g, 0, 0) = norm;
     *part_ptr(a, g, 1, 0) = logdet;
@@ -373,7 +427,7 @@ __global__ __launch_bounds__(kWG) void k_iter_single(Nll a, const double2* __res
 }
 
 // ---------------------------------------------------------------- n > 4096: forward row pass
-template <int P2, typename T, int PG>
+template <int P2, typename T, int PG, int D>
 __global__ __launch_bounds__(kWG) void k_fwd_rows(Nll a, const double2* __restrict__ tw, const double2* __restrict__ twm) {
   constexpr int N2 = 1 << P2, TL = N2 / 16, RPW = kTile / N2;
   __shared__ T lds[kTile + kTile / 16];
@@ -385,7 +439,7 @@ __global__ __launch_bounds__(kWG) void k_fwd_rows(Nll a, const double2* __restri
   const int row0 = (int)(blockIdx.x % tiles) * RPW;
   const int tid = threadIdx.x;
   Hyp h;
-  load_hyp(a, g, h);
+  load_hyp_wave(a, g, h);
   PSrc src;
   psrc_init(a, g, src);
   const int64_t base = (int64_t)row0 * N2;
@@ -395,7 +449,7 @@ __global__ __launch_bounds__(kWG) void k_fwd_rows(Nll a, const double2* __restri
     double sum = 0.0;
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) {
-      kv[kk] = k1_pair<PG>(a, h, src, n, base + 2 * tid + 512 * kk);
+      kv[kk] = k1_pair<PG, D>(a, h, src, n, base + 2 * tid + 512 * kk);
       sum += kv[kk].x + kv[kk].y;
     }
     const double mean = block_sum(sum, (double*)red) * (1.0 / N2);
@@ -414,7 +468,7 @@ __global__ __launch_bounds__(kWG) void k_fwd_rows(Nll a, const double2* __restri
 #pragma unroll 2
     for (int kk = 0; kk < 8; ++kk) {
       const int e = 2 * tid + 512 * kk;
-      const double2 kv = k1_pair<PG>(a, h, src, n, base + e);
+      const double2 kv = k1_pair<PG, D>(a, h, src, n, base + e);
       sum += kv.x + kv.y;
       lds[padi(e)] = real_to_T<T>(kv.x);
       lds[padi(e + 1)] = real_to_T<T>(kv.y);
@@ -432,7 +486,7 @@ __global__ __launch_bounds__(kWG) void k_fwd_rows(Nll a, const double2* __restri
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) {
       const int e = 2 * tid + 512 * kk;
-      const double2 kv = k1_pair<PG>(a, h, src, n, base + e);
+      const double2 kv = k1_pair<PG, D>(a, h, src, n, base + e);
       lds[padi(e)] = real_to_T<T>(kv.x);
       lds[padi(e + 1)] = real_to_T<T>(kv.y);
     }
@@ -518,7 +572,7 @@ __global__ __launch_bounds__(kWG) void k_fwd_cols(Nll a, const double2* __restri
     return;
   }
   Hyp h;
-  load_hyp(a, g, h);
+  load_hyp_wave(a, g, h);
   const double* yg = a.ysq + (int64_t)g * a.ysq_stride + c0;
   double norm = 0.0, logdet = 0.0, dnoise = 0.0;
   // element e = tid + 256 k lies in column e mod C = cl for every k: the thread's 16 values share a
@@ -569,7 +623,7 @@ __global__ __launch_bounds__(kWG) void k_fwd_cols(Nll a, const double2* __restri
 }
 
 // ---------------------------------------------------------------- n > 4096: adjoint row pass + gradient terms
-template <int P2, typename T, int PG>
+template <int P2, typename T, int PG, int D>
 __global__ __launch_bounds__(kWG) void k_bwd_rows(Nll a, const double2* __restrict__ tw, const double2* __restrict__ twm) {
   constexpr int N2 = 1 << P2, TL = N2 / 16, RPW = kTile / N2;
   constexpr bool FFT = sizeof(T) == 16;   // FFT: adjoint network + conj twiddle; WHT: self-adjoint
@@ -623,25 +677,26 @@ __global__ __launch_bounds__(kWG) void k_bwd_rows(Nll a, const double2* __restri
     center_transform<P2, FFT>(s, tid % TL, 1, red, tw);
   }
   Hyp h;
-  load_hyp(a, g, h);
+  load_hyp_wave(a, g, h);
   PSrc src;
   psrc_init(a, g, src);
   const double inv_rootn = 1.0 / sqrt((double)n);
-  double acc[1 + FGP_MAX_D];
+  constexpr int ND = Dims<D>::N;
+  double acc[1 + ND];
 #pragma unroll
-  for (int q = 0; q < 1 + FGP_MAX_D; ++q) acc[q] = 0.0;
+  for (int q = 0; q < 1 + ND; ++q) acc[q] = 0.0;
 #pragma unroll 2
   for (int kk = 0; kk < 8; ++kk) {
     const int e = 2 * tid + 512 * kk;
-    double p0[FGP_MAX_D], p1[FGP_MAX_D];
-    parts_pair<PG>(a, src, n, base + e, p0, p1);
-    grad_terms_p(h, p0, re(lds[padi(e)]) * inv_rootn, acc);
-    grad_terms_p(h, p1, re(lds[padi(e + 1)]) * inv_rootn, acc);
+    double p0[ND], p1[ND];
+    parts_pair<PG, D>(a, src, n, base + e, p0, p1);
+    grad_terms_p<D>(h, p0, re(lds[padi(e)]) * inv_rootn, acc);
+    grad_terms_p<D>(h, p1, re(lds[padi(e + 1)]) * inv_rootn, acc);
   }
 #pragma unroll
-  for (int q = 0; q < 1 + FGP_MAX_D; ++q) {
+  for (int q = 0; q < 1 + ND; ++q) {
     if (q <= a.d) {
-      const double v = block_sum(acc[q], redd);
+      const double v = block_sum(acc[q], redd) * grad_factor(h, q);
       if (tid == 0) *part_ptr(a, g, 3 + q, blk) = v;
     }
   }
@@ -890,6 +945,21 @@ static int with_pg(const Nll& a, Fn&& fn) {
   return fn(std::integral_constant<int, 0>{});
 }
 
+// Calls fn(std::integral_constant<int, D>{}) with d (1 .. FGP_MAX_D) as a compile-time value.
+template <typename Fn>
+static void with_d(int d, Fn&& fn) {
+  switch (d) {
+    case 1: fn(std::integral_constant<int, 1>{}); break;
+    case 2: fn(std::integral_constant<int, 2>{}); break;
+    case 3: fn(std::integral_constant<int, 3>{}); break;
+    case 4: fn(std::integral_constant<int, 4>{}); break;
+    case 5: fn(std::integral_constant<int, 5>{}); break;
+    case 6: fn(std::integral_constant<int, 6>{}); break;
+    case 7: fn(std::integral_constant<int, 7>{}); break;
+    default: fn(std::integral_constant<int, 8>{}); break;
+  }
+}
+
 template <typename T>
 static int launch_iter_single(const Nll& a, const Tables* tb, hipStream_t st, bool emit = false) {
   const int P = a.log2n;
@@ -917,9 +987,14 @@ static int launch_rows_fwd(const Nll& a, const Tables* tb, hipStream_t st) {
   return with_pg<T>(a, [&](auto pgc) {
     constexpr int PG = decltype(pgc)::value;
     switch (m2) {
-#define FGP_C(PP) case PP: k_fwd_rows<PP, T, PG><<<grid, kWG, 0, st>>>(a, tb->tw4096, tb->twm[m]); break;
-      FGP_C(9) FGP_C(10) FGP_C(11) FGP_C(12)
+#define FGP_C(PP) case PP: k_fwd_rows<PP, T, PG, 0><<<grid, kWG, 0, st>>>(a, tb->tw4096, tb->twm[m]); break;
+      FGP_C(9) FGP_C(10) FGP_C(11)
 #undef FGP_C
+      case 12:   // n >= 2^16: the dimension count as a compile-time constant
+        with_d(a.d, [&](auto dc) {
+          k_fwd_rows<12, T, PG, decltype(dc)::value><<<grid, kWG, 0, st>>>(a, tb->tw4096, tb->twm[m]);
+        });
+        break;
       default: return set_error(kErrInvalid, "bad m2");
     }
     return check_launch("k_fwd_rows");
@@ -950,9 +1025,14 @@ static int launch_rows_bwd(const Nll& a, const Tables* tb, hipStream_t st) {
   return with_pg<T>(a, [&](auto pgc) {
     constexpr int PG = decltype(pgc)::value;
     switch (m2) {
-#define FGP_C(PP) case PP: k_bwd_rows<PP, T, PG><<<grid, kWG, 0, st>>>(a, tb->tw4096, tb->twm[m]); break;
-      FGP_C(9) FGP_C(10) FGP_C(11) FGP_C(12)
+#define FGP_C(PP) case PP: k_bwd_rows<PP, T, PG, 0><<<grid, kWG, 0, st>>>(a, tb->tw4096, tb->twm[m]); break;
+      FGP_C(9) FGP_C(10) FGP_C(11)
 #undef FGP_C
+      case 12:
+        with_d(a.d, [&](auto dc) {
+          k_bwd_rows<12, T, PG, decltype(dc)::value><<<grid, kWG, 0, st>>>(a, tb->tw4096, tb->twm[m]);
+        });
+        break;
       default: return set_error(kErrInvalid, "bad m2");
     }
     return check_launch("k_bwd_rows");

@@ -2,7 +2,7 @@
 
   python tools/fit_kernels.py [--log2n 20] [--d 5] [--shifts 8] [--iters 5] [--parts-array]
 
-Builds the same batched engine as bench.py's step (bench.Shift + fastgaussianprocesses_amd.batch)
+Builds the same batched engine as bench.py's step (bench.Shifts + fastgaussianprocesses_amd.batch)
 and runs `--iters` iterations of stage 0/1/2 + fit step, so a counter pass sees a few dispatches of
 k_fwd_rows / k_fwd_cols / k_bwd_rows at the bench's grid.
 """
@@ -31,10 +31,9 @@ def main():
     import bench
     import fastgaussianprocesses_amd as F
     dev = torch.device("cuda", 0)
-    shifts = [bench.Shift(F, a.d, 2 ** a.log2n, 1000 + s, dev) for s in range(a.shifts)]
-    for sh in shifts:
-        sh.reset()
-    eng = F.batch.batched_engine([sh.gp for sh in shifts], a.iters)
+    shifts = bench.Shifts(F, a.d, 2 ** a.log2n, [1000 + s for s in range(a.shifts)], dev)
+    shifts.reset()
+    eng = F.batch.batched_engine(shifts.gps, a.iters)
     for it in range(a.iters):
         for k in range(3):
             eng.stage(k)
