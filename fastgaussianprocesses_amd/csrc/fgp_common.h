@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace fgp {
 
 constexpr int kWG = 256;         // threads per workgroup
@@ -200,6 +202,99 @@ __device__ __forceinline__ void lds_transform(T* s, int tt, const double2* __res
     lds_dit_all<P, 0>(s, tt, tw);
   }
 }
+
+// f(std::integral_constant<int, I>{}) for I = B .. E-1 (compile-time loop index)
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+// ---------------------------------------------------------------- register-resident passes
+// The radix-2^RL pass of lds_pass on a thread's 16 elements held in registers: group j of the thread
+// (q = tt + j TL) owns the elements at pass_pos<P, S, RL>(tt, j, t), t < 2^RL, in v[j 2^RL + t].
+// Same butterflies and twiddles as lds_pass, so the same results; the data only goes through LDS to
+// change hands between passes (reg_exchange), not before / after every pass.
+template <int P, int S> struct PassRL { static constexpr int value = (P - S) < 4 ? (P - S) : 4; };
+template <int P> struct LastPass { static constexpr int S = ((P - 1) / 4) * 4; };
+
+template <int P, int S, int RL>
+__device__ __forceinline__ int pass_pos(int tt, int j, int t) {
+  constexpr int TL = (1 << P) / 16;
+  const int q = tt + j * TL;
+  const int blo = q & ((1 << S) - 1);
+  return blo + ((q >> S) << (S + RL)) + (t << S);
+}
+
+template <int P, int S, int RL, bool ADJ, typename T>
+__device__ __forceinline__ void reg_pass(T* v, int tt, const double2* __restrict__ tw) {
+  constexpr int R = 1 << RL;
+  constexpr int GPT = 16 / R;
+  constexpr int TL = (1 << P) / 16;
+#pragma unroll
+  for (int j = 0; j < GPT; ++j) {
+    const int q = tt + j * TL;
+    const int blo = q & ((1 << S) - 1);
+    double2 wb[RL];
+#pragma unroll
+    for (int q2 = 0; q2 < RL; ++q2) {
+      if constexpr (S > 0 && sizeof(T) == 16) wb[q2] = tw[blo << (11 - S - q2)];
+      else wb[q2] = make_double2(1.0, 0.0);
+    }
+    if constexpr (!ADJ) stages_dit<0, RL, S, false>(v + j * R, wb);
+    else stages_dif<RL - 1, RL, S, true>(v + j * R, wb);
+  }
+}
+
+// Hand the 16 elements over from pass (SA, RLA) to pass (SB, RLB) through the thread's transform image
+// `col` in LDS.  PAD = false: positions as they are (column images of stride = 1 mod 16 with
+// consecutive lanes on consecutive columns are conflict-free); PAD = true: padi(position) (one
+// transform per workgroup, lanes along the transform).  Leading barrier: readers of the previous
+// exchange are done.
+template <bool PAD>
+__device__ __forceinline__ int img_pos(int pos) { return PAD ? padi(pos) : pos; }
+
+template <int P, int SA, int RLA, int SB, int RLB, bool PAD, typename T>
+__device__ __forceinline__ void reg_exchange(T* v, T* col, int tt) {
+  constexpr int RA = 1 << RLA, RB = 1 << RLB;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 16 / RA; ++j)
+#pragma unroll
+    for (int t = 0; t < RA; ++t) col[img_pos<PAD>(pass_pos<P, SA, RLA>(tt, j, t))] = v[j * RA + t];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 16 / RB; ++j)
+#pragma unroll
+    for (int t = 0; t < RB; ++t) v[j * RB + t] = col[img_pos<PAD>(pass_pos<P, SB, RLB>(tt, j, t))];
+}
+
+// forward (DIT) passes S, S + 4, ... < P
+template <int P, int S, bool PAD, typename T>
+__device__ __forceinline__ void fwd_reg_passes(T* v, T* col, int tt, const double2* __restrict__ tw) {
+  constexpr int RL = PassRL<P, S>::value;
+  if constexpr (S > 0) reg_exchange<P, S - 4, 4, S, RL, PAD>(v, col, tt);
+  reg_pass<P, S, RL, false>(v, tt, tw);
+  if constexpr (S + 4 < P) fwd_reg_passes<P, S + 4, PAD>(v, col, tt, tw);
+}
+
+// adjoint (DIF) passes S, S - 4, ..., 0 (start at LastPass<P>::S: the elements the forward passes end on)
+template <int P, int S, bool PAD, typename T>
+__device__ __forceinline__ void adj_reg_passes(T* v, T* col, int tt, const double2* __restrict__ tw) {
+  constexpr int RL = PassRL<P, S>::value;
+  reg_pass<P, S, RL, true>(v, tt, tw);
+  if constexpr (S >= 4) {
+    reg_exchange<P, S, RL, S - 4, 4, PAD>(v, col, tt);
+    adj_reg_passes<P, S - 4, PAD>(v, col, tt, tw);
+  }
+}
+
+// 4-bit bit reversal as a compile-time constant
+template <int T4> struct Brev4 {
+  static constexpr unsigned value = ((T4 & 1) << 3) | ((T4 & 2) << 1) | ((T4 & 4) >> 1) | ((T4 & 8) >> 3);
+};
 
 // ---------------------------------------------------------------- reductions
 __device__ __forceinline__ double shfl_xor_d(double v, int o) { return __shfl_xor(v, o, 64); }

@@ -312,20 +312,117 @@ __device__ __forceinline__ void grad_terms_p(const Hyp& h, const double* pj, dou
   }
 }
 
+// brev_m(i0 + t) for i0 a multiple of 16: brev_m(i0) | brev_4(t) << (m - 4)
+template <int T4>
+__device__ __forceinline__ unsigned brev_run(unsigned br0, int m) { return br0 | (Brev4<T4>::value << (m - 4)); }
+
+__device__ __forceinline__ double re(double2 v) { return v.x; }
+__device__ __forceinline__ double re(double v) { return v; }
+template <typename T> __device__ __forceinline__ T real_to_T(double v);
+template <> __device__ __forceinline__ double2 real_to_T<double2>(double v) { return make_double2(v, 0.0); }
+template <> __device__ __forceinline__ double real_to_T<double>(double v) { return v; }
+
+// k1 at the 16 consecutive elements i0 + t (i0 a multiple of 16) into v[t]; sum accumulates them in
+// order t.  Generated parts, or the parts array read as 16-byte pairs.
+template <int PG, int D, typename T>
+__device__ __forceinline__ void k1_run16(const Nll& a, const Hyp& h, const PSrc& s, int64_t n, int64_t i0, T* v,
+                                         double& sum) {
+  double r[16];
+  if constexpr (PG != 0) {
+    const int m = a.log2n;
+    const unsigned br0 = brev_bits((unsigned)i0, m), mask = (unsigned)(n - 1);
+    const double inv_n = ldexp(1.0, -m);
+    static_for<0, 16>([&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+      const unsigned br = brev_run<t>(br0, m);
+      double p[Dims<D>::N];
+#pragma unroll
+      for (int j = 0; j < Dims<D>::N; ++j) p[j] = dim_on<D>(a, j) ? gen_part<PG>(a, s, j, br, mask, inv_n) : 0.0;
+      r[t] = k1_from<D>(h, p);
+    });
+  } else {
+#pragma unroll
+    for (int t = 0; t < 16; ++t) r[t] = 1.0;
+#pragma unroll
+    for (int j = 0; j < Dims<D>::N; ++j) {
+      if (dim_on<D>(a, j)) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const double2 pv = *reinterpret_cast<const double2*>(s.pg + (int64_t)j * n + i0 + 2 * u);
+          r[2 * u] *= __builtin_fma(h.ls[j], pv.x, 1.0);
+          r[2 * u + 1] *= __builtin_fma(h.ls[j], pv.y, 1.0);
+        }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 16; ++t) r[t] = h.scale * r[t];
+  }
+#pragma unroll
+  for (int t = 0; t < 16; ++t) {
+    sum += r[t];
+    v[t] = real_to_T<T>(r[t]);
+  }
+}
+
+// Gradient terms of the 16 consecutive elements i0 + t with dL/dk1 = g[t] * gs.  g is the thread's
+// private run of 16 values in LDS (stride-17 slots: conflict-free): a rolled loop keeps the register
+// footprint of the regenerated parts bounded (fully unrolled, they spill to AGPRs).
+template <int PG, int D>
+__device__ __forceinline__ void grad_run16(const Nll& a, const Hyp& h, const PSrc& s, int64_t n, int64_t i0,
+                                           const double* g, double gs, double* acc) {
+  if constexpr (PG != 0) {
+    const int m = a.log2n;
+    const unsigned br0 = brev_bits((unsigned)i0, m), mask = (unsigned)(n - 1);
+    const double inv_n = ldexp(1.0, -m);
+#pragma unroll 2
+    for (int t = 0; t < 16; ++t) {
+      const unsigned br = br0 | ((__builtin_bitreverse32((unsigned)t) >> 28) << (m - 4));
+      double p[Dims<D>::N];
+#pragma unroll
+      for (int j = 0; j < Dims<D>::N; ++j) p[j] = dim_on<D>(a, j) ? gen_part<PG>(a, s, j, br, mask, inv_n) : 0.0;
+      grad_terms_p<D>(h, p, g[t] * gs, acc);
+    }
+  } else {
+#pragma unroll 2
+    for (int u = 0; u < 8; ++u) {
+      double p0[Dims<D>::N], p1[Dims<D>::N];
+      parts_pair<PG, D>(a, s, n, i0 + 2 * u, p0, p1);
+      grad_terms_p<D>(h, p0, g[2 * u] * gs, acc);
+      grad_terms_p<D>(h, p1, g[2 * u + 1] * gs, acc);
+    }
+  }
+}
+
 // factor applied to the reduced gradient partial q (0: scale, 1 + j: scale l_j)
 __device__ __forceinline__ double grad_factor(const Hyp& h, int q) {
   return q == 0 ? h.scale : h.scale * h.ls[q - 1];
 }
 
-// eigenvalue terms for one frequency: returns dL/dlambda, accumulates norm / logdet / dnoise
+// log|ev| accumulated as a product of frexp mantissas (each in [0.5, 1): 16 factors stay >= 2^-16)
+// and a sum of exponents, one log per thread instead of one per frequency:
+//   sum_k log|ev_k| = log(prod_k mant_k) + ln 2 sum_k exp_k
+struct LogAcc {
+  double mant = 1.0;
+  int ex = 0;
+  __device__ __forceinline__ void add(double v) {   // v > 0 (or 0 / inf / nan: propagate as log would)
+    int e;
+    mant *= frexp(v, &e);
+    ex += e;
+  }
+  __device__ __forceinline__ double log_sum(double half) const {
+    return half * (log(mant) + (double)ex * 0.69314718055994530942);
+  }
+};
+
+// eigenvalue terms for one frequency: returns dL/dlambda, accumulates norm / log|ev| / dnoise
 __device__ __forceinline__ double2 eig_terms(double2 lam, double rootn, double noise, double Y, double w,
-                                             double& norm, double& logdet, double& dnoise) {
+                                             double& norm, LogAcc& la, double& dnoise) {
   const double ar = rootn * lam.x + noise, ai = rootn * lam.y;    // ev = sqrt(n) lam + noise
   const double den = ar * ar + ai * ai;
   const double inv = 1.0 / den;
   const double rr = ar * inv, ri = -ai * inv;                      // 1/ev
   norm += Y * rr;
-  logdet += 0.5 * log(den);                                        // log|ev|
+  la.add(den);                                                     // log|ev| = 1/2 log(den)
   // G_e = 1/2 conj(w/ev - Y/ev^2) ; 1/ev^2 = (rr^2 - ri^2, 2 rr ri)
   const double qr = w * rr - Y * (rr * rr - ri * ri);
   const double qi = w * ri - Y * (2.0 * rr * ri);
@@ -334,21 +431,17 @@ __device__ __forceinline__ double2 eig_terms(double2 lam, double rootn, double n
   return make_double2(rootn * ger, rootn * gei);
 }
 __device__ __forceinline__ double eig_terms(double lam, double rootn, double noise, double Y, double w, double& norm,
-                                            double& logdet, double& dnoise) {
+                                            LogAcc& la, double& dnoise) {
   const double e = rootn * lam + noise;
   const double r = 1.0 / e;
   norm += Y * r;
-  logdet += log(fabs(e));
+  la.add(fabs(e));
   const double ge = 0.5 * (w * r - Y * r * r);
   dnoise += ge;
   return rootn * ge;
 }
-
-template <typename T> __device__ __forceinline__ T real_to_T(double v);
-template <> __device__ __forceinline__ double2 real_to_T<double2>(double v) { return make_double2(v, 0.0); }
-template <> __device__ __forceinline__ double real_to_T<double>(double v) { return v; }
-__device__ __forceinline__ double re(double2 v) { return v.x; }
-__device__ __forceinline__ double re(double v) { return v; }
+// 1/2 for the lattice (log of |ev|^2), 1 for nets (log of |ev|)
+template <typename T> struct LogHalf { static constexpr double value = sizeof(T) == 16 ? 0.5 : 1.0; };
 
 __device__ __forceinline__ double* part_ptr(const Nll& a, int g, int q, int blk) {
   return a.partials + ((int64_t)g * a.nq + q) * a.nb + blk;
@@ -391,15 +484,16 @@ __global__ __launch_bounds__(kWG) void k_iter_single(Nll a, const double2* __res
     return;
   }
   const double* yg = a.ysq + (int64_t)g * a.ysq_stride;
-  double norm = 0.0, logdet = 0.0, dnoise = 0.0;
+  double norm = 0.0, dnoise = 0.0;
+  LogAcc la;
 #pragma unroll 4
   for (int j = 0; j < 16; ++j) {
     const int k = tt + j * TL;
     const T lam = s[padi(k)] * inv_rootn;
-    s[padi(k)] = eig_terms(lam, rootn, h.noise, yg[k], a.logdet_weight, norm, logdet, dnoise);
+    s[padi(k)] = eig_terms(lam, rootn, h.noise, yg[k], a.logdet_weight, norm, la, dnoise);
   }
   norm = group_sum<TL>(norm, redd);
-  logdet = group_sum<TL>(logdet, redd);
+  double logdet = group_sum<TL>(la.log_sum(LogHalf<T>::value), redd);
   dnoise = group_sum<TL>(dnoise, redd);
   __syncthreads();
   center_transform<P, true>(s, tt, 1, red, tw);
@@ -443,45 +537,28 @@ __global__ __launch_bounds__(kWG) void k_fwd_rows(Nll a, const double2* __restri
   PSrc src;
   psrc_init(a, g, src);
   const int64_t base = (int64_t)row0 * N2;
-  // k1 for element pairs (2 tid + 512 kk, +1): 16-byte loads of every dimension's parts, or generated
-  if constexpr (RPW == 1 && PG == 0) {
-    double2 kv[8];   // all loads in flight first
+  T* out = static_cast<T*>(a.work) + (int64_t)g * n + base;
+  if constexpr (RPW == 1) {
+    // register-resident row transform: k1 at the thread's 16 consecutive elements 16 tid + t (the first
+    // radix-16 pass's inputs), centred by the row mean, 3 passes with 2 LDS hand-overs, output at
+    // elements tid + 256 t (coalesced stores) with the inter-pass twiddle
+    T v[16];
     double sum = 0.0;
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) {
-      kv[kk] = k1_pair<PG, D>(a, h, src, n, base + 2 * tid + 512 * kk);
-      sum += kv[kk].x + kv[kk].y;
-    }
+    k1_run16<PG, D>(a, h, src, n, base + 16 * tid, v, sum);
     const double mean = block_sum(sum, (double*)red) * (1.0 / N2);
 #pragma unroll
-    for (int kk = 0; kk < 8; ++kk) {
-      const int e = 2 * tid + 512 * kk;
-      lds[padi(e)] = real_to_T<T>(kv[kk].x - mean);
-      lds[padi(e + 1)] = real_to_T<T>(kv[kk].y - mean);
-    }
-    __syncthreads();
-    transform_add_mean<P2, false>(lds, tid, real_to_T<T>(mean), tw);
-  } else if constexpr (RPW == 1) {
-    // generated parts: pure ALU, written straight to the thread's own LDS slots (bounded registers),
-    // centred in a second sweep over the same slots once the block mean is known
-    double sum = 0.0;
-#pragma unroll 2
-    for (int kk = 0; kk < 8; ++kk) {
-      const int e = 2 * tid + 512 * kk;
-      const double2 kv = k1_pair<PG, D>(a, h, src, n, base + e);
-      sum += kv.x + kv.y;
-      lds[padi(e)] = real_to_T<T>(kv.x);
-      lds[padi(e + 1)] = real_to_T<T>(kv.y);
-    }
-    const double mean = block_sum(sum, (double*)red) * (1.0 / N2);
+    for (int t = 0; t < 16; ++t) v[t] -= real_to_T<T>(mean);
+    fwd_reg_passes<P2, 0, true>(v, lds, tid, tw);
+    if (tid == 0) v[0] += real_to_T<T>(mean) * (double)N2;
+    if constexpr (sizeof(T) == 16) {
+      const RowTwiddle rt((unsigned)row0, tid, P2, m1, tw, twm);
 #pragma unroll
-    for (int kk = 0; kk < 8; ++kk) {
-      const int e = 2 * tid + 512 * kk;
-      lds[padi(e)] -= real_to_T<T>(mean);
-      lds[padi(e + 1)] -= real_to_T<T>(mean);
+      for (int k = 0; k < 16; ++k) out[tid + k * kWG] = tw_mul<T>(v[k], rt.at(k, P2, m1, tw, twm), false);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) out[tid + k * kWG] = v[k];
     }
-    __syncthreads();
-    transform_add_mean<P2, false>(lds, tid, real_to_T<T>(mean), tw);
+    return;
   } else {
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) {
@@ -494,15 +571,7 @@ __global__ __launch_bounds__(kWG) void k_fwd_rows(Nll a, const double2* __restri
     T* s = lds + (tid / TL) * (N2 + N2 / 16);
     center_transform<P2, false>(s, tid % TL, 1, red, tw);
   }
-  T* out = static_cast<T*>(a.work) + (int64_t)g * n + base;
-  if constexpr (sizeof(T) == 16 && RPW == 1) {
-    const RowTwiddle rt((unsigned)row0, tid, P2, m1, tw, twm);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int e = tid + k * kWG;
-      out[e] = tw_mul<T>(lds[padi(e)], rt.at(k, P2, m1, tw, twm), false);
-    }
-  } else {
+  {
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const int e = tid + k * kWG;
@@ -517,24 +586,20 @@ __global__ __launch_bounds__(kWG) void k_fwd_rows(Nll a, const double2* __restri
 }
 
 // ---------------------------------------------------------------- n > 4096: forward column pass + eigen terms
-template <int P1, typename T>
-struct ColLay {
-  static constexpr int N1 = 1 << P1;
-  static constexpr int C = kTile / N1;
-  static constexpr int PADLEN = N1 + N1 / 16;
-  static constexpr int CS = (PADLEN % 2 == 0) ? PADLEN + 1 : PADLEN;
-};
-
 // Column pass of the forward transform.  EMIT (fgp_nll_lam): write lambda.  Otherwise (the fit):
-// eigen terms -> dL/dlambda kept in LDS -> the adjoint column transform of it, written back in place
-// over the column tile of `work` this workgroup read (k_bwd_rows finishes the adjoint).  Per
-// iteration the forward column output therefore never leaves the workgroup.
+// eigen terms -> dL/dlambda -> the adjoint column transform of it, written back in place over the
+// column tile of `work` this workgroup read (k_bwd_rows finishes the adjoint).  Per iteration the
+// forward column output therefore never leaves the workgroup.
+// Register-resident: thread (column c = tid mod C, tt = tid / C) keeps its 16 elements in registers
+// through every radix-16 pass; LDS only hands them over between passes (reg_exchange).  The last
+// forward pass and the first adjoint pass own the same elements (frequencies), so the eigen terms
+// are evaluated in registers in between.
 template <int P1, typename T, bool EMIT>
 __global__ __launch_bounds__(kWG) void k_fwd_cols(Nll a, const double2* __restrict__ tw) {
-  using Lay = ColLay<P1, T>;
-  constexpr int N1 = Lay::N1, C = Lay::C, CS = Lay::CS, TL = N1 / 16;
-  constexpr bool FFT = sizeof(T) == 16;
-  __shared__ T lds[kLds];
+  constexpr int N1 = 1 << P1, C = kTile / N1, CS = N1 + 1;
+  constexpr int RL0 = PassRL<P1, 0>::value, R0 = 1 << RL0;
+  constexpr int SL = LastPass<P1>::S, RLL = PassRL<P1, SL>::value, RLAST = 1 << RLL;
+  __shared__ T lds[C * CS];
   __shared__ T part[ColPart<C>::size];
   __shared__ double redd[kWG / 64];
   const int m = a.log2n;
@@ -544,74 +609,62 @@ __global__ __launch_bounds__(kWG) void k_fwd_cols(Nll a, const double2* __restri
   const int blk = (int)(blockIdx.x % tiles);
   const int64_t c0 = (int64_t)blk * C;
   const int tid = threadIdx.x;
-  T* wk = static_cast<T*>(a.work) + (int64_t)g * n + c0;
-  const int cl = tid % C, col = tid / TL;
+  const int c = tid % C, tt = tid / C;
+  T* wk = static_cast<T*>(a.work) + (int64_t)g * n + c0 + c;
+  T* col = lds + c * CS;
   T v[16];
+#pragma unroll
+  for (int j = 0; j < 16 / R0; ++j)
+#pragma unroll
+    for (int t = 0; t < R0; ++t) v[j * R0 + t] = wk[(int64_t)pass_pos<P1, 0, RL0>(tt, j, t) * N2];
+  double y[16];
+  if constexpr (!EMIT) {   // Y at the frequencies this thread ends the forward transform on: in flight early
+    const double* yg = a.ysq + (int64_t)g * a.ysq_stride + c0 + c;
+#pragma unroll
+    for (int j = 0; j < 16 / RLAST; ++j)
+#pragma unroll
+      for (int t = 0; t < RLAST; ++t) y[j * RLAST + t] = yg[(int64_t)pass_pos<P1, SL, RLL>(tt, j, t) * N2];
+  }
   T sum = zero_v<T>();
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    v[k] = wk[(int64_t)((tid + k * kWG) / C) * N2 + cl];
-    sum += v[k];
-  }
+  for (int k = 0; k < 16; ++k) sum += v[k];
   column_partials<C>(sum, part);
-  T mean_l = column_total<C>(cl, part) * (1.0 / N1);
-  T mean_t = column_total<C>(col, part) * (1.0 / N1);
+  T mean = column_total<C>(c, part) * (1.0 / N1);
 #pragma unroll
-  for (int k = 0; k < 16; ++k) lds[cl * CS + padi((tid + k * kWG) / C)] = v[k] - mean_l;
-  __syncthreads();
-  transform_add_mean<P1, false>(lds + col * CS, tid % TL, mean_t, tw);
+  for (int k = 0; k < 16; ++k) v[k] -= mean;
+  fwd_reg_passes<P1, 0, false>(v, col, tt, tw);
+  if (tt == 0) v[0] += mean * (double)N1;          // frequency 0 (AbstractFastGP.ft's mean)
   const double rootn = sqrt((double)n), inv_rootn = 1.0 / rootn;
   if constexpr (EMIT) {   // lambda = ft(k1) (fgp_nll_lam)
-    T* gl = static_cast<T*>(a.grad_lam) + (int64_t)g * n + c0;
+    T* gl = static_cast<T*>(a.grad_lam) + (int64_t)g * n + c0 + c;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int e = tid + k * kWG;
-      const int c = e % C, r = e / C;
-      gl[(int64_t)r * N2 + c] = lds[c * CS + padi(r)] * inv_rootn;
-    }
+    for (int j = 0; j < 16 / RLAST; ++j)
+#pragma unroll
+      for (int t = 0; t < RLAST; ++t)
+        gl[(int64_t)pass_pos<P1, SL, RLL>(tt, j, t) * N2] = v[j * RLAST + t] * inv_rootn;
     return;
   }
   Hyp h;
   load_hyp_wave(a, g, h);
-  const double* yg = a.ysq + (int64_t)g * a.ysq_stride + c0;
-  double norm = 0.0, logdet = 0.0, dnoise = 0.0;
-  // element e = tid + 256 k lies in column e mod C = cl for every k: the thread's 16 values share a
-  // column.  dL/dlambda overwrites lambda in the thread's own LDS slots, then a second sweep centres
-  // them by their column mean.
-  // Y is read in groups of 4 with the next group's loads in flight (software pipelined); a fully
-  // unrolled 16-wide divide/log sequence would spill past the 2-waves/SIMD register budget.
+  double norm = 0.0, dnoise = 0.0;
+  LogAcc la;
   sum = zero_v<T>();
-  double y4[4], yn[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) y4[j] = yg[(int64_t)((tid + j * kWG) / C) * N2 + cl];
-#pragma unroll 1
-  for (int k0 = 0; k0 < 16; k0 += 4) {
-    if (k0 + 4 < 16) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) yn[j] = yg[(int64_t)((tid + (k0 + 4 + j) * kWG) / C) * N2 + cl];
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      T* slot = lds + cl * CS + padi((tid + (k0 + j) * kWG) / C);
-      const T gv = eig_terms(*slot * inv_rootn, rootn, h.noise, y4[j], a.logdet_weight, norm, logdet, dnoise);
-      *slot = gv;
-      sum += gv;
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) y4[j] = yn[j];
-  }
-  column_partials<C>(sum, part);
-  mean_l = column_total<C>(cl, part) * (1.0 / N1);
-  mean_t = column_total<C>(col, part) * (1.0 / N1);
-#pragma unroll
-  for (int k = 0; k < 16; ++k) lds[cl * CS + padi((tid + k * kWG) / C)] -= mean_l;
-  __syncthreads();
-  transform_add_mean<P1, FFT>(lds + col * CS, tid % TL, mean_t, tw);   // adjoint (WHT: self-adjoint)
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
-    const int r = (tid + k * kWG) / C;
-    wk[(int64_t)r * N2 + cl] = lds[cl * CS + padi(r)];
+    v[k] = eig_terms(v[k] * inv_rootn, rootn, h.noise, y[k], a.logdet_weight, norm, la, dnoise);
+    sum += v[k];
   }
+  double logdet = la.log_sum(LogHalf<T>::value);
+  column_partials<C>(sum, part);
+  mean = column_total<C>(c, part) * (1.0 / N1);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v[k] -= mean;
+  adj_reg_passes<P1, SL, false>(v, col, tt, tw);   // adjoint (WHT: self-adjoint, w = 1)
+  if (tt == 0) v[0] += mean * (double)N1;
+#pragma unroll
+  for (int j = 0; j < 16 / R0; ++j)
+#pragma unroll
+    for (int t = 0; t < R0; ++t) wk[(int64_t)pass_pos<P1, 0, RL0>(tt, j, t) * N2] = v[j * R0 + t];
   norm = block_sum(norm, redd);
   logdet = block_sum(logdet, redd);
   dnoise = block_sum(dnoise, redd);
@@ -658,9 +711,32 @@ __global__ __launch_bounds__(kWG) void k_bwd_rows(Nll a, const double2* __restri
     }
     const T mean = block_sum_t(sum, red) * (1.0 / N2);
 #pragma unroll
-    for (int k = 0; k < 16; ++k) lds[padi(tid + k * kWG)] = v[k] - mean;
-    __syncthreads();
-    transform_add_mean<P2, FFT>(lds, tid, mean, tw);
+    for (int k = 0; k < 16; ++k) v[k] -= mean;
+    // register-resident adjoint row transform: the loaded elements tid + 256 k are the first DIF
+    // pass's; 3 passes with 2 LDS hand-overs end on the elements 16 tid + t (WHT: self-adjoint)
+    adj_reg_passes<P2, LastPass<P2>::S, true>(v, lds, tid, tw);
+    if (tid == 0) v[0] += mean * (double)N2;
+    Hyp h;
+    load_hyp_wave(a, g, h);
+    PSrc src;
+    psrc_init(a, g, src);
+    constexpr int ND = Dims<D>::N;
+    double acc[1 + ND];
+#pragma unroll
+    for (int q = 0; q < 1 + ND; ++q) acc[q] = 0.0;
+    double* gl = reinterpret_cast<double*>(lds) + 17 * tid;   // the thread's private slots
+    __syncthreads();                                          // last hand-over's readers are done
+#pragma unroll
+    for (int t = 0; t < 16; ++t) gl[t] = re(v[t]);
+    grad_run16<PG, D>(a, h, src, n, base + 16 * tid, gl, 1.0 / sqrt((double)n), acc);
+#pragma unroll
+    for (int q = 0; q < 1 + ND; ++q) {
+      if (q <= a.d) {
+        const double r = block_sum(acc[q], redd) * grad_factor(h, q);
+        if (tid == 0) *part_ptr(a, g, 3 + q, blk) = r;
+      }
+    }
+    return;
   } else {
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
