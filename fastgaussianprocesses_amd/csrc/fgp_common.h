@@ -271,22 +271,56 @@ __device__ __forceinline__ void reg_exchange(T* v, T* col, int tt) {
     for (int t = 0; t < RB; ++t) v[j * RB + t] = col[img_pos<PAD>(pass_pos<P, SB, RLB>(tt, j, t))];
 }
 
+// The same hand-over for complex elements through a real (8-byte) image of half the size: real parts,
+// then imaginary parts.  Halves the LDS a workgroup holds (more workgroups per CU) for two more barriers.
+template <int P, int SA, int RLA, int SB, int RLB, bool PAD>
+__device__ __forceinline__ void reg_exchange_split(double2* v, double* img, int tt) {
+  constexpr int RA = 1 << RLA, RB = 1 << RLB;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 16 / RA; ++j)
+#pragma unroll
+    for (int t = 0; t < RA; ++t) img[img_pos<PAD>(pass_pos<P, SA, RLA>(tt, j, t))] = v[j * RA + t].x;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 16 / RB; ++j)
+#pragma unroll
+    for (int t = 0; t < RB; ++t) v[j * RB + t].x = img[img_pos<PAD>(pass_pos<P, SB, RLB>(tt, j, t))];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 16 / RA; ++j)
+#pragma unroll
+    for (int t = 0; t < RA; ++t) img[img_pos<PAD>(pass_pos<P, SA, RLA>(tt, j, t))] = v[j * RA + t].y;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 16 / RB; ++j)
+#pragma unroll
+    for (int t = 0; t < RB; ++t) v[j * RB + t].y = img[img_pos<PAD>(pass_pos<P, SB, RLB>(tt, j, t))];
+}
+
+// hand-over through an image of element type I: T itself, or (I = double, T = double2) split halves
+template <int P, int SA, int RLA, int SB, int RLB, bool PAD, typename T, typename I>
+__device__ __forceinline__ void reg_handover(T* v, I* img, int tt) {
+  if constexpr (std::is_same<T, I>::value) reg_exchange<P, SA, RLA, SB, RLB, PAD>(v, img, tt);
+  else reg_exchange_split<P, SA, RLA, SB, RLB, PAD>(v, img, tt);
+}
+
 // forward (DIT) passes S, S + 4, ... < P
-template <int P, int S, bool PAD, typename T>
-__device__ __forceinline__ void fwd_reg_passes(T* v, T* col, int tt, const double2* __restrict__ tw) {
+template <int P, int S, bool PAD, typename T, typename I>
+__device__ __forceinline__ void fwd_reg_passes(T* v, I* col, int tt, const double2* __restrict__ tw) {
   constexpr int RL = PassRL<P, S>::value;
-  if constexpr (S > 0) reg_exchange<P, S - 4, 4, S, RL, PAD>(v, col, tt);
+  if constexpr (S > 0) reg_handover<P, S - 4, 4, S, RL, PAD>(v, col, tt);
   reg_pass<P, S, RL, false>(v, tt, tw);
   if constexpr (S + 4 < P) fwd_reg_passes<P, S + 4, PAD>(v, col, tt, tw);
 }
 
 // adjoint (DIF) passes S, S - 4, ..., 0 (start at LastPass<P>::S: the elements the forward passes end on)
-template <int P, int S, bool PAD, typename T>
-__device__ __forceinline__ void adj_reg_passes(T* v, T* col, int tt, const double2* __restrict__ tw) {
+template <int P, int S, bool PAD, typename T, typename I>
+__device__ __forceinline__ void adj_reg_passes(T* v, I* col, int tt, const double2* __restrict__ tw) {
   constexpr int RL = PassRL<P, S>::value;
   reg_pass<P, S, RL, true>(v, tt, tw);
   if constexpr (S >= 4) {
-    reg_exchange<P, S, RL, S - 4, 4, PAD>(v, col, tt);
+    reg_handover<P, S, RL, S - 4, 4, PAD>(v, col, tt);
     adj_reg_passes<P, S - 4, PAD>(v, col, tt, tw);
   }
 }

@@ -524,7 +524,10 @@ __global__ __launch_bounds__(kWG) void k_iter_single(Nll a, const double2* __res
 template <int P2, typename T, int PG, int D>
 __global__ __launch_bounds__(kWG) void k_fwd_rows(Nll a, const double2* __restrict__ tw, const double2* __restrict__ twm) {
   constexpr int N2 = 1 << P2, TL = N2 / 16, RPW = kTile / N2;
-  __shared__ T lds[kTile + kTile / 16];
+  // one row per workgroup (register-resident passes): a real 8-byte hand-over image (34.8 KB, complex
+  // elements in two halves) leaves room for 4 workgroups per CU; several rows: the T-typed LDS tile
+  __shared__ T lds[RPW == 1 ? 1 : kTile + kTile / 16];
+  __shared__ double ldsd[RPW == 1 ? kTile + kTile / 16 : 1];
   __shared__ T red[kWG / 64];
   const int m = a.log2n, m1 = m - P2;
   const int64_t n = (int64_t)1 << m;
@@ -548,7 +551,7 @@ __global__ __launch_bounds__(kWG) void k_fwd_rows(Nll a, const double2* __restri
     const double mean = block_sum(sum, (double*)red) * (1.0 / N2);
 #pragma unroll
     for (int t = 0; t < 16; ++t) v[t] -= real_to_T<T>(mean);
-    fwd_reg_passes<P2, 0, true>(v, lds, tid, tw);
+    fwd_reg_passes<P2, 0, true>(v, ldsd, tid, tw);
     if (tid == 0) v[0] += real_to_T<T>(mean) * (double)N2;
     if constexpr (sizeof(T) == 16) {
       const RowTwiddle rt((unsigned)row0, tid, P2, m1, tw, twm);
@@ -680,7 +683,8 @@ template <int P2, typename T, int PG, int D>
 __global__ __launch_bounds__(kWG) void k_bwd_rows(Nll a, const double2* __restrict__ tw, const double2* __restrict__ twm) {
   constexpr int N2 = 1 << P2, TL = N2 / 16, RPW = kTile / N2;
   constexpr bool FFT = sizeof(T) == 16;   // FFT: adjoint network + conj twiddle; WHT: self-adjoint
-  __shared__ T lds[kTile + kTile / 16];
+  __shared__ T lds[RPW == 1 ? 1 : kTile + kTile / 16];           // (as k_fwd_rows)
+  __shared__ double ldsd[RPW == 1 ? kTile + kTile / 16 : 1];
   __shared__ T red[kWG / 64];
   __shared__ double redd[kWG / 64];
   const int m = a.log2n, m1 = m - P2;
@@ -714,7 +718,7 @@ __global__ __launch_bounds__(kWG) void k_bwd_rows(Nll a, const double2* __restri
     for (int k = 0; k < 16; ++k) v[k] -= mean;
     // register-resident adjoint row transform: the loaded elements tid + 256 k are the first DIF
     // pass's; 3 passes with 2 LDS hand-overs end on the elements 16 tid + t (WHT: self-adjoint)
-    adj_reg_passes<P2, LastPass<P2>::S, true>(v, lds, tid, tw);
+    adj_reg_passes<P2, LastPass<P2>::S, true>(v, ldsd, tid, tw);
     if (tid == 0) v[0] += mean * (double)N2;
     Hyp h;
     load_hyp_wave(a, g, h);
@@ -724,7 +728,7 @@ __global__ __launch_bounds__(kWG) void k_bwd_rows(Nll a, const double2* __restri
     double acc[1 + ND];
 #pragma unroll
     for (int q = 0; q < 1 + ND; ++q) acc[q] = 0.0;
-    double* gl = reinterpret_cast<double*>(lds) + 17 * tid;   // the thread's private slots
+    double* gl = ldsd + 17 * tid;                             // the thread's private slots
     __syncthreads();                                          // last hand-over's readers are done
 #pragma unroll
     for (int t = 0; t < 16; ++t) gl[t] = re(v[t]);
