@@ -57,6 +57,12 @@ def _fit_loop(eng, iterations, stop_crit_improvement_threshold, stop_crit_wait_i
     P = eng.G
     total = iterations + 1
     eng.ensure_history(total)
+    if wait_max > iterations:
+        # no problem can stop early: every one runs to `iterations` and restores its best iterate
+        # (the first minimum of its loss history).  Nothing to decide on the host -> no host sync; the
+        # best iterations are found on the device (_best_raw) and losses are copied back only on request.
+        eng.run(0, total, final_no_update=True)
+        return [dict(stop=iterations, best_i=None, losses=None, p=p, eng=eng) for p in range(P)]
     reader = _LossReader(eng.device)
     state = [dict(best=math.inf, save=math.inf, waited=0, best_i=0, stop=None, losses=[]) for _ in range(P)]
     pending = collections.deque()
@@ -99,16 +105,25 @@ def _fit_loop(eng, iterations, stop_crit_improvement_threshold, stop_crit_wait_i
 
 def _best_raw(eng, state, dl):
     """[P, 2 + dl] = (raw scale, raw lengthscales, raw noise) of every problem at its best iteration
-    (one gather from the per-iteration parameter history)."""
+    (one gather from the per-iteration parameter history).  Best iterations decided on the device
+    (best_i None: the first minimum of each loss history, = the host rule `lv < best`) stay there."""
     P = eng.G
     S, L, _ = eng.sizes
-    rows, cols = [], []
-    for p, s in enumerate(state):
-        c = [p] + [S + p * dl + j for j in range(dl)] + [S + L + p]
-        rows += [s["best_i"]] * len(c)
-        cols += c
-    idx_r = torch.tensor(rows, dtype=torch.int64).to(eng.device, non_blocking=True)
-    idx_c = torch.tensor(cols, dtype=torch.int64).to(eng.device, non_blocking=True)
+    cols = []
+    for p in range(P):
+        cols += [p] + [S + p * dl + j for j in range(dl)] + [S + L + p]
+    idx_c = torch.tensor(cols, dtype=torch.int64).pin_memory().to(eng.device, non_blocking=True)
+    if state[0]["best_i"] is None:
+        total = state[0]["stop"] + 1
+        lh = eng.loss_hist[:total, :, 0]
+        lh = torch.where(torch.isnan(lh), torch.full_like(lh, math.inf), lh)   # NaN never becomes best
+        best = lh.argmin(0)                                                 # [P], first minimum
+        idx_r = best.repeat_interleave(2 + dl)
+    else:
+        rows = []
+        for s in state:
+            rows += [s["best_i"]] * (2 + dl)
+        idx_r = torch.tensor(rows, dtype=torch.int64).pin_memory().to(eng.device, non_blocking=True)
     return eng.raw_hist[idx_r, idx_c].reshape(P, 2 + dl)
 
 
@@ -168,10 +183,16 @@ def _engine(gps, n, ysq, parts, gen, lr, iterations):
 
 def _fit_data(state, store):
     out = []
+    lh = None
     for s in state:
         data = {"iterations": s["stop"]}
         if store:
-            data["loss_hist"] = torch.tensor([-v for v in s["losses"]])
+            if s["losses"] is None:          # device-decided run: copy the histories back now
+                if lh is None:
+                    lh = s["eng"].loss_hist[:s["stop"] + 1, :, 0].cpu()
+                data["loss_hist"] = -lh[:, s["p"]].clone()
+            else:
+                data["loss_hist"] = torch.tensor([-v for v in s["losses"]])
         out.append(data)
     return out
 
@@ -228,6 +249,7 @@ class GPBatch(object):
         self._y = None
         self._st = {}
         self._src = None
+        self._unit_ok = {}
 
     # ---------------------------------------------------------------------------- data / parameters
     def set_data(self, y):
@@ -349,8 +371,15 @@ class GPBatch(object):
         x = x.to(device=self.device, dtype=torch.float64)
         assert (x.ndim == 2 and x.size(1) == self.d) or (x.ndim == 3 and x.shape[0] == self.P and x.size(2) == self.d), \
             "x must have shape (N, d) (shared) or (P, N, d)"
-        assert bool(((0 <= x) & (x <= 1)).all()), "x should have all elements in [0,1]"
         x = x.contiguous()
+        # the [0, 1] range check of the reference (fast_gp_lattice.py:264-265) synchronises; a tensor
+        # already checked (same storage, version, shape) is not checked again (the tensor is held)
+        key = (x.data_ptr(), x._version, tuple(x.shape))
+        if key not in self._unit_ok:
+            assert bool(((0 <= x) & (x <= 1)).all()), "x should have all elements in [0,1]"
+            self._unit_ok[key] = x
+            if len(self._unit_ok) > 8:
+                self._unit_ok.pop(next(iter(self._unit_ok)))
         return x, (0 if x.ndim == 2 else x.stride(0)), x.shape[-2]
 
     def post_mean(self, x):

@@ -230,6 +230,16 @@ def test_gpbatch_equals_individual_gps(family, m, d):
     again = b.fit(iterations=40, store_loss_hist=True)
     for a, bd in zip(datas, again):
         assert torch.equal(a["loss_hist"], bd["loss_hist"])
+    # early stopping disabled (wait > iterations): the host-sync-free path (device-side best iterate)
+    solo2 = [make(s) for s in seeds]
+    d2 = [gp.fit(iterations=25, verbose=0, store_loss_hist=True, stop_crit_wait_iterations=26) for gp in solo2]
+    b.set_raw(raw0)
+    bd2 = b.fit(iterations=25, stop_crit_wait_iterations=26, store_loss_hist=True)
+    for a, bd, ga, gb in zip(d2, bd2, solo2, gps):
+        assert a["iterations"] == bd["iterations"] == 25
+        assert torch.equal(a["loss_hist"], bd["loss_hist"])
+        assert torch.equal(ga.raw_lengthscales, gb.raw_lengthscales)
+        assert torch.equal(ga.raw_scale, gb.raw_scale)
 
 
 @pytest.mark.parametrize("family,m", [("lattice", 6), ("lattice", 13), ("lattice", 16), ("net", 12), ("net", 15)])
