@@ -12,7 +12,7 @@ import torch
 
 _LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
 LIB_PATH = os.path.join(_LIB_DIR, "libfgp_hip.so")
-ABI_VERSION = 4
+ABI_VERSION = 5
 MAX_D = 8
 PARTS_ARRAY = 0
 PARTS_LATTICE = 1
@@ -67,6 +67,7 @@ class PredDesc(ctypes.Structure):
         ("order", _c_int * 8), ("coef", _c_dbl * 8),
         ("z", _c_vp), ("z_stride", _c_i64), ("hyp", _c_vp), ("hyp_stride", _c_i64),
         ("coeffs", _c_vp), ("coeff_stride", _c_i64), ("wa", _c_vp), ("wa_stride", _c_i64),
+        ("points_gen", _c_int), ("gen_z", _c_i64 * 8), ("gen_shift", _c_vp), ("gen_shift_stride", _c_i64),
     ]
 
 

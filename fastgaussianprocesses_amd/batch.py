@@ -365,6 +365,13 @@ class GPBatch(object):
         for j in range(self.d):
             desc.order[j] = order[j]
             desc.coef[j] = coef[j]
+        _, gen = self._source()
+        if gen is not None:     # post_var regenerates the lattice points instead of reading z
+            desc.points_gen = N.PARTS_LATTICE
+            for j in range(self.d):
+                desc.gen_z[j] = gen.z[j]
+            desc.gen_shift = gen.shift.data_ptr()
+            desc.gen_shift_stride = self.d if gen.shift.shape[0] > 1 else 0
         return desc
 
     def _points(self, x):

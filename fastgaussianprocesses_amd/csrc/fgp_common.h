@@ -379,6 +379,20 @@ __device__ __forceinline__ unsigned brev_bits(unsigned u, int bits) {
   return bits == 0 ? 0u : (__builtin_bitreverse32(u) >> (32 - bits));
 }
 
+// low 32 bits of a 24 x 24-bit product (full-rate v_mul_u32_u24; v_mul_lo_u32 is quarter rate):
+// brev_m(i) and z_j mod n are < 2^24, and only the low m <= 24 bits of the product are used
+__device__ __forceinline__ unsigned mul_u24(unsigned a, unsigned b) {
+  unsigned r;
+  asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+// Natural-order rank-1 lattice coordinate of point i (brev = brev_m(i), zm = z_j mod n):
+//   x = ((brev z_j mod n) / n + shift_j) % 1   -- the host generator's value (seqs.Lattice), bit for bit
+__device__ __forceinline__ double lattice_coord(unsigned brev, unsigned zm, unsigned mask, double inv_n, double sh) {
+  return __builtin_amdgcn_fract(__builtin_fma((double)(mul_u24(brev, zm) & mask), inv_n, sh));
+}
+
 // Inter-pass twiddle of a length-2^m transform split as N1 = 2^m1 rows of N2 = 2^P2:
 //   w_n^e, e < n, from the two-level table  twm[e mod N2] * tw[(e >> P2) << (12 - m1)]
 __device__ __forceinline__ double2 inter_tw(unsigned e, int P2, int m1, const double2* __restrict__ tw,

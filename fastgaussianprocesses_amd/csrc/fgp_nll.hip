@@ -179,14 +179,6 @@ __device__ __forceinline__ void psrc_init(const Nll& a, int g, PSrc& s) {
 // vector entry zj mod n, coefficient coef, shift sh = x_0):
 //   x = ((br zj mod n) / n + sh) % 1  (the host generator's exact value and rounding, seqs.Lattice),
 //   delta = torch.remainder(x - x_0, 1),  part = coef B_ORD(delta)  (k_lattice_parts).
-// low 32 bits of a 24 x 24-bit product (full-rate v_mul_u32_u24; v_mul_lo_u32 is quarter rate):
-// brev_m(i) and z_j mod n are < 2^24, and only the low m <= 24 bits of the product are used
-__device__ __forceinline__ unsigned mul_u24(unsigned a, unsigned b) {
-  unsigned r;
-  asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
-
 // Lattice part from k = (brev(i) z_j) mod n:
 //   x = (k / n + sh) % 1     one rounding (k / n exact); v_fract on [0, 2) is exact
 //   delta = (x - sh) % 1     v_fract on (-1, 1): x - sh, or RN(x - sh + 1) -- torch.remainder's value

@@ -12,6 +12,7 @@
 // chunk are staged through LDS in slabs; per-chunk partial sums are reduced in fixed order by a
 // second kernel (bitwise reproducible, no atomics).
 #include <cmath>
+#include <type_traits>
 
 #include "fgp_common.h"
 #include "fgp_runtime.h"
@@ -120,45 +121,77 @@ __global__ __launch_bounds__(kWG) void k_post_mean(const double* __restrict__ xt
       }
     }
   }
+  // Folded B4 factors (ORD = 4, every a != 0): 1 + a B4(t) = a (u^2 + c'), c' = (1 - a/30) / a, with
+  // prod_j a_j moved into the output scale -- 4 operations per dimension and pair instead of 5 (this
+  // kernel is FP64-VALU bound).  a c' = 1 - a/30 = O(1), so the rounding stays at the factor's ulp.
+  bool fold = FAM == 0 && ORD == 4;
+  double cp[NB][D];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      fold = fold && fa[b][j] != 0.0;
+      cp[b][j] = fc[b][j] / fa[b][j];
+    }
+  }
   double acc[NB];
 #pragma unroll
   for (int b = 0; b < NB; ++b) acc[b] = 0.0;
   const int64_t i0 = (int64_t)blockIdx.x * kChunk;
   const int64_t i1 = i0 + kChunk < n ? i0 + kChunk : n;
-  for (int64_t s0 = i0; s0 < i1; s0 += kSlab) {
-    const int cnt = (int)((i1 - s0) < kSlab ? (i1 - s0) : kSlab);
-    __syncthreads();
-    if (tid < cnt) {
+  auto slabs = [&](auto fold_c) {
+    constexpr bool FOLD = decltype(fold_c)::value;
+    for (int64_t s0 = i0; s0 < i1; s0 += kSlab) {
+      const int cnt = (int)((i1 - s0) < kSlab ? (i1 - s0) : kSlab);
+      __syncthreads();
+      if (tid < cnt) {
 #pragma unroll
-      for (int j = 0; j < D; ++j) {
-        if constexpr (FAM == 0) zs[j][tid] = static_cast<const double*>(z)[(int64_t)j * n + s0 + tid];
-        else zs[j][tid] = __longlong_as_double(static_cast<const long long*>(z)[(int64_t)j * n + s0 + tid]);
-      }
-#pragma unroll
-      for (int b = 0; b < NB; ++b) cs[b][tid] = b < B ? coeffs[(int64_t)b * coeff_stride + s0 + tid] : 0.0;
-    }
-    __syncthreads();
-#pragma unroll 2
-    for (int i = 0; i < cnt; ++i) {
-      double p[NB];
-#pragma unroll
-      for (int b = 0; b < NB; ++b) p[b] = 1.0;
-#pragma unroll
-      for (int j = 0; j < D; ++j) {
-        if constexpr (FAM == 0) {
-          const double tj = fabs(xv[j] - zs[j][i]);
-          const int ord = ORD ? ORD : spec.order[j];
-#pragma unroll
-          for (int b = 0; b < NB; ++b) p[b] *= lat_factor(ord, tj, fa[b][j], fc[b][j]);
-        } else {
-          const unsigned long long delta = xbv[j] ^ (unsigned long long)__double_as_longlong(zs[j][i]);
-#pragma unroll
-          for (int b = 0; b < NB; ++b) p[b] *= net_factor(delta, tbits, fa[b][j], fc[b][j]);
+        for (int j = 0; j < D; ++j) {
+          if constexpr (FAM == 0) zs[j][tid] = static_cast<const double*>(z)[(int64_t)j * n + s0 + tid];
+          else zs[j][tid] = __longlong_as_double(static_cast<const long long*>(z)[(int64_t)j * n + s0 + tid]);
         }
-      }
 #pragma unroll
-      for (int b = 0; b < NB; ++b) acc[b] = fma(p[b], cs[b][i], acc[b]);
+        for (int b = 0; b < NB; ++b) cs[b][tid] = b < B ? coeffs[(int64_t)b * coeff_stride + s0 + tid] : 0.0;
+      }
+      __syncthreads();
+#pragma unroll 2
+      for (int i = 0; i < cnt; ++i) {
+        double p[NB];
+#pragma unroll
+        for (int b = 0; b < NB; ++b) p[b] = 1.0;
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+          if constexpr (FAM == 0) {
+            const double tj = fabs(xv[j] - zs[j][i]);
+            if constexpr (FOLD) {
+              const double u = fma(tj, tj, -tj);
+#pragma unroll
+              for (int b = 0; b < NB; ++b) p[b] *= fma(u, u, cp[b][j]);
+            } else {
+              const int ord = ORD ? ORD : spec.order[j];
+#pragma unroll
+              for (int b = 0; b < NB; ++b) p[b] *= lat_factor(ord, tj, fa[b][j], fc[b][j]);
+            }
+          } else {
+            const unsigned long long delta = xbv[j] ^ (unsigned long long)__double_as_longlong(zs[j][i]);
+#pragma unroll
+            for (int b = 0; b < NB; ++b) p[b] *= net_factor(delta, tbits, fa[b][j], fc[b][j]);
+          }
+        }
+#pragma unroll
+        for (int b = 0; b < NB; ++b) acc[b] = fma(p[b], cs[b][i], acc[b]);
+      }
     }
+  };
+  if (FAM == 0 && ORD == 4 && fold) {
+    slabs(std::integral_constant<bool, FAM == 0 && ORD == 4>{});
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+#pragma unroll
+      for (int j = 0; j < D; ++j) sc[b] *= fa[b][j];
+    }
+  } else {
+    slabs(std::integral_constant<bool, false>{});
   }
   if (live) {
 #pragma unroll
@@ -227,6 +260,12 @@ struct QfArgs {
   void* work;                // [P][N][n]
   double* partial;           // [P][N][n / 4096]
   ProbStrides ps;            // per-problem strides of xt, z, hyp, wa (batched GPs; 0 for one problem)
+  // lattice training points regenerated in the kernel instead of read from z (natural-order rank-1
+  // lattice: x_ij = ((brev_m(i) z_j mod n) / n + shift_j) % 1, shift row of problem p at gshift + p * gss)
+  int gen;
+  unsigned gz[FGP_MAX_D];
+  const double* gshift;
+  int64_t gss;
 };
 
 template <int P2, typename T>
@@ -264,15 +303,28 @@ __global__ __launch_bounds__(kWG) void k_qf_rows(QfArgs q, const double2* __rest
   const int64_t base = (int64_t)row0 * N2;
   double kv0[8], kv1[8];
   double sum = 0.0;
+  const bool gen = FAM == 0 && q.gen;                // uniform
+  const unsigned mask = (unsigned)(n - 1);
+  const double inv_n = ldexp(1.0, -m);
+  double gsh[FGP_MAX_D];
+#pragma unroll
+  for (int j = 0; j < FGP_MAX_D; ++j) gsh[j] = (gen && j < q.d) ? q.gshift[pb * q.gss + j] : 0.0;
 #pragma unroll 2
   for (int kk = 0; kk < 8; ++kk) {
     const int e = 2 * tid + 512 * kk;
     double p0 = scale, p1 = scale;
+    const unsigned br0 = gen ? brev_bits((unsigned)(base + e), m) : 0u, br1 = br0 + (unsigned)(n >> 1);
 #pragma unroll
     for (int j = 0; j < FGP_MAX_D; ++j) {
       if (j < q.d) {
         if constexpr (FAM == 0) {
-          const double2 zv = *reinterpret_cast<const double2*>(static_cast<const double*>(zp) + (int64_t)j * n + base + e);
+          double2 zv;
+          if (gen) {   // brev_m(i + 1) = brev_m(i) + n/2 for even i
+            zv = make_double2(lattice_coord(br0, q.gz[j], mask, inv_n, gsh[j]),
+                              lattice_coord(br1, q.gz[j], mask, inv_n, gsh[j]));
+          } else {
+            zv = *reinterpret_cast<const double2*>(static_cast<const double*>(zp) + (int64_t)j * n + base + e);
+          }
           p0 *= lat_factor(q.spec.order[j], fabs(xv[j] - zv.x), fa[j], fc[j]);
           p1 *= lat_factor(q.spec.order[j], fabs(xv[j] - zv.y), fa[j], fc[j]);
         } else {
@@ -527,7 +579,7 @@ namespace fgp {
 // quadratic-form partials of P problems x N test points (k_qf_rows + k_qf_cols)
 static int launch_qf(int family, const double* xt, int64_t N, const void* z, int log2n, int d, int tbits,
                      const PredSpec& spec, const double* hyp, const double* wa, void* work, double* partial, int64_t P,
-                     const ProbStrides& ps, hipStream_t st) {
+                     const ProbStrides& ps, hipStream_t st, const fgp_pred_desc* gdesc = nullptr) {
   const Tables* tb = get_tables(st);
   if (!tb) return set_error(kErrHip, "twiddle table initialisation failed");
   QfArgs q;
@@ -543,6 +595,23 @@ static int launch_qf(int family, const double* xt, int64_t N, const void* z, int
   q.work = work;
   q.partial = partial;
   q.ps = ps;
+  q.gen = 0;
+  q.gshift = nullptr;
+  q.gss = 0;
+  for (int j = 0; j < FGP_MAX_D; ++j) q.gz[j] = 0u;
+  if (gdesc && gdesc->points_gen == FGP_PARTS_LATTICE && family == FGP_FAMILY_LATTICE) {
+    const uint64_t zmask = ((uint64_t)1 << log2n) - 1;
+    for (int j = 0; j < d; ++j) {
+      if (gdesc->gen_z[j] <= 0 || gdesc->gen_z[j] >= ((int64_t)1 << (53 - log2n)))
+        return set_error(kErrUnsupported, "generating vector entry %lld outside (0, 2^(53-log2n))",
+                         (long long)gdesc->gen_z[j]);
+      q.gz[j] = (unsigned)((uint64_t)gdesc->gen_z[j] & zmask);
+    }
+    if (!gdesc->gen_shift) return set_error(kErrInvalid, "null gen_shift");
+    q.gen = 1;
+    q.gshift = gdesc->gen_shift;
+    q.gss = gdesc->gen_shift_stride;
+  }
   int rc;
   const int m2 = split_m2(log2n), m1 = log2n - m2;
   const dim3 grid((unsigned)((P * N) << (log2n - kTileLog)));
@@ -630,7 +699,8 @@ int fgp_post_var_batched(const fgp_pred_desc* pd, const double* xt, int64_t xt_s
       pd->P < 1)
     return set_error(kErrInvalid, "fgp_post_var_batched: needs n = 2^m, 13 <= m <= 24, 1 <= d <= %d", FGP_MAX_D);
   if (N == 0) return kOk;
-  if (!xt || !pd->z || !pd->hyp || !pd->wa || !part0 || !out || !work || !partial)
+  if (!xt || (!pd->z && pd->points_gen != FGP_PARTS_LATTICE) || !pd->hyp || !pd->wa || !part0 || !out || !work ||
+      !partial)
     return set_error(kErrInvalid, "fgp_post_var_batched: null pointer");
   if (((int64_t)pd->P * N << (log2n - kTileLog)) >= ((int64_t)1 << 31))
     return set_error(kErrUnsupported, "fgp_post_var_batched: P * N too large");
@@ -643,7 +713,7 @@ int fgp_post_var_batched(const fgp_pred_desc* pd, const double* xt, int64_t xt_s
   }
   hipStream_t st = (hipStream_t)stream;
   rc = launch_qf(pd->family, xt, N, pd->z, log2n, d, pd->tbits, spec, pd->hyp, pd->wa, work, partial, pd->P,
-                 ProbStrides{xt_stride, pd->z_stride, pd->hyp_stride, pd->wa_stride}, st);
+                 ProbStrides{xt_stride, pd->z_stride, pd->hyp_stride, pd->wa_stride}, st, pd);
   if (rc != kOk) return rc;
   k_qf_finish<<<(unsigned)((int64_t)pd->P * N), kWG, 0, st>>>(partial, (int64_t)1 << (log2n - kTileLog), pd->hyp,
                                                                pd->hyp_stride, p0, d, N, out);

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define FGP_ABI_VERSION 4
+#define FGP_ABI_VERSION 5
 
 #define FGP_OK 0
 #define FGP_ERR_INVALID (-1)     /* bad argument (shape, stride, null pointer) */
@@ -235,6 +235,14 @@ typedef struct fgp_pred_desc {
   int64_t coeff_stride;
   const double* wa;
   int64_t wa_stride;
+  /* Training points source for fgp_post_var_batched: FGP_PARTS_ARRAY reads z; FGP_PARTS_LATTICE
+   * regenerates the natural-order rank-1 lattice points x_ij = ((brev_m(i) z_j mod n) / n + shift_j) % 1
+   * (bit-identical to fgp_lattice_points) from gen_z (host, 0 < gen_z[j] < 2^(53 - log2 n)) and the
+   * device shift rows gen_shift + p * gen_shift_stride; z may then be NULL. */
+  int points_gen;
+  int64_t gen_z[FGP_MAX_D];
+  const double* gen_shift;
+  int64_t gen_shift_stride;
 } fgp_pred_desc;
 
 /* out[p, t] = sum_i K_p(xt_p[t], z_p[:, i]) coeffs_p[i]; xt_p = xt + p*xt_stride ([N, d]; stride 0 =

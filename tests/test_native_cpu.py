@@ -51,7 +51,7 @@ def test_struct_layouts_match_header(tmp_path):
         pytest.skip("gcc not available")
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "fgp_hip.h"', "int main(void) {"]
     expect = []
-    for cname, cls in (("fgp_nll_desc", N.NllDesc), ("fgp_fit_desc", N.FitDesc)):
+    for cname, cls in (("fgp_nll_desc", N.NllDesc), ("fgp_fit_desc", N.FitDesc), ("fgp_pred_desc", N.PredDesc)):
         lines.append('printf("%%zu\\n", sizeof(%s));' % cname)
         expect.append(ctypes.sizeof(cls))
         for fname, _ in cls._fields_:
