@@ -857,20 +857,61 @@ __global__ __launch_bounds__(kWG) void k_fit_step(Nll a, Fit f, int iter, int do
 }
 
 // Independent problems (per_problem): one workgroup per GP reduces its partials, records its loss
-// and parameters and applies Rprop to the parameters it owns -- no cross-problem dependency.
+// and parameters and applies Rprop to the parameters it owns -- no cross-problem dependency.  The
+// kernel is a pure latency chain (it sits between two iterations), so every load is issued up front:
+// each thread's partials of all quantities at once, and the parameter-owning threads' Rprop state
+// before the reduction.  Per-quantity order of the sum is as block_sum's (fixed, deterministic).
 __global__ __launch_bounds__(kWG) void k_fit_reduce_step(Nll a, Fit f, int iter, int do_update) {
-  __shared__ double redd[kWG / 64];
-  __shared__ double vals[4 + FGP_MAX_D];
+  constexpr int NQ = 4 + FGP_MAX_D, NW = kWG / 64;
+  __shared__ double red[NQ * NW];
+  __shared__ double vals[NQ];
   const int g = blockIdx.x;
-  for (int q = 0; q < a.nq; ++q) {
-    double v = 0.0;
-    for (int b = threadIdx.x; b < a.nb; b += kWG) v += *part_ptr(a, g, q, b);
-    v = block_sum(v, redd);
-    if (threadIdx.x == 0) vals[q] = v;
+  const int k = threadIdx.x;
+  const int dl = a.ls_pd ? a.d : 1;
+  // the parameter thread k owns: 0 scale, 1..dl lengthscales, dl + 1 noise
+  int p = 0, rg = 0;
+  if (k == 0) {
+    p = a.scale_off + (a.scale_pp ? g : 0);
+    rg = f.scale_rg;
+  } else if (k <= dl) {
+    p = a.ls_off + (a.ls_pp ? g : 0) * dl + (k - 1);
+    rg = f.ls_rg;
+  } else {
+    p = a.noise_off + (a.noise_pp ? g : 0);
+    rg = f.noise_rg;
+  }
+  const bool owner = k < 2 + dl;
+  double raw_p = 0.0, prev_p = 0.0, step_p = 0.0;
+  if (owner) {
+    raw_p = f.raw[p];
+    prev_p = f.prev[p];
+    step_p = f.step[p];
+  }
+  double s[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) s[q] = 0.0;
+  for (int b = k; b < a.nb; b += kWG) {
+    double v[NQ];   // quantities past nq re-read q = 0 (unused)
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) v[q] = *part_ptr(a, g, q < a.nq ? q : 0, b);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) s[q] += v[q];
+  }
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    double v = s[q];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if ((k & 63) == 0) red[q * NW + (k >> 6)] = v;
   }
   __syncthreads();
-  const int dl = a.ls_pd ? a.d : 1;
-  const int k = threadIdx.x;
+  if (k < NQ) {
+    double tot = 0.0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) tot += red[k * NW + w];
+    vals[k] = tot;
+  }
+  __syncthreads();
   if (k == 0) {
     const double term2 = a.logdet_weight * vals[1];
     double* lh = f.loss_hist + ((int64_t)iter * a.G + g) * 3;
@@ -878,31 +919,32 @@ __global__ __launch_bounds__(kWG) void k_fit_reduce_step(Nll a, Fit f, int iter,
     lh[1] = vals[0];
     lh[2] = term2;
   }
-  if (k < 2 + dl) {
-    int p, rg;
-    double gp;
-    if (k == 0) {
-      p = a.scale_off + (a.scale_pp ? g : 0);
-      gp = vals[3];
-      rg = f.scale_rg;
-    } else if (k <= dl) {
-      p = a.ls_off + (a.ls_pp ? g : 0) * dl + (k - 1);
-      if (a.ls_pd) {
-        gp = vals[4 + (k - 1)];
-      } else {
-        gp = 0.0;
-        for (int j = 0; j < a.d; ++j) gp += vals[4 + j];
-      }
-      rg = f.ls_rg;
+  if (!owner) return;
+  double gp;
+  if (k == 0) {
+    gp = vals[3];
+  } else if (k <= dl) {
+    if (a.ls_pd) {
+      gp = vals[4 + (k - 1)];
     } else {
-      p = a.noise_off + (a.noise_pp ? g : 0);
-      gp = exp(a.raw[p]) * vals[2];
-      rg = f.noise_rg;
+      gp = 0.0;
+      for (int j = 0; j < a.d; ++j) gp += vals[4 + j];
     }
-    f.raw_hist[(int64_t)iter * f.n_params + p] = f.raw[p];
-    f.grad_out[p] = gp;
-    if (do_update && rg) rprop_update(f, p, gp);
+  } else {
+    gp = exp(raw_p) * vals[2];
   }
+  f.raw_hist[(int64_t)iter * f.n_params + p] = raw_p;
+  f.grad_out[p] = gp;
+  if (!(do_update && rg)) return;
+  // torch.optim.Rprop single-tensor semantics (as rprop_update, on the prefetched state)
+  const double prod = gp * prev_p;
+  const double sgn = prod > 0.0 ? f.eta_plus : (prod < 0.0 ? f.eta_minus : 1.0);
+  const double st = fmin(fmax(step_p * sgn, f.step_min), f.step_max);
+  f.step[p] = st;
+  const double gg = (sgn == f.eta_minus) ? 0.0 : gp;
+  const double gs = gg > 0.0 ? 1.0 : (gg < 0.0 ? -1.0 : 0.0);
+  f.raw[p] = raw_p + (-1.0) * (gs * st);
+  f.prev[p] = gg;
 }
 
 // ------------------------------------------------------------------------------------------------

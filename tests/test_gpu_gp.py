@@ -301,10 +301,10 @@ def test_lattice_parts_generator_bit_identical(monkeypatch, m, d, alpha):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("family,m", [("lattice", 10), ("lattice", 16), ("net", 15)])
+@pytest.mark.parametrize("family,m", [("lattice", 10), ("lattice", 13), ("lattice", 16), ("net", 14), ("net", 15)])
 def test_stage_launches_equal_fit_run(family, m):
     """fgp_nll_stage 0/1/2 + fgp_fit_step (the per-kernel timing path of bench.py) is the same
-    computation as fgp_fit_run."""
+    computation as fgp_fit_run, bit for bit, across two runs and a final no-update iteration."""
     from oracle.fgp_oracle import f_ackley
     d, n = 3, 2 ** m
 
@@ -316,17 +316,20 @@ def test_stage_launches_equal_fit_run(family, m):
         gp.add_y_next(f_ackley(gp.get_x_next(n)))
         return gp
 
-    gps = [make(s) for s in range(2)]
-    e1 = F.batch.batched_engine(gps, 8)
-    e1.run(0, 6)
-    e2 = F.batch.batched_engine(gps, 8)
-    for it in range(6):
+    gps = [make(s) for s in range(3)]
+    e1 = F.batch.batched_engine(gps, 12)
+    e1.run(0, 5)
+    e1.run(5, 5, final_no_update=True)
+    e2 = F.batch.batched_engine(gps, 12)
+    for it in range(10):
         for k in range(3):
             e2.stage(k)
-        e2.fit_step(it)
+        e2.fit_step(it, update=it < 9)
     torch.cuda.synchronize()
-    assert torch.equal(e1.loss_hist[:6], e2.loss_hist[:6])
+    assert torch.equal(e1.loss_hist[:10], e2.loss_hist[:10])
+    assert torch.equal(e1.raw_hist[:10], e2.raw_hist[:10])
     assert torch.equal(e1.raw, e2.raw)
+    assert torch.equal(e1.grad, e2.grad)
 
 
 def test_sharded_multi_output_fit_matches_unsharded():
