@@ -12,7 +12,7 @@ import torch
 
 _LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
 LIB_PATH = os.path.join(_LIB_DIR, "libfgp_hip.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 MAX_D = 8
 PARTS_ARRAY = 0
 PARTS_LATTICE = 1
@@ -84,7 +84,7 @@ _SIGNATURES = {
     "fgp_lattice_parts": [_c_vp, _c_i64, _c_vp, _c_i64, _c_int, _c_pi, _c_pd, _c_vp, _c_vp],
     "fgp_lattice_points": [_c_pl, _c_vp, _c_i64, _c_i64, _c_int, _c_vp, _c_vp],
     "fgp_lattice_parts_gen": [_c_pl, _c_vp, _c_int, _c_int, _c_int, _c_pd, _c_vp, _c_vp],
-    "fgp_net_parts": [_c_vp, _c_i64, _c_vp, _c_i64, _c_int, _c_int, _c_vp, _c_vp],
+    "fgp_net_parts": [_c_vp, _c_i64, _c_vp, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_vp],
     "fgp_nll_fwd": [_P_NLL, _c_vp],
     "fgp_nll_bwd": [_P_NLL, _c_vp],
     "fgp_nll_lam": [_P_NLL, _c_vp],

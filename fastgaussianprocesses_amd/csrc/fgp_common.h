@@ -511,4 +511,38 @@ __device__ __forceinline__ void transform_add_mean(T* s, int tt, T mean, const d
   __syncthreads();
 }
 
+// ---------------------------------------------------------------- Walsh kernels of order 2..4
+// Per-dimension part of FastGPDigitalNetB2 of order a = alpha - beta - kappa in 2..4
+// (fast_gp_digital_net_b2.py:295-301: qmcpy.kernel_methods.weighted_walsh_funcs(a, delta, t) - 1):
+//   omega_a(x) = sum_{k >= 1} 2^(-mu_a(k)) wal_k(x),   x = delta / 2^t,
+// mu_a(k) = sum_{i <= min(a, v)} (a_i + 1) for k = 2^a_1 + ... + 2^a_v, a_1 > ... > a_v (Dick's weight).
+// With beta = -floor(log2 x) and t1 = 2^-beta the series sums to
+//   omega_2 = -beta x + 5/2 (1 - t1) - 1
+//   omega_3 =  beta x^2 - 5 (1 - t1) x + 43/18 (1 - t1^2) - 1
+// and omega_4 by the digit recursion (y_a = s_a 2^-(a+1), s_a = (-1)^(bit a+1 of x), e_r = elementary
+// symmetric sums of the y above the current digit, seeded with the all-zero tail a >= t):
+//   omega_a = sum_{r < a} e_r(all) + sum_{b < beta} s_b e_{a-1}(y_{>b}) / 2.
+// omega_a(0) = 3/2, 25/18, 407/294.  (tests/test_oracle_golden.py checks the closed forms and the
+// recursion against the truncated series itself.)
+__device__ __forceinline__ double walsh_omega(int ord, unsigned long long delta, int t) {
+  if (delta == 0ull) return ord == 2 ? 1.5 : (ord == 3 ? 25.0 / 18.0 : 407.0 / 294.0);
+  const int beta = t - (63 - __clzll((long long)delta));
+  const double x = ldexp((double)delta, -t);
+  const double t1 = ldexp(1.0, -beta), b = (double)beta;
+  if (ord == 2) return __builtin_fma(-b, x, 2.5 * (1.0 - t1)) - 1.0;
+  if (ord == 3)
+    return __builtin_fma(b * x, x, __builtin_fma(-5.0 * (1.0 - t1), x, (43.0 / 18.0) * __builtin_fma(-t1, t1, 1.0))) - 1.0;
+  const double c = ldexp(1.0, -(t + 1));
+  double e1 = 2.0 * c, e2 = (4.0 / 3.0) * c * c, e3 = (8.0 / 21.0) * c * c * c, E = 0.0;
+  for (int a = t - 1; a >= 0; --a) {
+    const double s = ((delta >> (t - 1 - a)) & 1ull) ? -1.0 : 1.0;
+    if (a < beta) E = __builtin_fma(0.5 * s, e3, E);
+    const double y = ldexp(s, -(a + 1));
+    e3 = __builtin_fma(y, e2, e3);
+    e2 = __builtin_fma(y, e1, e2);
+    e1 += y;
+  }
+  return e1 + e2 + e3 + E;
+}
+
 }  // namespace fgp

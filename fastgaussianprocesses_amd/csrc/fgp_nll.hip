@@ -90,14 +90,18 @@ __global__ __launch_bounds__(kWG) void k_lattice_parts(const double* __restrict_
   }
 }
 
+struct NetOrders {
+  int order[FGP_MAX_D];   // Walsh kernel order per dimension, 1..4
+};
+
 __global__ __launch_bounds__(kWG) void k_net_parts(const int64_t* __restrict__ xb, int64_t xs,
                                                     const int64_t* __restrict__ z, int64_t n, int d, int t,
-                                                    double* __restrict__ parts) {
+                                                    NetOrders no, double* __restrict__ parts) {
   const int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x;
   if (i >= n) return;
   for (int j = 0; j < d; ++j) {
     const unsigned long long delta = (unsigned long long)(xb[i * xs + j] ^ z[j]);
-    parts[(int64_t)j * n + i] = walsh1(delta, t);
+    parts[(int64_t)j * n + i] = no.order[j] == 1 ? walsh1(delta, t) : walsh_omega(no.order[j], delta, t);
   }
 }
 
@@ -512,6 +516,18 @@ __global__ __launch_bounds__(kWG) void k_iter_single(Nll a, const double2* __res
   }
 }
 
+// ---------------------------------------------------------------- n > 4096: layout of `work`
+// The two-pass intermediate is stored as column tiles [N2 / C][N1][C] (C = kTile / N1 columns, the
+// column kernel's tile): element (row u, column k) of the N1 x N2 view at
+//   (k / C) kTile + u C + k mod C.
+// The column kernel (HBM-bound) then streams one contiguous 64 KB block per workgroup; the row
+// kernels (FP64-VALU-bound, with bandwidth to spare) take the strided side: runs of C elements
+// (256 B at C = 16) spaced kTile elements apart.
+__device__ __forceinline__ int64_t work_pos(int64_t u, int64_t k, int P1) {
+  const int CL = kTileLog - P1;
+  return ((k >> CL) << kTileLog) + (u << CL) + (k & ((1 << CL) - 1));
+}
+
 // ---------------------------------------------------------------- n > 4096: forward row pass
 template <int P2, typename T, int PG, int D>
 __global__ __launch_bounds__(kWG) void k_fwd_rows(Nll a, const double2* __restrict__ tw, const double2* __restrict__ twm) {
@@ -532,7 +548,7 @@ __global__ __launch_bounds__(kWG) void k_fwd_rows(Nll a, const double2* __restri
   PSrc src;
   psrc_init(a, g, src);
   const int64_t base = (int64_t)row0 * N2;
-  T* out = static_cast<T*>(a.work) + (int64_t)g * n + base;
+  T* out = static_cast<T*>(a.work) + (int64_t)g * n;
   if constexpr (RPW == 1) {
     // register-resident row transform: k1 at the thread's 16 consecutive elements 16 tid + t (the first
     // radix-16 pass's inputs), centred by the row mean, 3 passes with 2 LDS hand-overs, output at
@@ -548,10 +564,10 @@ __global__ __launch_bounds__(kWG) void k_fwd_rows(Nll a, const double2* __restri
     if constexpr (sizeof(T) == 16) {
       const RowTwiddle rt((unsigned)row0, tid, P2, m1, tw, twm);
 #pragma unroll
-      for (int k = 0; k < 16; ++k) out[tid + k * kWG] = tw_mul<T>(v[k], rt.at(k, P2, m1, tw, twm), false);
+      for (int k = 0; k < 16; ++k) out[work_pos(row0, tid + k * kWG, m1)] = tw_mul<T>(v[k], rt.at(k, P2, m1, tw, twm), false);
     } else {
 #pragma unroll
-      for (int k = 0; k < 16; ++k) out[tid + k * kWG] = v[k];
+      for (int k = 0; k < 16; ++k) out[work_pos(row0, tid + k * kWG, m1)] = v[k];
     }
     return;
   } else {
@@ -575,7 +591,7 @@ __global__ __launch_bounds__(kWG) void k_fwd_rows(Nll a, const double2* __restri
         const unsigned ex = brev_bits((unsigned)(row0 + (e >> P2)), m1) * (unsigned)(e & (N2 - 1));
         v = tw_mul<T>(v, inter_tw(ex, P2, m1, tw, twm), false);
       }
-      out[e] = v;
+      out[work_pos(row0 + (e >> P2), e & (N2 - 1), m1)] = v;
     }
   }
 }
@@ -605,13 +621,13 @@ __global__ __launch_bounds__(kWG) void k_fwd_cols(Nll a, const double2* __restri
   const int64_t c0 = (int64_t)blk * C;
   const int tid = threadIdx.x;
   const int c = tid % C, tt = tid / C;
-  T* wk = static_cast<T*>(a.work) + (int64_t)g * n + c0 + c;
+  T* wk = static_cast<T*>(a.work) + (int64_t)g * n + (int64_t)blk * kTile + c;   // contiguous tile (work_pos)
   T* col = lds + c * CS;
   T v[16];
 #pragma unroll
   for (int j = 0; j < 16 / R0; ++j)
 #pragma unroll
-    for (int t = 0; t < R0; ++t) v[j * R0 + t] = wk[(int64_t)pass_pos<P1, 0, RL0>(tt, j, t) * N2];
+    for (int t = 0; t < R0; ++t) v[j * R0 + t] = wk[pass_pos<P1, 0, RL0>(tt, j, t) * C];
   double y[16];
   if constexpr (!EMIT) {   // Y at the frequencies this thread ends the forward transform on: in flight early
     const double* yg = a.ysq + (int64_t)g * a.ysq_stride + c0 + c;
@@ -659,7 +675,7 @@ __global__ __launch_bounds__(kWG) void k_fwd_cols(Nll a, const double2* __restri
 #pragma unroll
   for (int j = 0; j < 16 / R0; ++j)
 #pragma unroll
-    for (int t = 0; t < R0; ++t) wk[(int64_t)pass_pos<P1, 0, RL0>(tt, j, t) * N2] = v[j * R0 + t];
+    for (int t = 0; t < R0; ++t) wk[pass_pos<P1, 0, RL0>(tt, j, t) * C] = v[j * R0 + t];
   norm = block_sum(norm, redd);
   logdet = block_sum(logdet, redd);
   dnoise = block_sum(dnoise, redd);
@@ -687,7 +703,7 @@ __global__ __launch_bounds__(kWG) void k_bwd_rows(Nll a, const double2* __restri
   const int row0 = blk * RPW;
   const int64_t base = (int64_t)blk * kTile;
   const int tid = threadIdx.x;
-  const T* in = static_cast<const T*>(a.work) + (int64_t)g * n + base;
+  const T* in = static_cast<const T*>(a.work) + (int64_t)g * n;   // column-tile layout (work_pos)
   if constexpr (RPW == 1) {
     T v[16];
     T sum = zero_v<T>();
@@ -695,13 +711,13 @@ __global__ __launch_bounds__(kWG) void k_bwd_rows(Nll a, const double2* __restri
       const RowTwiddle rt((unsigned)row0, tid, P2, m1, tw, twm);
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
-        v[k] = tw_mul<T>(in[tid + k * kWG], rt.at(k, P2, m1, tw, twm), true);
+        v[k] = tw_mul<T>(in[work_pos(row0, tid + k * kWG, m1)], rt.at(k, P2, m1, tw, twm), true);
         sum += v[k];
       }
     } else {
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
-        v[k] = in[tid + k * kWG];
+        v[k] = in[work_pos(row0, tid + k * kWG, m1)];
         sum += v[k];
       }
     }
@@ -737,7 +753,7 @@ __global__ __launch_bounds__(kWG) void k_bwd_rows(Nll a, const double2* __restri
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const int e = tid + k * kWG;
-      T v = in[e];
+      T v = in[work_pos(row0 + (e >> P2), e & (N2 - 1), m1)];
       if constexpr (FFT) {
         const unsigned ex = brev_bits((unsigned)(row0 + (e >> P2)), m1) * (unsigned)(e & (N2 - 1));
         v = tw_mul<T>(v, inter_tw(ex, P2, m1, tw, twm), true);
@@ -1242,12 +1258,17 @@ int fgp_lattice_parts(const double* x, int64_t x_row_stride, const double* z, in
   return check_launch("k_lattice_parts");
 }
 
-int fgp_net_parts(const int64_t* xb, int64_t xb_row_stride, const int64_t* z, int64_t n, int d, int t, double* parts,
-                  void* stream) {
+int fgp_net_parts(const int64_t* xb, int64_t xb_row_stride, const int64_t* z, int64_t n, int d, int t,
+                  const int* order, double* parts, void* stream) {
   if (n < 0 || d < 1 || d > FGP_MAX_D || t < 1 || t > 63) return set_error(kErrInvalid, "fgp_net_parts: bad n/d/t");
+  NetOrders no;
+  for (int j = 0; j < FGP_MAX_D; ++j) {
+    no.order[j] = (order && j < d) ? order[j] : 1;
+    if (no.order[j] < 1 || no.order[j] > 4) return set_error(kErrUnsupported, "fgp_net_parts: Walsh order %d unsupported", no.order[j]);
+  }
   if (n == 0) return kOk;
   if (!xb || !z || !parts) return set_error(kErrInvalid, "fgp_net_parts: null pointer");
-  k_net_parts<<<(unsigned)((n + kWG - 1) / kWG), kWG, 0, (hipStream_t)stream>>>(xb, xb_row_stride, z, n, d, t, parts);
+  k_net_parts<<<(unsigned)((n + kWG - 1) / kWG), kWG, 0, (hipStream_t)stream>>>(xb, xb_row_stride, z, n, d, t, no, parts);
   return check_launch("k_net_parts");
 }
 

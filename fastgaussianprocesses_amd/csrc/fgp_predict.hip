@@ -69,6 +69,14 @@ __device__ __forceinline__ double net_factor(unsigned long long delta, int tbits
   return c1 - ldexp(c3, fl - tbits);
 }
 
+// Net factor of Walsh order ord: order 1 as above (fa = 1 + l, fc = 3 l); orders 2..4
+// 1 + l omega_ord(delta) (fa = l; walsh_omega, fgp_common.h)
+__device__ __forceinline__ double net_fa(int ord, double l) { return ord <= 1 ? 1.0 + l : l; }
+__device__ __forceinline__ double net_factor_o(int ord, unsigned long long delta, int tbits, double fa, double fc) {
+  if (ord <= 1) return net_factor(delta, tbits, fa, fc);
+  return __builtin_fma(fa, walsh_omega(ord, delta, tbits), 1.0);
+}
+
 __device__ __forceinline__ unsigned long long to_bits(double v, int tbits) {
   double r = fmod(v, 1.0);
   if (r != 0.0 && r < 0.0) r += 1.0;                 // torch.remainder(v, 1)
@@ -116,8 +124,8 @@ __global__ __launch_bounds__(kWG) void k_post_mean(const double* __restrict__ xt
         fa[b][j] = l * spec.coef[j];
         fc[b][j] = fac_const(ord, fa[b][j]);
       } else {
-        fa[b][j] = 1.0 + l;   // c1
-        fc[b][j] = 3.0 * l;   // c3
+        fa[b][j] = net_fa(spec.order[j], l);   // c1 (order 1) / l
+        fc[b][j] = 3.0 * l;                     // c3
       }
     }
   }
@@ -175,7 +183,7 @@ __global__ __launch_bounds__(kWG) void k_post_mean(const double* __restrict__ xt
           } else {
             const unsigned long long delta = xbv[j] ^ (unsigned long long)__double_as_longlong(zs[j][i]);
 #pragma unroll
-            for (int b = 0; b < NB; ++b) p[b] *= net_factor(delta, tbits, fa[b][j], fc[b][j]);
+            for (int b = 0; b < NB; ++b) p[b] *= net_factor_o(spec.order[j], delta, tbits, fa[b][j], fc[b][j]);
           }
         }
 #pragma unroll
@@ -237,7 +245,7 @@ __global__ __launch_bounds__(kWG) void k_kernel_rows(const double* __restrict__ 
         const double a = l * spec.coef[j];
         p *= lat_factor(spec.order[j], tv[j], a, fac_const(spec.order[j], a));
       } else {
-        p *= net_factor(dv[j], tbits, 1.0 + l, 3.0 * l);
+        p *= net_factor_o(spec.order[j], dv[j], tbits, net_fa(spec.order[j], l), 3.0 * l);
       }
     }
     rows[((int64_t)g * N + t) * n + i] = hyp[g * (1 + D)] * p;
@@ -296,7 +304,7 @@ __global__ __launch_bounds__(kWG) void k_qf_rows(QfArgs q, const double2* __rest
       fc[j] = fac_const(q.spec.order[j], fa[j]);
     } else {
       xb[j] = to_bits(xv[j], q.tbits);
-      fa[j] = 1.0 + l;
+      fa[j] = net_fa(q.spec.order[j], l);
       fc[j] = 3.0 * l;
     }
   }
@@ -329,8 +337,8 @@ __global__ __launch_bounds__(kWG) void k_qf_rows(QfArgs q, const double2* __rest
           p1 *= lat_factor(q.spec.order[j], fabs(xv[j] - zv.y), fa[j], fc[j]);
         } else {
           const longlong2 zv = *reinterpret_cast<const longlong2*>(static_cast<const long long*>(zp) + (int64_t)j * n + base + e);
-          p0 *= net_factor(xb[j] ^ (unsigned long long)zv.x, q.tbits, fa[j], fc[j]);
-          p1 *= net_factor(xb[j] ^ (unsigned long long)zv.y, q.tbits, fa[j], fc[j]);
+          p0 *= net_factor_o(q.spec.order[j], xb[j] ^ (unsigned long long)zv.x, q.tbits, fa[j], fc[j]);
+          p1 *= net_factor_o(q.spec.order[j], xb[j] ^ (unsigned long long)zv.y, q.tbits, fa[j], fc[j]);
         }
       }
     }
@@ -539,12 +547,21 @@ static int launch_rows(int d, const double* xt, int64_t N, const void* z, int64_
   return check_launch("k_kernel_rows");
 }
 
+// Lattice: Bernoulli order 2 alpha and coefficient per dimension.  Net: Walsh order alpha per dimension
+// (1..4; order = NULL or 0 entries: 1), coefficients unused.
 static int make_spec(int family, int d, const int* order, const double* coef, PredSpec& spec) {
+  const bool lat = family == FGP_FAMILY_LATTICE;
   for (int j = 0; j < FGP_MAX_D; ++j) {
-    spec.order[j] = (family == FGP_FAMILY_LATTICE && j < d) ? order[j] : 0;
-    spec.coef[j] = (family == FGP_FAMILY_LATTICE && j < d) ? coef[j] : 0.0;
-    if (family == FGP_FAMILY_LATTICE && j < d && (order[j] < 2 || order[j] > 8 || (order[j] & 1)))
-      return set_error(kErrUnsupported, "Bernoulli order %d unsupported", order[j]);
+    if (lat) {
+      spec.order[j] = j < d ? order[j] : 0;
+      spec.coef[j] = j < d ? coef[j] : 0.0;
+      if (j < d && (order[j] < 2 || order[j] > 8 || (order[j] & 1)))
+        return set_error(kErrUnsupported, "Bernoulli order %d unsupported", order[j]);
+    } else {
+      spec.order[j] = (order && j < d && order[j] > 0) ? order[j] : 1;
+      spec.coef[j] = 0.0;
+      if (spec.order[j] > 4) return set_error(kErrUnsupported, "Walsh order %d unsupported", spec.order[j]);
+    }
   }
   return kOk;
 }

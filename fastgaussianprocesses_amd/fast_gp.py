@@ -1038,8 +1038,11 @@ class FastGPLattice(AbstractFastGP):
 class FastGPDigitalNetB2(AbstractFastGP):
     """Fast GP on digitally shifted base-2 digital nets with digitally-shift-invariant (Walsh)
     kernels: the Gram matrix is diagonalised by the FWHT (fastgps/fast_gp_digital_net_b2.py:7-301).
-    Order-1 Walsh kernels (alpha=1) are supported; orders 2-4 need qmcpy.weighted_walsh_funcs,
-    whose values are unpinned offline and raise NotImplementedError."""
+    Walsh orders alpha = 1..4 (default 2).  Order 1 follows the reference's inline formula
+    (:297-298); orders 2-4 are the series omega_a = sum_{k>=1} 2^(-mu_a(k)) wal_k that the reference
+    takes from qmcpy.kernel_methods.weighted_walsh_funcs(a, ., t) - 1 (:300) -- restated here from
+    that definition (walsh_omega in csrc/fgp_common.h); qmcpy is absent offline, so parity at that
+    boundary is unpinned."""
 
     _FAMILY = ops.NET
     _XBDTYPE = torch.int64
@@ -1064,9 +1067,6 @@ class FastGPDigitalNetB2(AbstractFastGP):
         assert (1 <= self.alpha).all() and (self.alpha <= 4).all()
         self.t = int(self.seq.t)
         assert self.t < 64, "each seq must have t<64"
-        if any(a != 1 for a in self._alphas):
-            raise NotImplementedError("digital-net kernels of order alpha>=2 need qmcpy.weighted_walsh_funcs, "
-                                      "which is not available offline (parity unpinned); use alpha=1")
 
     def _default_seq(self, d, seed):
         return _seqs.DigitalNetB2(d, seed=seed, randomize="DS")
@@ -1103,21 +1103,57 @@ class FastGPDigitalNetB2(AbstractFastGP):
         return ops.fwht(x, stable=True)
 
     def _compute_parts(self, xb, x0, out=None):
-        return ops.net_parts(xb, x0, self.t, out=out)
+        return ops.net_parts(xb, x0, self.t, out=out, alphas=self._alphas)
 
     def _part_at_zero(self):
-        return torch.ones(self.d, dtype=torch.float64)
+        return torch.tensor([_WALSH_AT_ZERO[a] for a in self._alphas], dtype=torch.float64)
 
     def _kernel_torch(self, x, z):
         xb = self._to_b(x) if torch.is_floating_point(x) else x
         zb = self._to_b(z) if torch.is_floating_point(z) else z
         delta = xb ^ zb
-        parts = 6 * (1 / 6 - 2 ** (torch.log2(delta).floor() - self.t - 1))
+        parts = torch.stack([walsh_part_t(a, delta[..., j], self.t) for j, a in enumerate(self._alphas)], -1)
         ndim = parts.ndim
         s = self.scale.reshape(self.scale.shape + torch.Size([1] * (ndim - 2)))
         ls = self.lengthscales.reshape(self.lengthscales.shape[:-1] + torch.Size([1] * (ndim - 1)) +
                                        self.lengthscales.shape[-1:])
         return s * (1 + ls * parts).prod(-1)
+
+
+# omega_a(0) = sum_{k>=1} 2^(-mu_a(k)) (order 1: the reference's 6 (1/6 - 0) = 1)
+_WALSH_AT_ZERO = {1: 1.0, 2: 1.5, 3: 25 / 18, 4: 407 / 294}
+
+
+def walsh_part_t(order, delta, t):
+    """Torch restatement of the device Walsh part (csrc/fgp_common.h walsh_omega; order 1:
+    fast_gp_digital_net_b2.py:297-298) for the generic autograd path (kernel(), derivative-free)."""
+    delta = delta.to(torch.int64)
+    if order == 1:
+        return 6 * (1 / 6 - 2 ** (torch.log2(delta.to(torch.float64)).floor() - t - 1))
+    nz = delta != 0
+    fl = torch.floor(torch.log2(torch.clamp(delta, min=1).to(torch.float64)))
+    beta = t - fl
+    x = delta.to(torch.float64) * 2.0 ** (-t)
+    t1 = 2.0 ** (-beta)
+    if order == 2:
+        v = -beta * x + 2.5 * (1 - t1) - 1
+    elif order == 3:
+        v = beta * x * x - 5 * (1 - t1) * x + 43 / 18 * (1 - t1 * t1) - 1
+    else:
+        c = 2.0 ** (-(t + 1))
+        e1 = torch.full_like(x, 2 * c)
+        e2 = torch.full_like(x, 4 / 3 * c * c)
+        e3 = torch.full_like(x, 8 / 21 * c ** 3)
+        E = torch.zeros_like(x)
+        for a in range(t - 1, -1, -1):
+            s = 1.0 - 2.0 * ((delta >> (t - 1 - a)) & 1).to(torch.float64)
+            E = torch.where(a < beta, E + 0.5 * s * e3, E)
+            y = s * 2.0 ** (-(a + 1))
+            e3 = e3 + y * e2
+            e2 = e2 + y * e1
+            e1 = e1 + y
+        v = e1 + e2 + e3 + E
+    return torch.where(nz, v, torch.full_like(v, _WALSH_AT_ZERO[order]))
 
 
 _BERN = {

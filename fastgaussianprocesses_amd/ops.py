@@ -196,8 +196,9 @@ def lattice_parts_gen(z, shift, alphas, n):
     return parts
 
 
-def net_parts(xb, z, t, out=None):
-    """Order-1 Walsh parts for delta = xb XOR z -> [d, n] (fast_gp_digital_net_b2.py:274-301)."""
+def net_parts(xb, z, t, out=None, alphas=None):
+    """Walsh parts of order alphas[j] (1..4, default 1) for delta = xb XOR z -> [d, n]
+    (fast_gp_digital_net_b2.py:274-301; see fgp_net_parts)."""
     require_device(xb, "net_parts")
     xb = xb.to(torch.int64)
     if xb.stride(-1) != 1:
@@ -207,7 +208,8 @@ def net_parts(xb, z, t, out=None):
     if out is None:
         out = torch.empty((d, n), dtype=torch.float64, device=xb.device)
     assert out.shape == (d, n) and out.is_contiguous() and out.dtype == torch.float64
-    N.call("fgp_net_parts", N.ptr(xb), xb.stride(0), N.ptr(z), n, d, int(t), N.ptr(out), _stream(xb))
+    order = N.int_array([int(a) for a in alphas]) if alphas is not None else None
+    N.call("fgp_net_parts", N.ptr(xb), xb.stride(0), N.ptr(z), n, d, int(t), order, N.ptr(out), _stream(xb))
     return out
 
 
@@ -215,7 +217,7 @@ def net_parts(xb, z, t, out=None):
 def _pred_args(family, alphas, d):
     if family == LATTICE:
         return N.int_array([2 * a for a in alphas]), N.double_array([lattice_coefficient(a) for a in alphas])
-    return N.int_array([0] * d), N.double_array([0.0] * d)
+    return N.int_array([int(a) for a in alphas] if alphas is not None else [1] * d), N.double_array([0.0] * d)
 
 
 def post_mean_matfree(family, xt, z_dn, hyp, coeffs, alphas=None, tbits=0, chunk=1024):

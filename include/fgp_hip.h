@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define FGP_ABI_VERSION 5
+#define FGP_ABI_VERSION 6
 
 #define FGP_OK 0
 #define FGP_ERR_INVALID (-1)     /* bad argument (shape, stride, null pointer) */
@@ -88,11 +88,16 @@ int fgp_fwht(const double* in, int64_t in_batch_stride, double* out, int64_t bat
 int fgp_lattice_parts(const double* x, int64_t x_row_stride, const double* z, int64_t n, int d, const int* order,
                       const double* coef, double* parts, void* stream);
 
-/* Digital-net first-column kernel parts, order-1 Walsh kernel (fastgps/fast_gp_digital_net_b2.py:274-301):
- *   delta = xb[i, j] XOR z[j];  parts[j, i] = 6*(1/6 - 2^(floor(log2 delta) - t - 1))  (1 when delta = 0).
- * xb: [n, d] int64 t-bit integers (row stride xb_row_stride), z: [d] int64 (device). */
-int fgp_net_parts(const int64_t* xb, int64_t xb_row_stride, const int64_t* z, int64_t n, int d, int t, double* parts,
-                  void* stream);
+/* Digital-net first-column kernel parts (fastgps/fast_gp_digital_net_b2.py:274-301), Walsh order
+ * order[j] in 1..4 per dimension (order = NULL: all 1):
+ *   delta = xb[i, j] XOR z[j];
+ *   order 1:    parts[j, i] = 6*(1/6 - 2^(floor(log2 delta) - t - 1))  (1 when delta = 0)  (:297-298)
+ *   order 2..4: parts[j, i] = omega_a(delta / 2^t) = sum_{k>=1} 2^(-mu_a(k)) wal_k  -- the reference's
+ *               qmcpy.kernel_methods.weighted_walsh_funcs(a, delta, t) - 1 (:300), restated from its
+ *               series definition (qmcpy itself is absent offline: parity unpinned at that boundary).
+ * xb: [n, d] int64 t-bit integers (row stride xb_row_stride), z: [d] int64 (device).  ABI 6: `order`. */
+int fgp_net_parts(const int64_t* xb, int64_t xb_row_stride, const int64_t* z, int64_t n, int d, int t,
+                  const int* order, double* parts, void* stream);
 
 /* On-device natural-order rank-1 lattice points (seqs.Lattice / qmcpy Lattice, the point generation
  * of AbstractGP.get_x_next, fastgps/abstract_gp.py:307-309 -> util.py:17-48), bit-identical to the host
@@ -197,7 +202,8 @@ int fgp_fit_run(const fgp_nll_desc* nll, const fgp_fit_desc* fit, int iter0, int
  *   out[b, t] = sum_i K_g(xt[t], z[:, i]) coeffs[b, i],  g = b mod Gk,
  *   K_g(x, z) = hyp[g, 0] * prod_j (1 + hyp[g, 1 + j] part_j(x, z))   (hyp holds scale, lengthscales)
  * lattice: part_j = coef[j] B_{order[j]}((x_j - z_j) % 1), z float64 [d][n];
- * net:     part_j = walsh1(floor((x_j % 1) 2^tbits) XOR z_j), z int64 [d][n] (order/coef unused).
+ * net:     part_j = walsh part of order order[j] (1..4, as fgp_net_parts; order = NULL: 1) of
+ *          floor((x_j % 1) 2^tbits) XOR z_j, z int64 [d][n] (coef unused).
  * xt: [N, d] float64 contiguous; coeffs: [B][n] with row stride coeff_stride; 1 <= B <= 4;
  * out: [B][N] row stride out_stride; work: float64 scratch of ceil(n/chunk) * B * N entries. */
 int fgp_post_mean(int family, const double* xt, int64_t N, const void* z, int64_t n, int d, int tbits, const int* order,

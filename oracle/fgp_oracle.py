@@ -127,12 +127,54 @@ def lattice_k1parts(x, alpha):
     return lattice_kernel_parts(x, x[:1], alpha)
 
 
+def walsh_omega(order, delta, t):
+    """omega_a(delta / 2^t) = sum_{k>=1} 2^(-mu_a(k)) wal_k(x) for Walsh order a in 2..4, the series
+    behind qmcpy.kernel_methods.weighted_walsh_funcs(a, delta, t) - 1 (fast_gp_digital_net_b2.py:300).
+    qmcpy is absent offline: this restates the series definition (Dick's weight mu_a(k) = sum of the
+    a highest bit positions of k, +1 each) by a digit recursion -- y_a = (-1)^(x_{a+1}) 2^-(a+1),
+    elementary symmetric sums e_r of the digits above the current one, seeded with the all-zero tail:
+        omega = sum_{r<a} e_r(all) + sum_{b < beta} (1/2) s_b e_{a-1}(y_{>b})
+    (the k whose lower bits are free sum to 2^b [x_1..x_b = 0]).  It is checked against the
+    truncated series itself in tests/test_oracle_golden.py.  PARITY UNPINNED against qmcpy."""
+    from math import prod
+    delta = torch.as_tensor(delta).to(torch.int64)
+    r1 = order - 1
+    c = 2.0 ** -(t + 1)
+    e = [torch.ones(delta.shape, dtype=torch.float64)]
+    for r in range(1, order):
+        e.append(torch.full(delta.shape, c ** r * 2.0 ** (-r * (r - 1) / 2) / prod(1 - 2.0 ** -i for i in range(1, r + 1)),
+                            dtype=torch.float64))
+    nz = delta != 0
+    hi = torch.zeros(delta.shape, dtype=torch.int64)          # floor(log2 delta), exact
+    for b in range(64):
+        hi = torch.where((delta >> b) > 0, torch.full_like(hi, b), hi)
+    beta = torch.where(nz, t - hi, torch.full_like(hi, 1 << 30))
+    E = torch.zeros(delta.shape, dtype=torch.float64)
+    for a in range(t - 1, -1, -1):
+        s = 1.0 - 2.0 * ((delta >> (t - 1 - a)) & 1).to(torch.float64)
+        E = E + torch.where(a < beta, 0.5 * s * e[r1], torch.zeros_like(E))
+        y = s * 2.0 ** -(a + 1)
+        for r in range(r1, 0, -1):
+            e[r] = e[r] + y * e[r - 1]
+    K = 2.0 ** (-r1 * (r1 - 1) / 2) / prod(1 - 2.0 ** -i for i in range(1, r1 + 1))
+    tail = 0.5 * K * 2.0 ** (-(t + 2) * r1) / (1 - 2.0 ** -r1)     # b >= t, reached only by delta = 0
+    E = E + torch.where(nz, torch.zeros_like(E), torch.full_like(E, tail))
+    return sum(e[1:]) + E
+
+
 def net_kernel_parts(xb, zb, t, alpha=1):
-    """Order-1 digitally-shift-invariant parts for delta = xb XOR zb (fast_gp_digital_net_b2.py:274-301)."""
-    assert alpha == 1 or (not np.isscalar(alpha) and all(a == 1 for a in alpha)), \
-        "only order-1 Walsh kernels are pinned (weighted_walsh_funcs orders 2-4 are parity unpinned)"
+    """Digitally-shift-invariant parts for delta = xb XOR zb (fast_gp_digital_net_b2.py:274-301):
+    order 1 by the reference's inline formula (:297-298), orders 2-4 by walsh_omega (:300)."""
     delta = xb ^ zb
-    return 6 * (1 / 6 - 2 ** (torch.log2(delta).floor() - t - 1))
+    d = delta.shape[-1]
+    alphas = [alpha] * d if np.isscalar(alpha) else list(alpha)
+    cols = []
+    for j in range(d):
+        if int(alphas[j]) == 1:
+            cols.append(6 * (1 / 6 - 2 ** (torch.log2(delta[..., j]).floor() - t - 1)))
+        else:
+            cols.append(walsh_omega(int(alphas[j]), delta[..., j], t))
+    return torch.stack(cols, -1)
 
 
 def net_k1parts(xb, t, alpha=1):

@@ -2,7 +2,10 @@
 
 bernoulli_poly(n, x): Bernoulli polynomial B_n(x), coefficients below, evaluated in Horner form.
 weighted_walsh_funcs(order, xb, t): order 1 follows fastgps' own inline formula
-(fast_gp_digital_net_b2.py:297-298); orders 2-4 are not restated (parity unpinned).
+(fast_gp_digital_net_b2.py:297-298); orders 2-4 return 1 + omega_order, the series
+sum_{k>=0} 2^(-mu_order(k)) wal_k (oracle.fgp_oracle.walsh_omega), so that the reference's
+`weighted_walsh_funcs(...) - 1` (:300) is omega.  qmcpy's own values are unavailable offline:
+parity at this boundary is unpinned.
 """
 from fractions import Fraction as _F
 
@@ -36,4 +39,5 @@ def bernoulli_poly(n, x):
 def weighted_walsh_funcs(order, xb, t):
     if int(order) == 1:
         return 6 * (1 / 6 - 2 ** (torch.log2(xb).floor() - t - 1))
-    raise NotImplementedError("weighted_walsh_funcs order>=2 is not restated (parity unpinned, SURVEY §8c)")
+    from oracle.fgp_oracle import walsh_omega
+    return 1 + walsh_omega(int(order), xb, int(t))

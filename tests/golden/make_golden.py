@@ -2,7 +2,7 @@
 
 Run in the build container only (the reference does not exist on the GPU box):
 
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [fixture names...]
 
 The reference is imported through oracle/refshim/load_reference.py (in-memory PEP-646 rewrite +
 qmcpy stand-in).  All point sets are EXPLICIT (generating vector / matrices + shift are
@@ -195,6 +195,13 @@ CASES = [
     ("net", 12, 5, 1, 0, False),
     ("net", 13, 2, 1, 0, False),
     ("net", 10, 2, 1, 3, False),
+    # Walsh orders 2-4 (the reference's default alpha = 2): the reference's pipeline with qmcpy's
+    # weighted_walsh_funcs restated by the stand-in (parity at that boundary unpinned)
+    ("net", 4, 2, 2, 0, False),
+    ("net", 10, 3, 2, 0, False),
+    ("net", 11, 2, 3, 0, False),
+    ("net", 9, 3, 4, 0, False),
+    ("net", 10, 2, 2, 3, False),
 ]
 
 
@@ -207,8 +214,11 @@ def main():
     torch.set_default_dtype(torch.float64)
     fg = import_reference()
     import qmcpy
+    only = set(sys.argv[1:])          # optional: regenerate only the named fixtures
     for c in CASES:
         name = case_name(c)
+        if only and name not in only:
+            continue
         out = gen_case(fg, qmcpy, *c)
         np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
         print("wrote", name, "loss=%.10e" % float(out["loss"]))

@@ -105,3 +105,42 @@ def test_oracle_fit_trajectory(name):
     rel_close(data["lengthscales_hist"].numpy(), g["fit_lengthscales_hist"], 1e-12)
     rel_close(o.raw_scale.detach().numpy(), g["fit_raw_scale"], 1e-12)
     rel_close(o.raw_lengthscales.detach().numpy(), g["fit_raw_lengthscales"], 1e-12)
+
+
+def _walsh_series(order, delta, t, T):
+    """sum_{1 <= k < 2^T} 2^(-mu_order(k)) wal_k(delta / 2^t): the definition, truncated (T > t)."""
+    x = np.asarray(delta, dtype=np.int64) << (T - t)
+    out = np.zeros(x.shape)
+    for k in range(1, 2 ** T):
+        bits = [i for i in range(k.bit_length() - 1, -1, -1) if (k >> i) & 1]
+        mu = sum(a + 1 for a in bits[:order])
+        par = np.zeros(x.shape, dtype=np.int64)
+        for i in bits:                       # wal_k(x) = (-1)^(sum_i k_i x_{i+1}), x_{i+1} = bit T-1-i
+            par ^= (x >> (T - 1 - i)) & 1
+        out += 2.0 ** -mu * (1 - 2 * par)
+    return out
+
+
+@pytest.mark.parametrize("order", [2, 3, 4])
+def test_walsh_omega_is_the_series(order):
+    """walsh_omega (the oracle's restatement of qmcpy.weighted_walsh_funcs - 1 for orders 2-4,
+    fast_gp_digital_net_b2.py:300) equals its defining series sum_{k>=1} 2^(-mu_a(k)) wal_k: the
+    series truncated at k < 2^T is within 2^-(T - t) of it, and the truncation error shrinks as T grows."""
+    t = 5
+    delta = np.arange(2 ** t)
+    om = O.walsh_omega(order, torch.from_numpy(delta), t).numpy()
+    e1 = np.max(np.abs(_walsh_series(order, delta, t, t + 8) - om))
+    e2 = np.max(np.abs(_walsh_series(order, delta, t, t + 12) - om))
+    assert e2 <= 2.0 ** -12 and e2 < e1 / 4
+    assert om[0] == pytest.approx({2: 1.5, 3: 25 / 18, 4: 407 / 294}[order], abs=1e-15)
+
+
+@pytest.mark.parametrize("order", [2, 3, 4])
+def test_walsh_part_host_matches_oracle(order):
+    """The package's closed forms (orders 2, 3) / digit recursion (order 4) used by its generic torch
+    path agree with the oracle's recursion to rounding, at t = 5 exhaustively and t = 40 sampled."""
+    from fastgaussianprocesses_amd.fast_gp import walsh_part_t
+    for t, delta in ((5, torch.arange(32)), (40, torch.randint(0, 2 ** 40, (2000,), generator=torch.Generator().manual_seed(3)))):
+        a = walsh_part_t(order, delta, t)
+        b = O.walsh_omega(order, delta, t)
+        assert float((a - b).abs().max()) <= 4e-15
