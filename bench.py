@@ -135,14 +135,22 @@ def phase_breakdown(sh, iters, xm, xv):
 STAGES = ("k_fwd_rows", "k_fwd_cols", "k_bwd_rows")
 
 
+def r2c_active(n):
+    """The lattice fit runs the half-length (R2C) kernels for n >= 2^17 unless FGP_R2C=0
+    (csrc/fgp_nll.hip to_nll)."""
+    return n >= 2 ** 17 and os.environ.get("FGP_R2C", "1")[:1] != "0"
+
+
 def stage_bytes(n, d, P, parts_array):
     """Algorithmic HBM bytes of one launch of each fit-iteration kernel over P lattice problems
-    (complex128 intermediate `work`, float64 Y; DESIGN.md 'Kernels'):
-      k_fwd_rows: write work 16n (+ read parts 8nd when not regenerated)
-      k_fwd_cols: read work 16n + read Y 8n + write work 16n
-      k_bwd_rows: read work 16n (+ read parts 8nd)"""
+    (complex128 intermediate `work` of L = n complex values, L = n/2 for the half-length R2C kernels;
+    float64 Y; DESIGN.md 'Kernels'):
+      k_fwd_rows: write work 16L (+ read parts 8nd when not regenerated)
+      k_fwd_cols: read work 16L + read Y 8n + write work 16L
+      k_bwd_rows: read work 16L (+ read parts 8nd)"""
     pb = 8 * n * d if parts_array else 0
-    return {"k_fwd_rows": (16 * n + pb) * P, "k_fwd_cols": 40 * n * P, "k_bwd_rows": (16 * n + pb) * P}
+    L = n // 2 if r2c_active(n) else n
+    return {"k_fwd_rows": (16 * L + pb) * P, "k_fwd_cols": (32 * L + 8 * n) * P, "k_bwd_rows": (16 * L + pb) * P}
 
 
 def roofline_fit_kernels(F, shifts, iters):
@@ -186,7 +194,7 @@ def pmc_traffic(kernel, grid):
         return None
     for k, v in summ.items():
         name, _, g = k.partition("|grid=")
-        if name.split("<")[0].endswith(kernel) and g == str(grid) and "traffic_bytes" in v:
+        if name.split("<")[0].split("::")[-1] == kernel and g == str(grid) and "traffic_bytes" in v:
             return v["traffic_bytes"]
     return None
 
@@ -275,13 +283,17 @@ def main():
     P = len(shifts.gps)
     sb = stage_bytes(n, d, P, parts_array)
     dom = max(STAGES, key=lambda k: us[k])
+    r2c = r2c_active(n)
+    kname = dom + ("_r2c" if r2c else "")
+    grid_wg = P * (n // 2 if r2c else n) // 4096
     ach = sb[dom] / (us[dom] * 1e-6) / 1e9
     # SURVEY §8(d) reference-dataflow bytes of one fit iteration: 16nd + 32n + 32nB per GP (B = 1)
     b_iter = (16 * n * d + 32 * n + 32 * n) * P
-    roof = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic(dom, P * n // 16),
+    roof = {"bound": "hbm", "kernel": kname, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic(kname, grid_wg * 256),
             "traffic_source": os.path.relpath(PMC_SUMMARY, os.path.dirname(os.path.abspath(__file__))), "algorithmic_bytes": sb[dom], "avg_us": us[dom],
-            "launch": "%d problems x n=2^%d (grid %d workgroups)" % (P, args.log2n, P * n // 4096),
+            "launch": "%d problems x n=2^%d (grid %d workgroups)" % (P, args.log2n, grid_wg),
+            "transform": "half-length R2C (n/2 complex)" if r2c else "full-length (n complex)",
             "kernels": {k: {"avg_us": us[k], "bytes": sb.get(k),
                             "GB/s": (sb[k] / (us[k] * 1e-6) / 1e9) if k in sb else None} for k in us},
             "parts": "array" if parts_array else "regenerated (FGP_PARTS_LATTICE)",

@@ -25,6 +25,7 @@
 //               each) or, with the lattice generator (FGP_PARTS_LATTICE), regenerated in registers.
 //   then k_fit_step (one workgroup: deterministic reduction of the per-block partials, loss
 //   assembly, histories, Rprop update).
+#include <cstdlib>
 #include <cmath>
 #include <type_traits>
 
@@ -120,6 +121,7 @@ struct Nll {
   unsigned gz[FGP_MAX_D];        // z_j mod n
   const double* gshift;
   int64_t gshift_stride;
+  int r2c;                       // lattice, n >= 2^17: half-length (R2C) fit kernels
 };
 
 struct Hyp {
@@ -784,6 +786,262 @@ __global__ __launch_bounds__(kWG) void k_bwd_rows(Nll a, const double2* __restri
   }
 }
 
+// ---------------------------------------------------------------- half-length (R2C) lattice fit, n >= 2^17
+// k1 is real, so the length-n bit-reversed-input FFT is done at half length (Stockham-free packing):
+// with a = x[brev_m], a[2j] = x[brev_{m-1}(j)] and a[2j+1] = x[n/2 + brev_{m-1}(j)], hence
+//   fftbr_n(x)[k], [k + n/2] = 1/2 (Z_k + conj Z_{n/2-k}) -/+ 1/2 i w_n^k (Z_k - conj Z_{n/2-k}),
+//   Z = fftbr_{n/2}(x[:n/2] + i x[n/2:]),
+// the existing engine at m - 1.  lambda, Y and dL/dlambda are Hermitian, so the adjoint needs no mirror:
+// with E_k = G_k + G_{k+n/2}, O_k = (G_k - G_{k+n/2}) conj(w_n^k), the adjoint half-length transform of
+// V = E + i O is grad_lo + i grad_hi (both real).  The mirror k <-> n/2 - k of the forward is column
+// c <-> N2 - c with rows reversed: the intermediate is stored in paired column tiles (work_pos_pair),
+// so both partners sit in one column workgroup and meet through one LDS exchange.
+//
+// Paired tile layout of the N1 x N2 half-length intermediate (C = kTile / N1 slots per tile):
+// tile 0 holds columns 0 and N2/2 (slots 0, 1) and the pairs (q, N2 - q), q = 1 .. C/2 - 1; tile
+// b >= 1 the pairs (b C/2 + q, N2 - b C/2 - q), q < C/2; slot 2q + (column > N2/2).
+__device__ __forceinline__ int64_t work_pos_pair(int64_t u, int64_t k, int P1, int64_t N2) {
+  const int CL = kTileLog - P1;
+  const int64_t h = N2 >> 1;
+  int64_t tile, slot;
+  if (k == 0) {
+    tile = 0;
+    slot = 0;
+  } else if (k == h) {
+    tile = 0;
+    slot = 1;
+  } else {
+    const int64_t c = k < h ? k : N2 - k;
+    tile = c >> (CL - 1);
+    slot = 2 * (c & ((1 << (CL - 1)) - 1)) + (k > h ? 1 : 0);
+  }
+  return (tile << kTileLog) + (u << CL) + slot;
+}
+__device__ __forceinline__ int64_t pair_col(int64_t tile, int slot, int C, int64_t N2) {
+  const int64_t c = tile * (C >> 1) + (slot >> 1);
+  if (c == 0) return (slot & 1) ? (N2 >> 1) : 0;
+  return (slot & 1) ? N2 - c : c;
+}
+
+template <int PG, int D>
+__global__ __launch_bounds__(kWG) void k_fwd_rows_r2c(Nll a, const double2* __restrict__ tw, const double2* __restrict__ twm) {
+  constexpr int P2 = 12, N2 = 1 << P2;
+  __shared__ double ldsd[kTile + kTile / 16];
+  __shared__ double2 red[kWG / 64];
+  const int mt = a.log2n - 1, m1 = mt - P2;
+  const int64_t n = (int64_t)1 << a.log2n, nt = n >> 1;
+  const int64_t tiles = nt >> kTileLog;
+  const int g = (int)(blockIdx.x / tiles);
+  const int row0 = (int)(blockIdx.x % tiles);
+  const int tid = threadIdx.x;
+  Hyp h;
+  load_hyp_wave(a, g, h);
+  PSrc src;
+  psrc_init(a, g, src);
+  const int64_t base = (int64_t)row0 * N2;
+  double2* out = static_cast<double2*>(a.work) + (int64_t)g * n;
+  double lo[16], hi[16];
+  double slo = 0.0, shi = 0.0;
+  k1_run16<PG, D>(a, h, src, n, base + 16 * tid, lo, slo);        // x[:n/2] -> real parts
+  k1_run16<PG, D>(a, h, src, n, nt + base + 16 * tid, hi, shi);   // x[n/2:] -> imaginary parts
+  double2 v[16];
+#pragma unroll
+  for (int t = 0; t < 16; ++t) v[t] = make_double2(lo[t], hi[t]);
+  const double2 mean = block_sum_t(make_double2(slo, shi), red) * (1.0 / N2);
+#pragma unroll
+  for (int t = 0; t < 16; ++t) v[t] -= mean;
+  fwd_reg_passes<P2, 0, true>(v, ldsd, tid, tw);
+  if (tid == 0) v[0] += mean * (double)N2;
+  const RowTwiddle rt((unsigned)row0, tid, P2, m1, tw, twm);
+#pragma unroll
+  for (int k = 0; k < 16; ++k)
+    out[work_pos_pair(row0, tid + k * kWG, m1, N2)] = tw_mul<double2>(v[k], rt.at(k, P2, m1, tw, twm), false);
+}
+
+// column pass at half length + mirror exchange + split into the length-n spectrum + eigen terms +
+// the adjoint packing V = E + i O + adjoint column pass, in place (k_fwd_cols for the R2C layout)
+template <int P1, bool EMIT>
+__global__ __launch_bounds__(kWG) void k_fwd_cols_r2c(Nll a, const double2* __restrict__ tw,
+                                                       const double2* __restrict__ twmf) {
+  constexpr int N1 = 1 << P1, C = kTile / N1, CS = N1 + 1;
+  constexpr int RL0 = PassRL<P1, 0>::value, R0 = 1 << RL0;
+  constexpr int SL = LastPass<P1>::S, RLL = PassRL<P1, SL>::value, RLAST = 1 << RLL;
+  __shared__ double2 lds[C * CS];
+  __shared__ double2 part[ColPart<C>::size];
+  __shared__ double redd[kWG / 64];
+  const int m = a.log2n, mt = m - 1;
+  const int64_t n = (int64_t)1 << m, nt = n >> 1, N2 = nt >> P1;
+  const int64_t tiles = nt >> kTileLog;
+  const int g = (int)(blockIdx.x / tiles);
+  const int blk = (int)(blockIdx.x % tiles);
+  const int tid = threadIdx.x;
+  const int sl = tid % C, tt = tid / C;
+  double2* wk = static_cast<double2*>(a.work) + (int64_t)g * n + (int64_t)blk * kTile + sl;
+  double2* col = lds + sl * CS;
+  double2 v[16];
+#pragma unroll
+  for (int j = 0; j < 16 / R0; ++j)
+#pragma unroll
+    for (int t = 0; t < R0; ++t) v[j * R0 + t] = wk[pass_pos<P1, 0, RL0>(tt, j, t) * C];
+  double2 sum = zero_v<double2>();
+#pragma unroll
+  for (int k = 0; k < 16; ++k) sum += v[k];
+  column_partials<C>(sum, part);
+  double2 mean = column_total<C>(sl, part) * (1.0 / N1);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v[k] -= mean;
+  fwd_reg_passes<P1, 0, false>(v, col, tt, tw);
+  if (tt == 0) v[0] += mean * (double)N1;
+  // (everything below is computed after the forward passes: the passes themselves sit at ~246
+  // VGPRs, so values kept live across them would spill)
+  const int64_t colx = pair_col(blk, sl, C, N2);
+  // (Y is read at use: prefetching its 32 values with the 16 partners needs too many registers)
+  // mirror exchange: Z at frequency nt - k lives in the partner slot, row reversed
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 16 / RLAST; ++j)
+#pragma unroll
+    for (int t = 0; t < RLAST; ++t) col[pass_pos<P1, SL, RLL>(tt, j, t)] = v[j * RLAST + t];
+  __syncthreads();
+  const bool self0 = blk == 0 && sl == 0, self1 = blk == 0 && sl == 1;
+  const double2* pc = lds + (self0 || self1 ? sl : (sl ^ 1)) * CS;
+  const int64_t colp = (self0 || self1) ? colx : pair_col(blk, sl ^ 1, C, N2);
+  const double rootn = sqrt((double)n), inv_rootn = 1.0 / rootn;
+  double2* gl = EMIT ? static_cast<double2*>(a.grad_lam) + (int64_t)g * n + colx : nullptr;
+  Hyp h;
+  if constexpr (!EMIT) load_hyp_wave(a, g, h);
+  double norm = 0.0, dnoise = 0.0;
+  LogAcc la;
+  sum = zero_v<double2>();
+  // N2 = 4096 (transform length >= 2^16): k = col + 4096 r, so w_n^k = twm_m[col] * w_n^(4096 r), the
+  // second factor a 4096-table entry (n = 2^m <= 2^24)
+  const double2 wcol = twmf[colx], wcolp = twmf[colp];
+  // Exact Hermitian symmetry: each mirror pair (k, n/2 - k) is evaluated once, by its PRIMARY element
+  // (even slot; in the self-mirrored columns 0 and N2/2 the smaller row), from (Z_k, Z_{n/2-k}, w_n^k,
+  // Y_k, Y_{k+n/2}); the SECONDARY element repeats the primary's arithmetic bit for bit and takes
+  // conjugates: lambda_{n/2-k} = conj lambda_{k+n/2}, G likewise, w_n^{n/2-k} = -conj w_n^k.  So
+  // dL/dlambda is exactly Hermitian and the half-length adjoint of V = E + i O has no leak of a
+  // rounding-level anti-Hermitian part (amplified by 1/ev^2 near the nugget) into the gradient.
+  // Streamed per element (arrays of the split spectrum would not fit registers).
+#pragma unroll
+  for (int j = 0; j < 16 / RLAST; ++j)
+#pragma unroll
+    for (int t = 0; t < RLAST; ++t) {
+      const int e = j * RLAST + t;
+      const int r = pass_pos<P1, SL, RLL>(tt, j, t);
+      const int pr = self0 ? ((N1 - r) & (N1 - 1)) : (N1 - 1 - r);
+      const bool primary = (self0 || self1) ? (r <= pr) : ((sl & 1) == 0);
+      const double2 zo = col[r], zq = pc[pr];         // own Z, partner Z
+      const double2 zk = primary ? zo : zq, zm = primary ? zq : zo;
+      const int64_t ck = primary ? colx : colp;
+      const int rk = primary ? r : pr;
+      const double2 S = make_double2(zk.x + zm.x, zk.y - zm.y);      // Z_k + conj Z_{nt-k}
+      const double2 Dd = make_double2(zk.x - zm.x, zk.y + zm.y);     // Z_k - conj Z_{nt-k}
+      const double2 W = cmul(primary ? wcol : wcolp, tw[rk << (24 - m)]);   // w_n^k, k = ck + 4096 rk
+      const double2 wd = cmul(W, Dd);
+      const double2 A0 = make_double2(0.5 * (S.x + wd.y), 0.5 * (S.y - wd.x));   // (S - i W D) / 2
+      const double2 A1 = make_double2(0.5 * (S.x - wd.y), 0.5 * (S.y + wd.x));   // (S + i W D) / 2
+      if constexpr (EMIT) {   // lambda = ft(k1) at the own k and k + n/2 (fgp_nll_lam)
+        const double2 l0 = primary ? A0 : make_double2(A1.x, -A1.y);
+        const double2 l1 = primary ? A1 : make_double2(A0.x, -A0.y);
+        gl[(int64_t)r * N2] = l0 * inv_rootn;
+        gl[(int64_t)r * N2 + nt] = l1 * inv_rootn;
+      } else {
+        const double* yk = a.ysq + (int64_t)g * a.ysq_stride + ck + (int64_t)rk * N2;
+        const double2 g0 = eig_terms(A0 * inv_rootn, rootn, h.noise, yk[0], a.logdet_weight, norm, la, dnoise);
+        const double2 g1 = eig_terms(A1 * inv_rootn, rootn, h.noise, yk[nt], a.logdet_weight, norm, la, dnoise);
+        // own G at k' and k' + n/2: the primary's, or the conjugates of the primary's (swapped)
+        const double2 G0 = primary ? g0 : make_double2(g1.x, -g1.y);
+        const double2 G1 = primary ? g1 : make_double2(g0.x, -g0.y);
+        const double2 Wo = primary ? W : make_double2(-W.x, W.y);      // w_n^{k'} = -conj w_n^k
+        const double2 Ek = G0 + G1;
+        const double2 Ok = cmulc(G0 - G1, Wo);                       // (G_k' - G_{k'+n/2}) conj(w_n^k')
+        v[e] = make_double2(Ek.x - Ok.y, Ek.y + Ok.x);               // V = E + i O
+        sum += v[e];
+      }
+      // compiler fence every 4 elements: bounds how many partner / Y / twiddle loads are hoisted
+      if ((e & 3) == 3) {
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  if constexpr (EMIT) return;
+  double logdet = la.log_sum(0.5);
+  column_partials<C>(sum, part);
+  mean = column_total<C>(sl, part) * (1.0 / N1);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v[k] -= mean;
+  adj_reg_passes<P1, SL, false>(v, col, tt, tw);
+  if (tt == 0) v[0] += mean * (double)N1;
+#pragma unroll
+  for (int j = 0; j < 16 / R0; ++j)
+#pragma unroll
+    for (int t = 0; t < R0; ++t) wk[pass_pos<P1, 0, RL0>(tt, j, t) * C] = v[j * R0 + t];
+  norm = block_sum(norm, redd);
+  logdet = block_sum(logdet, redd);
+  dnoise = block_sum(dnoise, redd);
+  if (tid == 0) {
+    *part_ptr(a, g, 0, blk) = norm;
+    *part_ptr(a, g, 1, blk) = logdet;
+    *part_ptr(a, g, 2, blk) = dnoise;
+  }
+}
+
+// adjoint half-length row pass: Re -> gradient terms of x[:n/2], Im -> of x[n/2:]
+template <int PG, int D>
+__global__ __launch_bounds__(kWG) void k_bwd_rows_r2c(Nll a, const double2* __restrict__ tw, const double2* __restrict__ twm) {
+  constexpr int P2 = 12, N2 = 1 << P2;
+  __shared__ double ldsd[kTile + kTile / 16];
+  __shared__ double2 red[kWG / 64];
+  __shared__ double redd[kWG / 64];
+  const int mt = a.log2n - 1, m1 = mt - P2;
+  const int64_t n = (int64_t)1 << a.log2n, nt = n >> 1;
+  const int64_t tiles = nt >> kTileLog;
+  const int g = (int)(blockIdx.x / tiles);
+  const int blk = (int)(blockIdx.x % tiles);
+  const int row0 = blk;
+  const int64_t base = (int64_t)blk * kTile;
+  const int tid = threadIdx.x;
+  const double2* in = static_cast<const double2*>(a.work) + (int64_t)g * n;
+  double2 v[16];
+  double2 sum = zero_v<double2>();
+  const RowTwiddle rt((unsigned)row0, tid, P2, m1, tw, twm);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    v[k] = tw_mul<double2>(in[work_pos_pair(row0, tid + k * kWG, m1, N2)], rt.at(k, P2, m1, tw, twm), true);
+    sum += v[k];
+  }
+  const double2 mean = block_sum_t(sum, red) * (1.0 / N2);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v[k] -= mean;
+  adj_reg_passes<P2, LastPass<P2>::S, true>(v, ldsd, tid, tw);
+  if (tid == 0) v[0] += mean * (double)N2;
+  Hyp h;
+  load_hyp_wave(a, g, h);
+  PSrc src;
+  psrc_init(a, g, src);
+  constexpr int ND = Dims<D>::N;
+  double acc[1 + ND];
+#pragma unroll
+  for (int q = 0; q < 1 + ND; ++q) acc[q] = 0.0;
+  double* gl = ldsd + 17 * tid;
+  const double gs = 1.0 / sqrt((double)n);
+  __syncthreads();
+#pragma unroll
+  for (int t = 0; t < 16; ++t) gl[t] = v[t].x;
+  grad_run16<PG, D>(a, h, src, n, base + 16 * tid, gl, gs, acc);
+#pragma unroll
+  for (int t = 0; t < 16; ++t) gl[t] = v[t].y;
+  grad_run16<PG, D>(a, h, src, n, nt + base + 16 * tid, gl, gs, acc);
+#pragma unroll
+  for (int q = 0; q < 1 + ND; ++q) {
+    if (q <= a.d) {
+      const double r = block_sum(acc[q], redd) * grad_factor(h, q);
+      if (tid == 0) *part_ptr(a, g, 3 + q, blk) = r;
+    }
+  }
+}
+
 // ---------------------------------------------------------------- fit step (one workgroup)
 struct Fit {
   int n_params;
@@ -1021,7 +1279,10 @@ static int to_nll(const fgp_nll_desc* d, Nll& a) {
   a.log2n = d->log2n;
   a.d = d->d;
   a.G = d->G;
-  a.nb = d->log2n > 12 ? 1 << (d->log2n - 12) : 1;
+  // half-length (R2C) fit kernels for lattices with n >= 2^17 (FGP_R2C=0 selects the full-length ones)
+  const char* r2c_env = getenv("FGP_R2C");
+  a.r2c = d->family == FGP_FAMILY_LATTICE && d->log2n >= 17 && !(r2c_env && r2c_env[0] == '0');
+  a.nb = d->log2n > 12 ? 1 << (d->log2n - 12 - (a.r2c ? 1 : 0)) : 1;
   a.nq = 4 + d->d;
   a.parts = d->parts;
   a.parts_stride = d->parts_stride;
@@ -1163,11 +1424,45 @@ static int launch_rows_bwd(const Nll& a, const Tables* tb, hipStream_t st) {
   });
 }
 
+// half-length (R2C) lattice kernels: transforms of length n/2 (rows of 4096, N1 = 2^(m - 13) rows)
+static int launch_r2c(const Nll& a, int stage, const Tables* tb, hipStream_t st, bool emit) {
+  const int m = a.log2n, mt = m - 1, p1 = mt - 12;
+  const unsigned grid = (unsigned)((int64_t)a.G << (mt - kTileLog));
+  if (stage == 0 || stage == 2) {
+    return with_pg<double2>(a, [&](auto pgc) {
+      constexpr int PG = decltype(pgc)::value;
+      with_d(a.d, [&](auto dc) {
+        constexpr int DD = decltype(dc)::value;
+        if (stage == 0) k_fwd_rows_r2c<PG, DD><<<grid, kWG, 0, st>>>(a, tb->tw4096, tb->twm[mt]);
+        else k_bwd_rows_r2c<PG, DD><<<grid, kWG, 0, st>>>(a, tb->tw4096, tb->twm[mt]);
+      });
+      return check_launch(stage == 0 ? "k_fwd_rows_r2c" : "k_bwd_rows_r2c");
+    });
+  }
+  switch (p1) {
+#define FGP_C(PP)                                                                              \
+  case PP:                                                                                     \
+    if (emit) k_fwd_cols_r2c<PP, true><<<grid, kWG, 0, st>>>(a, tb->tw4096, tb->twm[m]);       \
+    else k_fwd_cols_r2c<PP, false><<<grid, kWG, 0, st>>>(a, tb->tw4096, tb->twm[m]);           \
+    break;
+    FGP_C(4) FGP_C(5) FGP_C(6) FGP_C(7) FGP_C(8) FGP_C(9) FGP_C(10) FGP_C(11)
+#undef FGP_C
+    default: return set_error(kErrInvalid, "bad r2c m1");
+  }
+  return check_launch("k_fwd_cols_r2c");
+}
+
 // one kernel of the pipeline: 0 = forward rows (n <= 4096: the single-kernel iteration), 1 = eigen
 // terms + adjoint columns, 2 = adjoint rows + gradient terms
 template <typename T>
 static int nll_stage_t(const Nll& a, int stage, const Tables* tb, hipStream_t st) {
   if (a.log2n <= 12) return stage == 0 ? launch_iter_single<T>(a, tb, st) : kOk;
+  if constexpr (sizeof(T) == 16) {
+    if (a.r2c) {
+      if (stage < 0 || stage > 2) return set_error(kErrInvalid, "bad stage %d", stage);
+      return launch_r2c(a, stage, tb, st, false);
+    }
+  }
   switch (stage) {
     case 0: return launch_rows_fwd<T>(a, tb, st);
     case 1: return launch_cols_fwd<T>(a, tb, st, false);
@@ -1328,6 +1623,10 @@ int fgp_nll_lam(const fgp_nll_desc* desc, void* stream) {
   if (!tb) return set_error(kErrHip, "twiddle table initialisation failed");
   const bool lat = desc->family == FGP_FAMILY_LATTICE;
   if (a.log2n <= 12) return lat ? launch_iter_single<double2>(a, tb, st, true) : launch_iter_single<double>(a, tb, st, true);
+  if (lat && a.r2c) {
+    rc = launch_r2c(a, 0, tb, st, true);
+    return rc != kOk ? rc : launch_r2c(a, 1, tb, st, true);
+  }
   if (lat) {
     rc = launch_rows_fwd<double2>(a, tb, st);
     return rc != kOk ? rc : launch_cols_fwd<double2>(a, tb, st, true);

@@ -7,7 +7,7 @@ torch.set_default_dtype(torch.float64)
 import fastgaussianprocesses_amd as F
 from oracle import fgp_oracle as O
 
-for family, m, d in [("lattice", 13, 2), ("lattice", 13, 3), ("lattice", 16, 2), ("lattice", 16, 3), ("net", 13, 2), ("net", 13, 3)]:
+for family, m, d in [("lattice", 13, 3), ("lattice", 17, 2), ("lattice", 17, 3), ("lattice", 18, 5), ("net", 13, 3)]:
     n = 2 ** m
     gp = F.FastGPLattice(F.Lattice(d, seed=7), device="cuda") if family == "lattice" else \
         F.FastGPDigitalNetB2(F.DigitalNetB2(d, seed=7), alpha=1, device="cuda")
