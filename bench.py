@@ -9,7 +9,8 @@ Inputs (points, y = f_ackley(x)) are resident in HBM before the timed region; GP
 initial hyper-parameters and all caches are dropped at the start of every step.
 value = (shifts * n * world_size) / (max-over-ranks seconds per step).
 
-Extra JSON keys: "roofline" for the dominant kernel (HIP-event timing of that kernel on its stream),
+Extra JSON keys: "roofline" for the dominant kernel (its launches timed live on the device clock,
+fgp_nll_desc.stamps, with the HIP-event figure beside it),
 "cpu_baseline" (the oracle = torch-CPU restatement of the reference, rank 0 at N=1, bounded sample),
 "phases_ms" (per-phase breakdown of one batched step, HIP events).
 """
@@ -95,11 +96,16 @@ class Shifts(object):
         self.batch.set_raw(self.raw0.clone())
 
 
-def step_batched(sh, args, xm, xv):
+def step_batched(sh, args, xm, xv, store_loss_hist=False):
+    """One timed step; returns (per-GP fit data, post_mean [P, N], post_var [P, N]) so the parity
+    test (tests/test_gpu_bench_path.py) checks exactly this sequence.  store_loss_hist only copies the
+    device loss history back after the fit (the device work is the same)."""
     sh.reset()
-    sh.batch.fit(iterations=args.fit_iters, stop_crit_wait_iterations=args.fit_iters + 1)
-    sh.batch.post_mean(xm)
-    sh.batch.post_var(xv)
+    data = sh.batch.fit(iterations=args.fit_iters, stop_crit_wait_iterations=args.fit_iters + 1,
+                        store_loss_hist=store_loss_hist)
+    pm = sh.batch.post_mean(xm)
+    pv = sh.batch.post_var(xv)
+    return data, pm, pv
 
 
 def step_sequential(sh, args, xm, xv):
@@ -142,43 +148,69 @@ def r2c_active(n):
 
 
 def stage_bytes(n, d, P, parts_array):
-    """Algorithmic HBM bytes of one launch of each fit-iteration kernel over P lattice problems
-    (complex128 intermediate `work` of L = n complex values, L = n/2 for the half-length R2C kernels;
-    float64 Y; DESIGN.md 'Kernels'):
+    """Algorithmic (compulsory) HBM bytes of one launch of each fit-iteration kernel over P lattice
+    problems (complex128 intermediate `work` of L = n complex values, L = n/2 for the half-length R2C
+    kernels; float64 Y; DESIGN.md 'Kernels'):
       k_fwd_rows: write work 16L (+ read parts 8nd when not regenerated)
-      k_fwd_cols: read work 16L + read Y 8n + write work 16L
+      k_fwd_cols: read work 16L + write work 16L + read Y: 8n full-length; 4n R2C (Y = |y~|^2 is even,
+                  Y_k = Y_{n-k}, and the kernel reads it only at each mirror pair's primary element:
+                  the n/2 values Y_k, Y_{k+n/2} of the primaries k)
       k_bwd_rows: read work 16L (+ read parts 8nd)"""
     pb = 8 * n * d if parts_array else 0
-    L = n // 2 if r2c_active(n) else n
-    return {"k_fwd_rows": (16 * L + pb) * P, "k_fwd_cols": (32 * L + 8 * n) * P, "k_bwd_rows": (16 * L + pb) * P}
+    r2c = r2c_active(n)
+    L = n // 2 if r2c else n
+    yb = 4 * n if r2c else 8 * n
+    return {"k_fwd_rows": (16 * L + pb) * P, "k_fwd_cols": (32 * L + yb) * P, "k_bwd_rows": (16 * L + pb) * P}
+
+
+def wall_clock_khz(F, device):
+    import ctypes
+    khz = ctypes.c_int(0)
+    F._native.call("fgp_wall_clock_khz", int(device.index or 0), ctypes.byref(khz))
+    return khz.value
 
 
 def roofline_fit_kernels(F, shifts, iters):
-    """HIP-event timing (torch's current stream = the stream the kernels are launched on) of every
-    kernel of the batched fit iteration, as launched in the step (same engine, same grid)."""
+    """Per-kernel timing of the batched fit iteration as launched in the step (same engine, same grid),
+    two ways:
+      * device clock (fgp_nll_desc.stamps): first-workgroup start to last-wave end of every launch --
+        the kernel duration rocprofv3 --kernel-trace reports; this is `avg_us` and prices `achieved`;
+      * HIP events recorded on torch's current stream (the stream the kernels are launched on) around
+        each launch behind a spin kernel that holds the stream while the host enqueues: kernel + the
+        dependent-launch gap (`avg_us_events`)."""
     shifts.reset()
     gps = shifts.gps
     n = shifts.n
+    dev = torch.device(gps[0].device)
     eng = F.batch.batched_engine(gps, iters)
     eng.run(0, 2)
     torch.cuda.synchronize()
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(iters)]
-    # hold the stream with a spin kernel while the host enqueues every launch and event, so the
-    # events time back-to-back kernels (no host launch gaps) -- the durations rocprofv3 reports
+    grid = eng.G * max(1, (n // 2 if r2c_active(n) else n) // 4096)      # workgroups per fit launch
+    stamps = torch.zeros((iters, 3, grid, 5), dtype=torch.int64, device=dev)   # fgp_nll_desc.stamps
     torch.cuda._sleep(int(2.4e9 * 4e-4 * iters))
     for it in range(iters):
         e = ev[it]
         e[0].record()
         for k in range(3):
+            eng._nll.stamps = stamps[it, k].data_ptr()
             eng.stage(k)
             e[k + 1].record()
+        eng._nll.stamps = None
         eng.fit_step(it)
         e[4].record()
     torch.cuda.synchronize()
-    us = {name: 1e3 * sum(e[k].elapsed_time(e[k + 1]) for e in ev) / iters for k, name in enumerate(STAGES)}
-    us["k_fit_reduce_step"] = 1e3 * sum(e[3].elapsed_time(e[4]) for e in ev) / iters
-    t_iter = sum(us.values()) / 1e6
-    return n, eng.gen is None, us, t_iter
+    eng._nll.stamps = None
+    khz = wall_clock_khz(F, dev)
+    st = stamps.cpu()
+    assert bool((st > 0).all()), "a fit launch did not write its device-clock stamps"
+    dur_us = (st[..., 1:].amax((2, 3)) - st[..., 0].amin(2)).double() * (1e3 / khz)     # [iters, 3]
+    us_ev = {name: 1e3 * sum(e[k].elapsed_time(e[k + 1]) for e in ev) / iters for k, name in enumerate(STAGES)}
+    us_ev["k_fit_reduce_step"] = 1e3 * sum(e[3].elapsed_time(e[4]) for e in ev) / iters
+    us = {name: float(dur_us[:, k].mean()) for k, name in enumerate(STAGES)}
+    us["k_fit_reduce_step"] = us_ev["k_fit_reduce_step"]
+    t_iter = sum(us_ev.values()) / 1e6
+    return n, eng.gen is None, us, us_ev, t_iter, khz
 
 
 PMC_SUMMARY = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_pmc_fit_kernels.json")
@@ -279,7 +311,7 @@ def main():
     value = args.shifts * n * world / sec_step
 
     phases = phase_breakdown(shifts, args.fit_iters, xm, xv)
-    n_, parts_array, us, t_iter = roofline_fit_kernels(F, shifts, args.fit_iters)
+    n_, parts_array, us, us_ev, t_iter, khz = roofline_fit_kernels(F, shifts, args.fit_iters)
     P = len(shifts.gps)
     sb = stage_bytes(n, d, P, parts_array)
     dom = max(STAGES, key=lambda k: us[k])
@@ -287,18 +319,18 @@ def main():
     kname = dom + ("_r2c" if r2c else "")
     grid_wg = P * (n // 2 if r2c else n) // 4096
     ach = sb[dom] / (us[dom] * 1e-6) / 1e9
-    # SURVEY §8(d) reference-dataflow bytes of one fit iteration: 16nd + 32n + 32nB per GP (B = 1)
-    b_iter = (16 * n * d + 32 * n + 32 * n) * P
     roof = {"bound": "hbm", "kernel": kname, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic(kname, grid_wg * 256),
-            "traffic_source": os.path.relpath(PMC_SUMMARY, os.path.dirname(os.path.abspath(__file__))), "algorithmic_bytes": sb[dom], "avg_us": us[dom],
+            "traffic_source": os.path.relpath(PMC_SUMMARY, os.path.dirname(os.path.abspath(__file__))),
+            "algorithmic_bytes": sb[dom], "avg_us": us[dom], "avg_us_source": "device clock (%d kHz), first "
+            "workgroup start to last wave end, mean of %d launches" % (khz, args.fit_iters),
+            "avg_us_events": us_ev[dom],
             "launch": "%d problems x n=2^%d (grid %d workgroups)" % (P, args.log2n, grid_wg),
             "transform": "half-length R2C (n/2 complex)" if r2c else "full-length (n complex)",
-            "kernels": {k: {"avg_us": us[k], "bytes": sb.get(k),
+            "kernels": {k: {"avg_us": us[k], "avg_us_events": us_ev[k], "bytes": sb.get(k),
                             "GB/s": (sb[k] / (us[k] * 1e-6) / 1e9) if k in sb else None} for k in us},
             "parts": "array" if parts_array else "regenerated (FGP_PARTS_LATTICE)",
-            "iteration": {"avg_us": t_iter * 1e6, "survey_bytes": b_iter,
-                          "survey_equiv_GB/s": b_iter / t_iter / 1e9}}
+            "iteration_us": t_iter * 1e6}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, n, d)

@@ -12,7 +12,7 @@ import torch
 
 _LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
 LIB_PATH = os.path.join(_LIB_DIR, "libfgp_hip.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 MAX_D = 8
 PARTS_ARRAY = 0
 PARTS_LATTICE = 1
@@ -44,6 +44,7 @@ class NllDesc(ctypes.Structure):
         ("grad_lam", _c_vp), ("work", _c_vp), ("partials", _c_vp),
         ("parts_gen", _c_int), ("gen_order", _c_int * 8), ("gen_coef", _c_dbl * 8), ("gen_z", _c_i64 * 8),
         ("gen_shift", _c_vp), ("gen_shift_stride", _c_i64),
+        ("stamps", _c_vp),
     ]
 
 
@@ -78,6 +79,7 @@ _P_PRED = ctypes.POINTER(PredDesc)
 # name -> argtypes (all return int status); must match include/fgp_hip.h
 _SIGNATURES = {
     "fgp_init": [_c_vp],
+    "fgp_wall_clock_khz": [_c_int, _c_pi],
     "fgp_fftbr": [_c_vp, _c_i64, _c_int, _c_vp, _c_i64, _c_int, _c_int, _c_vp],
     "fgp_ifftbr": [_c_vp, _c_i64, _c_vp, _c_int, _c_vp, _c_i64, _c_int, _c_int, _c_vp],
     "fgp_fwht": [_c_vp, _c_i64, _c_vp, _c_i64, _c_int, _c_int, _c_vp],

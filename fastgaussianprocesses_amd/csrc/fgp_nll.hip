@@ -122,7 +122,21 @@ struct Nll {
   const double* gshift;
   int64_t gshift_stride;
   int r2c;                       // lattice, n >= 2^17: half-length (R2C) fit kernels
+  unsigned long long* stamps;    // optional device-clock timing of the launch (fgp_nll_desc.stamps)
 };
+
+// Device-clock kernel timing (fgp_nll_desc.stamps; off when NULL -- a uniform branch on a kernel
+// argument): plain vector stores of the wall clock into the launch's record [gridDim.x][1 + kWG/64]:
+// [b][0] = start of workgroup b (its first wave), [b][1 + w] = end of its wave w.  No atomics (one
+// contended address serialises thousands of them and slows the kernel being timed).
+constexpr int kStampStride = 1 + kWG / 64;
+__device__ __forceinline__ void stamp_begin(const Nll& a) {
+  if (a.stamps && threadIdx.x == 0) a.stamps[(int64_t)blockIdx.x * kStampStride] = (unsigned long long)wall_clock64();
+}
+__device__ __forceinline__ void stamp_end(const Nll& a) {
+  if (a.stamps && (threadIdx.x & 63) == 0)
+    a.stamps[(int64_t)blockIdx.x * kStampStride + 1 + (threadIdx.x >> 6)] = (unsigned long long)wall_clock64();
+}
 
 struct Hyp {
   double scale, noise;
@@ -539,6 +553,7 @@ __global__ __launch_bounds__(kWG) void k_fwd_rows(Nll a, const double2* __restri
   const int g = (int)(blockIdx.x / tiles);
   const int row0 = (int)(blockIdx.x % tiles) * RPW;
   const int tid = threadIdx.x;
+  stamp_begin(a);
   Hyp h;
   load_hyp_wave(a, g, h);
   PSrc src;
@@ -565,6 +580,7 @@ __global__ __launch_bounds__(kWG) void k_fwd_rows(Nll a, const double2* __restri
 #pragma unroll
       for (int k = 0; k < 16; ++k) out[work_pos(row0, tid + k * kWG, m1)] = v[k];
     }
+    stamp_end(a);
     return;
   } else {
 #pragma unroll
@@ -590,6 +606,7 @@ __global__ __launch_bounds__(kWG) void k_fwd_rows(Nll a, const double2* __restri
       out[work_pos(row0 + (e >> P2), e & (N2 - 1), m1)] = v;
     }
   }
+  stamp_end(a);
 }
 
 // ---------------------------------------------------------------- n > 4096: forward column pass + eigen terms
@@ -617,6 +634,7 @@ __global__ __launch_bounds__(kWG) void k_fwd_cols(Nll a, const double2* __restri
   const int64_t c0 = (int64_t)blk * C;
   const int tid = threadIdx.x;
   const int c = tid % C, tt = tid / C;
+  stamp_begin(a);
   T* wk = static_cast<T*>(a.work) + (int64_t)g * n + (int64_t)blk * kTile + c;   // contiguous tile (work_pos)
   T* col = lds + c * CS;
   T v[16];
@@ -649,6 +667,7 @@ __global__ __launch_bounds__(kWG) void k_fwd_cols(Nll a, const double2* __restri
 #pragma unroll
       for (int t = 0; t < RLAST; ++t)
         gl[(int64_t)pass_pos<P1, SL, RLL>(tt, j, t) * N2] = v[j * RLAST + t] * inv_rootn;
+    stamp_end(a);
     return;
   }
   Hyp h;
@@ -680,6 +699,7 @@ __global__ __launch_bounds__(kWG) void k_fwd_cols(Nll a, const double2* __restri
     *part_ptr(a, g, 1, blk) = logdet;
     *part_ptr(a, g, 2, blk) = dnoise;
   }
+  stamp_end(a);
 }
 
 // ---------------------------------------------------------------- n > 4096: adjoint row pass + gradient terms
@@ -699,6 +719,7 @@ __global__ __launch_bounds__(kWG) void k_bwd_rows(Nll a, const double2* __restri
   const int row0 = blk * RPW;
   const int64_t base = (int64_t)blk * kTile;
   const int tid = threadIdx.x;
+  stamp_begin(a);
   const T* in = static_cast<const T*>(a.work) + (int64_t)g * n;   // column-tile layout (work_pos)
   if constexpr (RPW == 1) {
     T v[16];
@@ -744,6 +765,7 @@ __global__ __launch_bounds__(kWG) void k_bwd_rows(Nll a, const double2* __restri
         if (tid == 0) *part_ptr(a, g, 3 + q, blk) = r;
       }
     }
+    stamp_end(a);
     return;
   } else {
 #pragma unroll
@@ -784,6 +806,7 @@ __global__ __launch_bounds__(kWG) void k_bwd_rows(Nll a, const double2* __restri
       if (tid == 0) *part_ptr(a, g, 3 + q, blk) = v;
     }
   }
+  stamp_end(a);
 }
 
 // ---------------------------------------------------------------- half-length (R2C) lattice fit, n >= 2^17
@@ -834,6 +857,7 @@ __global__ __launch_bounds__(kWG) void k_fwd_rows_r2c(Nll a, const double2* __re
   const int g = (int)(blockIdx.x / tiles);
   const int row0 = (int)(blockIdx.x % tiles);
   const int tid = threadIdx.x;
+  stamp_begin(a);
   Hyp h;
   load_hyp_wave(a, g, h);
   PSrc src;
@@ -856,6 +880,7 @@ __global__ __launch_bounds__(kWG) void k_fwd_rows_r2c(Nll a, const double2* __re
 #pragma unroll
   for (int k = 0; k < 16; ++k)
     out[work_pos_pair(row0, tid + k * kWG, m1, N2)] = tw_mul<double2>(v[k], rt.at(k, P2, m1, tw, twm), false);
+  stamp_end(a);
 }
 
 // column pass at half length + mirror exchange + split into the length-n spectrum + eigen terms +
@@ -876,6 +901,7 @@ __global__ __launch_bounds__(kWG) void k_fwd_cols_r2c(Nll a, const double2* __re
   const int blk = (int)(blockIdx.x % tiles);
   const int tid = threadIdx.x;
   const int sl = tid % C, tt = tid / C;
+  stamp_begin(a);
   double2* wk = static_cast<double2*>(a.work) + (int64_t)g * n + (int64_t)blk * kTile + sl;
   double2* col = lds + sl * CS;
   double2 v[16];
@@ -965,7 +991,10 @@ __global__ __launch_bounds__(kWG) void k_fwd_cols_r2c(Nll a, const double2* __re
         __builtin_amdgcn_sched_barrier(0);
       }
     }
-  if constexpr (EMIT) return;
+  if constexpr (EMIT) {
+    stamp_end(a);
+    return;
+  }
   double logdet = la.log_sum(0.5);
   column_partials<C>(sum, part);
   mean = column_total<C>(sl, part) * (1.0 / N1);
@@ -985,6 +1014,7 @@ __global__ __launch_bounds__(kWG) void k_fwd_cols_r2c(Nll a, const double2* __re
     *part_ptr(a, g, 1, blk) = logdet;
     *part_ptr(a, g, 2, blk) = dnoise;
   }
+  stamp_end(a);
 }
 
 // adjoint half-length row pass: Re -> gradient terms of x[:n/2], Im -> of x[n/2:]
@@ -1002,6 +1032,7 @@ __global__ __launch_bounds__(kWG) void k_bwd_rows_r2c(Nll a, const double2* __re
   const int row0 = blk;
   const int64_t base = (int64_t)blk * kTile;
   const int tid = threadIdx.x;
+  stamp_begin(a);
   const double2* in = static_cast<const double2*>(a.work) + (int64_t)g * n;
   double2 v[16];
   double2 sum = zero_v<double2>();
@@ -1040,6 +1071,7 @@ __global__ __launch_bounds__(kWG) void k_bwd_rows_r2c(Nll a, const double2* __re
       if (tid == 0) *part_ptr(a, g, 3 + q, blk) = r;
     }
   }
+  stamp_end(a);
 }
 
 // ---------------------------------------------------------------- fit step (one workgroup)
@@ -1311,6 +1343,7 @@ static int to_nll(const fgp_nll_desc* d, Nll& a) {
   }
   a.gshift = d->gen_shift;
   a.gshift_stride = d->gen_shift_stride;
+  a.stamps = reinterpret_cast<unsigned long long*>(d->stamps);
   return kOk;
 }
 

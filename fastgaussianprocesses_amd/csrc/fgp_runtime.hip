@@ -72,6 +72,13 @@ const char* fgp_last_error(void) { return fgp::g_err; }
 
 int fgp_abi_version(void) { return FGP_ABI_VERSION; }
 
+int fgp_wall_clock_khz(int device, int* khz) {
+  if (!khz) return fgp::set_error(fgp::kErrInvalid, "fgp_wall_clock_khz: null output");
+  if (hipDeviceGetAttribute(khz, hipDeviceAttributeWallClockRate, device) != hipSuccess)
+    return fgp::set_error(fgp::kErrHip, "fgp_wall_clock_khz: hipDeviceGetAttribute failed");
+  return fgp::kOk;
+}
+
 int fgp_init(void* stream) {
   return fgp::get_tables((hipStream_t)stream) ? fgp::kOk
                                               : fgp::set_error(fgp::kErrHip, "fgp_init: table allocation failed");

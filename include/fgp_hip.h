@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define FGP_ABI_VERSION 6
+#define FGP_ABI_VERSION 7
 
 #define FGP_OK 0
 #define FGP_ERR_INVALID (-1)     /* bad argument (shape, stride, null pointer) */
@@ -38,6 +38,8 @@ const char* fgp_last_error(void);
 /* Optional eager initialisation of the per-device twiddle tables on `stream` (otherwise done on
  * first use; call before hipGraph capture). */
 int fgp_init(void* stream);
+/* Frequency (kHz) of the device wall clock that fgp_nll_desc.stamps records (hipDeviceAttributeWallClockRate). */
+int fgp_wall_clock_khz(int device, int* khz);
 
 /* Orthonormal DFT of bit-reversed-order input along the last axis:
  *   out[b, k] = n^-1/2 * sum_i in[b, brev_m(i)] exp(-2 pi i k i / n),  n = 2^log2n, 0 <= log2n <= 24.
@@ -146,6 +148,12 @@ typedef struct fgp_nll_desc {
   int64_t gen_z[FGP_MAX_D];   /* generating vector */
   const double* gen_shift;    /* device [G][d] (row stride gen_shift_stride; 0 = shared): x[0] = shift */
   int64_t gen_shift_stride;
+  /* Optional device-clock kernel timing (ABI 7; NULL = off): a fit kernel launched with this desc
+   * stores the wall clock (fgp_wall_clock_khz ticks) into stamps[b * 5] when workgroup b starts and
+   * into stamps[b * 5 + 1 + w] when its wave w ends (b < grid size of the launch, 256-thread
+   * workgroups); max(ends) - min(starts) is the kernel's duration as rocprofv3 --kernel-trace sees it,
+   * measured in-process without the dependent-launch gap that HIP events include. */
+  uint64_t* stamps;
 } fgp_nll_desc;
 
 #define FGP_PARTS_ARRAY 0

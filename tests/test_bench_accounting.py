@@ -18,8 +18,9 @@ def test_stage_bytes_half_length(monkeypatch):
     n, d, P = 2 ** 20, 5, 8
     assert bench.r2c_active(n) and not bench.r2c_active(2 ** 16)
     sb = bench.stage_bytes(n, d, P, parts_array=False)
-    # work of n/2 complex values: 8n per pass; the column kernel also reads Y (8n)
-    assert sb == {"k_fwd_rows": 8 * n * P, "k_fwd_cols": 24 * n * P, "k_bwd_rows": 8 * n * P}
+    # work of n/2 complex values: 8n per pass; the column kernel also reads Y at the mirror pairs'
+    # primaries only (n/2 values of the even Y: 4n)
+    assert sb == {"k_fwd_rows": 8 * n * P, "k_fwd_cols": 20 * n * P, "k_bwd_rows": 8 * n * P}
     # below 2^17 the full-length kernels run
     assert bench.stage_bytes(2 ** 16, d, P, False)["k_fwd_cols"] == 40 * 2 ** 16 * P
 
