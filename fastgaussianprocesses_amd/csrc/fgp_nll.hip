@@ -883,18 +883,58 @@ __global__ __launch_bounds__(kWG) void k_fwd_rows_r2c(Nll a, const double2* __re
   stamp_end(a);
 }
 
-// column pass at half length + mirror exchange + split into the length-n spectrum + eigen terms +
-// the adjoint packing V = E + i O + adjoint column pass, in place (k_fwd_cols for the R2C layout)
+// Mirror-pair evaluation of the R2C column kernel.  The pair (k, nt - k) of the half-length spectrum Z
+// (primary Z_k = zk, partner Z_{nt-k} = zm, W = w_n^k) gives the length-n spectrum at k and k + n/2:
+//   A0, A1 = (S -/+ i W D) / 2,  S = Z_k + conj Z_{nt-k},  D = Z_k - conj Z_{nt-k}
+// (lambda = A / sqrt(n)); the partner's frequencies nt - k, n - k are their mirrors (lambda Hermitian).
+// Returns dL/dlambda at k and k + n/2 (g0, g1) and accumulates that pair's loss terms.
+struct EigAcc {
+  double norm = 0.0, dnoise = 0.0;
+  LogAcc la;
+};
+
+__device__ __forceinline__ void pair_eval(double2 zk, double2 zm, double2 W, double y0, double y1, double rootn,
+                                          double inv_rootn, double noise, double wlog, EigAcc& acc, double2& g0,
+                                          double2& g1, double2& A0, double2& A1) {
+  const double2 S = make_double2(zk.x + zm.x, zk.y - zm.y);      // Z_k + conj Z_{nt-k}
+  const double2 Dd = make_double2(zk.x - zm.x, zk.y + zm.y);     // Z_k - conj Z_{nt-k}
+  const double2 wd = cmul(W, Dd);
+  A0 = make_double2(0.5 * (S.x + wd.y), 0.5 * (S.y - wd.x));     // (S - i W D) / 2
+  A1 = make_double2(0.5 * (S.x - wd.y), 0.5 * (S.y + wd.x));     // (S + i W D) / 2
+  g0 = eig_terms(A0 * inv_rootn, rootn, noise, y0, wlog, acc.norm, acc.la, acc.dnoise);
+  g1 = eig_terms(A1 * inv_rootn, rootn, noise, y1, wlog, acc.norm, acc.la, acc.dnoise);
+}
+
+// Column pass at half length + mirror exchange + split into the length-n spectrum + eigen terms + the
+// adjoint packing V = E + i O + adjoint column pass, in place (k_fwd_cols for the R2C layout).
+//
+// Exact Hermitian symmetry, each mirror pair evaluated ONCE: after the forward passes the tile's
+// spectrum goes to the LDS image; thread (q, rr) then takes the pairs of pair-column q (slots 2q,
+// 2q + 1 = columns c and N2 - c) at rows rr, rr + RSTEP, ...: from (Z_k, Z_{nt-k}, w_n^k, Y_k,
+// Y_{k+n/2}) it evaluates the eigen terms of k and k + n/2 once and writes both elements' V back into
+// the image: the primary's V = E + i O, E = G_k + G_{k+n/2}, O = (G_k - G_{k+n/2}) conj(w_n^k), and the
+// partner's, whose G are the conjugates of the primary's (swapped) and whose twiddle is -conj(w_n^k):
+// V' = (E.x + O.y, O.x - E.y), bit for bit the conjugate arithmetic.  So dL/dlambda is exactly
+// Hermitian and the half-length adjoint of V has no leak of a rounding-level anti-Hermitian part
+// (amplified by 1/ev^2 near the nugget) into the gradient.  A regular pair's loss terms count twice
+// (its mirror frequencies); the self-mirrored frequencies 0, n/2 (column 0, row 0) and n/4, 3n/4
+// (column 0, row N1/2) once.  Tile 0's pair-column 0 holds the self-mirrored columns 0 (rows r <->
+// N1 - r) and N2/2 (rows r <-> N1 - 1 - r): its job rr < N1/2 is a column-0 pair (rr = 0: the two
+// self pairs), rr >= N1/2 a column-N2/2 pair.
+// Lanes run over q (consecutive columns: coalesced Y reads; the image reads of consecutive lanes fall
+// on distinct bank quads).  Y for the thread's jobs is loaded before the forward passes.
 template <int P1, bool EMIT>
-__global__ __launch_bounds__(kWG) void k_fwd_cols_r2c(Nll a, const double2* __restrict__ tw,
-                                                       const double2* __restrict__ twmf) {
-  constexpr int N1 = 1 << P1, C = kTile / N1, CS = N1 + 1;
+__global__ __launch_bounds__(kWG, 2) void k_fwd_cols_r2c(Nll a, const double2* __restrict__ tw,
+                                                          const double2* __restrict__ twmf) {
+  constexpr int N1 = 1 << P1, C = kTile / N1, CS = N1 + 1, HC = C / 2;
   constexpr int RL0 = PassRL<P1, 0>::value, R0 = 1 << RL0;
   constexpr int SL = LastPass<P1>::S, RLL = PassRL<P1, SL>::value, RLAST = 1 << RLL;
+  constexpr int JOBS = kTile / 2 / kWG, RSTEP = kWG / HC;     // JOBS * RSTEP = N1
+  static_assert(JOBS * RSTEP == N1, "pair jobs cover the tile");
   __shared__ double2 lds[C * CS];
   __shared__ double2 part[ColPart<C>::size];
   __shared__ double redd[kWG / 64];
-  const int m = a.log2n, mt = m - 1;
+  const int m = a.log2n;
   const int64_t n = (int64_t)1 << m, nt = n >> 1, N2 = nt >> P1;
   const int64_t tiles = nt >> kTileLog;
   const int g = (int)(blockIdx.x / tiles);
@@ -904,6 +944,34 @@ __global__ __launch_bounds__(kWG) void k_fwd_cols_r2c(Nll a, const double2* __re
   stamp_begin(a);
   double2* wk = static_cast<double2*>(a.work) + (int64_t)g * n + (int64_t)blk * kTile + sl;
   double2* col = lds + sl * CS;
+  // pair jobs of this thread: pair-column q, rows rr0 + RSTEP j
+  const int q = tid % HC, rr0 = tid / HC;
+  const bool col0 = blk == 0 && q == 0;                      // tile 0's self-mirrored columns
+  const int64_t cp_gen = (int64_t)blk * HC + q;              // primary column (q >= 1 or blk >= 1)
+  const double* yg = a.ysq + (int64_t)g * a.ysq_stride;
+  // primary (slot, row, column) of job j
+  auto job_primary = [&](int j, int& sp, int& rp, int64_t& cp) {
+    const int rr = rr0 + RSTEP * j;
+    if (!col0) {
+      sp = 2 * q; rp = rr; cp = cp_gen;
+    } else if (rr < N1 / 2) {
+      sp = 0; rp = rr; cp = 0;
+    } else {
+      sp = 1; rp = rr - N1 / 2; cp = N2 >> 1;
+    }
+  };
+  double y0[JOBS], y1[JOBS];
+  if constexpr (!EMIT) {
+#pragma unroll
+    for (int j = 0; j < JOBS; ++j) {
+      int sp, rp;
+      int64_t cp;
+      job_primary(j, sp, rp, cp);
+      const double* yk = yg + cp + (int64_t)rp * N2;
+      y0[j] = yk[0];
+      y1[j] = yk[nt];
+    }
+  }
   double2 v[16];
 #pragma unroll
   for (int j = 0; j < 16 / R0; ++j)
@@ -918,84 +986,98 @@ __global__ __launch_bounds__(kWG) void k_fwd_cols_r2c(Nll a, const double2* __re
   for (int k = 0; k < 16; ++k) v[k] -= mean;
   fwd_reg_passes<P1, 0, false>(v, col, tt, tw);
   if (tt == 0) v[0] += mean * (double)N1;
-  // (everything below is computed after the forward passes: the passes themselves sit at ~246
-  // VGPRs, so values kept live across them would spill)
-  const int64_t colx = pair_col(blk, sl, C, N2);
-  // (Y is read at use: prefetching its 32 values with the 16 partners needs too many registers)
-  // mirror exchange: Z at frequency nt - k lives in the partner slot, row reversed
+  // the tile's half-length spectrum into the image
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < 16 / RLAST; ++j)
 #pragma unroll
     for (int t = 0; t < RLAST; ++t) col[pass_pos<P1, SL, RLL>(tt, j, t)] = v[j * RLAST + t];
   __syncthreads();
-  const bool self0 = blk == 0 && sl == 0, self1 = blk == 0 && sl == 1;
-  const double2* pc = lds + (self0 || self1 ? sl : (sl ^ 1)) * CS;
-  const int64_t colp = (self0 || self1) ? colx : pair_col(blk, sl ^ 1, C, N2);
   const double rootn = sqrt((double)n), inv_rootn = 1.0 / rootn;
-  double2* gl = EMIT ? static_cast<double2*>(a.grad_lam) + (int64_t)g * n + colx : nullptr;
   Hyp h;
   if constexpr (!EMIT) load_hyp_wave(a, g, h);
-  double norm = 0.0, dnoise = 0.0;
-  LogAcc la;
-  sum = zero_v<double2>();
-  // N2 = 4096 (transform length >= 2^16): k = col + 4096 r, so w_n^k = twm_m[col] * w_n^(4096 r), the
-  // second factor a 4096-table entry (n = 2^m <= 2^24)
-  const double2 wcol = twmf[colx], wcolp = twmf[colp];
-  // Exact Hermitian symmetry: each mirror pair (k, n/2 - k) is evaluated once, by its PRIMARY element
-  // (even slot; in the self-mirrored columns 0 and N2/2 the smaller row), from (Z_k, Z_{n/2-k}, w_n^k,
-  // Y_k, Y_{k+n/2}); the SECONDARY element repeats the primary's arithmetic bit for bit and takes
-  // conjugates: lambda_{n/2-k} = conj lambda_{k+n/2}, G likewise, w_n^{n/2-k} = -conj w_n^k.  So
-  // dL/dlambda is exactly Hermitian and the half-length adjoint of V = E + i O has no leak of a
-  // rounding-level anti-Hermitian part (amplified by 1/ev^2 near the nugget) into the gradient.
-  // Streamed per element (arrays of the split spectrum would not fit registers).
-#pragma unroll
-  for (int j = 0; j < 16 / RLAST; ++j)
-#pragma unroll
-    for (int t = 0; t < RLAST; ++t) {
-      const int e = j * RLAST + t;
-      const int r = pass_pos<P1, SL, RLL>(tt, j, t);
-      const int pr = self0 ? ((N1 - r) & (N1 - 1)) : (N1 - 1 - r);
-      const bool primary = (self0 || self1) ? (r <= pr) : ((sl & 1) == 0);
-      const double2 zo = col[r], zq = pc[pr];         // own Z, partner Z
-      const double2 zk = primary ? zo : zq, zm = primary ? zq : zo;
-      const int64_t ck = primary ? colx : colp;
-      const int rk = primary ? r : pr;
-      const double2 S = make_double2(zk.x + zm.x, zk.y - zm.y);      // Z_k + conj Z_{nt-k}
-      const double2 Dd = make_double2(zk.x - zm.x, zk.y + zm.y);     // Z_k - conj Z_{nt-k}
-      const double2 W = cmul(primary ? wcol : wcolp, tw[rk << (24 - m)]);   // w_n^k, k = ck + 4096 rk
-      const double2 wd = cmul(W, Dd);
-      const double2 A0 = make_double2(0.5 * (S.x + wd.y), 0.5 * (S.y - wd.x));   // (S - i W D) / 2
-      const double2 A1 = make_double2(0.5 * (S.x - wd.y), 0.5 * (S.y + wd.x));   // (S + i W D) / 2
-      if constexpr (EMIT) {   // lambda = ft(k1) at the own k and k + n/2 (fgp_nll_lam)
-        const double2 l0 = primary ? A0 : make_double2(A1.x, -A1.y);
-        const double2 l1 = primary ? A1 : make_double2(A0.x, -A0.y);
-        gl[(int64_t)r * N2] = l0 * inv_rootn;
-        gl[(int64_t)r * N2 + nt] = l1 * inv_rootn;
-      } else {
-        const double* yk = a.ysq + (int64_t)g * a.ysq_stride + ck + (int64_t)rk * N2;
-        const double2 g0 = eig_terms(A0 * inv_rootn, rootn, h.noise, yk[0], a.logdet_weight, norm, la, dnoise);
-        const double2 g1 = eig_terms(A1 * inv_rootn, rootn, h.noise, yk[nt], a.logdet_weight, norm, la, dnoise);
-        // own G at k' and k' + n/2: the primary's, or the conjugates of the primary's (swapped)
-        const double2 G0 = primary ? g0 : make_double2(g1.x, -g1.y);
-        const double2 G1 = primary ? g1 : make_double2(g0.x, -g0.y);
-        const double2 Wo = primary ? W : make_double2(-W.x, W.y);      // w_n^{k'} = -conj w_n^k
-        const double2 Ek = G0 + G1;
-        const double2 Ok = cmulc(G0 - G1, Wo);                       // (G_k' - G_{k'+n/2}) conj(w_n^k')
-        v[e] = make_double2(Ek.x - Ok.y, Ek.y + Ok.x);               // V = E + i O
-        sum += v[e];
+  EigAcc acc2, acc1;          // regular pairs (weight 2), self-mirrored frequencies (weight 1)
+  double2* gl = EMIT ? static_cast<double2*>(a.grad_lam) + (int64_t)g * n : nullptr;
+  const double2 wcp = twmf[col0 ? 0 : cp_gen];
+#pragma unroll 2
+  for (int j = 0; j < JOBS; ++j) {
+    int sp, rp;
+    int64_t cp;
+    job_primary(j, sp, rp, cp);
+    int ss, rs;
+    if (!col0) {
+      ss = sp + 1; rs = N1 - 1 - rp;
+    } else if (sp == 0) {
+      ss = 0; rs = (N1 - rp) & (N1 - 1);
+    } else {
+      ss = 1; rs = N1 - 1 - rp;
+    }
+    const bool self = col0 && sp == 0 && rp == 0;   // frequencies 0, n/2 and (second pair) n/4, 3n/4
+    const double2 wc = col0 ? twmf[cp] : wcp;
+    const double2 W = cmul(wc, tw[rp << (24 - m)]);                 // w_n^k, k = cp + N2 rp
+    double2* ip = lds + sp * CS + rp;
+    double2* is = lds + ss * CS + rs;
+    const double2 zk = *ip, zm = *is;
+    double2 g0, g1, A0, A1;
+    double ya = 0.0, yb = 0.0;
+    if constexpr (!EMIT) {
+      ya = y0[j];
+      yb = y1[j];
+    }
+    EigAcc& ac = self ? acc1 : acc2;
+    pair_eval(zk, zm, W, ya, yb, rootn, inv_rootn, h.noise, a.logdet_weight, ac, g0, g1, A0, A1);
+    if constexpr (EMIT) {   // lambda at k, k + n/2 and (conjugates, swapped) at the partner's nt - k, n - k
+      const int64_t kp = cp + (int64_t)rp * N2;
+      gl[kp] = A0 * inv_rootn;
+      gl[kp + nt] = A1 * inv_rootn;
+      if (!self) {
+        const int64_t ks = (col0 ? cp : N2 - cp) + (int64_t)rs * N2;
+        gl[ks] = make_double2(A1.x, -A1.y) * inv_rootn;
+        gl[ks + nt] = make_double2(A0.x, -A0.y) * inv_rootn;
       }
-      // compiler fence every 4 elements: bounds how many partner / Y / twiddle loads are hoisted
-      if ((e & 3) == 3) {
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
+    } else {
+      const double2 E = g0 + g1;
+      const double2 O = cmulc(g0 - g1, W);
+      *ip = make_double2(E.x - O.y, E.y + O.x);                     // V = E + i O
+      if (!self) *is = make_double2(E.x + O.y, O.x - E.y);          // the partner's (conjugate arithmetic)
+    }
+    if (self) {   // the second self-mirrored element of column 0: row N1/2 (frequencies n/4, 3n/4)
+      constexpr int rh = N1 / 2;
+      double2* ih = lds + rh;
+      const double2 zh = *ih;
+      const double2 Wh = tw[rh << (24 - m)];
+      double yc = 0.0, yd = 0.0;
+      if constexpr (!EMIT) {
+        yc = yg[(int64_t)rh * N2];
+        yd = yg[(int64_t)rh * N2 + nt];
+      }
+      pair_eval(zh, zh, Wh, yc, yd, rootn, inv_rootn, h.noise, a.logdet_weight, acc1, g0, g1, A0, A1);
+      if constexpr (EMIT) {
+        gl[(int64_t)rh * N2] = A0 * inv_rootn;
+        gl[(int64_t)rh * N2 + nt] = A1 * inv_rootn;
+      } else {
+        const double2 E = g0 + g1;
+        const double2 O = cmulc(g0 - g1, Wh);
+        *ih = make_double2(E.x - O.y, E.y + O.x);
       }
     }
+  }
   if constexpr (EMIT) {
     stamp_end(a);
     return;
   }
-  double logdet = la.log_sum(0.5);
+  double norm = 2.0 * acc2.norm + acc1.norm;
+  double dnoise = 2.0 * acc2.dnoise + acc1.dnoise;
+  double logdet = 2.0 * acc2.la.log_sum(0.5) + acc1.la.log_sum(0.5);
+  __syncthreads();
+  sum = zero_v<double2>();
+#pragma unroll
+  for (int j = 0; j < 16 / RLAST; ++j)
+#pragma unroll
+    for (int t = 0; t < RLAST; ++t) {
+      v[j * RLAST + t] = col[pass_pos<P1, SL, RLL>(tt, j, t)];
+      sum += v[j * RLAST + t];
+    }
   column_partials<C>(sum, part);
   mean = column_total<C>(sl, part) * (1.0 / N1);
 #pragma unroll
