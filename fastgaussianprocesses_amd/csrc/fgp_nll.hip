@@ -820,30 +820,25 @@ __global__ __launch_bounds__(kWG) void k_bwd_rows(Nll a, const double2* __restri
 // c <-> N2 - c with rows reversed: the intermediate is stored in paired column tiles (work_pos_pair),
 // so both partners sit in one column workgroup and meet through one LDS exchange.
 //
-// Paired tile layout of the N1 x N2 half-length intermediate (C = kTile / N1 slots per tile):
-// tile 0 holds columns 0 and N2/2 (slots 0, 1) and the pairs (q, N2 - q), q = 1 .. C/2 - 1; tile
-// b >= 1 the pairs (b C/2 + q, N2 - b C/2 - q), q < C/2; slot 2q + (column > N2/2).
+// Paired tile layout of the N1 x N2 half-length intermediate (C = kTile / N1 slots per tile, HC = C/2
+// pair-columns): tile b holds the pair-columns q < HC, i.e. columns c = b HC + q in slots q and their
+// mirrors N2 - c in slots HC + q -- except tile 0's pair-column 0, which holds the self-mirrored
+// columns 0 (slot 0) and N2/2 (slot HC).  A row's consecutive columns c < N2/2 are therefore
+// consecutive slots (runs of HC elements = 256 B at C = 32), and so are its columns > N2/2 (in
+// descending order): the row kernels' 16-B-per-lane accesses are contiguous.
 __device__ __forceinline__ int64_t work_pos_pair(int64_t u, int64_t k, int P1, int64_t N2) {
   const int CL = kTileLog - P1;
   const int64_t h = N2 >> 1;
   int64_t tile, slot;
-  if (k == 0) {
+  if (k == h) {
     tile = 0;
-    slot = 0;
-  } else if (k == h) {
-    tile = 0;
-    slot = 1;
+    slot = (int64_t)1 << (CL - 1);
   } else {
-    const int64_t c = k < h ? k : N2 - k;
+    const int64_t c = k < h ? k : N2 - k;     // (k = 0: c = 0, tile 0, slot 0)
     tile = c >> (CL - 1);
-    slot = 2 * (c & ((1 << (CL - 1)) - 1)) + (k > h ? 1 : 0);
+    slot = (c & ((1 << (CL - 1)) - 1)) + (k > h ? ((int64_t)1 << (CL - 1)) : 0);
   }
   return (tile << kTileLog) + (u << CL) + slot;
-}
-__device__ __forceinline__ int64_t pair_col(int64_t tile, int slot, int C, int64_t N2) {
-  const int64_t c = tile * (C >> 1) + (slot >> 1);
-  if (c == 0) return (slot & 1) ? (N2 >> 1) : 0;
-  return (slot & 1) ? N2 - c : c;
 }
 
 template <int PG, int D>
@@ -909,8 +904,8 @@ __device__ __forceinline__ void pair_eval(double2 zk, double2 zm, double2 W, dou
 // adjoint packing V = E + i O + adjoint column pass, in place (k_fwd_cols for the R2C layout).
 //
 // Exact Hermitian symmetry, each mirror pair evaluated ONCE: after the forward passes the tile's
-// spectrum goes to the LDS image; thread (q, rr) then takes the pairs of pair-column q (slots 2q,
-// 2q + 1 = columns c and N2 - c) at rows rr, rr + RSTEP, ...: from (Z_k, Z_{nt-k}, w_n^k, Y_k,
+// spectrum goes to the LDS image; thread (q, rr) then takes the pairs of pair-column q (slots q,
+// HC + q = columns c and N2 - c) at rows rr, rr + RSTEP, ...: from (Z_k, Z_{nt-k}, w_n^k, Y_k,
 // Y_{k+n/2}) it evaluates the eigen terms of k and k + n/2 once and writes both elements' V back into
 // the image: the primary's V = E + i O, E = G_k + G_{k+n/2}, O = (G_k - G_{k+n/2}) conj(w_n^k), and the
 // partner's, whose G are the conjugates of the primary's (swapped) and whose twiddle is -conj(w_n^k):
@@ -953,11 +948,11 @@ __global__ __launch_bounds__(kWG, 2) void k_fwd_cols_r2c(Nll a, const double2* _
   auto job_primary = [&](int j, int& sp, int& rp, int64_t& cp) {
     const int rr = rr0 + RSTEP * j;
     if (!col0) {
-      sp = 2 * q; rp = rr; cp = cp_gen;
+      sp = q; rp = rr; cp = cp_gen;
     } else if (rr < N1 / 2) {
       sp = 0; rp = rr; cp = 0;
     } else {
-      sp = 1; rp = rr - N1 / 2; cp = N2 >> 1;
+      sp = HC; rp = rr - N1 / 2; cp = N2 >> 1;
     }
   };
   double y0[JOBS], y1[JOBS];
@@ -1006,11 +1001,11 @@ __global__ __launch_bounds__(kWG, 2) void k_fwd_cols_r2c(Nll a, const double2* _
     job_primary(j, sp, rp, cp);
     int ss, rs;
     if (!col0) {
-      ss = sp + 1; rs = N1 - 1 - rp;
+      ss = sp + HC; rs = N1 - 1 - rp;
     } else if (sp == 0) {
       ss = 0; rs = (N1 - rp) & (N1 - 1);
     } else {
-      ss = 1; rs = N1 - 1 - rp;
+      ss = HC; rs = N1 - 1 - rp;
     }
     const bool self = col0 && sp == 0 && rp == 0;   // frequencies 0, n/2 and (second pair) n/4, 3n/4
     const double2 wc = col0 ? twmf[cp] : wcp;

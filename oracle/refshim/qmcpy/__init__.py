@@ -19,8 +19,11 @@ Restated algorithms (qmcpy's documented definitions):
   * DigitalNetB2: base-2 digital net in NATURAL order, t-bit integers
     xb_i = XOR_{k: bit k of i set} C[:, k], then XOR digital shift; x = xb * 2^-t.
   * kernel_methods.bernoulli_poly(n, x): Bernoulli polynomials B_n, Horner form.
-  * kernel_methods.weighted_walsh_funcs: orders >= 2 are NOT restated (parity unpinned,
-    SURVEY §8c) and raise NotImplementedError.
+  * kernel_methods.weighted_walsh_funcs(order, xb, t): order 1 as fastgps spells it out
+    (fast_gp_digital_net_b2.py:297-298); orders 2..4 restated from the Walsh-series definition
+    omega_a(x) = sum_{k>=1} 2^(-mu_a(k)) wal_k(x) (kernel_methods/__init__.py; qmcpy's own values are
+    unpinned offline, SURVEY §8c, and tests/test_oracle_golden.py checks the restatement against
+    the truncated series).
 """
 import numpy as np
 import torch
