@@ -52,6 +52,9 @@ def parse():
     p.add_argument("--sequential", dest="batched", action="store_false",
                    help="fit and predict the shifts one by one (default: one GPBatch over all shifts)")
     p.add_argument("--cpu-sample-iters", type=int, default=3)
+    p.add_argument("--no-secondary", dest="secondary", action="store_false",
+                   help="skip the secondary BASELINE configs (C2, C3, C5) reported under 'secondary'")
+    p.add_argument("--c5-outputs", type=int, default=512)
     return p.parse_args()
 
 
@@ -114,6 +117,115 @@ def step_sequential(sh, args, xm, xv):
         gp.fit(iterations=args.fit_iters, stop_crit_wait_iterations=args.fit_iters + 1, verbose=0)
         gp.post_mean(xm)
         gp.post_var(xv)
+
+
+class SingleGP(object):
+    """BASELINE configs C2 / C3: one fast GP of n = 2^16, d = 3 (lattice / digital net with the
+    reference's default alpha = 2), inputs resident; reset = fresh data ingest + initial parameters."""
+
+    def __init__(self, F, family, log2n, d, device):
+        n = 2 ** log2n
+        if family == "lattice":
+            self.gp = F.FastGPLattice(F.Lattice(d, seed=7), device=device)
+        else:
+            self.gp = F.FastGPDigitalNetB2(F.DigitalNetB2(d, seed=7), device=device)
+        self.y = f_ackley(self.gp.get_x_next(n)).contiguous()
+        self.raw0 = [p.detach().clone() for p in (self.gp.raw_scale, self.gp.raw_lengthscales, self.gp.raw_noise)]
+        self.n, self.outputs = n, 1
+
+    def reset(self):
+        gp = self.gp
+        gp._y[0] = gp._y[0][..., :0]
+        gp._nh = 0
+        gp.add_y_next(self.y)
+        for name, v in zip(("raw_scale", "raw_lengthscales", "raw_noise"), self.raw0):
+            old = getattr(gp, name)
+            setattr(gp, name, torch.nn.Parameter(v.clone(), requires_grad=old.requires_grad))
+        gp._cache, gp._snap = {}, None
+
+
+class MultiOutputGP(SingleGP):
+    """BASELINE config C5: one FastGPLattice, n = 2^18, d = 3, shape_batch = [B] outputs sharing the
+    reference's default hyper-parameters (shape_scale = [1], shape_lengthscales = [d]):
+    y_b = f_ackley(x) (1 + b / B) + 0.01 randn (seeded).  fp64 (the reference's precision)."""
+
+    def __init__(self, F, log2n, d, outputs, device, data_dtype=torch.float64):
+        n = 2 ** log2n
+        self.gp = F.FastGPLattice(F.Lattice(d, seed=7), shape_batch=[outputs], device=device, data_dtype=data_dtype)
+        f = f_ackley(self.gp.get_x_next(n))
+        g = torch.Generator(device=device).manual_seed(5)
+        b = torch.arange(outputs, device=device, dtype=torch.float64)[:, None]
+        self.y = (f[None, :] * (1 + b / outputs) + 0.01 * torch.randn((outputs, n), generator=g, device=device,
+                                                                         dtype=torch.float64)).to(data_dtype).contiguous()
+        self.raw0 = [p.detach().clone() for p in (self.gp.raw_scale, self.gp.raw_lengthscales, self.gp.raw_noise)]
+        self.n, self.outputs = n, outputs
+
+
+def step_single(sg, args, xm, xv):
+    sg.reset()
+    sg.gp.fit(iterations=args.fit_iters, stop_crit_wait_iterations=args.fit_iters + 1, verbose=0)
+    pm = sg.gp.post_mean(xm)
+    pv = sg.gp.post_var(xv)
+    return pm, pv
+
+
+def time_steps(fn, steps, warmup):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
+def secondary_configs(F, args, device):
+    """The other BASELINE.json configs on this GPU (rank 0, N = 1), each timed as its own step
+    (fit K Rprop iterations without early stopping + post_mean N + post_var N):
+    C2 FastGPLattice n=2^16 d=3, C3 FastGPDigitalNetB2 n=2^16 d=3 (default alpha = 2),
+    C5 multi-output FastGPLattice n=2^18 d=3 x B outputs (fp64; the reference cannot run fp32)."""
+    g = torch.Generator().manual_seed(17)
+    out = []
+    for name, make, log2n, d in (("C2: FastGPLattice n=2^16 d=3", lambda: SingleGP(F, "lattice", 16, 3, device), 16, 3),
+                                 ("C3: FastGPDigitalNetB2 n=2^16 d=3 alpha=2", lambda: SingleGP(F, "net", 16, 3, device),
+                                  16, 3),
+                                 ("C5: FastGPLattice n=2^18 d=3 x %d outputs (shared hyper-parameters), fp64"
+                                  % args.c5_outputs, lambda: MultiOutputGP(F, 18, 3, args.c5_outputs, device), 18, 3),
+                                 ("C5 mixed: FastGPLattice n=2^18 d=3 x %d outputs, fp32 observations + complex64 "
+                                  "ytilde for the MLL, fp64 eigenvalues / coefficients / posteriors" % args.c5_outputs,
+                                  lambda: MultiOutputGP(F, 18, 3, args.c5_outputs, device, torch.float32), 18, 3)):
+        sg = make()
+        xm = torch.rand((args.n_mean, d), generator=g).to(device)
+        xv = torch.rand((args.n_var, d), generator=g).to(device)
+        sec = time_steps(lambda: step_single(sg, args, xm, xv), max(1, args.steps), 1)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
+        sg.reset()
+        ev[0].record()
+        sg.gp.fit(iterations=args.fit_iters, stop_crit_wait_iterations=args.fit_iters + 1, verbose=0)
+        ev[1].record()
+        with torch.no_grad():
+            sg.gp.coeffs                 # the graph-free coefficients post_mean uses
+        ev[2].record()
+        sg.gp.post_mean(xm)
+        ev[3].record()
+        sg.gp.post_var(xv)
+        ev[4].record()
+        torch.cuda.synchronize()
+        phases = {k: ev[i].elapsed_time(ev[i + 1]) for i, k in enumerate(("ytilde+fit", "coeffs", "post_mean",
+                                                                          "post_var"))}
+        out.append({"metric": "GP fit+predict points/sec" if sg.outputs == 1 else
+                    "multi-output GP fit+predict output-points/sec",
+                    "value": sg.n * sg.outputs / sec, "unit": "points/s" if sg.outputs == 1 else "output-points/s",
+                    "ms_per_step": sec * 1e3, "steps": max(1, args.steps),
+                    "dtype": "f64" if sg.gp.data_dtype == torch.float64 else "f32 data / f64 eigenvalues",
+                    "config": {"workload": "%s: fit %d Rprop iters + post_mean N=%d + post_var N=%d"
+                                           % (name, args.fit_iters, args.n_mean, args.n_var),
+                               "n": sg.n, "outputs": sg.outputs},
+                    "phases_ms": phases})
+        del sg
+        torch.cuda.empty_cache()
+    return out
 
 
 def phase_breakdown(sh, iters, xm, xv):
@@ -334,6 +446,9 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, n, d)
+    secondary = None
+    if rank == 0 and world == 1 and args.secondary:
+        secondary = secondary_configs(F, args, device)
     if rank == 0:
         out = {"metric": "GP fit+predict points/sec at n=2^20 fp64; achieved HBM GB/s vs roofline",
                "value": value, "unit": "points/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -343,7 +458,7 @@ def main():
                                       "post_mean N=%d + post_var N=%d per shift" %
                                       (args.log2n, d, args.shifts, args.fit_iters, args.n_mean, args.n_var),
                           "global_shifts": args.shifts * world, "parallelism": "replicas%d" % world},
-               "roofline": roof, "cpu_baseline": cpu, "phases_ms": phases}
+               "roofline": roof, "cpu_baseline": cpu, "phases_ms": phases, "secondary": secondary}
         print(json.dumps(out))
     if dist:
         tdist.destroy_process_group()

@@ -83,6 +83,12 @@ _SIGNATURES = {
     "fgp_fftbr": [_c_vp, _c_i64, _c_int, _c_vp, _c_i64, _c_int, _c_int, _c_vp],
     "fgp_ifftbr": [_c_vp, _c_i64, _c_vp, _c_int, _c_vp, _c_i64, _c_int, _c_int, _c_vp],
     "fgp_fwht": [_c_vp, _c_i64, _c_vp, _c_i64, _c_int, _c_int, _c_vp],
+    "fgp_fftbr_c64": [_c_vp, _c_i64, _c_int, _c_vp, _c_i64, _c_int, _c_int, _c_vp],
+    "fgp_ifftbr_c64": [_c_vp, _c_i64, _c_vp, _c_int, _c_vp, _c_i64, _c_int, _c_int, _c_vp],
+    "fgp_fwht_f32": [_c_vp, _c_i64, _c_vp, _c_i64, _c_int, _c_int, _c_vp],
+    "fgp_ifftbr_mul": [_c_int, _c_int, _c_vp, _c_i64, _c_vp, _c_i64, _c_vp, _c_int, _c_vp, _c_i64, _c_int, _c_int,
+                       _c_vp],
+    "fgp_sum_sq": [_c_vp, _c_i64, _c_int, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp],
     "fgp_lattice_parts": [_c_vp, _c_i64, _c_vp, _c_i64, _c_int, _c_pi, _c_pd, _c_vp, _c_vp],
     "fgp_lattice_points": [_c_pl, _c_vp, _c_i64, _c_i64, _c_int, _c_vp, _c_vp],
     "fgp_lattice_parts_gen": [_c_pl, _c_vp, _c_int, _c_int, _c_int, _c_pd, _c_vp, _c_vp],

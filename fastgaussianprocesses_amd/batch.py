@@ -307,7 +307,7 @@ class GPBatch(object):
     def ysq(self):
         if "ysq" not in self._st:
             yt = self.ytilde()
-            self._st["ysq"] = (yt.real ** 2 + yt.imag ** 2) if yt.is_complex() else yt ** 2
+            self._st["ysq"] = ops.sum_sq(yt, G=self.P)          # |ytilde|^2 per GP (fgp_sum_sq)
         return self._st["ysq"]
 
     # ---------------------------------------------------------------------------- fit

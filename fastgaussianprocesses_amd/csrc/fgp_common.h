@@ -48,6 +48,38 @@ template <typename T> __device__ __forceinline__ T zero_v();
 template <> __device__ __forceinline__ double zero_v<double>() { return 0.0; }
 template <> __device__ __forceinline__ double2 zero_v<double2>() { return make_double2(0.0, 0.0); }
 
+// ---------------------------------------------------------------- single precision (c64 / f32)
+// The same engine instantiated on float2 / float (fgp_fftbr_c64, fgp_ifftbr_c64, fgp_fwht_f32):
+// arithmetic in fp32 with explicit fmaf, twiddles read from the fp64 tables and rounded once.
+__device__ __forceinline__ float2 operator+(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 operator-(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 operator*(float2 a, double s) {
+  const float f = (float)s;
+  return make_float2(a.x * f, a.y * f);
+}
+__device__ __forceinline__ float2& operator+=(float2& a, float2 b) { a.x += b.x; a.y += b.y; return a; }
+__device__ __forceinline__ float2& operator-=(float2& a, float2 b) { a.x -= b.x; a.y -= b.y; return a; }
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+  return make_float2(__builtin_fmaf(a.x, b.x, -(a.y * b.y)), __builtin_fmaf(a.x, b.y, a.y * b.x));
+}
+__device__ __forceinline__ float2 cmulc(float2 a, float2 w) {  // a * conj(w)
+  return make_float2(__builtin_fmaf(a.x, w.x, a.y * w.y), __builtin_fmaf(a.y, w.x, -(a.x * w.y)));
+}
+__device__ __forceinline__ float2 to_f2(double2 w) { return make_float2((float)w.x, (float)w.y); }
+template <> __device__ __forceinline__ float zero_v<float>() { return 0.0f; }
+template <> __device__ __forceinline__ float2 zero_v<float2>() { return make_float2(0.0f, 0.0f); }
+
+// Element traits: real scalar, complex type (twiddles / complex products), complex-ness.
+template <typename T> struct Elem;
+template <> struct Elem<double> { using R = double; using C = double2; static constexpr bool cx = false; };
+template <> struct Elem<double2> { using R = double; using C = double2; static constexpr bool cx = true; };
+template <> struct Elem<float> { using R = float; using C = float2; static constexpr bool cx = false; };
+template <> struct Elem<float2> { using R = float; using C = float2; static constexpr bool cx = true; };
+// a twiddle from the fp64 tables in the complex type C of the data
+template <typename C> __device__ __forceinline__ C twid(double2 w);
+template <> __device__ __forceinline__ double2 twid<double2>(double2 w) { return w; }
+template <> __device__ __forceinline__ float2 twid<float2>(double2 w) { return to_f2(w); }
+
 // ---------------------------------------------------------------- butterflies
 // tw = exp(-2 pi i k / 4096), k < 4096 (full circle); a stage of span 2h = 2^(s+1) uses
 // w = exp(-2 pi i pos / 2h) = tw[pos << (11 - s)].
@@ -68,6 +100,26 @@ __device__ __forceinline__ void bfly_dif(double2& a, double2& b, const double2* 
 }
 __device__ __forceinline__ void bfly_dif(double& a, double& b, const double2* __restrict__, int) {
   const double t = a;
+  a = t + b;
+  b = t - b;
+}
+__device__ __forceinline__ void bfly_dit(float2& a, float2& b, const double2* __restrict__ tw, int k) {
+  const float2 bw = cmul(b, to_f2(tw[k]));
+  b = a - bw;
+  a = a + bw;
+}
+__device__ __forceinline__ void bfly_dit(float& a, float& b, const double2* __restrict__, int) {
+  const float t = a;
+  a = t + b;
+  b = t - b;
+}
+__device__ __forceinline__ void bfly_dif(float2& a, float2& b, const double2* __restrict__ tw, int k) {
+  const float2 d = a - b;
+  a = a + b;
+  b = cmulc(d, to_f2(tw[k]));
+}
+__device__ __forceinline__ void bfly_dif(float& a, float& b, const double2* __restrict__, int) {
+  const float t = a;
   a = t + b;
   b = t - b;
 }
@@ -96,48 +148,80 @@ __device__ __forceinline__ double2 mul_root(double2 v) {
   }
 }
 
+template <int K, int J, bool CONJ>
+__device__ __forceinline__ float2 mul_root(float2 v) {
+  constexpr int j = (J * (16 / K)) & 15;
+  constexpr float c16[16] = {1.0f, 0.92387953251128673848f, 0.70710678118654752440f, 0.38268343236508978178f,
+                             0.0f, -0.38268343236508978178f, -0.70710678118654752440f, -0.92387953251128673848f,
+                             -1.0f, -0.92387953251128673848f, -0.70710678118654752440f, -0.38268343236508978178f,
+                             0.0f, 0.38268343236508978178f, 0.70710678118654752440f, 0.92387953251128673848f};
+  constexpr float cr = c16[j];
+  constexpr float ci = CONJ ? -c16[(j + 4) & 15] : c16[(j + 4) & 15];
+  if constexpr (j == 0) {
+    return v;
+  } else if constexpr (j == 8) {
+    return make_float2(-v.x, -v.y);
+  } else if constexpr (j == 4) {
+    return CONJ ? make_float2(-v.y, v.x) : make_float2(v.y, -v.x);
+  } else if constexpr (j == 12) {
+    return CONJ ? make_float2(v.y, -v.x) : make_float2(-v.y, v.x);
+  } else {
+    return make_float2(__builtin_fmaf(cr, v.x, -(ci * v.y)), __builtin_fmaf(cr, v.y, ci * v.x));
+  }
+}
+
 // DIT / DIF butterflies at stage Q2 of a register group for element pair (t, t | 2^Q2), given the
 // group's base twiddle wb = exp(-2 pi i blo / 2^(S+Q2+1)) (unused when S == 0): the full twiddle is
 // wb * exp(-2 pi i (t mod 2^Q2) / 2^(Q2+1)).
-template <int S, int Q2, int T0, bool ADJ>
-__device__ __forceinline__ void group_bfly(double2& a, double2& b, double2 wb) {
+template <int S, int Q2, int T0, bool ADJ, typename C>
+__device__ __forceinline__ void group_bfly_cx(C& a, C& b, C wb) {
   constexpr int J = T0 & ((1 << Q2) - 1);
   if constexpr (!ADJ) {
-    double2 bw = mul_root<(2 << Q2), J, false>(b);
+    C bw = mul_root<(2 << Q2), J, false>(b);
     if constexpr (S > 0) bw = cmul(bw, wb);
     b = a - bw;
     a = a + bw;
   } else {
-    double2 d = a - b;
+    C d = a - b;
     a = a + b;
     if constexpr (S > 0) d = cmulc(d, wb);
     b = mul_root<(2 << Q2), J, true>(d);
   }
 }
 template <int S, int Q2, int T0, bool ADJ>
+__device__ __forceinline__ void group_bfly(double2& a, double2& b, double2 wb) { group_bfly_cx<S, Q2, T0, ADJ>(a, b, wb); }
+template <int S, int Q2, int T0, bool ADJ>
+__device__ __forceinline__ void group_bfly(float2& a, float2& b, float2 wb) { group_bfly_cx<S, Q2, T0, ADJ>(a, b, wb); }
+template <int S, int Q2, int T0, bool ADJ>
 __device__ __forceinline__ void group_bfly(double& a, double& b, double2) {
   const double t = a;
   a = t + b;
   b = t - b;
 }
+template <int S, int Q2, int T0, bool ADJ>
+__device__ __forceinline__ void group_bfly(float& a, float& b, float2) {
+  const float t = a;
+  a = t + b;
+  b = t - b;
+}
 
-template <int Q2, int T, int RL, int S, bool ADJ, typename E>
-__device__ __forceinline__ void stage_pairs(E* v, double2 wb) {
+template <int Q2, int T, int RL, int S, bool ADJ, typename E, typename W>
+__device__ __forceinline__ void stage_pairs(E* v, W wb) {
   if constexpr (T < (1 << RL)) {
     if constexpr (!(T & (1 << Q2))) group_bfly<S, Q2, T, ADJ>(v[T], v[T | (1 << Q2)], wb);
     stage_pairs<Q2, T + 1, RL, S, ADJ>(v, wb);
   }
 }
 
-template <int Q2, int RL, int S, bool ADJ, typename E>
-__device__ __forceinline__ void stages_dit(E* v, const double2* wb) {
+template <int Q2, int RL, int S, bool ADJ, typename E, typename W>
+__device__ __forceinline__ void stages_dit(E* v, const W* wb) {
   if constexpr (Q2 < RL) {
     stage_pairs<Q2, 0, RL, S, ADJ>(v, wb[Q2]);
     stages_dit<Q2 + 1, RL, S, ADJ>(v, wb);
   }
 }
-template <int Q2, int RL, int S, bool ADJ, typename E>
-__device__ __forceinline__ void stages_dif(E* v, const double2* wb) {
+template <int Q2, int RL, int S, bool ADJ, typename E, typename W>
+__device__ __forceinline__ void stages_dif(E* v, const W* wb) {
   if constexpr (Q2 >= 0) {
     stage_pairs<Q2, 0, RL, S, ADJ>(v, wb[Q2]);
     stages_dif<Q2 - 1, RL, S, ADJ>(v, wb);
@@ -158,11 +242,12 @@ __device__ __forceinline__ void lds_pass(T* s, int tt, const double2* __restrict
     const int q = tt + j * TL;
     const int blo = q & ((1 << S) - 1);
     const int base = blo + ((q >> S) << (S + RL));
-    double2 wb[RL];
+    using C = typename Elem<T>::C;
+    C wb[RL];
 #pragma unroll
     for (int q2 = 0; q2 < RL; ++q2) {
-      if constexpr (S > 0 && sizeof(T) == 16) wb[q2] = tw[blo << (11 - S - q2)];
-      else wb[q2] = make_double2(1.0, 0.0);
+      if constexpr (S > 0 && Elem<T>::cx) wb[q2] = twid<C>(tw[blo << (11 - S - q2)]);
+      else wb[q2] = twid<C>(make_double2(1.0, 0.0));
     }
     T v[R];
 #pragma unroll
@@ -237,11 +322,12 @@ __device__ __forceinline__ void reg_pass(T* v, int tt, const double2* __restrict
   for (int j = 0; j < GPT; ++j) {
     const int q = tt + j * TL;
     const int blo = q & ((1 << S) - 1);
-    double2 wb[RL];
+    using C = typename Elem<T>::C;
+    C wb[RL];
 #pragma unroll
     for (int q2 = 0; q2 < RL; ++q2) {
-      if constexpr (S > 0 && sizeof(T) == 16) wb[q2] = tw[blo << (11 - S - q2)];
-      else wb[q2] = make_double2(1.0, 0.0);
+      if constexpr (S > 0 && Elem<T>::cx) wb[q2] = twid<C>(tw[blo << (11 - S - q2)]);
+      else wb[q2] = twid<C>(make_double2(1.0, 0.0));
     }
     if constexpr (!ADJ) stages_dit<0, RL, S, false>(v + j * R, wb);
     else stages_dif<RL - 1, RL, S, true>(v + j * R, wb);
@@ -334,6 +420,10 @@ template <int T4> struct Brev4 {
 __device__ __forceinline__ double shfl_xor_d(double v, int o) { return __shfl_xor(v, o, 64); }
 __device__ __forceinline__ double2 shfl_xor_d(double2 v, int o) {
   return make_double2(__shfl_xor(v.x, o, 64), __shfl_xor(v.y, o, 64));
+}
+__device__ __forceinline__ float shfl_xor_d(float v, int o) { return __shfl_xor(v, o, 64); }
+__device__ __forceinline__ float2 shfl_xor_d(float2 v, int o) {
+  return make_float2(__shfl_xor(v.x, o, 64), __shfl_xor(v.y, o, 64));
 }
 
 // Sum over a group of TL consecutive threads (TL a power of two, groups aligned to TL).
@@ -433,11 +523,34 @@ __device__ __forceinline__ void store_out(void* p, int64_t i, double2 v, int out
 }
 __device__ __forceinline__ void store_out(void* p, int64_t i, double v, int) { static_cast<double*>(p)[i] = v; }
 
+template <> __device__ __forceinline__ float2 load_in<float2>(const void* p, int64_t i, int in_real) {
+  if (in_real) return make_float2(static_cast<const float*>(p)[i], 0.0f);
+  return static_cast<const float2*>(p)[i];
+}
+template <> __device__ __forceinline__ float load_in<float>(const void* p, int64_t i, int) {
+  return static_cast<const float*>(p)[i];
+}
+__device__ __forceinline__ void store_out(void* p, int64_t i, float2 v, int out_real) {
+  if (out_real) static_cast<float*>(p)[i] = v.x;
+  else static_cast<float2*>(p)[i] = v;
+}
+__device__ __forceinline__ void store_out(void* p, int64_t i, float v, int) { static_cast<float*>(p)[i] = v; }
+
+// v * s in the element's own precision
+__device__ __forceinline__ double scaled(double v, double s) { return v * s; }
+__device__ __forceinline__ double2 scaled(double2 v, double s) { return v * s; }
+__device__ __forceinline__ float scaled(float v, double s) { return v * (float)s; }
+__device__ __forceinline__ float2 scaled(float2 v, double s) { return v * s; }
+
 template <typename T> __device__ __forceinline__ T tw_mul(T v, double2 w, bool conj);
 template <> __device__ __forceinline__ double2 tw_mul<double2>(double2 v, double2 w, bool conj) {
   return conj ? cmulc(v, w) : cmul(v, w);
 }
 template <> __device__ __forceinline__ double tw_mul<double>(double v, double2, bool) { return v; }
+template <> __device__ __forceinline__ float2 tw_mul<float2>(float2 v, double2 w, bool conj) {
+  return conj ? cmulc(v, to_f2(w)) : cmul(v, to_f2(w));
+}
+template <> __device__ __forceinline__ float tw_mul<float>(float v, double2, bool) { return v; }
 
 
 // Centre (optional) -> in-LDS transform -> add the mean back to bin 0, for one length-2^P

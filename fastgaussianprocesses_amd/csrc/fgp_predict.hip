@@ -12,6 +12,7 @@
 // chunk are staged through LDS in slabs; per-chunk partial sums are reduced in fixed order by a
 // second kernel (bitwise reproducible, no atomics).
 #include <cmath>
+#include <cstdlib>
 #include <type_traits>
 
 #include "fgp_common.h"
@@ -449,6 +450,227 @@ __global__ __launch_bounds__(kWG) void k_qf_cols(QfArgs q, const double2* __rest
   if (tid == 0) q.partial[(int64_t)tg * tiles + blk] = acc;
 }
 
+// ---------------------------------------------------------------- half-length (R2C) quadratic form
+// Lattice, n >= 2^17 (as the fit kernels, FGP_R2C=0 selects the full-length ones): the kernel row
+// r_t is real, so its spectrum comes from the half-length transform of r_t[:n/2] + i r_t[n/2:]
+// (csrc/fgp_nll.hip, k_fwd_rows_r2c / k_fwd_cols_r2c: same engine, same paired column tiles) and
+//   sum_k wa_k |ft(r_t)_k|^2 = sum over mirror pairs (k, n/2 - k) of w (wa_k |A0|^2 + wa_{k+n/2} |A1|^2) / n
+// with A0, A1 the unnormalised spectrum at k, k + n/2 and w = 2 for a regular pair (its mirror
+// frequencies n/2 - k, n - k have the same |.|^2 and, ev being Hermitian, the same wa) and 1 for the
+// self-mirrored frequencies.  Per test point: 8n bytes written + 8n + 4n read instead of 32n + 8n.
+//
+// Row kernel: register-resident half-length row transform of the kernel values of 16 consecutive
+// points per half.  With regenerated lattice points (gen) the distance is formed from the lattice index
+// directly, delta = (x_t - shift - k/n) % 1 with k = brev_m(i) z_j mod n (k/n exact): one fract instead
+// of the generated point's two and |x - z|; it differs from |x_t - x_i| of the materialised points by
+// rounding only (the reference's own kmat carries the rounding of its generated points).
+template <int D, int ORD>
+__device__ __forceinline__ void qf_row16(const QfArgs& q, int64_t n, int64_t i0, const double* xv, const double* cv,
+                                         const double* fa, const double* fc, const void* zp, bool gen, double scale,
+                                         double* r, double& sum) {
+  const int m = q.log2n;
+  const unsigned mask = (unsigned)(n - 1);
+  const double inv_n = ldexp(1.0, -m);
+  if (gen) {
+    const unsigned br0 = brev_bits((unsigned)i0, m);
+    static_for<0, 16>([&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+      const unsigned br = br0 | (Brev4<t>::value << (m - 4));
+      double pr = scale;
+#pragma unroll
+      for (int j = 0; j < D; ++j) {
+        const double kf = (double)(mul_u24(br, q.gz[j]) & mask);
+        const double dl = __builtin_amdgcn_fract(__builtin_fma(-kf, inv_n, cv[j]));
+        pr *= lat_factor(ORD ? ORD : q.spec.order[j], dl, fa[j], fc[j]);
+      }
+      r[t] = pr;
+    });
+  } else {
+#pragma unroll
+    for (int t = 0; t < 16; ++t) r[t] = scale;
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const double2 zv = *reinterpret_cast<const double2*>(static_cast<const double*>(zp) + (int64_t)j * n + i0 + 2 * u);
+        r[2 * u] *= lat_factor(ORD ? ORD : q.spec.order[j], fabs(xv[j] - zv.x), fa[j], fc[j]);
+        r[2 * u + 1] *= lat_factor(ORD ? ORD : q.spec.order[j], fabs(xv[j] - zv.y), fa[j], fc[j]);
+      }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 16; ++t) sum += r[t];
+}
+
+// paired column-tile position of (row u, column k) of the N1 x N2 half-length intermediate
+// (the layout of csrc/fgp_nll.hip work_pos_pair)
+__device__ __forceinline__ int64_t qf_pos_pair(int64_t u, int64_t k, int P1, int64_t N2) {
+  const int CL = kTileLog - P1;
+  const int64_t h = N2 >> 1;
+  int64_t tile, slot;
+  if (k == h) {
+    tile = 0;
+    slot = (int64_t)1 << (CL - 1);
+  } else {
+    const int64_t c = k < h ? k : N2 - k;
+    tile = c >> (CL - 1);
+    slot = (c & ((1 << (CL - 1)) - 1)) + (k > h ? ((int64_t)1 << (CL - 1)) : 0);
+  }
+  return (tile << kTileLog) + (u << CL) + slot;
+}
+
+// ORD: the Bernoulli order of every dimension (4 = the default alpha = 2), 0 = per-dimension orders
+template <int D, int ORD>
+__global__ __launch_bounds__(kWG) void k_qf_rows_r2c(QfArgs q, const double2* __restrict__ tw, const double2* __restrict__ twm) {
+  constexpr int P2 = 12, N2 = 1 << P2;
+  __shared__ double ldsd[kTile + kTile / 16];
+  __shared__ double2 red[kWG / 64];
+  const int mt = q.log2n - 1, m1 = mt - P2;
+  const int64_t n = (int64_t)1 << q.log2n, nt = n >> 1;
+  const int64_t tiles = nt >> kTileLog;
+  const int tg = (int)(blockIdx.x / tiles);           // (problem, test point) row of work
+  const int pb = tg / q.N, t = tg % q.N;
+  const int row0 = (int)(blockIdx.x % tiles);
+  const int tid = threadIdx.x;
+  const double* xt = q.xt + pb * q.ps.x;
+  const double* hyp = q.hyp + pb * q.ps.h;
+  const void* zp = static_cast<const char*>(q.z) + pb * q.ps.z * 8;
+  const bool gen = q.gen;
+  double xv[D], cv[D], fa[D], fc[D];
+  const double scale = hyp[0];
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+    xv[j] = xt[(int64_t)t * D + j];
+    cv[j] = gen ? xv[j] - q.gshift[pb * q.gss + j] : 0.0;
+    fa[j] = hyp[1 + j] * q.spec.coef[j];
+    fc[j] = fac_const(q.spec.order[j], fa[j]);
+  }
+  const int64_t base = (int64_t)row0 * N2;
+  double lo[16], hi[16];
+  double slo = 0.0, shi = 0.0;
+  qf_row16<D, ORD>(q, n, base + 16 * tid, xv, cv, fa, fc, zp, gen, scale, lo, slo);
+  qf_row16<D, ORD>(q, n, nt + base + 16 * tid, xv, cv, fa, fc, zp, gen, scale, hi, shi);
+  double2 v[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v[k] = make_double2(lo[k], hi[k]);
+  const double2 mean = block_sum_t(make_double2(slo, shi), red) * (1.0 / N2);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v[k] -= mean;
+  fwd_reg_passes<P2, 0, true>(v, ldsd, tid, tw);
+  if (tid == 0) v[0] += mean * (double)N2;
+  const RowTwiddle rt((unsigned)row0, tid, P2, m1, tw, twm);
+  double2* out = static_cast<double2*>(q.work) + (int64_t)tg * n;
+#pragma unroll
+  for (int k = 0; k < 16; ++k)
+    out[qf_pos_pair(row0, tid + k * kWG, m1, N2)] = cmul(v[k], rt.at(k, P2, m1, tw, twm));
+}
+
+// column pass at half length + mirror split + weighted Parseval sum; one partial per column tile
+template <int P1>
+__global__ __launch_bounds__(kWG, 2) void k_qf_cols_r2c(QfArgs q, const double2* __restrict__ tw,
+                                                         const double2* __restrict__ twmf) {
+  constexpr int N1 = 1 << P1, C = kTile / N1, CS = N1 + 1, HC = C / 2;
+  constexpr int RL0 = PassRL<P1, 0>::value, R0 = 1 << RL0;
+  constexpr int SL = LastPass<P1>::S, RLL = PassRL<P1, SL>::value, RLAST = 1 << RLL;
+  constexpr int JOBS = kTile / 2 / kWG, RSTEP = kWG / HC;
+  static_assert(JOBS * RSTEP == N1, "pair jobs cover the tile");
+  __shared__ double2 lds[C * CS];
+  __shared__ double2 part[ColPart<C>::size];
+  __shared__ double redd[kWG / 64];
+  const int m = q.log2n;
+  const int64_t n = (int64_t)1 << m, nt = n >> 1, N2 = nt >> P1;
+  const int64_t tiles = nt >> kTileLog;
+  const int tg = (int)(blockIdx.x / tiles);
+  const int blk = (int)(blockIdx.x % tiles);
+  const int tid = threadIdx.x;
+  const int sl = tid % C, tt = tid / C;
+  const double2* wk = static_cast<const double2*>(q.work) + (int64_t)tg * n + (int64_t)blk * kTile + sl;
+  const double* wa = q.wa + (tg / q.N) * q.ps.c;
+  double2* col = lds + sl * CS;
+  const int jq = tid % HC, rr0 = tid / HC;
+  const bool col0 = blk == 0 && jq == 0;
+  const int64_t cp_gen = (int64_t)blk * HC + jq;
+  auto job_primary = [&](int j, int& sp, int& rp, int64_t& cp) {
+    const int rr = rr0 + RSTEP * j;
+    if (!col0) {
+      sp = jq; rp = rr; cp = cp_gen;
+    } else if (rr < N1 / 2) {
+      sp = 0; rp = rr; cp = 0;
+    } else {
+      sp = HC; rp = rr - N1 / 2; cp = N2 >> 1;
+    }
+  };
+  double w0[JOBS], w1[JOBS];
+#pragma unroll
+  for (int j = 0; j < JOBS; ++j) {
+    int sp, rp;
+    int64_t cp;
+    job_primary(j, sp, rp, cp);
+    const double* wp = wa + cp + (int64_t)rp * N2;
+    w0[j] = wp[0];
+    w1[j] = wp[nt];
+  }
+  double2 v[16];
+#pragma unroll
+  for (int j = 0; j < 16 / R0; ++j)
+#pragma unroll
+    for (int t = 0; t < R0; ++t) v[j * R0 + t] = wk[pass_pos<P1, 0, RL0>(tt, j, t) * C];
+  double2 sum = zero_v<double2>();
+#pragma unroll
+  for (int k = 0; k < 16; ++k) sum += v[k];
+  column_partials<C>(sum, part);
+  const double2 mean = column_total<C>(sl, part) * (1.0 / N1);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v[k] -= mean;
+  fwd_reg_passes<P1, 0, false>(v, col, tt, tw);
+  if (tt == 0) v[0] += mean * (double)N1;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 16 / RLAST; ++j)
+#pragma unroll
+    for (int t = 0; t < RLAST; ++t) col[pass_pos<P1, SL, RLL>(tt, j, t)] = v[j * RLAST + t];
+  __syncthreads();
+  double acc2 = 0.0, acc1 = 0.0;
+  const double2 wcp = twmf[col0 ? 0 : cp_gen];
+  auto split = [&](double2 zk, double2 zm, double2 W, double wk0, double wk1) {
+    const double2 S = make_double2(zk.x + zm.x, zk.y - zm.y);
+    const double2 Dd = make_double2(zk.x - zm.x, zk.y + zm.y);
+    const double2 wd = cmul(W, Dd);
+    const double2 A0 = make_double2(0.5 * (S.x + wd.y), 0.5 * (S.y - wd.x));
+    const double2 A1 = make_double2(0.5 * (S.x - wd.y), 0.5 * (S.y + wd.x));
+    return __builtin_fma(wk0, sqabs(A0), wk1 * sqabs(A1));
+  };
+#pragma unroll 2
+  for (int j = 0; j < JOBS; ++j) {
+    int sp, rp;
+    int64_t cp;
+    job_primary(j, sp, rp, cp);
+    int ss, rs;
+    if (!col0) {
+      ss = sp + HC; rs = N1 - 1 - rp;
+    } else if (sp == 0) {
+      ss = 0; rs = (N1 - rp) & (N1 - 1);
+    } else {
+      ss = HC; rs = N1 - 1 - rp;
+    }
+    const bool self = col0 && sp == 0 && rp == 0;
+    const double2 wc = col0 ? twmf[cp] : wcp;
+    const double2 W = cmul(wc, tw[rp << (24 - m)]);
+    const double s = split(lds[sp * CS + rp], lds[ss * CS + rs], W, w0[j], w1[j]);
+    if (self) {
+      acc1 += s;
+      constexpr int rh = N1 / 2;     // second self-mirrored element of column 0 (frequencies n/4, 3n/4)
+      const double2 zh = lds[rh];
+      acc1 += split(zh, zh, tw[rh << (24 - m)], wa[(int64_t)rh * N2], wa[(int64_t)rh * N2 + nt]);
+    } else {
+      acc2 += s;
+    }
+  }
+  double acc = __builtin_fma(2.0, acc2, acc1) * (1.0 / (double)n);
+  acc = block_sum(acc, redd);
+  if (tid == 0) q.partial[(int64_t)tg * tiles + blk] = acc;
+}
+
 // Posterior variance of (problem p, test point t) from its quadratic-form partials:
 //   out = K(x, x) - sum_c partial[c], negative values set to 0 (abstract_gp.py:407-413), with
 //   K(x, x) = scale * prod_j (1 + l_j part0_j), AbstractFastGP._kernel at zero distance.
@@ -593,6 +815,13 @@ int fgp_post_mean(int family, const double* xt, int64_t N, const void* z, int64_
 }  // extern "C"
 
 namespace fgp {
+// partials per (problem, test point) written by launch_qf: one per column tile of the transform
+static int64_t qf_partials(int family, int log2n) {
+  const char* r2c_env = getenv("FGP_R2C");
+  const bool r2c = family == FGP_FAMILY_LATTICE && log2n >= 17 && !(r2c_env && r2c_env[0] == '0');
+  return (int64_t)1 << (log2n - kTileLog - (r2c ? 1 : 0));
+}
+
 // quadratic-form partials of P problems x N test points (k_qf_rows + k_qf_cols)
 static int launch_qf(int family, const double* xt, int64_t N, const void* z, int log2n, int d, int tbits,
                      const PredSpec& spec, const double* hyp, const double* wa, void* work, double* partial, int64_t P,
@@ -630,6 +859,32 @@ static int launch_qf(int family, const double* xt, int64_t N, const void* z, int
     q.gss = gdesc->gen_shift_stride;
   }
   int rc;
+  const char* r2c_env = getenv("FGP_R2C");
+  if (family == FGP_FAMILY_LATTICE && log2n >= 17 && !(r2c_env && r2c_env[0] == '0')) {
+    // half-length (R2C) quadratic form: (P N) x (n/2 / 4096) workgroups per pass
+    const int mt = log2n - 1, p1 = mt - 12;
+    const dim3 grid((unsigned)((P * N) << (mt - kTileLog)));
+    bool uniform4 = true;
+    for (int j = 0; j < d; ++j) uniform4 = uniform4 && spec.order[j] == 4;
+    switch (d) {
+#define FGP_C(DD)                                                                          \
+  case DD:                                                                                 \
+    if (uniform4) k_qf_rows_r2c<DD, 4><<<grid, kWG, 0, st>>>(q, tb->tw4096, tb->twm[mt]);  \
+    else k_qf_rows_r2c<DD, 0><<<grid, kWG, 0, st>>>(q, tb->tw4096, tb->twm[mt]);           \
+    break;
+      FGP_C(1) FGP_C(2) FGP_C(3) FGP_C(4) FGP_C(5) FGP_C(6) FGP_C(7) FGP_C(8)
+#undef FGP_C
+      default: return set_error(kErrUnsupported, "post_var: d=%d unsupported", d);
+    }
+    if ((rc = check_launch("k_qf_rows_r2c")) != kOk) return rc;
+    switch (p1) {
+#define FGP_C(PP) case PP: k_qf_cols_r2c<PP><<<grid, kWG, 0, st>>>(q, tb->tw4096, tb->twm[log2n]); break;
+      FGP_C(4) FGP_C(5) FGP_C(6) FGP_C(7) FGP_C(8) FGP_C(9) FGP_C(10) FGP_C(11)
+#undef FGP_C
+      default: return set_error(kErrInvalid, "bad r2c m1");
+    }
+    return check_launch("k_qf_cols_r2c");
+  }
   const int m2 = split_m2(log2n), m1 = log2n - m2;
   const dim3 grid((unsigned)((P * N) << (log2n - kTileLog)));
   const double2* tw = tb->tw4096;
@@ -681,7 +936,7 @@ int fgp_post_var_qf(int family, const double* xt, int64_t N, const void* z, int 
   hipStream_t st = (hipStream_t)stream;
   rc = launch_qf(family, xt, N, z, log2n, d, tbits, spec, hyp, wa, work, partial, 1, ProbStrides{0, 0, 0, 0}, st);
   if (rc != kOk) return rc;
-  k_sum_chunks<<<(unsigned)N, kWG, 0, st>>>(partial, (int64_t)1 << (log2n - kTileLog), out, N, N);
+  k_sum_chunks<<<(unsigned)N, kWG, 0, st>>>(partial, qf_partials(family, log2n), out, N, N);
   return check_launch("k_sum_chunks");
 }
 
@@ -732,7 +987,7 @@ int fgp_post_var_batched(const fgp_pred_desc* pd, const double* xt, int64_t xt_s
   rc = launch_qf(pd->family, xt, N, pd->z, log2n, d, pd->tbits, spec, pd->hyp, pd->wa, work, partial, pd->P,
                  ProbStrides{xt_stride, pd->z_stride, pd->hyp_stride, pd->wa_stride}, st, pd);
   if (rc != kOk) return rc;
-  k_qf_finish<<<(unsigned)((int64_t)pd->P * N), kWG, 0, st>>>(partial, (int64_t)1 << (log2n - kTileLog), pd->hyp,
+  k_qf_finish<<<(unsigned)((int64_t)pd->P * N), kWG, 0, st>>>(partial, qf_partials(pd->family, log2n), pd->hyp,
                                                                pd->hyp_stride, p0, d, N, out);
   return check_launch("k_qf_finish");
 }

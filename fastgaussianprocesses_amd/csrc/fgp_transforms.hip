@@ -23,11 +23,26 @@
 
 namespace fgp {
 
+// Optional elementwise factor applied to the input of the inverse's first pass (fgp_ifftbr_mul):
+// element i of row b is multiplied by f[b * bs + i] (bs = 0: one row shared by all) -- the
+// tilde-domain solve A * y~ of gram_matrix_solve (util.py:341-343) fused into the load.
+struct Pre {
+  const void* f;
+  int64_t bs;
+};
+template <typename T>
+__device__ __forceinline__ T pre_mul(T v, const Pre& p, int64_t b, int64_t i) {
+  if (!p.f) return v;
+  const T w = static_cast<const T*>(p.f)[b * p.bs + i];
+  if constexpr (Elem<T>::cx) return cmul(v, w);
+  else return v * w;
+}
+
 // ------------------------------------------------------------------ m <= 3: registers only
 template <int P, typename T, bool ADJ>
 __global__ __launch_bounds__(kWG) void k_tiny(const void* in, int64_t in_bs, int in_real, void* out,
                                                int64_t out_bs, int out_real, int64_t batch, int stable,
-                                               double scale, const double2* __restrict__ tw) {
+                                               double scale, const double2* __restrict__ tw, Pre pre) {
   constexpr int L = 1 << P;
   const int64_t b = (int64_t)blockIdx.x * kWG + threadIdx.x;
   if (b >= batch) return;
@@ -35,7 +50,7 @@ __global__ __launch_bounds__(kWG) void k_tiny(const void* in, int64_t in_bs, int
   T mean = zero_v<T>();
 #pragma unroll
   for (int i = 0; i < L; ++i) {
-    v[i] = load_in<T>(in, b * in_bs + i, in_real);
+    v[i] = pre_mul(load_in<T>(in, b * in_bs + i, in_real), pre, b, i);
     mean += v[i];
   }
   mean = mean * (1.0 / L);
@@ -58,14 +73,14 @@ __global__ __launch_bounds__(kWG) void k_tiny(const void* in, int64_t in_bs, int
   }
   if (stable) v[0] += mean * (double)L;
 #pragma unroll
-  for (int i = 0; i < L; ++i) store_out(out, b * out_bs + i, v[i] * scale, out_real);
+  for (int i = 0; i < L; ++i) store_out(out, b * out_bs + i, scaled(v[i], scale), out_real);
 }
 
 // ------------------------------------------------------------------ 4 <= m <= 12: one LDS pass
 template <int P, typename T, bool ADJ>
 __global__ __launch_bounds__(kWG) void k_single(const void* in, int64_t in_bs, int in_real, void* out,
                                                  int64_t out_bs, int out_real, int64_t batch, int stable,
-                                                 double scale, const double2* __restrict__ tw) {
+                                                 double scale, const double2* __restrict__ tw, Pre pre) {
   constexpr int L = 1 << P;
   constexpr int TL = L / 16;
   constexpr int TPW = kTile / L;
@@ -78,7 +93,7 @@ __global__ __launch_bounds__(kWG) void k_single(const void* in, int64_t in_bs, i
     const int e = tid + k * kWG;
     const int64_t b = b0 + (e >> P);
     T v = zero_v<T>();
-    if (b < batch) v = load_in<T>(in, b * in_bs + (e & (L - 1)), in_real);
+    if (b < batch) v = pre_mul(load_in<T>(in, b * in_bs + (e & (L - 1)), in_real), pre, b, e & (L - 1));
     lds[padi(e)] = v;
   }
   __syncthreads();
@@ -89,7 +104,7 @@ __global__ __launch_bounds__(kWG) void k_single(const void* in, int64_t in_bs, i
   for (int k = 0; k < 16; ++k) {
     const int e = tid + k * kWG;
     const int64_t b = b0 + (e >> P);
-    if (b < batch) store_out(out, b * out_bs + (e & (L - 1)), lds[padi(e)] * scale, out_real);
+    if (b < batch) store_out(out, b * out_bs + (e & (L - 1)), scaled(lds[padi(e)], scale), out_real);
   }
 }
 
@@ -106,7 +121,7 @@ __global__ __launch_bounds__(kWG) void k_rows(const void* in, int64_t in_bs, int
   constexpr int N2 = 1 << P2;
   constexpr int TL = N2 / 16;
   constexpr int RPW = kTile / N2;
-  constexpr bool FFT = sizeof(T) == 16;
+  constexpr bool FFT = Elem<T>::cx;
   __shared__ T lds[kTile + kTile / 16];
   __shared__ T red[kWG / 64];
   const int m1 = m - P2;
@@ -137,7 +152,7 @@ __global__ __launch_bounds__(kWG) void k_rows(const void* in, int64_t in_bs, int
       const int e = tid + k * kWG;
       T r = lds[padi(e)];
       if (!ADJ && FFT && twiddle) r = tw_mul<T>(r, rt.at(k, P2, m1, tw, twm), false);
-      store_out(out, obase + e, r * scale, out_real);
+      store_out(out, obase + e, scaled(r, scale), out_real);
     }
     return;
   }
@@ -162,7 +177,7 @@ __global__ __launch_bounds__(kWG) void k_rows(const void* in, int64_t in_bs, int
       const unsigned ex = brev_bits((unsigned)(row0 + (e >> P2)), m1) * (unsigned)(e & (N2 - 1));   // < 2^m
       v = tw_mul<T>(v, inter_tw(ex, P2, m1, tw, twm), false);
     }
-    store_out(out, obase + e, v * scale, out_real);
+    store_out(out, obase + e, scaled(v, scale), out_real);
   }
 }
 
@@ -186,7 +201,7 @@ template <int P1, typename T, bool ADJ>
 __global__ __launch_bounds__(kWG) void k_cols(const void* in, int64_t in_bs, int in_real, void* out,
                                                int64_t out_bs, int out_real, int m, int stable, double scale,
                                                int twiddle, const double2* __restrict__ tw,
-                                               const double2* __restrict__ twm) {
+                                               const double2* __restrict__ twm, Pre pre) {
   using Lay = ColLayout<P1>;
   constexpr int N1 = Lay::N1, C = Lay::C, CS = Lay::CS, TL = N1 / 16;
   __shared__ T lds[kLds];
@@ -206,7 +221,7 @@ __global__ __launch_bounds__(kWG) void k_cols(const void* in, int64_t in_bs, int
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     const int e = tid + k * kWG;
-    v[k] = load_in<T>(in, ibase + (int64_t)(e / C) * N2 + cl, in_real);
+    v[k] = pre_mul(load_in<T>(in, ibase + (int64_t)(e / C) * N2 + cl, in_real), pre, b, (int64_t)(e / C) * N2 + c0 + cl);
     sum += v[k];
   }
   T mean_l = zero_v<T>(), mean_t = zero_v<T>();
@@ -225,21 +240,21 @@ __global__ __launch_bounds__(kWG) void k_cols(const void* in, int64_t in_bs, int
   for (int k = 0; k < 16; ++k) {
     const int e = tid + k * kWG;
     const int r = e / C;
-    store_out(out, obase + (int64_t)r * N2 + cl, lds[cl * CS + padi(r)] * scale, out_real);
+    store_out(out, obase + (int64_t)r * N2 + cl, scaled(lds[cl * CS + padi(r)], scale), out_real);
   }
 }
 
 // ------------------------------------------------------------------ launch helpers
 template <typename T, bool ADJ>
 static int launch_tiny(int m, const void* in, int64_t in_bs, int in_real, void* out, int out_real, int64_t batch,
-                       int stable, double scale, const double2* tw, hipStream_t st) {
+                       int stable, double scale, const double2* tw, hipStream_t st, Pre pre = Pre{nullptr, 0}) {
   const dim3 g((unsigned)((batch + kWG - 1) / kWG));
   const int64_t n = (int64_t)1 << m;
   switch (m) {
-    case 0: k_tiny<0, T, ADJ><<<g, kWG, 0, st>>>(in, in_bs, in_real, out, n, out_real, batch, stable, scale, tw); break;
-    case 1: k_tiny<1, T, ADJ><<<g, kWG, 0, st>>>(in, in_bs, in_real, out, n, out_real, batch, stable, scale, tw); break;
-    case 2: k_tiny<2, T, ADJ><<<g, kWG, 0, st>>>(in, in_bs, in_real, out, n, out_real, batch, stable, scale, tw); break;
-    case 3: k_tiny<3, T, ADJ><<<g, kWG, 0, st>>>(in, in_bs, in_real, out, n, out_real, batch, stable, scale, tw); break;
+    case 0: k_tiny<0, T, ADJ><<<g, kWG, 0, st>>>(in, in_bs, in_real, out, n, out_real, batch, stable, scale, tw, pre); break;
+    case 1: k_tiny<1, T, ADJ><<<g, kWG, 0, st>>>(in, in_bs, in_real, out, n, out_real, batch, stable, scale, tw, pre); break;
+    case 2: k_tiny<2, T, ADJ><<<g, kWG, 0, st>>>(in, in_bs, in_real, out, n, out_real, batch, stable, scale, tw, pre); break;
+    case 3: k_tiny<3, T, ADJ><<<g, kWG, 0, st>>>(in, in_bs, in_real, out, n, out_real, batch, stable, scale, tw, pre); break;
     default: return set_error(kErrInvalid, "launch_tiny: bad m");
   }
   return check_launch("k_tiny");
@@ -248,12 +263,13 @@ static int launch_tiny(int m, const void* in, int64_t in_bs, int in_real, void* 
 #define FGP_SINGLE_CASE(P)                                                                                   \
   case P:                                                                                                    \
     k_single<P, T, ADJ><<<dim3((unsigned)((batch + (kTile >> P) - 1) / (kTile >> P))), kWG, 0, st>>>(      \
-        in, in_bs, in_real, out, (int64_t)1 << P, out_real, batch, stable, scale, tw);                       \
+        in, in_bs, in_real, out, (int64_t)1 << P, out_real, batch, stable, scale, tw, pre);                  \
     break;
 
 template <typename T, bool ADJ>
 static int launch_single(int m, const void* in, int64_t in_bs, int in_real, void* out, int out_real,
-                         int64_t batch, int stable, double scale, const double2* tw, hipStream_t st) {
+                         int64_t batch, int stable, double scale, const double2* tw, hipStream_t st,
+                         Pre pre = Pre{nullptr, 0}) {
   switch (m) {
     FGP_SINGLE_CASE(4) FGP_SINGLE_CASE(5) FGP_SINGLE_CASE(6) FGP_SINGLE_CASE(7) FGP_SINGLE_CASE(8)
     FGP_SINGLE_CASE(9) FGP_SINGLE_CASE(10) FGP_SINGLE_CASE(11) FGP_SINGLE_CASE(12)
@@ -287,12 +303,13 @@ static int launch_rows(int m, const void* in, int64_t in_bs, int in_real, void* 
 #define FGP_COLS_CASE(P)                                                                                       \
   case P:                                                                                                      \
     k_cols<P, T, ADJ><<<g, kWG, 0, st>>>(in, in_bs, in_real, out, out_bs, out_real, m, stable, scale, twiddle, \
-                                         tw, twm);                                                             \
+                                         tw, twm, pre);                                                        \
     break;
 
 template <typename T, bool ADJ>
 static int launch_cols(int m, const void* in, int64_t in_bs, int in_real, void* out, int64_t out_bs, int out_real,
-                       int64_t batch, int stable, double scale, int twiddle, const Tables* tb, hipStream_t st) {
+                       int64_t batch, int stable, double scale, int twiddle, const Tables* tb, hipStream_t st,
+                       Pre pre = Pre{nullptr, 0}) {
   const int m1 = m - split_m2(m);
   const dim3 g((unsigned)(batch << (m - kTileLog)));
   const double2* tw = tb->tw4096;
@@ -323,6 +340,84 @@ int cols_adjoint_launch(bool fft, int m, const void* in, void* out, int64_t batc
   return launch_cols<double, false>(m, in, n, 0, out, n, 0, batch, 1, 1.0, 0, tb, st);
 }
 
+// Y[g, k] = sum_{r < R} |x[r G + g, k]|^2 in fp64 (fastgaussianprocesses_amd.fast_gp._ysq: the data
+// term of the MLL, Y = sum over the outputs sharing problem g of |y~|^2, util.py:364-370).  Thread per
+// (g, k): loads coalesced along k, rows summed in fixed ascending order (deterministic).
+template <typename T>
+__global__ __launch_bounds__(kWG) void k_sum_sq(const T* __restrict__ x, int64_t xs, int64_t R, int64_t G, int64_t n,
+                                                 double* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * kWG + threadIdx.x;
+  if (e >= G * n) return;
+  const int64_t g = e / n, k = e % n;
+  const T* p = x + g * xs + k;
+  double acc = 0.0;
+#pragma unroll 8
+  for (int64_t r = 0; r < R; ++r) {
+    const T v = p[r * G * xs];
+    if constexpr (Elem<T>::cx) acc += (double)v.x * (double)v.x + (double)v.y * (double)v.y;
+    else acc += (double)v * (double)v;
+  }
+  out[e] = acc;
+}
+
+// Entry-point bodies for the fp64 (T = double2 / double) and fp32 (T = float2 / float) variants.
+template <typename T>
+static int fftbr_impl(const void* in, int64_t in_bs, int in_real, void* out, int64_t batch, int log2n, int stable,
+                      hipStream_t st) {
+  int rc = validate(in, out, batch, log2n, in_bs);
+  if (rc != kOk || batch == 0) return rc;
+  const Tables* tb = get_tables(st);
+  if (!tb) return set_error(kErrHip, "twiddle table initialisation failed");
+  const int64_t n = (int64_t)1 << log2n;
+  const double scale = 1.0 / sqrt((double)n);
+  if (log2n <= 3) return launch_tiny<T, false>(log2n, in, in_bs, in_real, out, 0, batch, stable, scale, tb->tw4096, st);
+  if (log2n <= 12) return launch_single<T, false>(log2n, in, in_bs, in_real, out, 0, batch, stable, scale, tb->tw4096, st);
+  rc = launch_rows<T, false>(log2n, in, in_bs, in_real, out, n, 0, batch, stable, 1.0, 1, tb, st);
+  if (rc != kOk) return rc;
+  return launch_cols<T, false>(log2n, out, n, 0, out, n, 0, batch, stable, scale, 0, tb, st);
+}
+
+template <typename T>
+static int ifftbr_impl(const void* in, int64_t in_bs, void* out, int out_real, void* work, int64_t batch, int log2n,
+                       int stable, hipStream_t st, Pre pre = Pre{nullptr, 0}) {
+  int rc = validate(in, out, batch, log2n, in_bs);
+  if (rc != kOk || batch == 0) return rc;
+  const Tables* tb = get_tables(st);
+  if (!tb) return set_error(kErrHip, "twiddle table initialisation failed");
+  const int64_t n = (int64_t)1 << log2n;
+  const double scale = 1.0 / sqrt((double)n);
+  if (log2n <= 3) return launch_tiny<T, true>(log2n, in, in_bs, 0, out, out_real, batch, stable, scale, tb->tw4096, st, pre);
+  if (log2n <= 12)
+    return launch_single<T, true>(log2n, in, in_bs, 0, out, out_real, batch, stable, scale, tb->tw4096, st, pre);
+  void* mid = out_real ? work : out;
+  if (mid == nullptr) return set_error(kErrInvalid, "ifftbr: out_real with n > 4096 needs a complex work buffer");
+  rc = launch_cols<T, true>(log2n, in, in_bs, 0, mid, n, 0, batch, stable, 1.0, 0, tb, st, pre);
+  if (rc != kOk) return rc;
+  return launch_rows<T, true>(log2n, mid, n, 0, out, n, out_real, batch, stable, scale, 1, tb, st);
+}
+
+template <typename T>
+static int fwht_impl(const void* in, int64_t in_bs, void* out, int64_t batch, int log2n, int stable, hipStream_t st,
+                     Pre pre = Pre{nullptr, 0}) {
+  int rc = validate(in, out, batch, log2n, in_bs);
+  if (rc != kOk || batch == 0) return rc;
+  const Tables* tb = get_tables(st);
+  if (!tb) return set_error(kErrHip, "twiddle table initialisation failed");
+  const int64_t n = (int64_t)1 << log2n;
+  const double scale = 1.0 / sqrt((double)n);
+  if (log2n <= 3) return launch_tiny<T, false>(log2n, in, in_bs, 0, out, 0, batch, stable, scale, tb->tw4096, st, pre);
+  if (log2n <= 12)
+    return launch_single<T, false>(log2n, in, in_bs, 0, out, 0, batch, stable, scale, tb->tw4096, st, pre);
+  if (pre.f) {   // the WHT is separable in any order: columns first (they take the factor), then rows
+    rc = launch_cols<T, false>(log2n, in, in_bs, 0, out, n, 0, batch, stable, 1.0, 0, tb, st, pre);
+    if (rc != kOk) return rc;
+    return launch_rows<T, false>(log2n, out, n, 0, out, n, 0, batch, stable, scale, 0, tb, st);
+  }
+  rc = launch_rows<T, false>(log2n, in, in_bs, 0, out, n, 0, batch, stable, 1.0, 0, tb, st);
+  if (rc != kOk) return rc;
+  return launch_cols<T, false>(log2n, out, n, 0, out, n, 0, batch, stable, scale, 0, tb, st);
+}
+
 }  // namespace fgp
 
 using namespace fgp;
@@ -331,52 +426,62 @@ extern "C" {
 
 int fgp_fftbr(const void* in, int64_t in_batch_stride, int in_is_real, void* out, int64_t batch, int log2n,
               int stable, void* stream) {
-  int rc = validate(in, out, batch, log2n, in_batch_stride);
-  if (rc != kOk || batch == 0) return rc;
-  hipStream_t st = (hipStream_t)stream;
-  const Tables* tb = get_tables(st);
-  if (!tb) return set_error(kErrHip, "twiddle table initialisation failed");
-  const int64_t n = (int64_t)1 << log2n;
-  const double scale = 1.0 / sqrt((double)n);
-  if (log2n <= 3) return launch_tiny<double2, false>(log2n, in, in_batch_stride, in_is_real, out, 0, batch, stable, scale, tb->tw4096, st);
-  if (log2n <= 12) return launch_single<double2, false>(log2n, in, in_batch_stride, in_is_real, out, 0, batch, stable, scale, tb->tw4096, st);
-  rc = launch_rows<double2, false>(log2n, in, in_batch_stride, in_is_real, out, n, 0, batch, stable, 1.0, 1, tb, st);
-  if (rc != kOk) return rc;
-  return launch_cols<double2, false>(log2n, out, n, 0, out, n, 0, batch, stable, scale, 0, tb, st);
+  return fftbr_impl<double2>(in, in_batch_stride, in_is_real, out, batch, log2n, stable, (hipStream_t)stream);
 }
 
 int fgp_ifftbr(const void* in, int64_t in_batch_stride, void* out, int out_real, void* work, int64_t batch,
                int log2n, int stable, void* stream) {
-  int rc = validate(in, out, batch, log2n, in_batch_stride);
-  if (rc != kOk || batch == 0) return rc;
-  hipStream_t st = (hipStream_t)stream;
-  const Tables* tb = get_tables(st);
-  if (!tb) return set_error(kErrHip, "twiddle table initialisation failed");
-  const int64_t n = (int64_t)1 << log2n;
-  const double scale = 1.0 / sqrt((double)n);
-  if (log2n <= 3) return launch_tiny<double2, true>(log2n, in, in_batch_stride, 0, out, out_real, batch, stable, scale, tb->tw4096, st);
-  if (log2n <= 12) return launch_single<double2, true>(log2n, in, in_batch_stride, 0, out, out_real, batch, stable, scale, tb->tw4096, st);
-  void* mid = out_real ? work : out;
-  if (mid == nullptr) return set_error(kErrInvalid, "fgp_ifftbr: out_real with n > 4096 needs a complex work buffer");
-  rc = launch_cols<double2, true>(log2n, in, in_batch_stride, 0, mid, n, 0, batch, stable, 1.0, 0, tb, st);
-  if (rc != kOk) return rc;
-  return launch_rows<double2, true>(log2n, mid, n, 0, out, n, out_real, batch, stable, scale, 1, tb, st);
+  return ifftbr_impl<double2>(in, in_batch_stride, out, out_real, work, batch, log2n, stable, (hipStream_t)stream);
 }
 
 int fgp_fwht(const double* in, int64_t in_batch_stride, double* out, int64_t batch, int log2n, int stable,
              void* stream) {
-  int rc = validate(in, out, batch, log2n, in_batch_stride);
-  if (rc != kOk || batch == 0) return rc;
+  return fwht_impl<double>(in, in_batch_stride, out, batch, log2n, stable, (hipStream_t)stream);
+}
+
+int fgp_fftbr_c64(const void* in, int64_t in_batch_stride, int in_is_real, void* out, int64_t batch, int log2n,
+                  int stable, void* stream) {
+  return fftbr_impl<float2>(in, in_batch_stride, in_is_real, out, batch, log2n, stable, (hipStream_t)stream);
+}
+
+int fgp_ifftbr_c64(const void* in, int64_t in_batch_stride, void* out, int out_real, void* work, int64_t batch,
+                   int log2n, int stable, void* stream) {
+  return ifftbr_impl<float2>(in, in_batch_stride, out, out_real, work, batch, log2n, stable, (hipStream_t)stream);
+}
+
+int fgp_fwht_f32(const float* in, int64_t in_batch_stride, float* out, int64_t batch, int log2n, int stable,
+                 void* stream) {
+  return fwht_impl<float>(in, in_batch_stride, out, batch, log2n, stable, (hipStream_t)stream);
+}
+
+int fgp_sum_sq(const void* x, int64_t x_row_stride, int kind, int64_t R, int64_t G, int64_t n, double* out,
+               void* stream) {
+  if (R < 1 || G < 1 || n < 1 || x_row_stride < n) return set_error(kErrInvalid, "fgp_sum_sq: bad sizes");
+  if (!x || !out) return set_error(kErrInvalid, "fgp_sum_sq: null pointer");
+  const unsigned grid = (unsigned)((G * n + kWG - 1) / kWG);
   hipStream_t st = (hipStream_t)stream;
-  const Tables* tb = get_tables(st);
-  if (!tb) return set_error(kErrHip, "twiddle table initialisation failed");
-  const int64_t n = (int64_t)1 << log2n;
-  const double scale = 1.0 / sqrt((double)n);
-  if (log2n <= 3) return launch_tiny<double, false>(log2n, in, in_batch_stride, 0, out, 0, batch, stable, scale, tb->tw4096, st);
-  if (log2n <= 12) return launch_single<double, false>(log2n, in, in_batch_stride, 0, out, 0, batch, stable, scale, tb->tw4096, st);
-  rc = launch_rows<double, false>(log2n, in, in_batch_stride, 0, out, n, 0, batch, stable, 1.0, 0, tb, st);
-  if (rc != kOk) return rc;
-  return launch_cols<double, false>(log2n, out, n, 0, out, n, 0, batch, stable, scale, 0, tb, st);
+  switch (kind) {
+    case 0: k_sum_sq<double><<<grid, kWG, 0, st>>>(static_cast<const double*>(x), x_row_stride, R, G, n, out); break;
+    case 1: k_sum_sq<double2><<<grid, kWG, 0, st>>>(static_cast<const double2*>(x), x_row_stride, R, G, n, out); break;
+    case 2: k_sum_sq<float><<<grid, kWG, 0, st>>>(static_cast<const float*>(x), x_row_stride, R, G, n, out); break;
+    case 3: k_sum_sq<float2><<<grid, kWG, 0, st>>>(static_cast<const float2*>(x), x_row_stride, R, G, n, out); break;
+    default: return set_error(kErrInvalid, "fgp_sum_sq: bad kind %d", kind);
+  }
+  return check_launch("k_sum_sq");
+}
+
+/* Inverse transform of in * f (fgp_hip.h fgp_ifftbr_mul): lattice complex128 / complex64 via ifftbr,
+ * net float64 / float32 via the (self-inverse) fwht. */
+int fgp_ifftbr_mul(int family, int single, const void* in, int64_t in_batch_stride, const void* f, int64_t f_batch_stride,
+                   void* out, int out_real, void* work, int64_t batch, int log2n, int stable, void* stream) {
+  if (!f) return set_error(kErrInvalid, "fgp_ifftbr_mul: null factor");
+  const Pre pre{f, f_batch_stride};
+  hipStream_t st = (hipStream_t)stream;
+  if (family == FGP_FAMILY_LATTICE)
+    return single ? ifftbr_impl<float2>(in, in_batch_stride, out, out_real, work, batch, log2n, stable, st, pre)
+                  : ifftbr_impl<double2>(in, in_batch_stride, out, out_real, work, batch, log2n, stable, st, pre);
+  return single ? fwht_impl<float>(in, in_batch_stride, out, batch, log2n, stable, st, pre)
+                : fwht_impl<double>(in, in_batch_stride, out, batch, log2n, stable, st, pre);
 }
 
 }  // extern "C"

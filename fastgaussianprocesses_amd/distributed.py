@@ -28,7 +28,13 @@ def allreduce_sum_(t, group=None):
     """In-place SUM all-reduce over the process group (identity without an initialised group)."""
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        if t.is_cuda and dist.get_backend(group) == "gloo":
+            # gloo reduces host memory: stage the device tensor (RCCL / "nccl" reduces it in place)
+            h = t.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
     return t
 
 

@@ -82,7 +82,8 @@ class AbstractFastGP(torch.nn.Module):
                  tfs_factor_task_kernel, tfs_noise_task_kernel, requires_grad_scale, requires_grad_lengthscales,
                  requires_grad_noise, requires_grad_factor_task_kernel, requires_grad_noise_task_kernel, shape_batch,
                  shape_scale, shape_lengthscales, shape_noise, shape_factor_task_kernel, shape_noise_task_kernel,
-                 derivatives, derivatives_coeffs, compile_fts, compile_fts_kwargs, adaptive_nugget):
+                 derivatives, derivatives_coeffs, compile_fts, compile_fts_kwargs, adaptive_nugget,
+                 data_dtype=torch.float64):
         super().__init__()
         assert torch.get_default_dtype() == torch.float64, \
             "fast transforms do not work without torch.float64 precision"
@@ -96,6 +97,13 @@ class AbstractFastGP(torch.nn.Module):
         if derivatives is not None or derivatives_coeffs is not None:
             raise NotImplementedError("derivative-informed kernels are not built yet (SURVEY §8f)")
         self.num_tasks = 1
+        # Extension (not in the reference, which is fp64-only, abstract_gp.py:46): data_dtype=float32
+        # stores the observations in fp32 and forms the MLL's data term from a complex64 ytilde
+        # (fgp_fftbr_c64, Y = sum |ytilde|^2 accumulated in fp64) -- the mixed-precision path of
+        # BASELINE config C5.  Eigenvalues, the MLL / gradient / Rprop loop, the coefficients
+        # (fp64 transform of the fp32 observations), post_mean and post_var stay fp64.
+        assert data_dtype in (torch.float64, torch.float32), "data_dtype must be torch.float64 or torch.float32"
+        self.data_dtype = data_dtype
         self.device = torch.device(device)
         if self.device.type != "cuda":
             raise RuntimeError("fastgaussianprocesses_amd runs on a HIP device (device='cuda'); got %s" % device)
@@ -310,8 +318,8 @@ class AbstractFastGP(torch.nn.Module):
             y_next = [y_next]
         assert isinstance(y_next, list) and len(y_next) == 1
         assert all(y.shape[:-1] == self.shape_batch for y in y_next)
-        y = y_next[0].to(device=self.device, dtype=torch.float64)
-        self._y[0] = torch.cat([self._y[0], y], -1)
+        y = y_next[0].to(device=self.device, dtype=self.data_dtype)
+        self._y[0] = torch.cat([self._y[0].to(self.data_dtype), y], -1)
         self._nh = int(self._y[0].size(-1))
         self.n = torch.tensor([self._nh], dtype=torch.int64, device=self.device)
         self.m = torch.tensor([self._nh.bit_length() - 1 if self._nh > 0 else -1], dtype=torch.int64, device=self.device)
@@ -425,11 +433,16 @@ class AbstractFastGP(torch.nn.Module):
         n = self._nh
         if self._gradmode() or n < 2:
             return self._solve(self._y[0], n)
-        # graph-free: reuse the cached ytilde = ft(y); real part fused into the inverse transform
-        yt = self.get_ytilde(0) * self._inv(n)
-        if self._FAMILY == ops.LATTICE:
-            return ops.ifftbr_raw(yt, stable=True, real_out=True)
-        return ops.fwht_raw(yt, stable=True)
+        # graph-free: reuse the cached ytilde = ft(y); A * ytilde fused into the inverse transform's
+        # first pass and its real part into the last (fgp_ifftbr_mul).  data_dtype=float32: the
+        # coefficients still come from an fp64 transform of the (fp32) observations -- cond(K) ~ n /
+        # noise makes fp32 coefficients useless for the posterior mean (measured O(1) relative error,
+        # tools/diag_mixed.py), so only the MLL's Y uses the complex64 ytilde.
+        yt = self.get_ytilde(0)
+        if self.data_dtype != torch.float64:
+            y = self._y[0].to(torch.float64)
+            yt = ops.fftbr_raw(y, stable=True) if self._FAMILY == ops.LATTICE else ops.fwht_raw(y, stable=True)
+        return ops.inverse_mul(self._FAMILY, yt, self._inv(n), real_out=True)
 
     @property
     def coeffs(self):
@@ -497,9 +510,9 @@ class AbstractFastGP(torch.nn.Module):
         return big, G
 
     def _ysq(self, pb_shape, G):
+        """Y[g] = sum over the outputs of problem g of |ytilde|^2 (fgp_sum_sq, one pass over ytilde)."""
         yt = self.get_ytilde(0)
-        ysq = (yt.real ** 2 + yt.imag ** 2) if yt.is_complex() else yt ** 2
-        return ysq.reshape((-1, G, ysq.shape[-1])).sum(0)
+        return ops.sum_sq(yt.reshape(-1, yt.shape[-1]), G)
 
     def _log_header(self, verbose, indent):
         if verbose:
@@ -964,7 +977,7 @@ class FastGPLattice(AbstractFastGP):
                  requires_grad_noise_task_kernel=None, shape_batch=torch.Size([]), shape_scale=torch.Size([1]),
                  shape_lengthscales=None, shape_noise=torch.Size([1]), shape_factor_task_kernel=None,
                  shape_noise_task_kernel=None, derivatives=None, derivatives_coeffs=None, compile_fts=False,
-                 compile_fts_kwargs={}, adaptive_nugget=False):
+                 compile_fts_kwargs={}, adaptive_nugget=False, data_dtype=torch.float64):
         assert isinstance(alpha, int) and alpha in (1, 2, 3, 4), "alpha must be in [1, 2, 3, 4]"
         super().__init__(seqs, num_tasks, seed_for_seq, alpha, scale, lengthscales, noise, factor_task_kernel,
                          rank_factor_task_kernel, noise_task_kernel, device, tfs_scale, tfs_lengthscales, tfs_noise,
@@ -972,7 +985,7 @@ class FastGPLattice(AbstractFastGP):
                          requires_grad_lengthscales, requires_grad_noise, requires_grad_factor_task_kernel,
                          requires_grad_noise_task_kernel, shape_batch, shape_scale, shape_lengthscales, shape_noise,
                          shape_factor_task_kernel, shape_noise_task_kernel, derivatives, derivatives_coeffs,
-                         compile_fts, compile_fts_kwargs, adaptive_nugget)
+                         compile_fts, compile_fts_kwargs, adaptive_nugget, data_dtype=data_dtype)
 
     def _default_seq(self, d, seed):
         return _seqs.Lattice(d, seed=seed, randomize="SHIFT")
@@ -1056,14 +1069,14 @@ class FastGPDigitalNetB2(AbstractFastGP):
                  requires_grad_noise_task_kernel=None, shape_batch=torch.Size([]), shape_scale=torch.Size([1]),
                  shape_lengthscales=None, shape_noise=torch.Size([1]), shape_factor_task_kernel=None,
                  shape_noise_task_kernel=None, derivatives=None, derivatives_coeffs=None, compile_fts=False,
-                 compile_fts_kwargs={}, adaptive_nugget=False):
+                 compile_fts_kwargs={}, adaptive_nugget=False, data_dtype=torch.float64):
         super().__init__(seqs, num_tasks, seed_for_seq, alpha, scale, lengthscales, noise, factor_task_kernel,
                          rank_factor_task_kernel, noise_task_kernel, device, tfs_scale, tfs_lengthscales, tfs_noise,
                          tfs_factor_task_kernel, tfs_noise_task_kernel, requires_grad_scale,
                          requires_grad_lengthscales, requires_grad_noise, requires_grad_factor_task_kernel,
                          requires_grad_noise_task_kernel, shape_batch, shape_scale, shape_lengthscales, shape_noise,
                          shape_factor_task_kernel, shape_noise_task_kernel, derivatives, derivatives_coeffs,
-                         compile_fts, compile_fts_kwargs, adaptive_nugget)
+                         compile_fts, compile_fts_kwargs, adaptive_nugget, data_dtype=data_dtype)
         assert (1 <= self.alpha).all() and (self.alpha <= 4).all()
         self.t = int(self.seq.t)
         assert self.t < 64, "each seq must have t<64"

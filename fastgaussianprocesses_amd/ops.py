@@ -49,50 +49,118 @@ def _stream(t):
 
 
 # ------------------------------------------------------------------------------------- transforms
+def _single(x):
+    """float32 / complex64 input selects the single-precision kernels (fgp_*_c64 / fgp_fwht_f32)."""
+    return x.dtype in (torch.float32, torch.complex64)
+
+
 def fftbr_raw(x, stable=True):
+    """fftbr (+ AbstractFastGP.ft's centring when stable) along the last dim: complex128 out for
+    float64 / complex128 input (fgp_fftbr), complex64 out for float32 / complex64 input (fgp_fftbr_c64)."""
     require_device(x, "fftbr")
-    if x.is_complex():
-        x = x.to(torch.complex128)
-    else:
-        x = x.to(torch.float64)
+    sp = _single(x)
+    rdt, cdt = (torch.float32, torch.complex64) if sp else (torch.float64, torch.complex128)
+    x = x.to(cdt) if x.is_complex() else x.to(rdt)
     shape = x.shape
     n = shape[-1]
     m = log2_exact(n)
     rows, bs = _as_rows(x)
-    out = torch.empty(rows.shape, dtype=torch.complex128, device=x.device)
-    N.call("fgp_fftbr", N.ptr(rows), bs, 0 if x.is_complex() else 1, N.ptr(out), rows.size(0), m, int(stable),
-           _stream(x))
+    out = torch.empty(rows.shape, dtype=cdt, device=x.device)
+    N.call("fgp_fftbr_c64" if sp else "fgp_fftbr", N.ptr(rows), bs, 0 if x.is_complex() else 1, N.ptr(out),
+           rows.size(0), m, int(stable), _stream(x))
     return out.reshape(shape)
 
 
 def ifftbr_raw(x, stable=True, real_out=False):
+    """ifftbr along the last dim (fgp_ifftbr / fgp_ifftbr_c64 for complex64 input); real_out keeps
+    only the real part (gram_matrix_solve's .real, util.py:343)."""
     require_device(x, "ifftbr")
-    x = x.to(torch.complex128)
+    sp = _single(x)
+    rdt, cdt = (torch.float32, torch.complex64) if sp else (torch.float64, torch.complex128)
+    x = x.to(cdt)
     shape = x.shape
     n = shape[-1]
     m = log2_exact(n)
     rows, bs = _as_rows(x)
     if real_out:
-        out = torch.empty(rows.shape, dtype=torch.float64, device=x.device)
-        work = torch.empty(rows.shape, dtype=torch.complex128, device=x.device) if m > 12 else None
+        out = torch.empty(rows.shape, dtype=rdt, device=x.device)
+        work = torch.empty(rows.shape, dtype=cdt, device=x.device) if m > 12 else None
     else:
-        out = torch.empty(rows.shape, dtype=torch.complex128, device=x.device)
+        out = torch.empty(rows.shape, dtype=cdt, device=x.device)
         work = None
-    N.call("fgp_ifftbr", N.ptr(rows), bs, N.ptr(out), int(real_out), N.ptr(work), rows.size(0), m, int(stable),
-           _stream(x))
+    N.call("fgp_ifftbr_c64" if sp else "fgp_ifftbr", N.ptr(rows), bs, N.ptr(out), int(real_out), N.ptr(work),
+           rows.size(0), m, int(stable), _stream(x))
     return out.reshape(shape)
 
 
 def fwht_raw(x, stable=True):
+    """Orthonormal Sylvester FWHT along the last dim (fgp_fwht, or fgp_fwht_f32 for float32 input)."""
     require_device(x, "fwht")
     if x.is_complex():
         return torch.complex(fwht_raw(x.real, stable), fwht_raw(x.imag, stable))
-    x = x.to(torch.float64)
+    sp = _single(x)
+    rdt = torch.float32 if sp else torch.float64
+    x = x.to(rdt)
     shape = x.shape
     m = log2_exact(shape[-1])
     rows, bs = _as_rows(x)
-    out = torch.empty(rows.shape, dtype=torch.float64, device=x.device)
-    N.call("fgp_fwht", N.ptr(rows), bs, N.ptr(out), rows.size(0), m, int(stable), _stream(x))
+    out = torch.empty(rows.shape, dtype=rdt, device=x.device)
+    N.call("fgp_fwht_f32" if sp else "fgp_fwht", N.ptr(rows), bs, N.ptr(out), rows.size(0), m, int(stable),
+           _stream(x))
+    return out.reshape(shape)
+
+
+def sum_sq(x, G=1):
+    """Y[g, k] = sum_r |x[r G + g, k]|^2 (fp64) over rows x [R G, n] (float64 / complex128 / float32 /
+    complex64) -> [G, n] (fgp_sum_sq: the MLL data term of outputs sharing eigen-problem g)."""
+    require_device(x, "sum_sq")
+    n = x.shape[-1]
+    rows, bs = _as_rows(x)
+    assert rows.size(0) % G == 0
+    kind = {torch.float64: 0, torch.complex128: 1, torch.float32: 2, torch.complex64: 3}[rows.dtype]
+    out = torch.empty((G, n), dtype=torch.float64, device=x.device)
+    N.call("fgp_sum_sq", N.ptr(rows), bs, kind, rows.size(0) // G, G, n, N.ptr(out), _stream(x))
+    return out
+
+
+def inverse_mul(family, x, f, real_out=False, stable=True):
+    """inverse(x * f) along the last dim in one call (fgp_ifftbr_mul): ifftbr for lattices (real_out:
+    the real part, gram_matrix_solve's .real, util.py:341-343), fwht for nets.  f [*, n] broadcasts
+    against x [*, n] when it is one row, or matches x's rows; else the product is formed first."""
+    require_device(x, "inverse_mul")
+    sp = _single(x)
+    n = x.shape[-1]
+    m = log2_exact(n)
+    if family == LATTICE:
+        cdt = torch.complex64 if sp else torch.complex128
+        x = x.to(cdt)
+        f = f.to(cdt)
+    else:
+        rdt = torch.float32 if sp else torch.float64
+        if x.is_complex() or f.is_complex():
+            return fwht_raw(x * f, stable)
+        x = x.to(rdt)
+        f = f.to(rdt)
+    rows, bs = _as_rows(x)
+    f2 = f.reshape(-1, n)
+    if f2.size(0) == 1:
+        fbs = 0
+    elif tuple(f.shape) == tuple(x.shape):
+        fbs = n
+    else:
+        prod = x * f
+        return ifftbr_raw(prod, stable, real_out) if family == LATTICE else fwht_raw(prod, stable)
+    f2 = f2.contiguous()
+    if family == LATTICE:
+        odt = (torch.float32 if sp else torch.float64) if real_out else rows.dtype
+        out = torch.empty(rows.shape, dtype=odt, device=x.device)
+        work = torch.empty(rows.shape, dtype=rows.dtype, device=x.device) if (real_out and m > 12) else None
+    else:
+        out = torch.empty(rows.shape, dtype=rows.dtype, device=x.device)
+        work = None
+    N.call("fgp_ifftbr_mul", int(family), int(sp), N.ptr(rows), bs, N.ptr(f2), fbs, N.ptr(out),
+           int(bool(real_out) and family == LATTICE), N.ptr(work), rows.size(0), m, int(stable), _stream(x))
+    shape = x.shape if not (real_out and family == LATTICE) else x.shape
     return out.reshape(shape)
 
 
@@ -231,10 +299,12 @@ def post_mean_matfree(family, xt, z_dn, hyp, coeffs, alphas=None, tbits=0, chunk
     n = z_dn.shape[1]
     hyp = hyp.to(torch.float64).contiguous()
     Gk = hyp.shape[0]
+    B = coeffs.shape[0]
+    if Gk == 1 and B >= GEMM_MIN_OUTPUTS:
+        return post_mean_gemm(family, xt, z_dn, hyp, coeffs, alphas=alphas, tbits=tbits)
     coeffs = coeffs.to(torch.float64)
     if coeffs.stride(-1) != 1:
         coeffs = coeffs.contiguous()
-    B = coeffs.shape[0]
     out = torch.empty((B, Nt), dtype=torch.float64, device=xt.device)
     order, coef = _pred_args(family, alphas, d)
     nchunks = (n + chunk - 1) // chunk
@@ -246,6 +316,35 @@ def post_mean_matfree(family, xt, z_dn, hyp, coeffs, alphas=None, tbits=0, chunk
         N.call("fgp_post_mean", family, N.ptr(xt), Nt, N.ptr(z_dn), n, d, int(tbits), order, coef, N.ptr(hyp_b),
                hyp_b.shape[0], N.ptr(cb), cb.stride(0) if cb.shape[0] > 1 else n, b1 - b0, N.ptr(out[b0:b1]),
                Nt, N.ptr(work), chunk, _stream(xt))
+    return out
+
+
+# outputs sharing one kernel from which the posterior mean is a GEMM (kernel rows + rocBLAS)
+GEMM_MIN_OUTPUTS = 8
+GEMM_ROWS_BYTES = 1 << 28          # kernel-row block materialised per GEMM (256 MB)
+
+
+def post_mean_gemm(family, xt, z_dn, hyp, coeffs, alphas=None, tbits=0):
+    """Posterior mean of B outputs sharing hyper-parameters (BASELINE config C5: shape_batch = [B],
+    shape_scale = [1]): out = coeffs @ K(xt, z)^T, [B, n] x [n, N] -- GEMM-shaped, so the kernel rows
+    K(xt, z) are generated by fgp_kernel_rows in blocks of test points and contracted by the library
+    GEMM (rocBLAS / hipBLASLt through torch.matmul, FP64 MFMA) instead of re-evaluating the kernel for
+    every output (abstract_gp.py:375-377: kmat [N, n] einsum coeffs).  fp64 throughout: the mean is
+    a heavily cancelling sum of K(x, z_i) c_i with |c| ~ |y| / noise, which an fp32 contraction does
+    not resolve."""
+    Nt, d = xt.shape
+    n = z_dn.shape[1]
+    B = coeffs.shape[0]
+    cdt = torch.float64
+    coeffs = coeffs.to(cdt)
+    if coeffs.stride(-1) != 1:
+        coeffs = coeffs.contiguous()
+    out = torch.empty((B, Nt), dtype=torch.float64, device=xt.device)
+    step = max(1, min(Nt, GEMM_ROWS_BYTES // (8 * n)))
+    for t0 in range(0, Nt, step):
+        t1 = min(Nt, t0 + step)
+        rows = kernel_rows(family, xt[t0:t1], z_dn, hyp, alphas=alphas, tbits=tbits)[0]   # [Nc, n]
+        out[:, t0:t1] = torch.matmul(coeffs, rows.to(cdt).T)
     return out
 
 

@@ -63,6 +63,34 @@ int fgp_ifftbr(const void* in, int64_t in_batch_stride, void* out, int out_real,
 int fgp_fwht(const double* in, int64_t in_batch_stride, double* out, int64_t batch, int log2n, int stable,
              void* stream);
 
+/* Single-precision variants (complex64 / float32; SURVEY §8(b) fgp_fftbr_c64 / fgp_ifftbr_c64 /
+ * fgp_fwht_f32): the same transforms, arguments and layouts with float / complex64 in place of
+ * double / complex128 (fgp_fftbr_c64: in float32 when in_is_real, else complex64; out complex64;
+ * fgp_ifftbr_c64: out complex64, or float32 real parts when out_real, work complex64).  fp32
+ * arithmetic (explicit fmaf) with twiddles rounded once from the fp64 tables.  The reference forbids
+ * fp32 (fastgps/abstract_gp.py:46); these serve the mixed-precision data path of BASELINE config C5
+ * (float32 observations, fp64 eigenvalues), tolerance stated where used. */
+int fgp_fftbr_c64(const void* in, int64_t in_batch_stride, int in_is_real, void* out, int64_t batch, int log2n,
+                  int stable, void* stream);
+int fgp_ifftbr_c64(const void* in, int64_t in_batch_stride, void* out, int out_real, void* work, int64_t batch,
+                   int log2n, int stable, void* stream);
+int fgp_fwht_f32(const float* in, int64_t in_batch_stride, float* out, int64_t batch, int log2n, int stable,
+                 void* stream);
+
+/* The tilde-domain solve + inverse transform of gram_matrix_solve (fastgps/util.py:341-343,
+ * ift(A * y~).real) in one call: out[b] = inverse(in[b] * f[b]) with f row b at f + b * f_batch_stride
+ * (0: one row shared by every b, e.g. A = 1/ev of outputs sharing their hyper-parameters), applied in
+ * the load of the inverse's first pass.  family LATTICE: ifftbr (complex128, or complex64 when single;
+ * out_real / work as fgp_ifftbr); family NET: fwht (float64 / float32, out_real ignored). */
+int fgp_ifftbr_mul(int family, int single, const void* in, int64_t in_batch_stride, const void* f, int64_t f_batch_stride,
+                   void* out, int out_real, void* work, int64_t batch, int log2n, int stable, void* stream);
+
+/* Y[g, k] = sum_{r < R} |x[r G + g, k]|^2 in float64, x rows of n elements (row stride x_row_stride) of
+ * kind 0 float64, 1 complex128, 2 float32, 3 complex64: the MLL's data term over the outputs sharing
+ * eigen-problem g (fastgps/util.py:364-370), summed in ascending r. */
+int fgp_sum_sq(const void* x, int64_t x_row_stride, int kind, int64_t R, int64_t G, int64_t n, double* out,
+               void* stream);
+
 
 /* ---------------------------------------------------------------------------------------------
  * Kernel parts and the fused negative-log-likelihood / gradient / Rprop fit step.

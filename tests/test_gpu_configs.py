@@ -83,3 +83,35 @@ def test_half_length_fit_kernels_match_oracle(monkeypatch, m, d, alpha):
     errs = {mode: (abs(f - float(oloss)) / abs(float(oloss)), float((gr[:1 + d] - og).abs().max()) / float(og.abs().max()))
             for mode, f, gr in (("r2c", f1, g1), ("full", f0, g0))}
     assert all(e[0] <= 2e-7 and e[1] <= 2e-7 for e in errs.values()), errs
+
+
+@pytest.mark.parametrize("m,d,alpha", [(17, 3, 2), (18, 2, 1), (19, 5, 2), (20, 3, 3)])
+def test_half_length_post_var_matches_full_length_and_oracle(monkeypatch, m, d, alpha):
+    """Posterior variance through the half-length (R2C) quadratic-form kernels (csrc/fgp_predict.hip
+    k_qf_rows_r2c / k_qf_cols_r2c, lattice n >= 2^17) -- single GP (materialised points) and GPBatch
+    (regenerated points, delta formed from the lattice index) -- against the full-length kernels
+    (FGP_R2C=0) to 1e-10 K(x,x) and against the CPU oracle (abstract_gp.py:381-416) to 1e-8 K(x,x)."""
+    n = 2 ** m
+    xt = torch.rand((5, d), generator=torch.Generator().manual_seed(23))
+    res = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("FGP_R2C", mode)
+        gps = []
+        for s in (31, 32):
+            gp = F.FastGPLattice(F.Lattice(d, seed=s), alpha=alpha, lengthscales=torch.linspace(0.7, 1.4, d), device=DEV)
+            gp.add_y_next(O.f_ackley(gp.get_x_next(n).cpu()).to(DEV))
+            gps.append(gp)
+        with torch.no_grad():
+            single = gps[0].post_var(xt.to(DEV)).cpu()
+        b = F.GPBatch(gps)
+        batched = b.post_var(xt.to(DEV)).cpu()
+        res[mode] = (single, batched)
+    o = O.OracleFastGP("lattice", gps[0].get_x(n=n).cpu(), None, gps[0].y.cpu(), alpha=alpha,
+                       lengthscales=torch.linspace(0.7, 1.4, d))
+    opv = o.post_var(xt)
+    kxx = float(o.kernel(xt, xt).detach().abs().max())
+    (s1, b1), (s0, b0) = res["1"], res["0"]
+    assert float((s1 - s0).abs().max()) <= 1e-10 * kxx
+    assert float((b1 - b0).abs().max()) <= 1e-10 * kxx
+    assert float((s1 - opv).abs().max()) <= 1e-8 * kxx
+    assert float((b1[0] - opv).abs().max()) <= 1e-8 * kxx

@@ -124,3 +124,68 @@ def test_golden_stable_transforms(name):
     ift = (lambda v: F.ops.ifftbr(v, stable=True)) if fam == "lattice" else (lambda v: F.ops.fwht(v, stable=True))
     _close(ft(torch.from_numpy(g["ft_in"]).to(DEV)), torch.from_numpy(g["ft_out"]), m)
     _close(ift(torch.from_numpy(g["ift_in"]).to(DEV)), torch.from_numpy(g["ift_out"]), m)
+
+
+# ---------------------------------------------------------------- single precision (c64 / f32)
+def _close32(a, b, m):
+    """fp32 transforms against the fp64 oracle: |err| <= 2e-7 (1 + m) max|oracle| (fp32 eps = 6e-8;
+    O(eps log n) backward-stable butterflies, twiddles rounded once from the fp64 tables)."""
+    a = a.detach().cpu().to(torch.complex128 if a.is_complex() else torch.float64)
+    b = b.detach().cpu()
+    err = float((a - b).abs().max())
+    scale = float(b.abs().max())
+    assert err <= 2e-7 * (1 + m) * scale, "fp32 err %.3e scale %.3e (m=%d)" % (err, scale, m)
+
+
+@pytest.mark.parametrize("m", [0, 1, 3, 4, 7, 12, 13, 16, 17, 20])
+def test_single_precision_transforms_match_oracle(m):
+    n = 2 ** m
+    g = torch.Generator().manual_seed(300 + m)
+    batch = 3 if m <= 16 else 1
+    xr = torch.randn((batch, n), generator=g) + 2.0
+    xc = torch.randn((batch, n), generator=g) + 1j * torch.randn((batch, n), generator=g)
+    xr32, xc32 = xr.float(), xc.to(torch.complex64)
+    # oracle on the fp32-rounded inputs (the comparison measures the transform, not the input rounding)
+    out = F.ops.fftbr_raw(xr32.to(DEV), stable=True)
+    assert out.dtype == torch.complex64
+    _close32(out, O.ft_stable(xr32.double(), O.fftbr), m)
+    _close32(F.ops.fftbr_raw(xc32.to(DEV), stable=False), O.fftbr(xc32.to(torch.complex128)), m)
+    inv = F.ops.ifftbr_raw(xc32.to(DEV), stable=True)
+    assert inv.dtype == torch.complex64
+    _close32(inv, O.ft_stable(xc32.to(torch.complex128), O.ifftbr), m)
+    re = F.ops.ifftbr_raw(xc32.to(DEV), stable=True, real_out=True)
+    assert re.dtype == torch.float32
+    _close32(re, O.ft_stable(xc32.to(torch.complex128), O.ifftbr).real, m)
+    w = F.ops.fwht_raw(xr32.to(DEV), stable=True)
+    assert w.dtype == torch.float32
+    _close32(w, O.ft_stable(xr32.double(), O.fwht), m)
+
+
+@pytest.mark.parametrize("m", [2, 10, 14, 18])
+def test_inverse_mul_and_sum_sq(m):
+    """fgp_ifftbr_mul (the factor fused into the inverse's first pass) equals the inverse of the
+    product; fgp_sum_sq equals the grouped sum of squares -- fp64 to the transform tolerance, fp32 to
+    its own."""
+    n = 2 ** m
+    g = torch.Generator().manual_seed(400 + m)
+    B = 6
+    x = (torch.randn((B, n), generator=g) + 1j * torch.randn((B, n), generator=g)).to(DEV)
+    f1 = (torch.randn((1, n), generator=g) + 1j * torch.randn((1, n), generator=g)).to(DEV)
+    fB = (torch.randn((B, n), generator=g) + 1j * torch.randn((B, n), generator=g)).to(DEV)
+    for f in (f1, fB):
+        got = F.ops.inverse_mul(F.ops.LATTICE, x, f, real_out=True)
+        ref = O.ft_stable((x * f).cpu(), O.ifftbr).real
+        _close(got, ref, m)
+        got32 = F.ops.inverse_mul(F.ops.LATTICE, x.to(torch.complex64), f.to(torch.complex64), real_out=True)
+        assert got32.dtype == torch.float32
+        _close32(got32, O.ft_stable((x.to(torch.complex64) * f.to(torch.complex64)).to(torch.complex128).cpu(),
+                                    O.ifftbr).real, m)
+        xr, fr = x.real.contiguous(), f.real.contiguous()
+        _close(F.ops.inverse_mul(F.ops.NET, xr, fr), O.ft_stable((xr * fr).cpu(), O.fwht), m)
+    for G in (1, 2, 3, 6):
+        s = F.ops.sum_sq(x, G=G).cpu()
+        ref = (x.abs() ** 2).cpu().reshape(-1, G, n).sum(0)
+        assert float((s - ref).abs().max()) <= 1e-14 * float(ref.abs().max())
+    s32 = F.ops.sum_sq(x.to(torch.complex64), G=1).cpu()
+    ref32 = (x.to(torch.complex64).to(torch.complex128).abs() ** 2).cpu().sum(0)
+    assert float((s32 - ref32).abs().max()) <= 1e-14 * float(ref32.abs().max())
