@@ -12,7 +12,8 @@ import torch
 
 _LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
 LIB_PATH = os.path.join(_LIB_DIR, "libfgp_hip.so")
-ABI_VERSION = 7
+ABI_VERSION = 8
+MT_MAX_TASKS = 16
 MAX_D = 8
 PARTS_ARRAY = 0
 PARTS_LATTICE = 1
@@ -72,7 +73,13 @@ class PredDesc(ctypes.Structure):
     ]
 
 
+class MtLayout(ctypes.Structure):
+    """Mirror of fgp_mt_layout (include/fgp_hip.h)."""
+    _fields_ = [("T", _c_int), ("n", _c_i64 * 16)]
+
+
 _P_NLL = ctypes.POINTER(NllDesc)
+_P_MT = ctypes.POINTER(MtLayout)
 _P_FIT = ctypes.POINTER(FitDesc)
 _P_PRED = ctypes.POINTER(PredDesc)
 
@@ -107,6 +114,12 @@ _SIGNATURES = {
                         _c_vp],
     "fgp_post_mean_batched": [_P_PRED, _c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp],
     "fgp_post_var_batched": [_P_PRED, _c_vp, _c_i64, _c_i64, _c_pd, _c_vp, _c_vp, _c_vp, _c_vp],
+    "fgp_mt_parts": [_c_int, _c_vp, _c_i64, _c_i64, _c_vp, _c_i64, _c_i64, _c_int, _c_int, _c_int, _c_vp, _c_vp,
+                     _c_vp, _c_int, _c_vp, _c_vp],
+    "fgp_mt_factor": [_P_MT, _c_vp, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp],
+    "fgp_mt_solve": [_P_MT, _c_vp, _c_i64, _c_vp, _c_i64, _c_i64, _c_vp, _c_vp],
+    "fgp_mt_selinv": [_P_MT, _c_vp, _c_i64, _c_vp, _c_vp],
+    "fgp_mt_mll_grad": [_P_MT, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_i64, _c_vp, _c_vp],
     "fgp_inv_eig": [_c_int, _c_vp, _c_vp, _c_i64, _c_vp, _c_i64, _c_i64, _c_int, _c_vp, _c_vp, _c_vp],
 }
 
@@ -166,6 +179,10 @@ def call(name, *args):
 
 def stream_ptr(device):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def byref_layout(lay):
+    return ctypes.byref(lay)
 
 
 def ptr(t):

@@ -658,4 +658,38 @@ __device__ __forceinline__ double walsh_omega(int ord, unsigned long long delta,
   return e1 + e2 + e3 + E;
 }
 
+// ---------------------------------------------------------------- kernel parts (shared by the fit,
+// parts and multitask kernels)
+// torch.remainder(v, 1.0) for floating point (fmod, then shift negative results by the divisor)
+__device__ __forceinline__ double mod1(double v) {
+  double r = fmod(v, 1.0);
+  if (r != 0.0 && r < 0.0) r += 1.0;
+  return r;
+}
+
+// Even Bernoulli polynomial B_order(x) as a polynomial in u = x (x - 1) (the even B_2a are symmetric
+// about 1/2):  B2 = u + 1/6,  B4 = u^2 - 1/30,  B6 = u^2 (u - 1/2) + 1/42,
+// B8 = u^2 (u (u - 4/3) + 2/3) - 1/30  -- 2 / 4 / 5 operations instead of Horner's 2 / 4 / 6 / 8 in x
+// (the fit row kernels are FP64-VALU bound and evaluate one per element and dimension).  Every
+// multiply-add is an explicit fma, so the value does not depend on the compiler's contraction choices
+// in the inlining context: the parts array (k_lattice_parts) and the parts regenerated inside the fit
+// kernels are bit-identical.
+__device__ __forceinline__ double bernoulli(int order, double x) {
+  const double u = __builtin_fma(x, x, -x);
+  switch (order) {
+    case 2: return u + 1.0 / 6.0;
+    case 4: return __builtin_fma(u, u, -1.0 / 30.0);
+    case 6: return __builtin_fma(u * u, u - 0.5, 1.0 / 42.0);
+    case 8: return __builtin_fma(u * u, __builtin_fma(u, u - 4.0 / 3.0, 2.0 / 3.0), -1.0 / 30.0);
+    default: return __builtin_nan("");
+  }
+}
+
+// Order-1 Walsh part for an XOR distance (fast_gp_digital_net_b2.py:297-298).
+__device__ __forceinline__ double walsh1(unsigned long long delta, int t) {
+  if (delta == 0ull) return 6.0 * (1.0 / 6.0 - 0.0);
+  const int fl = 63 - __clzll((long long)delta);   // floor(log2(delta)), exact
+  return 6.0 * (1.0 / 6.0 - ldexp(1.0, fl - t - 1));
+}
+
 }  // namespace fgp

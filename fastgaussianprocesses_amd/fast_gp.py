@@ -12,10 +12,10 @@ misuse.  Every numerical hot spot runs in the HIP library (include/fgp_hip.h):
   post_mean                 -> fgp_post_mean (matrix-free cross-kernel contraction)
   post_var / post_cov       -> fgp_kernel_rows + the transform solve
 
-Scope of this round: single-task GPs (num_tasks=None or 1) without derivative information
-(beta = kappa = 0); multitask / derivative-informed GPs are the next row of SURVEY.md §8(f) and
-raise NotImplementedError.  Hyper-parameter fits other than (MLL, default optimizer, no masks,
-default log/exp transforms) run a generic path: torch autograd through the HIP transforms and
+This module holds single-task GPs (num_tasks=None or 1) without derivative information
+(beta = kappa = 0); multitask (num_tasks > 1) and derivative-informed GPs are built by the same
+constructors and run multitask.py.  Hyper-parameter fits other than (MLL, default optimizer, no
+masks, default log/exp transforms) run a generic path: torch autograd through the HIP transforms and
 torch device ops, with the caller's torch optimizer.
 """
 import math
@@ -70,12 +70,31 @@ class _Hyper(object):
         return value
 
 
+def _wants_multitask(cls, args, kwargs):
+    """num_tasks > 1, or derivative information, in a family constructor's arguments."""
+    import inspect
+    bound = inspect.signature(cls.__init__).bind_partial(None, *args, **kwargs).arguments
+    nt = bound.get("num_tasks")
+    return (nt is not None and nt != 1) or bound.get("derivatives") is not None or \
+        bound.get("derivatives_coeffs") is not None
+
+
 class AbstractFastGP(torch.nn.Module):
-    """Shared machinery of FastGPLattice / FastGPDigitalNetB2 (single task, beta=kappa=0)."""
+    """Shared machinery of FastGPLattice / FastGPDigitalNetB2 (single task, beta=kappa=0).
+
+    Constructing FastGPLattice / FastGPDigitalNetB2 with num_tasks > 1 or with derivatives /
+    derivatives_coeffs returns the family's multitask class instead (multitask.py)."""
 
     _FAMILY = None
     _XBDTYPE = None
     _FTOUTDTYPE = None
+    _MULTITASK = False
+
+    def __new__(cls, *args, **kwargs):
+        if not cls._MULTITASK and cls._FAMILY is not None and _wants_multitask(cls, args, kwargs):
+            from .multitask import multitask_class
+            cls = multitask_class(cls)
+        return super().__new__(cls)
 
     def __init__(self, seqs, num_tasks, seed_for_seq, alpha, scale, lengthscales, noise, factor_task_kernel,
                  rank_factor_task_kernel, noise_task_kernel, device, tfs_scale, tfs_lengthscales, tfs_noise,
@@ -92,10 +111,9 @@ class AbstractFastGP(torch.nn.Module):
         else:
             assert isinstance(num_tasks, int) and num_tasks > 0
             self.solo_task, self.default_task = False, torch.arange(num_tasks)
-        if num_tasks != 1:
-            raise NotImplementedError("multi-task fast GPs (num_tasks > 1) are the next build row (SURVEY §8f)")
-        if derivatives is not None or derivatives_coeffs is not None:
-            raise NotImplementedError("derivative-informed kernels are not built yet (SURVEY §8f)")
+        if num_tasks != 1 or derivatives is not None or derivatives_coeffs is not None:
+            raise AssertionError("multitask / derivative-informed GPs are built through FastGPLattice / "
+                                 "FastGPDigitalNetB2 (multitask.py)")
         self.num_tasks = 1
         # Extension (not in the reference, which is fp64-only, abstract_gp.py:46): data_dtype=float32
         # stores the observations in fp32 and forms the MLL's data term from a complex64 ytilde

@@ -35,8 +35,15 @@ def log2_exact(n):
     return n.bit_length() - 1
 
 
+def resolved(x):
+    """x with torch's lazy conjugate / negation bits materialised: the kernels read raw memory, and a
+    `.conj()` view (e.g. the gradient autograd hands through a conj) shares its unconjugated storage."""
+    return x.resolve_conj().resolve_neg() if x.is_complex() else x.resolve_neg()
+
+
 def _as_rows(x):
     """View x[..., n] as [batch, n] with unit inner stride; returns (rows, batch_stride)."""
+    x = resolved(x)
     n = x.shape[-1]
     r = x.reshape(-1, n)
     if r.stride(-1) != 1 or (r.size(0) > 1 and r.stride(0) < n):
@@ -142,7 +149,7 @@ def inverse_mul(family, x, f, real_out=False, stable=True):
         x = x.to(rdt)
         f = f.to(rdt)
     rows, bs = _as_rows(x)
-    f2 = f.reshape(-1, n)
+    f2 = resolved(f).reshape(-1, n)
     if f2.size(0) == 1:
         fbs = 0
     elif tuple(f.shape) == tuple(x.shape):
@@ -382,3 +389,106 @@ def post_var_quadform(family, xt, z_dn, hyp, wa, alphas=None, tbits=0):
     N.call("fgp_post_var_qf", family, N.ptr(xt), Nt, N.ptr(z_dn), m, d, int(tbits), order, coef,
            N.ptr(hyp.to(torch.float64).contiguous()), N.ptr(wa), N.ptr(work), N.ptr(partial), N.ptr(out), _stream(xt))
     return out
+
+
+# ------------------------------------------------------------------------------------- multitask
+def mt_layout(ns_sorted):
+    """fgp_mt_layout of the active tasks (n > 0, sorted by n descending)."""
+    ns = [int(v) for v in ns_sorted]
+    assert 1 <= len(ns) <= N.MT_MAX_TASKS, "multitask: %d active tasks (at most %d)" % (len(ns), N.MT_MAX_TASKS)
+    lay = N.MtLayout()
+    lay.T = len(ns)
+    for k, v in enumerate(ns):
+        lay.n[k] = v
+    return lay
+
+
+def mt_parts(family, x, z, order, coef, add, tbits=0, zip_pairs=False):
+    """Derivative kernel parts (fgp_mt_parts): x [N, d], z [M, d] (float64 lattice / int64 net points);
+    order / coef / add [P, d] host lists -> [N, M, P, d] (or [N, P, d] with zip_pairs, N == M)."""
+    require_device(x, "mt_parts")
+    dt = torch.float64 if family == LATTICE else torch.int64
+    x = x.to(dt)
+    z = z.to(dt)
+    x = x if x.stride(-1) == 1 else x.contiguous()
+    z = z if z.stride(-1) == 1 else z.contiguous()
+    Nx, d = x.shape
+    M = z.shape[0]
+    P = len(order)
+    dev = x.device
+    o = torch.tensor(order, dtype=torch.int32, device=dev).reshape(P, d).contiguous()
+    c = torch.tensor(coef, dtype=torch.float64, device=dev).reshape(P, d).contiguous()
+    a = torch.tensor(add, dtype=torch.float64, device=dev).reshape(P, d).contiguous()
+    shape = (Nx, P, d) if zip_pairs else (Nx, M, P, d)
+    out = torch.empty(shape, dtype=torch.float64, device=dev)
+    N.call("fgp_mt_parts", int(family), N.ptr(x), x.stride(0) if Nx > 1 else d, Nx, N.ptr(z),
+           z.stride(0) if M > 1 else d, M, int(bool(zip_pairs)), d, P, N.ptr(o), N.ptr(c), N.ptr(a), int(tbits),
+           N.ptr(out), _stream(x))
+    return out
+
+
+def mt_factor(lay, lams):
+    """Structured LDL^H of G problems' Gram blocks (fgp_mt_factor): lams [G, L] complex128 ->
+    (factor [G, L], logdet per frequency class [G, nmin], info [1] int32 device flag)."""
+    require_device(lams, "mt_factor")
+    lams = resolved(lams.to(torch.complex128)).contiguous()
+    G = lams.shape[0]
+    nmin = int(lay.n[lay.T - 1])
+    fac = torch.empty_like(lams)
+    ld = torch.empty((G, nmin), dtype=torch.float64, device=lams.device)
+    info = torch.zeros(1, dtype=torch.int32, device=lams.device)
+    N.call("fgp_mt_factor", N.byref_layout(lay), N.ptr(lams), G, N.ptr(fac), N.ptr(ld), N.ptr(info), _stream(lams))
+    return fac, ld, info
+
+
+def mt_solve(lay, fac, v):
+    """out[b] = Lambda_{b mod G}^-1 v[b] (fgp_mt_solve), v [B, R nmin] complex128."""
+    require_device(v, "mt_solve")
+    v = resolved(v.to(torch.complex128))
+    v = v if v.stride(-1) == 1 and (v.shape[0] <= 1 or v.stride(0) >= v.shape[1]) else v.contiguous()
+    B = v.shape[0]
+    out = torch.empty((B, v.shape[1]), dtype=torch.complex128, device=v.device)
+    N.call("fgp_mt_solve", N.byref_layout(lay), N.ptr(fac), fac.shape[0], N.ptr(v), v.stride(0) if B > 1 else v.shape[1],
+           B, N.ptr(out), _stream(v))
+    return out
+
+
+def mt_selinv(lay, fac):
+    """Entries of the inverse on the coupling pattern (fgp_mt_selinv) -> [G, L]."""
+    out = torch.empty_like(fac)
+    N.call("fgp_mt_selinv", N.byref_layout(lay), N.ptr(fac), fac.shape[0], N.ptr(out), _stream(fac))
+    return out
+
+
+class _MtMLL(torch.autograd.Function):
+    """(norm_b = Re(y_b^H Lambda^-1 y_b), logdet_g) of packed lams [G, L] and tilde data Y [B, R nmin]
+    (util.py:364-370 with the block inverse of util.py:275-337); backward by fgp_mt_selinv +
+    fgp_mt_mll_grad (gradient w.r.t. the lams only; the data carry none)."""
+
+    @staticmethod
+    def forward(ctx, lams, Y, lay):
+        fac, ld, _ = mt_factor(lay, lams)
+        z = mt_solve(lay, fac, Y)
+        norm = (Y.conj() * z).real.sum(-1)
+        ctx.lay = lay
+        ctx.save_for_backward(fac, z)
+        return norm, ld.sum(-1)
+
+    @staticmethod
+    def backward(ctx, gn, gl):
+        fac, z = ctx.saved_tensors
+        lay = ctx.lay
+        G, B = fac.shape[0], z.shape[0]
+        zinv = mt_selinv(lay, fac)
+        gn = (gn if gn is not None else torch.zeros(B, device=z.device, dtype=torch.float64)).to(torch.float64).contiguous()
+        gl = (gl if gl is not None else torch.zeros(G, device=z.device, dtype=torch.float64)).to(torch.float64).contiguous()
+        glp = torch.empty_like(fac)
+        N.call("fgp_mt_mll_grad", N.byref_layout(lay), N.ptr(zinv), N.ptr(z), N.ptr(gn), N.ptr(gl), B, G, N.ptr(glp),
+               _stream(z))
+        return glp, None, None
+
+
+def mt_mll_terms(lay, lams, Y):
+    """Differentiable (norm [B], logdet [G]) for the multitask MLL (HIP factor / solve / gradient)."""
+    return _MtMLL.apply(resolved(lams.to(torch.complex128)).contiguous(),
+                        resolved(Y.to(torch.complex128)).contiguous(), lay)

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define FGP_ABI_VERSION 7
+#define FGP_ABI_VERSION 8
 
 #define FGP_OK 0
 #define FGP_ERR_INVALID (-1)     /* bad argument (shape, stride, null pointer) */
@@ -310,6 +310,62 @@ int fgp_inv_eig(int family, const void* lam, const void* ytilde, int64_t yt_stri
  * N <= 65535: the kmat of AbstractGP.post_var / post_cov (fastgps/abstract_gp.py:407-411,452-457). */
 int fgp_kernel_rows(int family, const double* xt, int64_t N, const void* z, int64_t n, int d, int tbits,
                     const int* order, const double* coef, const double* hyp, int Gk, double* rows, void* stream);
+
+
+/* ---------------------------------------------------------------------------------------------
+ * Multitask / derivative-informed fast GPs (num_tasks > 1 or derivative multi-indices).
+ * Reference: fastgps/util.py:275-363 (_FastInverseLogDetCache with num_tasks > 1),
+ * abstract_fast_gp.py:29-31,155-191 (task-pair lam caches, kernel parts with beta / kappa),
+ * fast_gp_lattice.py:267-273 and fast_gp_digital_net_b2.py:289-301 (derivative parts).
+ *
+ * Block layout: the T ACTIVE tasks (n > 0) sorted by n descending (util.py:273), n[k] powers of two,
+ * nmin = n[T-1], R = sum_k n[k] / nmin block rows.  The packed "lams" array of one problem holds, for
+ * every pair k <= l (row-major over k, then l), the n[k] values lams[k, l] (the reference's
+ * sqrt(n_l) lam_{k,l} * K_task[k, l] with the nugget on the diagonal pairs, util.py:284-298):
+ * offset(k, l) = sum of n[k'] over the pairs before (k, l); L = sum_{k <= l} n[k] per problem.
+ * Value q nmin + j of pair (k, l) is the coupling of block row (k, q) with (l, q mod (n[l]/nmin)) in
+ * frequency class j.  All multitask arrays are complex128, [problem][L], problem stride L. */
+#define FGP_MT_MAX_TASKS 16
+#define FGP_MT_MAX_ROWS (1 << 24)
+
+typedef struct fgp_mt_layout {
+  int T;                              /* active tasks, 1 .. FGP_MT_MAX_TASKS */
+  int64_t n[FGP_MT_MAX_TASKS];        /* their n, descending */
+} fgp_mt_layout;
+
+/* Kernel parts with derivative orders (_kernel_parts, abstract_fast_gp.py:173-180):
+ *   parts[i][k][p][j], i < N (points x, row stride x_row_stride), k < M (points z), p < P (beta, kappa)
+ *   pairs, j < d:  lattice (family 0, float64 points): coef[p d + j] * B_order((x_ij - z_kj) mod 1),
+ *   order 1..8 (fast_gp_lattice.py:269-273);  net (family 1, int64 t-bit points):
+ *   coef[p d + j] * (add[p d + j] + omega_order(xb_ij ^ zb_kj)), order 1..4 (fast_gp_digital_net_b2.py:
+ *   291-301).  order / coef / add are DEVICE arrays [P][d].  zip = 1 (N == M): only the pairs (x_i, z_i),
+ *   parts[i][p][j] (the kernel of x with itself in post_var, abstract_gp.py:407). */
+int fgp_mt_parts(int family, const void* x, int64_t x_row_stride, int64_t N, const void* z, int64_t z_row_stride,
+                 int64_t M, int zip, int d, int P, const int* order, const double* coef, const double* add, int tbits,
+                 double* parts, void* stream);
+
+/* Factor the transform-domain Gram blocks of G problems (replaces _FastInverseLogDetCache.__call__,
+ * util.py:275-337): structured LDL^H per frequency class in the packed layout (factor [G][L]),
+ * logdet [G][nmin] per class (sum over the classes = the reference's logdet), *info set to 1 (device
+ * int, zeroed by the caller) if a pivot is not positive. */
+int fgp_mt_factor(const fgp_mt_layout* layout, const void* lams, int64_t G, void* factor, double* logdet, int* info,
+                  void* stream);
+
+/* out[b] = Lambda_{b mod G}^-1 v[b] for B vectors v [B][R nmin] (row stride v_row_stride >= R nmin):
+ * the tilde-domain solve of _gram_matrix_solve_tilde_to_tilde (util.py:354-363); out [B][R nmin]. */
+int fgp_mt_solve(const fgp_mt_layout* layout, const void* factor, int64_t G, const void* v, int64_t v_row_stride,
+                 int64_t B, void* out, void* stream);
+
+/* Entries of A = Lambda^-1 on the packed coupling pattern (zinv [G][L]): the entries of the reference's
+ * dense inverse `inv` (util.py:336) that the MLL gradient and post_cubature_var / cov
+ * (abstract_fast_gp.py:82-154, inv[mvec, mvec, 0]) read. */
+int fgp_mt_selinv(const fgp_mt_layout* layout, const void* factor, int64_t G, void* zinv, void* stream);
+
+/* d(loss)/d(packed lams) for loss = f(norm_b, logdet_g), norm_b = Re(y_b^H A y_b), logdet_g = log det:
+ * z = A y [B][R nmin] (fgp_mt_solve), grad_norm [B], grad_logdet [G], B a multiple of G (output b uses
+ * problem b mod G); grad_lams [G][L] in torch's complex-gradient convention (dL/dRe + i dL/dIm). */
+int fgp_mt_mll_grad(const fgp_mt_layout* layout, const void* zinv, const void* z, const double* grad_norm,
+                    const double* grad_logdet, int64_t B, int64_t G, void* grad_lams, void* stream);
 
 #ifdef __cplusplus
 }

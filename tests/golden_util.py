@@ -7,8 +7,12 @@ import numpy as np
 GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
-def golden_names(family=None):
+def golden_names(family=None, multitask=False):
+    """Single-task fixtures (make_golden.py) by default; multitask=True: the multitask /
+    derivative-informed ones (make_golden_multitask.py, names mt_* / deriv_*)."""
     names = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz")))
+    mt = [n for n in names if n.startswith("mt_") or n.startswith("deriv_")]
+    names = mt if multitask else [n for n in names if n not in mt]
     if family is not None:
         names = [n for n in names if n.startswith(family)]
     return names

@@ -189,3 +189,24 @@ def test_inverse_mul_and_sum_sq(m):
     s32 = F.ops.sum_sq(x.to(torch.complex64), G=1).cpu()
     ref32 = (x.to(torch.complex64).to(torch.complex128).abs() ** 2).cpu().sum(0)
     assert float((s32 - ref32).abs().max()) <= 1e-14 * float(ref32.abs().max())
+
+
+@pytest.mark.parametrize("m", [5, 14])
+def test_lazy_conj_and_neg_views_are_materialised(m):
+    """x.conj() / -x views share unconjugated storage; the kernels must see their values (the gradient
+    through lam.conj() of the multitask blocks, util.py:284, arrives as such a view)."""
+    g = torch.Generator().manual_seed(3)
+    n = 2 ** m
+    z = (torch.randn((2, n), generator=g) + 1j * torch.randn((2, n), generator=g)).to(DEV)
+    for op in (F.ops.fftbr, F.ops.ifftbr):
+        for stable in (False, True):
+            assert torch.equal(op(z.conj(), stable=stable), op(z.conj().resolve_conj(), stable=stable))
+            assert torch.equal(op(-z, stable=stable), op((-z).resolve_neg(), stable=stable))
+    assert torch.equal(F.ops.fwht(z.conj(), stable=True), F.ops.fwht(z.conj().resolve_conj(), stable=True))
+    zc = z.clone().requires_grad_(True)
+    y = F.ops.fftbr(zc.conj(), stable=True)
+    gz, = torch.autograd.grad((y.real * torch.arange(n, device=DEV)).sum(), zc)
+    zr = z.clone().requires_grad_(True)
+    yr = F.ops.fftbr(zr.conj().resolve_conj(), stable=True)
+    gr, = torch.autograd.grad((yr.real * torch.arange(n, device=DEV)).sum(), zr)
+    assert torch.allclose(gz, gr, rtol=0, atol=1e-12)

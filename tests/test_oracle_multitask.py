@@ -9,7 +9,7 @@ from oracle.fgp_oracle_mt import OracleMultiTaskFastGP
 
 torch.set_default_dtype(torch.float64)
 
-MT_NAMES = [n for n in golden_names() if n.startswith("mt_") or n.startswith("deriv_")]
+MT_NAMES = golden_names(multitask=True)
 
 # Fixtures where the REFERENCE's own block inverse is inaccurate, with the relative error it carries.
 # deriv_lattice_d2_a3_equal: (f, df/dx0, df/dx1), alpha = 3, n = 128 each.  At frequency classes 12 and
