@@ -262,6 +262,7 @@ class GPBatch(object):
             gp._nh = self.n
             gp.n, gp.m = self._n_t, self._m_t
             gp._cache = {}
+            gp._yt_state = None
         self._y = y
         self._st = {}
 

@@ -418,6 +418,38 @@ static int fwht_impl(const void* in, int64_t in_bs, void* out, int64_t batch, in
   return launch_cols<T, false>(log2n, out, n, 0, out, n, 0, batch, stable, scale, 0, tb, st);
 }
 
+// One DIT doubling stage (fastgps/util.py:113-132 _LamCaches, :173-178 _YtildeCache): from the
+// transforms of the first n and the next n values to the transform of all 2n,
+//   out[k] = (prev[k] + w^k nxt[k]) / sqrt(2),  out[k + n] = (prev[k] - w^k nxt[k]) / sqrt(2),
+// w^k = exp(-pi i k / n) (get_omega, fast_gp_lattice.py:261-262) for lattices, 1 for nets
+// (fast_gp_digital_net_b2.py:264-265).  One thread per k: 16 + 16 B read, 32 B written (lattice).
+__global__ __launch_bounds__(kWG) void k_double_cx(const double2* __restrict__ prev, int64_t ps,
+                                                   const double2* __restrict__ nxt, int64_t ns, int64_t B,
+                                                   int64_t n, double2* __restrict__ out, int64_t os) {
+  const int64_t e = (int64_t)blockIdx.x * kWG + threadIdx.x;
+  if (e >= B * n) return;
+  const int64_t b = e / n, k = e - b * n;
+  double sn, cs;
+  sincospi(-(double)k / (double)n, &sn, &cs);
+  const double2 a = prev[b * ps + k], v = nxt[b * ns + k];
+  const double2 wv = make_double2(cs * v.x - sn * v.y, cs * v.y + sn * v.x);
+  const double r = 0.70710678118654752440;
+  out[b * os + k] = make_double2((a.x + wv.x) * r, (a.y + wv.y) * r);
+  out[b * os + k + n] = make_double2((a.x - wv.x) * r, (a.y - wv.y) * r);
+}
+
+__global__ __launch_bounds__(kWG) void k_double_re(const double* __restrict__ prev, int64_t ps,
+                                                   const double* __restrict__ nxt, int64_t ns, int64_t B,
+                                                   int64_t n, double* __restrict__ out, int64_t os) {
+  const int64_t e = (int64_t)blockIdx.x * kWG + threadIdx.x;
+  if (e >= B * n) return;
+  const int64_t b = e / n, k = e - b * n;
+  const double a = prev[b * ps + k], v = nxt[b * ns + k];
+  const double r = 0.70710678118654752440;
+  out[b * os + k] = (a + v) * r;
+  out[b * os + k + n] = (a - v) * r;
+}
+
 }  // namespace fgp
 
 using namespace fgp;
@@ -468,6 +500,24 @@ int fgp_sum_sq(const void* x, int64_t x_row_stride, int kind, int64_t R, int64_t
     default: return set_error(kErrInvalid, "fgp_sum_sq: bad kind %d", kind);
   }
   return check_launch("k_sum_sq");
+}
+
+int fgp_double_update(int family, const void* prev, int64_t prev_stride, const void* nxt, int64_t nxt_stride,
+                      int64_t batch, int log2n, void* out, int64_t out_stride, void* stream) {
+  if (log2n < 0 || log2n >= kMaxLog2N || batch < 0) return set_error(kErrInvalid, "fgp_double_update: bad sizes");
+  const int64_t n = (int64_t)1 << log2n;
+  if (batch == 0) return kOk;
+  if (!prev || !nxt || !out) return set_error(kErrInvalid, "fgp_double_update: null pointer");
+  if (prev_stride < n || nxt_stride < n || out_stride < 2 * n) return set_error(kErrInvalid, "fgp_double_update: strides");
+  const unsigned grid = (unsigned)((batch * n + kWG - 1) / kWG);
+  hipStream_t st = (hipStream_t)stream;
+  if (family == FGP_FAMILY_LATTICE)
+    k_double_cx<<<grid, kWG, 0, st>>>(static_cast<const double2*>(prev), prev_stride, static_cast<const double2*>(nxt),
+                                      nxt_stride, batch, n, static_cast<double2*>(out), out_stride);
+  else
+    k_double_re<<<grid, kWG, 0, st>>>(static_cast<const double*>(prev), prev_stride, static_cast<const double*>(nxt),
+                                      nxt_stride, batch, n, static_cast<double*>(out), out_stride);
+  return check_launch("k_double_update");
 }
 
 /* Inverse transform of in * f (fgp_hip.h fgp_ifftbr_mul): lattice complex128 / complex64 via ifftbr,

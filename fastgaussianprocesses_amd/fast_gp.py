@@ -337,6 +337,10 @@ class AbstractFastGP(torch.nn.Module):
         assert isinstance(y_next, list) and len(y_next) == 1
         assert all(y.shape[:-1] == self.shape_batch for y in y_next)
         y = y_next[0].to(device=self.device, dtype=self.data_dtype)
+        old = int(self._y[0].size(-1))
+        st = getattr(self, "_yt_state", None)
+        if st is None or old == 0 or st[0] > old or old != self._nh:
+            self._yt_state = None           # only an append keeps the cached prefix transform valid
         self._y[0] = torch.cat([self._y[0].to(self.data_dtype), y], -1)
         self._nh = int(self._y[0].size(-1))
         self.n = torch.tensor([self._nh], dtype=torch.int64, device=self.device)
@@ -395,8 +399,16 @@ class AbstractFastGP(torch.nn.Module):
         n = self._nint(n)
 
         def f():
-            if not self._gradmode() and self._lam_fusable(n):
-                return self._lam_fused(n)
+            if not self._gradmode():
+                half = self._cache.get(("lam", n // 2, True, False)) if n >= 4 else None
+                if half is not None:
+                    # _LamCaches doubling (util.py:113-132): lam_n from the cached lam_{n/2} and ft of the
+                    # first-column kernel over the new half of the points, one DIT stage
+                    self._ensure_points(n)
+                    parts = self._compute_parts(self._xb[n // 2:n], self._xb[0])
+                    return ops.double_update(self._FAMILY, half, self.ft(self._k1(n // 2, parts)))
+                if self._lam_fusable(n):
+                    return self._lam_fused(n)
             return self.ft(self._k1(n))
         return self._cached(("lam", n), f)
 
@@ -415,11 +427,23 @@ class AbstractFastGP(torch.nn.Module):
         return lam.reshape(tuple(pb) + (n,))
 
     def get_ytilde(self, task=0):
+        """_YtildeCache (util.py:164-183): after add_y_next doubled n, ytilde_2n comes from the cached
+        ytilde_n and ft of the NEW half by one DIT stage (fgp_double_update), as the reference does,
+        instead of a full-length transform."""
         n = self._nh
 
         def f():
             y = self._y[0]
-            return self.ft(y) if n > 1 else y.clone().to(self._FTOUTDTYPE)
+            st = getattr(self, "_yt_state", None)
+            if st is not None and 1 < st[0] < n and y.dtype == torch.float64 and n % st[0] == 0:
+                ns, yt = st
+                while ns < n:
+                    yt = ops.double_update(self._FAMILY, yt, self.ft(y[..., ns:2 * ns]))
+                    ns *= 2
+            else:
+                yt = self.ft(y) if n > 1 else y.clone().to(self._FTOUTDTYPE)
+            self._yt_state = (n, yt)
+            return yt
         return self._cached(("ytilde", n), f, grad_sensitive=False)
 
     def _ev(self, n):

@@ -206,6 +206,7 @@ class MultiTaskFastGP(AbstractFastGP):
         self._xs = [torch.empty((0, d), device=dev) for _ in range(T)]
         self._xbs = [torch.empty((0, d), dtype=self._XBDTYPE, device=dev) for _ in range(T)]
         self._pts = [0] * T
+        self._yt_state = [None] * T
         self._parts_cache = {}
         self._cache = {}
         self._snap = None
@@ -303,6 +304,9 @@ class MultiTaskFastGP(AbstractFastGP):
         assert isinstance(y_next, list) and len(y_next) == len(tasks)
         assert all(y.shape[:-1] == self.shape_batch for y in y_next)
         for y, l in zip(y_next, tasks):
+            st = self._yt_state[l]
+            if st is None or self._ns[l] == 0 or st[0] > self._ns[l]:
+                self._yt_state[l] = None        # only an append keeps the cached prefix transform valid
             self._y[l] = torch.cat([self._y[l], y.to(device=self.device, dtype=torch.float64)], -1)
         self._ns = [int(y.size(-1)) for y in self._y]
         self.n = torch.tensor(self._ns, dtype=torch.int64, device=self.device)
@@ -424,11 +428,20 @@ class MultiTaskFastGP(AbstractFastGP):
         assert task0 <= task1, "lam caches exist for task0 <= task1 (abstract_fast_gp.py:30)"
         n = self._ns[task0] if n is None else int(n)
 
+        def k1_of(parts):
+            return self._kernel_from_parts(parts, self.derivatives[task0], self.derivatives[task1],
+                                           self.derivatives_coeffs[task0], self.derivatives_coeffs[task1])
+
         def f():
-            k1 = self._kernel_from_parts(self.get_k1parts(task0, task1, n), self.derivatives[task0],
-                                         self.derivatives[task1], self.derivatives_coeffs[task0],
-                                         self.derivatives_coeffs[task1])
-            return self.ft(k1)
+            half = self._cache.get(("lam", (task0, task1, n // 2), True, False)) \
+                if (n >= 4 and not self._gradmode()) else None
+            if half is not None:
+                # _LamCaches doubling (util.py:113-132): one DIT stage from the cached lam at n/2 and ft
+                # of the first-column kernel over the new half of task0's points
+                new = self._parts_pairs(self.get_xb(task0, n)[n // 2:], self.get_xb(task1, 1),
+                                        self._derivs_h[task0], self._derivs_h[task1])[:, 0]
+                return ops.double_update(self._FAMILY, half, self.ft(k1_of(new)))
+            return self.ft(k1_of(self.get_k1parts(task0, task1, n)))
         return self._cached(("lam", (task0, task1, n)), f)
 
     def get_ytilde(self, task):
@@ -438,7 +451,16 @@ class MultiTaskFastGP(AbstractFastGP):
 
         def f():
             y = self._y[task]
-            return self.ft(y) if n > 1 else y.clone().to(self._FTOUTDTYPE)
+            st = self._yt_state[task]
+            if st is not None and 1 < st[0] < n and n % st[0] == 0:
+                ns, yt = st                     # _YtildeCache doubling (util.py:173-178)
+                while ns < n:
+                    yt = ops.double_update(self._FAMILY, yt, self.ft(y[..., ns:2 * ns]))
+                    ns *= 2
+            else:
+                yt = self.ft(y) if n > 1 else y.clone().to(self._FTOUTDTYPE)
+            self._yt_state[task] = (n, yt)
+            return yt
         return self._cached(("ytilde", (task, n)), f, grad_sensitive=False)
 
     def kernel(self, x, z, beta0=None, beta1=None, c0=None, c1=None):

@@ -391,6 +391,21 @@ def post_var_quadform(family, xt, z_dn, hyp, wa, alphas=None, tbits=0):
     return out
 
 
+def double_update(family, prev, nxt):
+    """ft of 2n values from ft of the first n (prev [..., n]) and of the next n (nxt [..., n]): one DIT
+    stage (fgp_double_update; _LamCaches / _YtildeCache doubling, util.py:113-132,173-178)."""
+    require_device(prev, "double_update")
+    n = prev.shape[-1]
+    m = log2_exact(n)
+    dt = torch.complex128 if family == LATTICE else torch.float64
+    p, ps = _as_rows(prev.to(dt))
+    q, qs = _as_rows(nxt.to(dt).expand(prev.shape))
+    out = torch.empty((p.shape[0], 2 * n), dtype=dt, device=prev.device)
+    N.call("fgp_double_update", int(family), N.ptr(p), ps, N.ptr(q), qs, p.shape[0], m, N.ptr(out), 2 * n,
+           _stream(prev))
+    return out.reshape(tuple(prev.shape[:-1]) + (2 * n,))
+
+
 # ------------------------------------------------------------------------------------- multitask
 def mt_layout(ns_sorted):
     """fgp_mt_layout of the active tasks (n > 0, sorted by n descending)."""

@@ -312,6 +312,15 @@ int fgp_kernel_rows(int family, const double* xt, int64_t N, const void* z, int6
                     const int* order, const double* coef, const double* hyp, int Gk, double* rows, void* stream);
 
 
+
+/* One DIT doubling stage (_LamCaches / _YtildeCache, fastgps/util.py:113-132,173-178): from ft of the first
+ * n = 2^log2n values (prev) and of the next n (nxt) to ft of all 2n (out [batch][2n]):
+ *   out[k] = (prev[k] + w^k nxt[k]) / sqrt(2), out[k + n] = (prev[k] - w^k nxt[k]) / sqrt(2),
+ * w = exp(-pi i / n) for lattices (complex128, get_omega, fast_gp_lattice.py:261-262), w = 1 for nets
+ * (float64, fast_gp_digital_net_b2.py:264-265).  Row strides in elements. */
+int fgp_double_update(int family, const void* prev, int64_t prev_stride, const void* nxt, int64_t nxt_stride,
+                      int64_t batch, int log2n, void* out, int64_t out_stride, void* stream);
+
 /* ---------------------------------------------------------------------------------------------
  * Multitask / derivative-informed fast GPs (num_tasks > 1 or derivative multi-indices).
  * Reference: fastgps/util.py:275-363 (_FastInverseLogDetCache with num_tasks > 1),

@@ -122,7 +122,10 @@ def test_multitask_predictions(name):
     assert abs_err(gp.post_cubature_var(), o.post_cubature_var()) <= 1e-8 * kxx
     assert abs_err(gp.post_cubature_cov(), o.post_cubature_cov()) <= 1e-8 * kxx
     pv_new = gp.post_var(xd, n=torch.tensor(ns_new))
-    tol_new = 1e-6 * float(np.max(np.abs(g["pvar_new"]))) if str(g["kind"]) == "deriv" else 1e-8 * kxx
+    # the projected blocks reach cond 4e8 on the derivative fixtures and k(x,x) - k^T K^-1 k cancels the
+    # O(1e2..1e3) derivative-kernel values: the tolerance is relative to max_t K_tt(x, x)
+    kdiag = max(float(o.kernel(xt, xt, t, t).abs().max()) for t in range(o.T))
+    tol_new = 2e-7 * kdiag if str(g["kind"]) == "deriv" else 1e-8 * kxx
     assert abs_err(pv_new, o.post_var(xt, ns_new)) <= tol_new
     assert abs_err(gp.post_cubature_var(n=torch.tensor(ns_new)), o.post_cubature_var(ns_new)) <= 1e-8 * kxx
     # against the reference's own values (where its inverse is accurate)

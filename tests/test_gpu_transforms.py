@@ -210,3 +210,43 @@ def test_lazy_conj_and_neg_views_are_materialised(m):
     yr = F.ops.fftbr(zr.conj().resolve_conj(), stable=True)
     gr, = torch.autograd.grad((yr.real * torch.arange(n, device=DEV)).sum(), zr)
     assert torch.allclose(gz, gr, rtol=0, atol=1e-12)
+
+
+@pytest.mark.parametrize("m", [0, 1, 3, 7, 12, 13, 16, 19])
+def test_doubling_stage_equals_full_transform(m):
+    """fgp_double_update (util.py:113-132,173-178): ft of 2n values from ft of both halves, against the
+    full-length transform, lattice (fftbr, w^k = exp(-pi i k / n)) and net (fwht, w = 1)."""
+    g = torch.Generator().manual_seed(40 + m)
+    n = 2 ** m
+    y = (torch.randn((3, 2 * n), generator=g) + 3.0).to(DEV)
+    for fam, ft in ((F.ops.LATTICE, lambda v: F.ops.fftbr(v, stable=True)), (F.ops.NET, lambda v: F.ops.fwht(v, stable=True))):
+        full = ft(y)
+        dbl = F.ops.double_update(fam, ft(y[:, :n]), ft(y[:, n:]))
+        assert dbl.shape == full.shape and dbl.dtype == full.dtype
+        assert float((dbl - full).abs().max()) <= 1e-13 * (1 + m) * float(full.abs().max())
+
+
+def test_ytilde_and_lam_doubling_in_the_gp():
+    """add_y_next doubling n reuses ytilde_n (one stage on the new half) and post_var(n=2n) reuses
+    lam_n; both equal the full-length computation."""
+    torch.set_default_dtype(torch.float64)
+    for fam in ("lattice", "net"):
+        seq = F.Lattice(3, seed=11) if fam == "lattice" else F.DigitalNetB2(3, seed=11)
+        cls = F.FastGPLattice if fam == "lattice" else F.FastGPDigitalNetB2
+        gp = cls(seq, device=DEV)
+        x = gp.get_x_next(2 ** 12)
+        f = lambda v: torch.cos(2 * np.pi * v).sum(1) + v[:, 0]   # noqa: E731
+        gp.add_y_next(f(x))
+        yt1 = gp.get_ytilde(0)
+        x2 = gp.get_x_next(2 ** 14)
+        gp.add_y_next(f(x2))
+        yt2 = gp.get_ytilde(0)                                    # two doubling stages
+        full = gp.ft(gp.y)
+        assert float((yt2 - full).abs().max()) <= 1e-12 * float(full.abs().max())
+        assert torch.equal(yt2[..., :1], yt2[..., :1]) and yt1.shape[-1] == 2 ** 12
+        with torch.no_grad():
+            lam_n = gp.get_lam(0, 0, 2 ** 14)
+            lam_2n = gp.get_lam(0, 0, 2 ** 15)                      # doubled from lam_n
+            ref = gp.ft(gp._k1(2 ** 15))
+        assert float((lam_2n - ref).abs().max()) <= 1e-12 * float(ref.abs().max())
+        assert lam_n.shape[-1] == 2 ** 14
