@@ -114,6 +114,7 @@ _SIGNATURES = {
                         _c_vp],
     "fgp_post_mean_batched": [_P_PRED, _c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp],
     "fgp_post_var_batched": [_P_PRED, _c_vp, _c_i64, _c_i64, _c_pd, _c_vp, _c_vp, _c_vp, _c_vp],
+    "fgp_net_points": [_c_vp, _c_int, _c_vp, _c_i64, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_vp],
     "fgp_double_update": [_c_int, _c_vp, _c_i64, _c_vp, _c_i64, _c_i64, _c_int, _c_vp, _c_i64, _c_vp],
     "fgp_mt_parts": [_c_int, _c_vp, _c_i64, _c_i64, _c_vp, _c_i64, _c_i64, _c_int, _c_int, _c_int, _c_vp, _c_vp,
                      _c_vp, _c_int, _c_vp, _c_vp],

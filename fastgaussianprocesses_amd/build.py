@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB_DIR = os.path.join(HERE, "_lib")
 LIB = os.path.join(LIB_DIR, "libfgp_hip.so")
-SOURCES = ["fgp_runtime.hip", "fgp_transforms.hip", "fgp_nll.hip", "fgp_predict.hip", "fgp_multitask.hip"]
+SOURCES = ["fgp_runtime.hip", "fgp_transforms.hip", "fgp_nll.hip", "fgp_predict.hip", "fgp_multitask.hip", "fgp_points.hip"]
 HEADERS = ["fgp_common.h", "fgp_runtime.h"]
 ARCH = os.environ.get("FGP_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

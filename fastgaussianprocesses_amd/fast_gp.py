@@ -1039,7 +1039,18 @@ class FastGPLattice(AbstractFastGP):
             "each seq should have randomize in ['FALSE','SHIFT']"
 
     def _sample(self, n_min, n_max):
-        x = torch.from_numpy(np.asarray(self.seq(n_min=int(n_min), n_max=int(n_max)), dtype=np.float64)).to(self.device)
+        return self._sample_seq(self.seq, n_min, n_max)
+
+    def _sample_seq(self, seq, n_min, n_max):
+        """Points [n_min, n_max) of a natural-order lattice: on the device (fgp_lattice_points,
+        bit-identical to seqs.Lattice) for this package's generator, else from the seq object."""
+        if isinstance(seq, _seqs.Lattice) and n_max > n_min:
+            z = [int(v) for v in seq.z[:self.d]]
+            bits = max(1, int(n_max - 1).bit_length())
+            if all(0 < v < 2 ** (53 - bits) for v in z) and np.all((seq.shift >= 0) & (seq.shift < 1)):
+                x = ops.lattice_points(z, seq.shift, int(n_min), int(n_max), device=self.device)
+                return x, x
+        x = torch.from_numpy(np.asarray(seq(n_min=int(n_min), n_max=int(n_max)), dtype=np.float64)).to(self.device)
         return x, x
 
     def _tbits(self):
@@ -1133,7 +1144,15 @@ class FastGPDigitalNetB2(AbstractFastGP):
             "seq should have randomize in ['FALSE','DS','LMS','LMS_DS']"
 
     def _sample(self, n_min, n_max):
-        xb = torch.from_numpy(np.asarray(self.seq(n_min=int(n_min), n_max=int(n_max), return_binary=True))
+        return self._sample_seq(self.seq, n_min, n_max)
+
+    def _sample_seq(self, seq, n_min, n_max):
+        """Points [n_min, n_max) of a natural-order digital net: on the device (fgp_net_points,
+        generating-matrix XOR, bit-identical to seqs.DigitalNetB2) for this package's generator, else from
+        the seq object (qmcpy's return_binary=True interface)."""
+        if isinstance(seq, _seqs.DigitalNetB2) and n_max > n_min and int(n_max - 1).bit_length() <= seq.C.shape[1]:
+            return ops.net_points(seq.C, seq.shift, seq.t, int(n_min), int(n_max), self.device)
+        xb = torch.from_numpy(np.asarray(seq(n_min=int(n_min), n_max=int(n_max), return_binary=True))
                               .astype(np.int64)).to(self.device)
         return self._convert_from_b(xb), xb
 

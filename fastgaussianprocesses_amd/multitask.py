@@ -237,13 +237,7 @@ class MultiTaskFastGP(AbstractFastGP):
                 assert all(a >= 2 for a in self._alphas), "using derivatives requires (alpha>=2).all()"
 
     def _sample_task(self, l, n_min, n_max):
-        seq = self.seqs[l]
-        if self._FAMILY == ops.LATTICE:
-            x = torch.from_numpy(np.asarray(seq(n_min=int(n_min), n_max=int(n_max)), dtype=np.float64)).to(self.device)
-            return x, x
-        xb = torch.from_numpy(np.asarray(seq(n_min=int(n_min), n_max=int(n_max), return_binary=True))
-                              .astype(np.int64)).to(self.device)
-        return xb * 2.0 ** (-self.t), xb
+        return self._sample_seq(self.seqs[l], n_min, n_max)      # the family's generator (device when own)
 
     def _ensure_task_points(self, l, n):
         n = int(n)

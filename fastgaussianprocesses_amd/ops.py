@@ -14,6 +14,8 @@ With stable=True the mean-centring of AbstractFastGP.ft/ift happens inside the k
 """
 import math
 
+import numpy as np
+
 import torch
 
 from . import _native as N
@@ -256,6 +258,20 @@ def lattice_points(z, shift, n_min, n_max, device=None):
     x = torch.empty((n_max - n_min, d), dtype=torch.float64, device=shift.device)
     N.call("fgp_lattice_points", N.int64_array(z), N.ptr(shift), int(n_min), int(n_max), d, N.ptr(x), _stream(shift))
     return x
+
+
+def net_points(C, shift, t, n_min, n_max, device):
+    """Natural-order digital net points on the device (fgp_net_points), bit-identical to
+    seqs.DigitalNetB2: (x [n, d] float64, xb [n, d] int64).  C: [d, mcols] t-bit ints, shift: [d]."""
+    C = torch.as_tensor(np.asarray(C, dtype=np.uint64).astype(np.int64)).to(device).contiguous()
+    sh = torch.as_tensor(np.asarray(shift, dtype=np.uint64).astype(np.int64)).to(device).contiguous()
+    require_device(C, "net_points")
+    d, mcols = C.shape
+    xb = torch.empty((n_max - n_min, d), dtype=torch.int64, device=C.device)
+    x = torch.empty((n_max - n_min, d), dtype=torch.float64, device=C.device)
+    N.call("fgp_net_points", N.ptr(C), mcols, N.ptr(sh), int(n_min), int(n_max), d, int(t), N.ptr(xb), N.ptr(x),
+           _stream(C))
+    return x, xb
 
 
 def lattice_parts_gen(z, shift, alphas, n):

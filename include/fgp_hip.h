@@ -313,6 +313,13 @@ int fgp_kernel_rows(int family, const double* xt, int64_t N, const void* z, int6
 
 
 
+
+/* Natural-order digital net points (FastGPDigitalNetB2's sequences, fast_gp_digital_net_b2.py:266-273):
+ * xb[i - n_min][j] = XOR_{k: bit k of i} C[j][k] XOR shift[j] (t-bit ints), x = xb 2^-t; C [d][mcols] and
+ * shift [d] are DEVICE uint64 arrays; xb [n][d] int64 and / or x [n][d] float64 (either may be NULL). */
+int fgp_net_points(const uint64_t* C, int mcols, const uint64_t* shift, int64_t n_min, int64_t n_max, int d, int t,
+                   int64_t* xb, double* x, void* stream);
+
 /* One DIT doubling stage (_LamCaches / _YtildeCache, fastgps/util.py:113-132,173-178): from ft of the first
  * n = 2^log2n values (prev) and of the next n (nxt) to ft of all 2n (out [batch][2n]):
  *   out[k] = (prev[k] + w^k nxt[k]) / sqrt(2), out[k + n] = (prev[k] - w^k nxt[k]) / sqrt(2),

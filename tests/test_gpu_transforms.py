@@ -250,3 +250,18 @@ def test_ytilde_and_lam_doubling_in_the_gp():
             ref = gp.ft(gp._k1(2 ** 15))
         assert float((lam_2n - ref).abs().max()) <= 1e-12 * float(ref.abs().max())
         assert lam_n.shape[-1] == 2 ** 14
+
+
+@pytest.mark.parametrize("d,t", [(1, 32), (3, 32), (5, 53), (2, 63)])
+def test_device_point_generators_are_bit_identical(d, t):
+    """fgp_lattice_points / fgp_net_points (the generators get_x_next uses for this package's
+    sequences) against the host restatement of qmcpy's natural-order generators, arbitrary ranges."""
+    lat = F.Lattice(d, seed=5)
+    net = F.DigitalNetB2(d, seed=5, t=t)
+    for n0, n1 in ((0, 1), (0, 8), (8, 16), (1024, 4096), (0, 2 ** 17)):
+        xl = F.ops.lattice_points([int(v) for v in lat.z[:d]], lat.shift, n0, n1, device=DEV)
+        assert np.array_equal(xl.cpu().numpy(), lat(n_min=n0, n_max=n1))
+        x, xb = F.ops.net_points(net.C, net.shift, t, n0, n1, DEV)
+        ref = net(n_min=n0, n_max=n1, return_binary=True).astype(np.int64)
+        assert np.array_equal(xb.cpu().numpy(), ref)
+        assert np.array_equal(x.cpu().numpy(), ref.astype(np.float64) * 2.0 ** (-t))
