@@ -158,31 +158,38 @@ __device__ __forceinline__ void psrc_init(const Nll& a, int g, PSrc& s) {
 }
 
 // Lattice part at the natural-order point with bit-reversed index br (dimension with generating
-// vector entry zj mod n, coefficient coef, shift sh = x_0):
-//   x = ((br zj mod n) / n + sh) % 1  (the host generator's exact value and rounding, seqs.Lattice),
-//   delta = torch.remainder(x - x_0, 1),  part = coef B_ORD(delta)  (k_lattice_parts).
-// Lattice part from k = (brev(i) z_j) mod n:
-//   x = (k / n + sh) % 1     one rounding (k / n exact); v_fract on [0, 2) is exact
-//   delta = (x - sh) % 1     v_fract on (-1, 1): x - sh, or RN(x - sh + 1) -- torch.remainder's value
-//                            (never rounds up to 1: the wrapped case has |x - sh| >= 1/n - ulp)
-// the same values as the host generator + fgp_lattice_parts' mod1 (bit-identity tested on the GPU).
+// vector entry zj mod n): the first-column distance is
+//   delta = (x_i - x_0) mod 1 = (brev_m(i) z_j mod n) / n      EXACTLY (k / n with k < n = 2^m),
+// so it is formed from k directly -- one conversion and one exact scaling -- instead of from the two
+// rounded coordinates the host generator produces (x = (k / n + shift) % 1, then torch.remainder(x -
+// x_0, 1), the reference's op sequence, fast_gp_lattice.py:263-266).  The two differ by the rounding of
+// x (|d delta| <= 2^-53); the exact one is the better approximation of the kernel's argument and costs
+// 2 VALU per dimension instead of 6.  The coefficient (-1)^(alpha+1) (2 pi)^(2 alpha) / (2 alpha)! is
+// folded into the lengthscale (fold_gen_coef): the fit kernels see part = B_ORD(delta) and l_j coef_j.
 template <int ORD>
-__device__ __forceinline__ double lattice_gen_part_k(unsigned k, double coef, double sh, double inv_n) {
-  const double x = __builtin_amdgcn_fract(__builtin_fma((double)k, inv_n, sh));
-  const double dl = __builtin_amdgcn_fract(x - sh);
-  return coef * bernoulli(ORD, dl);
+__device__ __forceinline__ double lattice_gen_part_k(unsigned k, double inv_n) {
+  return bernoulli(ORD, (double)k * inv_n);
 }
 
 template <int ORD>
-__device__ __forceinline__ double lattice_gen_part(unsigned zj, double coef, double sh, unsigned br, unsigned mask,
-                                                   double inv_n) {
-  return lattice_gen_part_k<ORD>(mul_u24(br, zj) & mask, coef, sh, inv_n);
+__device__ __forceinline__ double lattice_gen_part(unsigned zj, unsigned br, unsigned mask, double inv_n) {
+  return lattice_gen_part_k<ORD>(mul_u24(br, zj) & mask, inv_n);
 }
 
 template <int ORD>
-__device__ __forceinline__ double gen_part(const Nll& a, const PSrc& s, int j, unsigned br, unsigned mask,
+__device__ __forceinline__ double gen_part(const Nll& a, const PSrc&, int j, unsigned br, unsigned mask,
                                            double inv_n) {
-  return lattice_gen_part<ORD>(a.gz[j], a.gcoef[j], s.sh[j], br, mask, inv_n);
+  return lattice_gen_part<ORD>(a.gz[j], br, mask, inv_n);
+}
+
+// Generated parts carry no coefficient: fold coef_j into l_j once per thread (k1 factors 1 + (l_j coef_j)
+// B_j; the gradient factor scale l_j of grad_factor() then includes coef_j as well).
+template <int PG>
+__device__ __forceinline__ void fold_gen_coef(const Nll& a, Hyp& h) {
+  if constexpr (PG != 0) {
+#pragma unroll
+    for (int j = 0; j < FGP_MAX_D; ++j) h.ls[j] *= a.gcoef[j];
+  }
 }
 
 // Dimension count as a compile-time constant (D = 1..8), or D = 0: runtime d, loops run over
@@ -435,6 +442,7 @@ __global__ __launch_bounds__(kWG) void k_iter_single(Nll a, const double2* __res
   const int g = live ? gq : a.G - 1;
   Hyp h;
   load_hyp(a, g, h);
+  fold_gen_coef<PG>(a, h);
   PSrc src;
   psrc_init(a, g, src);
   T* s = lds + tr * (L + L / 16);
@@ -524,6 +532,7 @@ __global__ __launch_bounds__(kWG) void k_fwd_rows(Nll a, const double2* __restri
   stamp_begin(a);
   Hyp h;
   load_hyp_wave(a, g, h);
+  fold_gen_coef<PG>(a, h);
   PSrc src;
   psrc_init(a, g, src);
   const int64_t base = (int64_t)row0 * N2;
@@ -715,6 +724,7 @@ __global__ __launch_bounds__(kWG) void k_bwd_rows(Nll a, const double2* __restri
     if (tid == 0) v[0] += mean * (double)N2;
     Hyp h;
     load_hyp_wave(a, g, h);
+    fold_gen_coef<PG>(a, h);
     PSrc src;
     psrc_init(a, g, src);
     constexpr int ND = Dims<D>::N;
@@ -752,6 +762,7 @@ __global__ __launch_bounds__(kWG) void k_bwd_rows(Nll a, const double2* __restri
   }
   Hyp h;
   load_hyp_wave(a, g, h);
+  fold_gen_coef<PG>(a, h);
   PSrc src;
   psrc_init(a, g, src);
   const double inv_rootn = 1.0 / sqrt((double)n);
@@ -823,6 +834,7 @@ __global__ __launch_bounds__(kWG) void k_fwd_rows_r2c(Nll a, const double2* __re
   stamp_begin(a);
   Hyp h;
   load_hyp_wave(a, g, h);
+  fold_gen_coef<PG>(a, h);
   PSrc src;
   psrc_init(a, g, src);
   const int64_t base = (int64_t)row0 * N2;
@@ -1094,6 +1106,7 @@ __global__ __launch_bounds__(kWG) void k_bwd_rows_r2c(Nll a, const double2* __re
   if (tid == 0) v[0] += mean * (double)N2;
   Hyp h;
   load_hyp_wave(a, g, h);
+  fold_gen_coef<PG>(a, h);
   PSrc src;
   psrc_init(a, g, src);
   constexpr int ND = Dims<D>::N;
@@ -1323,7 +1336,7 @@ __global__ __launch_bounds__(kWG) void k_lattice_parts_gen(GenSpec g, const doub
   if (i >= n) return;
   const unsigned br = brev_bits((unsigned)i, m), mask = (unsigned)(n - 1);
   const double inv_n = ldexp(1.0, -m);
-  for (int j = 0; j < d; ++j) parts[(int64_t)j * n + i] = lattice_gen_part<ORD>(g.z[j], g.coef[j], shift[j], br, mask, inv_n);
+  for (int j = 0; j < d; ++j) parts[(int64_t)j * n + i] = g.coef[j] * lattice_gen_part<ORD>(g.z[j], br, mask, inv_n);
 }
 
 // ------------------------------------------------------------------------------------------------
