@@ -255,24 +255,47 @@ STAGES = ("k_fwd_rows", "k_fwd_cols", "k_bwd_rows")
 
 
 def r2c_active(n):
-    """The lattice fit runs the half-length (R2C) kernels for n >= 2^17 unless FGP_R2C=0
-    (csrc/fgp_nll.hip to_nll)."""
-    return n >= 2 ** 17 and os.environ.get("FGP_R2C", "1")[:1] != "0"
+    """The lattice fit runs the half-length (R2C) or real-even (RE) kernels for n >= 2^17 unless
+    FGP_R2C=0 (csrc/fgp_nll.hip to_nll)."""
+    return n >= 2 ** 17 and os.environ.get("FGP_R2C", "2")[:1] != "0"
 
 
-def stage_bytes(n, d, P, parts_array):
+def fit_variant(n, parts_array):
+    """'re' (real-even kernels: n >= 2^17 with regenerated parts, the default), 'r2c' (FGP_R2C=1, or a
+    parts array) or 'full' (n < 2^17 or FGP_R2C=0) -- the choice of csrc/fgp_nll.hip to_nll."""
+    if not r2c_active(n):
+        return "full"
+    if parts_array or os.environ.get("FGP_R2C", "2")[:1] == "1":
+        return "r2c"
+    return "re"
+
+
+def fit_grid(n, P, variant):
+    """Workgroups per fit launch and threads per workgroup of each stage kernel."""
+    if variant == "re":
+        g = P * max(1, n // 16384)
+        return g, {"k_fwd_rows": 512, "k_fwd_cols": 256, "k_bwd_rows": 512}
+    g = P * max(1, (n // 2 if variant == "r2c" else n) // 4096)
+    return g, {k: 256 for k in STAGES}
+
+
+def stage_bytes(n, d, P, parts_array, variant=None):
     """Algorithmic (compulsory) HBM bytes of one launch of each fit-iteration kernel over P lattice
-    problems (complex128 intermediate `work` of L = n complex values, L = n/2 for the half-length R2C
-    kernels; float64 Y; DESIGN.md 'Kernels'):
-      k_fwd_rows: write work 16L (+ read parts 8nd when not regenerated)
-      k_fwd_cols: read work 16L + write work 16L + read Y: 8n full-length; 4n R2C (Y = |y~|^2 is even,
-                  Y_k = Y_{n-k}, and the kernel reads it only at each mirror pair's primary element:
-                  the n/2 values Y_k, Y_{k+n/2} of the primaries k)
-      k_bwd_rows: read work 16L (+ read parts 8nd)"""
+    problems (complex128 intermediate `work` of L complex values; float64 Y; DESIGN.md 'Kernels'):
+      full (L = n):  rows 16L write (+ 8nd parts), cols 16L + 16L + Y 8n, bwd rows 16L (+ 8nd)
+      r2c (L = n/2): as full with Y 4n (Y = |y~|^2 is even, Y_k = Y_{n-k}, and the kernel reads it only
+                     at each mirror pair's primary element: the n/2 values Y_k, Y_{k+n/2})
+      re (L = n/4, columns [0, N2/2) of the n/2-point transform, N1 = n/8192 rows):
+                     rows 16L + the Nyquist column 16 N1; cols 16L + 16L + Y 4n (the pairs (Y_2k, Y_2k+1)
+                     of its frequencies) + Nyquist 16 N1 read + 4 N1 written; bwd rows 16L + 4 N1"""
+    variant = variant or fit_variant(n, parts_array)
     pb = 8 * n * d if parts_array else 0
-    r2c = r2c_active(n)
-    L = n // 2 if r2c else n
-    yb = 4 * n if r2c else 8 * n
+    if variant == "re":
+        L, N1 = n // 4, n // 8192
+        return {"k_fwd_rows": (16 * L + 16 * N1) * P, "k_fwd_cols": (32 * L + 4 * n + 20 * N1) * P,
+                "k_bwd_rows": (16 * L + 4 * N1) * P}
+    L = n // 2 if variant == "r2c" else n
+    yb = 4 * n if variant == "r2c" else 8 * n
     return {"k_fwd_rows": (16 * L + pb) * P, "k_fwd_cols": (32 * L + yb) * P, "k_bwd_rows": (16 * L + pb) * P}
 
 
@@ -299,7 +322,7 @@ def roofline_fit_kernels(F, shifts, iters):
     eng.run(0, 2)
     torch.cuda.synchronize()
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(iters)]
-    grid = eng.G * max(1, (n // 2 if r2c_active(n) else n) // 4096)      # workgroups per fit launch
+    grid, _ = fit_grid(n, eng.G, fit_variant(n, eng.gen is None))      # workgroups per fit launch
     stamps = torch.zeros((iters, 3, grid, 5), dtype=torch.int64, device=dev)   # fgp_nll_desc.stamps
     torch.cuda._sleep(int(2.4e9 * 4e-4 * iters))
     for it in range(iters):
@@ -454,17 +477,17 @@ def main():
     P = len(shifts.gps)
     sb = stage_bytes(n, d, P, parts_array)
     dom = max(STAGES, key=lambda k: us[k])
-    r2c = r2c_active(n)
-    kname = dom + ("_r2c" if r2c else "")
-    grid_wg = P * (n // 2 if r2c else n) // 4096
+    variant = fit_variant(n, parts_array)
+    kname = dom + {"re": "_re", "r2c": "_r2c", "full": ""}[variant]
+    grid_wg, wg_threads = fit_grid(n, P, variant)
     # achieved / frac are priced on the rocprofv3 kernel-trace average of this same command (committed
     # under profiles/) when it is there -- the duration the profiler reports, including the dispatch
     # ramp; the live device-clock figure (first workgroup start to last wave end) is reported beside it
-    us_rp = rocprof_avg_us(kname, grid_wg * 256)
+    us_rp = rocprof_avg_us(kname, grid_wg * wg_threads[dom])
     us_price = us_rp if us_rp is not None else us[dom]
     ach = sb[dom] / (us_price * 1e-6) / 1e9
     roof = {"bound": "hbm", "kernel": kname, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic(kname, grid_wg * 256),
+            "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic(kname, grid_wg * wg_threads[dom]),
             "traffic_source": os.path.relpath(PMC_SUMMARY, ROOT),
             "algorithmic_bytes": sb[dom],
             "avg_us": us_price, "avg_us_source": ("rocprofv3 --kernel-trace average, %s" % os.path.relpath(
@@ -474,7 +497,8 @@ def main():
             "frac_device_clock": sb[dom] / (us[dom] * 1e-6) / 1e9 / HBM_PEAK_GBS,
             "avg_us_events": us_ev[dom],
             "launch": "%d problems x n=2^%d (grid %d workgroups)" % (P, args.log2n, grid_wg),
-            "transform": "half-length R2C (n/2 complex)" if r2c else "full-length (n complex)",
+            "transform": {"re": "real-even: n/2-point transform, columns [0, N2/2) (n/4 complex)",
+                          "r2c": "half-length R2C (n/2 complex)", "full": "full-length (n complex)"}[variant],
             "kernels": {k: {"avg_us": us[k], "avg_us_events": us_ev[k], "bytes": sb.get(k),
                             "GB/s": (sb[k] / (us[k] * 1e-6) / 1e9) if k in sb else None} for k in us},
             "parts": "array" if parts_array else "regenerated (FGP_PARTS_LATTICE)",

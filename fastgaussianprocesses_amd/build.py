@@ -13,8 +13,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB_DIR = os.path.join(HERE, "_lib")
 LIB = os.path.join(LIB_DIR, "libfgp_hip.so")
-SOURCES = ["fgp_runtime.hip", "fgp_transforms.hip", "fgp_nll.hip", "fgp_predict.hip", "fgp_multitask.hip", "fgp_points.hip"]
-HEADERS = ["fgp_common.h", "fgp_runtime.h"]
+OBJ_DIR = os.path.join(LIB_DIR, "obj")
+SOURCES = ["fgp_runtime.hip", "fgp_transforms.hip", "fgp_nll.hip", "fgp_nll_re.hip", "fgp_predict.hip", "fgp_multitask.hip", "fgp_points.hip"]
+HEADERS = ["fgp_common.h", "fgp_runtime.h", "fgp_nll.h"]
 ARCH = os.environ.get("FGP_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
@@ -34,14 +35,19 @@ def needs_build():
 def build(force=False, verbose=True):
     if not force and not needs_build():
         return LIB
-    os.makedirs(LIB_DIR, exist_ok=True)
+    os.makedirs(OBJ_DIR, exist_ok=True)
     objs = []
     procs = []
+    hdr_t = max(os.path.getmtime(p) for p in _inputs() if not p.endswith(".hip"))
     for src in SOURCES:
-        obj = os.path.join(LIB_DIR, src.replace(".hip", ".o"))
-        cmd = [HIPCC, "-O3", "-std=c++17", "-ffp-contract=off", "--offload-arch=" + ARCH, "-fPIC", "-c", os.path.join(CSRC, src), "-o", obj]
-        procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
+        obj = os.path.join(OBJ_DIR, src.replace(".hip", ".o"))
         objs.append(obj)
+        srcp = os.path.join(CSRC, src)
+        # per-source objects (git- and gpurun-ignored): a source is recompiled when it or a header changed
+        if not force and os.path.isfile(obj) and os.path.getmtime(obj) > max(hdr_t, os.path.getmtime(srcp)):
+            continue
+        cmd = [HIPCC, "-O3", "-std=c++17", "-ffp-contract=off", "--offload-arch=" + ARCH, "-fPIC", "-c", srcp, "-o", obj]
+        procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
     for cmd, p in procs:
         out, _ = p.communicate()
         if p.returncode != 0:
@@ -52,8 +58,6 @@ def build(force=False, verbose=True):
     if r.returncode != 0:
         raise RuntimeError("link failed: %s\n%s" % (" ".join(cmd), r.stdout.decode(errors="replace")))
     os.replace(tmp, LIB)
-    for o in objs:
-        os.remove(o)
     if verbose:
         print("built", LIB)
     return LIB

@@ -26,12 +26,8 @@
 //   then k_fit_step (one workgroup: deterministic reduction of the per-block partials, loss
 //   assembly, histories, Rprop update).
 #include <cstdlib>
-#include <cmath>
-#include <type_traits>
 
-#include "fgp_common.h"
-#include "fgp_runtime.h"
-#include "../../include/fgp_hip.h"
+#include "fgp_nll.h"
 
 namespace fgp {
 
@@ -70,364 +66,6 @@ __global__ __launch_bounds__(kWG) void k_net_parts(const int64_t* __restrict__ x
 
 // ------------------------------------------------------------------------------------------------
 // fused MLL
-struct Nll {
-  int log2n, d, G, nb, nq;
-  const double* parts;
-  int64_t parts_stride;
-  const double* ysq;
-  int64_t ysq_stride;
-  const double* raw;
-  int scale_off, scale_pp, ls_off, ls_pp, ls_pd, noise_off, noise_pp;
-  double logdet_weight;
-  void* grad_lam;
-  void* work;
-  double* partials;
-  // lattice parts generator (FGP_PARTS_LATTICE); pg = its Bernoulli order (0: parts array)
-  int pgen, pg;
-  int gorder[FGP_MAX_D];
-  double gcoef[FGP_MAX_D];
-  unsigned gz[FGP_MAX_D];        // z_j mod n
-  const double* gshift;
-  int64_t gshift_stride;
-  int r2c;                       // lattice, n >= 2^17: half-length (R2C) fit kernels
-  unsigned long long* stamps;    // optional device-clock timing of the launch (fgp_nll_desc.stamps)
-};
-
-// Device-clock kernel timing (fgp_nll_desc.stamps; off when NULL -- a uniform branch on a kernel
-// argument): plain vector stores of the wall clock into the launch's record [gridDim.x][1 + kWG/64]:
-// [b][0] = start of workgroup b (its first wave), [b][1 + w] = end of its wave w.  No atomics (one
-// contended address serialises thousands of them and slows the kernel being timed).
-constexpr int kStampStride = 1 + kWG / 64;
-__device__ __forceinline__ void stamp_begin(const Nll& a) {
-  if (a.stamps && threadIdx.x == 0) a.stamps[(int64_t)blockIdx.x * kStampStride] = (unsigned long long)wall_clock64();
-}
-__device__ __forceinline__ void stamp_end(const Nll& a) {
-  if (a.stamps && (threadIdx.x & 63) == 0)
-    a.stamps[(int64_t)blockIdx.x * kStampStride + 1 + (threadIdx.x >> 6)] = (unsigned long long)wall_clock64();
-}
-
-struct Hyp {
-  double scale, noise;
-  double ls[FGP_MAX_D];
-};
-
-__device__ __forceinline__ void load_hyp(const Nll& a, int g, Hyp& h) {
-  h.scale = exp(a.raw[a.scale_off + (a.scale_pp ? g : 0)]);
-  h.noise = exp(a.raw[a.noise_off + (a.noise_pp ? g : 0)]);
-  const int lb = a.ls_off + (a.ls_pp ? g : 0) * (a.ls_pd ? a.d : 1);
-#pragma unroll
-  for (int j = 0; j < FGP_MAX_D; ++j) h.ls[j] = (j < a.d) ? exp(a.raw[lb + (a.ls_pd ? j : 0)]) : 0.0;
-}
-
-__device__ __forceinline__ double read_lane(double v, int lane) {
-  const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
-  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
-  return __hiloint2double(hi, lo);
-}
-
-// load_hyp for a problem index g that is uniform over the wave: one exp per parameter, evaluated
-// lane-parallel (lane 0 scale, 1 noise, 2 + j lengthscale j) and broadcast, instead of 2 + d
-// exps in every lane.  Same libm exp, so the same values as load_hyp.
-__device__ __forceinline__ void load_hyp_wave(const Nll& a, int g, Hyp& h) {
-  const int lane = threadIdx.x & 63;
-  const int lb = a.ls_off + (a.ls_pp ? g : 0) * (a.ls_pd ? a.d : 1);
-  int idx = -1;
-  if (lane == 0) idx = a.scale_off + (a.scale_pp ? g : 0);
-  else if (lane == 1) idx = a.noise_off + (a.noise_pp ? g : 0);
-  else if (lane < 2 + a.d) idx = lb + (a.ls_pd ? lane - 2 : 0);
-  const double e = exp(idx >= 0 ? a.raw[idx] : 0.0);
-  h.scale = read_lane(e, 0);
-  h.noise = read_lane(e, 1);
-#pragma unroll
-  for (int j = 0; j < FGP_MAX_D; ++j) h.ls[j] = (j < a.d) ? read_lane(e, 2 + j) : 0.0;
-}
-
-// ------------------------------------------------------------------ parts source (array / generated)
-// Per-problem source of the kernel parts: the parts array, or (FGP_PARTS_LATTICE) the lattice point
-// x_0 = shift from which the parts of element i are regenerated with fgp_lattice_parts' arithmetic.
-struct PSrc {
-  const double* pg;
-  double sh[FGP_MAX_D];
-};
-
-__device__ __forceinline__ void psrc_init(const Nll& a, int g, PSrc& s) {
-  s.pg = a.parts + (int64_t)g * a.parts_stride;
-#pragma unroll
-  for (int j = 0; j < FGP_MAX_D; ++j)
-    s.sh[j] = (a.pgen && j < a.d) ? a.gshift[(int64_t)g * a.gshift_stride + j] : 0.0;   // (x_0 = shift)
-}
-
-// Lattice part at the natural-order point with bit-reversed index br (dimension with generating
-// vector entry zj mod n): the first-column distance is
-//   delta = (x_i - x_0) mod 1 = (brev_m(i) z_j mod n) / n      EXACTLY (k / n with k < n = 2^m),
-// so it is formed from k directly -- one conversion and one exact scaling -- instead of from the two
-// rounded coordinates the host generator produces (x = (k / n + shift) % 1, then torch.remainder(x -
-// x_0, 1), the reference's op sequence, fast_gp_lattice.py:263-266).  The two differ by the rounding of
-// x (|d delta| <= 2^-53); the exact one is the better approximation of the kernel's argument and costs
-// 2 VALU per dimension instead of 6.  The coefficient (-1)^(alpha+1) (2 pi)^(2 alpha) / (2 alpha)! is
-// folded into the lengthscale (fold_gen_coef): the fit kernels see part = B_ORD(delta) and l_j coef_j.
-template <int ORD>
-__device__ __forceinline__ double lattice_gen_part_k(unsigned k, double inv_n) {
-  return bernoulli(ORD, (double)k * inv_n);
-}
-
-template <int ORD>
-__device__ __forceinline__ double lattice_gen_part(unsigned zj, unsigned br, unsigned mask, double inv_n) {
-  return lattice_gen_part_k<ORD>(mul_u24(br, zj) & mask, inv_n);
-}
-
-template <int ORD>
-__device__ __forceinline__ double gen_part(const Nll& a, const PSrc&, int j, unsigned br, unsigned mask,
-                                           double inv_n) {
-  return lattice_gen_part<ORD>(a.gz[j], br, mask, inv_n);
-}
-
-// Generated parts carry no coefficient: fold coef_j into l_j once per thread (k1 factors 1 + (l_j coef_j)
-// B_j; the gradient factor scale l_j of grad_factor() then includes coef_j as well).
-template <int PG>
-__device__ __forceinline__ void fold_gen_coef(const Nll& a, Hyp& h) {
-  if constexpr (PG != 0) {
-#pragma unroll
-    for (int j = 0; j < FGP_MAX_D; ++j) h.ls[j] *= a.gcoef[j];
-  }
-}
-
-// Dimension count as a compile-time constant (D = 1..8), or D = 0: runtime d, loops run over
-// FGP_MAX_D zero-padded dimensions (part 0 and lengthscale 0, so a padded factor 1 + l p is exactly 1).
-template <int D> struct Dims { static constexpr int N = D ? D : FGP_MAX_D; };
-template <int D> __device__ __forceinline__ bool dim_on(const Nll& a, int j) { return D ? true : j < a.d; }
-
-// Parts source as a compile-time choice: PG = 0 reads the parts array, PG = 2/4/6/8 regenerates the
-// lattice parts with Bernoulli order PG (FGP_PARTS_LATTICE, one order for every dimension).
-// parts of element i (p[j], zero-padded)
-template <int PG, int D>
-__device__ __forceinline__ void parts_one(const Nll& a, const PSrc& s, int64_t n, int64_t i, double* p) {
-  if constexpr (PG != 0) {
-    const int m = a.log2n;
-    const unsigned br = brev_bits((unsigned)i, m), mask = (unsigned)(n - 1);
-    const double inv_n = ldexp(1.0, -m);
-#pragma unroll
-    for (int j = 0; j < Dims<D>::N; ++j) p[j] = dim_on<D>(a, j) ? gen_part<PG>(a, s, j, br, mask, inv_n) : 0.0;
-  } else {
-#pragma unroll
-    for (int j = 0; j < Dims<D>::N; ++j) p[j] = dim_on<D>(a, j) ? s.pg[(int64_t)j * n + i] : 0.0;
-  }
-}
-
-// parts of the consecutive elements (i, i+1), i even: 16-byte loads, or generated (brev_m(i + 1) =
-// brev_m(i) + n/2)
-template <int PG, int D>
-__device__ __forceinline__ void parts_pair(const Nll& a, const PSrc& s, int64_t n, int64_t i, double* p0,
-                                           double* p1) {
-  if constexpr (PG != 0) {
-    const int m = a.log2n;
-    const unsigned br = brev_bits((unsigned)i, m), mask = (unsigned)(n - 1);
-    const unsigned br1 = br + (unsigned)(n >> 1);
-    const double inv_n = ldexp(1.0, -m);
-#pragma unroll
-    for (int j = 0; j < Dims<D>::N; ++j) {
-      p0[j] = dim_on<D>(a, j) ? gen_part<PG>(a, s, j, br, mask, inv_n) : 0.0;
-      p1[j] = dim_on<D>(a, j) ? gen_part<PG>(a, s, j, br1, mask, inv_n) : 0.0;
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < Dims<D>::N; ++j) {
-      double2 pv = make_double2(0.0, 0.0);
-      if (dim_on<D>(a, j)) pv = *reinterpret_cast<const double2*>(s.pg + (int64_t)j * n + i);
-      p0[j] = pv.x;
-      p1[j] = pv.y;
-    }
-  }
-}
-
-// k1 = scale prod_j (1 + l_j p_j); padded dimensions multiply by exactly 1
-template <int D>
-__device__ __forceinline__ double k1_from(const Hyp& h, const double* p) {
-  double r = 1.0;
-#pragma unroll
-  for (int j = 0; j < Dims<D>::N; ++j) r *= __builtin_fma(h.ls[j], p[j], 1.0);
-  return h.scale * r;
-}
-
-// k1 at the consecutive elements (i, i+1), i even
-template <int PG, int D>
-__device__ __forceinline__ double2 k1_pair(const Nll& a, const Hyp& h, const PSrc& s, int64_t n, int64_t i) {
-  if constexpr (PG == 0) {   // product accumulated as each dimension's 16-byte load arrives
-    double r0 = 1.0, r1 = 1.0;
-#pragma unroll
-    for (int j = 0; j < Dims<D>::N; ++j) {
-      if (dim_on<D>(a, j)) {
-        const double2 pv = *reinterpret_cast<const double2*>(s.pg + (int64_t)j * n + i);
-        r0 *= __builtin_fma(h.ls[j], pv.x, 1.0);
-        r1 *= __builtin_fma(h.ls[j], pv.y, 1.0);
-      }
-    }
-    return make_double2(h.scale * r0, h.scale * r1);
-  } else {
-    double p0[Dims<D>::N], p1[Dims<D>::N];
-    parts_pair<PG, D>(a, s, n, i, p0, p1);
-    return make_double2(k1_from<D>(h, p0), k1_from<D>(h, p1));
-  }
-}
-
-// Gradient terms at element i with dL/dk1_i = g:
-//   acc[0]   += g prod_m f_m                      (x scale after the reduction  = dL/draw_scale)
-//   acc[1+j] += (g p_j) prod_{m != j} f_m        (x scale l_j after the reduction = dL/draw_l_j)
-// f_m = 1 + l_m p_m (prefix / suffix products; padded dimensions contribute f = 1, p = 0).
-template <int D>
-__device__ __forceinline__ void grad_terms_p(const Hyp& h, const double* pj, double gi, double* acc) {
-  constexpr int ND = Dims<D>::N;
-  double f[ND];
-#pragma unroll
-  for (int j = 0; j < ND; ++j) f[j] = __builtin_fma(h.ls[j], pj[j], 1.0);
-  double suf[ND + 1];
-  suf[ND] = 1.0;
-#pragma unroll
-  for (int j = ND - 1; j >= 0; --j) suf[j] = suf[j + 1] * f[j];
-  acc[0] = __builtin_fma(gi, suf[0], acc[0]);
-  double pre = 1.0;
-#pragma unroll
-  for (int j = 0; j < ND; ++j) {
-    acc[1 + j] = __builtin_fma(gi * pj[j], pre * suf[j + 1], acc[1 + j]);
-    pre *= f[j];
-  }
-}
-
-// brev_m(i0 + t) for i0 a multiple of 16: brev_m(i0) | brev_4(t) << (m - 4)
-template <int T4>
-__device__ __forceinline__ unsigned brev_run(unsigned br0, int m) { return br0 | (Brev4<T4>::value << (m - 4)); }
-
-__device__ __forceinline__ double re(double2 v) { return v.x; }
-__device__ __forceinline__ double re(double v) { return v; }
-template <typename T> __device__ __forceinline__ T real_to_T(double v);
-template <> __device__ __forceinline__ double2 real_to_T<double2>(double v) { return make_double2(v, 0.0); }
-template <> __device__ __forceinline__ double real_to_T<double>(double v) { return v; }
-
-// k1 at the 16 consecutive elements i0 + t (i0 a multiple of 16) into v[t]; sum accumulates them in
-// order t.  Generated parts, or the parts array read as 16-byte pairs.
-template <int PG, int D, typename T>
-__device__ __forceinline__ void k1_run16(const Nll& a, const Hyp& h, const PSrc& s, int64_t n, int64_t i0, T* v,
-                                         double& sum) {
-  double r[16];
-  if constexpr (PG != 0) {
-    const int m = a.log2n;
-    const unsigned br0 = brev_bits((unsigned)i0, m), mask = (unsigned)(n - 1);
-    const double inv_n = ldexp(1.0, -m);
-    static_for<0, 16>([&](auto tc) {
-      constexpr int t = decltype(tc)::value;
-      const unsigned br = brev_run<t>(br0, m);
-      double p[Dims<D>::N];
-#pragma unroll
-      for (int j = 0; j < Dims<D>::N; ++j) p[j] = dim_on<D>(a, j) ? gen_part<PG>(a, s, j, br, mask, inv_n) : 0.0;
-      r[t] = k1_from<D>(h, p);
-    });
-  } else {
-#pragma unroll
-    for (int t = 0; t < 16; ++t) r[t] = 1.0;
-#pragma unroll
-    for (int j = 0; j < Dims<D>::N; ++j) {
-      if (dim_on<D>(a, j)) {
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const double2 pv = *reinterpret_cast<const double2*>(s.pg + (int64_t)j * n + i0 + 2 * u);
-          r[2 * u] *= __builtin_fma(h.ls[j], pv.x, 1.0);
-          r[2 * u + 1] *= __builtin_fma(h.ls[j], pv.y, 1.0);
-        }
-      }
-    }
-#pragma unroll
-    for (int t = 0; t < 16; ++t) r[t] = h.scale * r[t];
-  }
-#pragma unroll
-  for (int t = 0; t < 16; ++t) {
-    sum += r[t];
-    v[t] = real_to_T<T>(r[t]);
-  }
-}
-
-// Gradient terms of the 16 consecutive elements i0 + t with dL/dk1 = g[t] * gs.  g is the thread's
-// private run of 16 values in LDS (stride-17 slots: conflict-free): a rolled loop keeps the register
-// footprint of the regenerated parts bounded (fully unrolled, they spill to AGPRs).
-template <int PG, int D>
-__device__ __forceinline__ void grad_run16(const Nll& a, const Hyp& h, const PSrc& s, int64_t n, int64_t i0,
-                                           const double* g, double gs, double* acc) {
-  if constexpr (PG != 0) {
-    const int m = a.log2n;
-    const unsigned br0 = brev_bits((unsigned)i0, m), mask = (unsigned)(n - 1);
-    const double inv_n = ldexp(1.0, -m);
-#pragma unroll 2
-    for (int t = 0; t < 16; ++t) {
-      const unsigned br = br0 | ((__builtin_bitreverse32((unsigned)t) >> 28) << (m - 4));
-      double p[Dims<D>::N];
-#pragma unroll
-      for (int j = 0; j < Dims<D>::N; ++j) p[j] = dim_on<D>(a, j) ? gen_part<PG>(a, s, j, br, mask, inv_n) : 0.0;
-      grad_terms_p<D>(h, p, g[t] * gs, acc);
-    }
-  } else {
-#pragma unroll 2
-    for (int u = 0; u < 8; ++u) {
-      double p0[Dims<D>::N], p1[Dims<D>::N];
-      parts_pair<PG, D>(a, s, n, i0 + 2 * u, p0, p1);
-      grad_terms_p<D>(h, p0, g[2 * u] * gs, acc);
-      grad_terms_p<D>(h, p1, g[2 * u + 1] * gs, acc);
-    }
-  }
-}
-
-// factor applied to the reduced gradient partial q (0: scale, 1 + j: scale l_j)
-__device__ __forceinline__ double grad_factor(const Hyp& h, int q) {
-  return q == 0 ? h.scale : h.scale * h.ls[q - 1];
-}
-
-// log|ev| accumulated as a product of frexp mantissas (each in [0.5, 1): 16 factors stay >= 2^-16)
-// and a sum of exponents, one log per thread instead of one per frequency:
-//   sum_k log|ev_k| = log(prod_k mant_k) + ln 2 sum_k exp_k
-struct LogAcc {
-  double mant = 1.0;
-  int ex = 0;
-  __device__ __forceinline__ void add(double v) {   // v > 0 (or 0 / inf / nan: propagate as log would)
-    int e;
-    mant *= frexp(v, &e);
-    ex += e;
-  }
-  __device__ __forceinline__ double log_sum(double half) const {
-    return half * (log(mant) + (double)ex * 0.69314718055994530942);
-  }
-};
-
-// eigenvalue terms for one frequency: returns dL/dlambda, accumulates norm / log|ev| / dnoise
-__device__ __forceinline__ double2 eig_terms(double2 lam, double rootn, double noise, double Y, double w,
-                                             double& norm, LogAcc& la, double& dnoise) {
-  const double ar = rootn * lam.x + noise, ai = rootn * lam.y;    // ev = sqrt(n) lam + noise
-  const double den = ar * ar + ai * ai;
-  const double inv = 1.0 / den;
-  const double rr = ar * inv, ri = -ai * inv;                      // 1/ev
-  norm += Y * rr;
-  la.add(den);                                                     // log|ev| = 1/2 log(den)
-  // G_e = 1/2 conj(w/ev - Y/ev^2) ; 1/ev^2 = (rr^2 - ri^2, 2 rr ri)
-  const double qr = w * rr - Y * (rr * rr - ri * ri);
-  const double qi = w * ri - Y * (2.0 * rr * ri);
-  const double ger = 0.5 * qr, gei = -0.5 * qi;
-  dnoise += ger;
-  return make_double2(rootn * ger, rootn * gei);
-}
-__device__ __forceinline__ double eig_terms(double lam, double rootn, double noise, double Y, double w, double& norm,
-                                            LogAcc& la, double& dnoise) {
-  const double e = rootn * lam + noise;
-  const double r = 1.0 / e;
-  norm += Y * r;
-  la.add(fabs(e));
-  const double ge = 0.5 * (w * r - Y * r * r);
-  dnoise += ge;
-  return rootn * ge;
-}
-// 1/2 for the lattice (log of |ev|^2), 1 for nets (log of |ev|)
-template <typename T> struct LogHalf { static constexpr double value = sizeof(T) == 16 ? 0.5 : 1.0; };
-
-__device__ __forceinline__ double* part_ptr(const Nll& a, int g, int q, int blk) {
-  return a.partials + ((int64_t)g * a.nq + q) * a.nb + blk;
-}
-
 // ---------------------------------------------------------------- n <= 4096: one kernel
 template <int P, typename T, bool EMIT, int PG>
 __global__ __launch_bounds__(kWG) void k_iter_single(Nll a, const double2* __restrict__ tw) {
@@ -502,17 +140,6 @@ __global__ __launch_bounds__(kWG) void k_iter_single(Nll a, const double2* __res
   }
 }
 
-// ---------------------------------------------------------------- n > 4096: layout of `work`
-// The two-pass intermediate is stored as column tiles [N2 / C][N1][C] (C = kTile / N1 columns, the
-// column kernel's tile): element (row u, column k) of the N1 x N2 view at
-//   (k / C) kTile + u C + k mod C.
-// The column kernel (HBM-bound) then streams one contiguous 64 KB block per workgroup; the row
-// kernels (FP64-VALU-bound, with bandwidth to spare) take the strided side: runs of C elements
-// (256 B at C = 16) spaced kTile elements apart.
-__device__ __forceinline__ int64_t work_pos(int64_t u, int64_t k, int P1) {
-  const int CL = kTileLog - P1;
-  return ((k >> CL) << kTileLog) + (u << CL) + (k & ((1 << CL) - 1));
-}
 
 // ---------------------------------------------------------------- n > 4096: forward row pass
 template <int P2, typename T, int PG, int D>
@@ -1369,10 +996,13 @@ static int to_nll(const fgp_nll_desc* d, Nll& a) {
   a.log2n = d->log2n;
   a.d = d->d;
   a.G = d->G;
-  // half-length (R2C) fit kernels for lattices with n >= 2^17 (FGP_R2C=0 selects the full-length ones)
+  // lattices with n >= 2^17: the real-even (RE) fit kernels when the parts are regenerated, else the
+  // half-length (R2C) ones.  FGP_R2C=1 forces R2C, FGP_R2C=0 the full-length kernels.
   const char* r2c_env = getenv("FGP_R2C");
-  a.r2c = d->family == FGP_FAMILY_LATTICE && d->log2n >= 17 && !(r2c_env && r2c_env[0] == '0');
-  a.nb = d->log2n > 12 ? 1 << (d->log2n - 12 - (a.r2c ? 1 : 0)) : 1;
+  const char mode = (r2c_env && r2c_env[0]) ? r2c_env[0] : '2';
+  a.r2c = d->family == FGP_FAMILY_LATTICE && d->log2n >= 17 && mode != '0';
+  a.re = a.r2c && d->parts_gen == FGP_PARTS_LATTICE && mode != '1';
+  a.nb = d->log2n > 12 ? 1 << (d->log2n - 12 - (a.r2c ? 1 : 0) - (a.re ? 1 : 0)) : 1;
   a.nq = 4 + d->d;
   a.parts = d->parts;
   a.parts_stride = d->parts_stride;
@@ -1405,36 +1035,6 @@ static int to_nll(const fgp_nll_desc* d, Nll& a) {
   return kOk;
 }
 
-// Calls fn(std::integral_constant<int, PG>) with the parts source of `a` as a compile-time value
-// (generated lattice parts exist only for the complex / lattice instantiations).
-template <typename T, typename Fn>
-static int with_pg(const Nll& a, Fn&& fn) {
-  if constexpr (sizeof(T) == 16) {
-    switch (a.pg) {
-      case 2: return fn(std::integral_constant<int, 2>{});
-      case 4: return fn(std::integral_constant<int, 4>{});
-      case 6: return fn(std::integral_constant<int, 6>{});
-      case 8: return fn(std::integral_constant<int, 8>{});
-      default: break;
-    }
-  }
-  return fn(std::integral_constant<int, 0>{});
-}
-
-// Calls fn(std::integral_constant<int, D>{}) with d (1 .. FGP_MAX_D) as a compile-time value.
-template <typename Fn>
-static void with_d(int d, Fn&& fn) {
-  switch (d) {
-    case 1: fn(std::integral_constant<int, 1>{}); break;
-    case 2: fn(std::integral_constant<int, 2>{}); break;
-    case 3: fn(std::integral_constant<int, 3>{}); break;
-    case 4: fn(std::integral_constant<int, 4>{}); break;
-    case 5: fn(std::integral_constant<int, 5>{}); break;
-    case 6: fn(std::integral_constant<int, 6>{}); break;
-    case 7: fn(std::integral_constant<int, 7>{}); break;
-    default: fn(std::integral_constant<int, 8>{}); break;
-  }
-}
 
 template <typename T>
 static int launch_iter_single(const Nll& a, const Tables* tb, hipStream_t st, bool emit = false) {
@@ -1551,7 +1151,7 @@ static int nll_stage_t(const Nll& a, int stage, const Tables* tb, hipStream_t st
   if constexpr (sizeof(T) == 16) {
     if (a.r2c) {
       if (stage < 0 || stage > 2) return set_error(kErrInvalid, "bad stage %d", stage);
-      return launch_r2c(a, stage, tb, st, false);
+      return a.re ? launch_re(a, stage, tb, st) : launch_r2c(a, stage, tb, st, false);
     }
   }
   switch (stage) {

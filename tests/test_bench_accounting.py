@@ -1,5 +1,5 @@
-"""bench.py roofline accounting on CPU: algorithmic bytes per fit kernel for the full-length and the
-half-length (R2C) lattice kernels, and the lookup of the committed PMC
+"""bench.py roofline accounting on CPU: algorithmic bytes per fit kernel for the full-length, the
+half-length (R2C) and the real-even (RE) lattice kernels, and the lookup of the committed PMC
 traffic for the kernel and grid the bench reports."""
 import bench
 
@@ -14,7 +14,7 @@ def test_stage_bytes_full_length(monkeypatch):
 
 
 def test_stage_bytes_half_length(monkeypatch):
-    monkeypatch.delenv("FGP_R2C", raising=False)
+    monkeypatch.setenv("FGP_R2C", "1")
     n, d, P = 2 ** 20, 5, 8
     assert bench.r2c_active(n) and not bench.r2c_active(2 ** 16)
     sb = bench.stage_bytes(n, d, P, parts_array=False)
@@ -23,6 +23,22 @@ def test_stage_bytes_half_length(monkeypatch):
     assert sb == {"k_fwd_rows": 8 * n * P, "k_fwd_cols": 20 * n * P, "k_bwd_rows": 8 * n * P}
     # below 2^17 the full-length kernels run
     assert bench.stage_bytes(2 ** 16, d, P, False)["k_fwd_cols"] == 40 * 2 ** 16 * P
+
+
+def test_stage_bytes_real_even(monkeypatch):
+    monkeypatch.delenv("FGP_R2C", raising=False)
+    n, d, P = 2 ** 20, 5, 8
+    N1 = n // 8192
+    assert bench.fit_variant(n, parts_array=False) == "re"
+    assert bench.fit_variant(n, parts_array=True) == "r2c"          # RE needs the parts generator
+    assert bench.fit_variant(2 ** 16, parts_array=False) == "full"
+    sb = bench.stage_bytes(n, d, P, parts_array=False)
+    # n/4 complex values of work per pass (4n B); Y read as the pairs (Y_2k, Y_2k+1) of those n/4
+    # frequencies (4n B); the Nyquist column (N1 complex) and its N1/2 adjoint values
+    assert sb == {"k_fwd_rows": (4 * n + 16 * N1) * P, "k_fwd_cols": (12 * n + 20 * N1) * P,
+                  "k_bwd_rows": (4 * n + 4 * N1) * P}
+    grid, thr = bench.fit_grid(n, P, "re")
+    assert grid == P * N1 // 2 and thr == {"k_fwd_rows": 512, "k_fwd_cols": 256, "k_bwd_rows": 512}
 
 
 def test_pmc_traffic_lookup_matches_kernel_and_grid():

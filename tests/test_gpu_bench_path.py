@@ -27,9 +27,9 @@ torch.set_default_dtype(torch.float64)
 ITERS = 5
 
 
-@pytest.mark.parametrize("m", [17, 20])
-def test_bench_step_matches_oracle_and_individual_fits(monkeypatch, m):
-    monkeypatch.setenv("FGP_R2C", "1")
+@pytest.mark.parametrize("m,mode", [(17, "2"), (20, "2"), (20, "1")])
+def test_bench_step_matches_oracle_and_individual_fits(monkeypatch, m, mode):
+    monkeypatch.setenv("FGP_R2C", mode)
     monkeypatch.setenv("FGP_PARTS_GEN", "1")
     d, n, P = 5, 2 ** m, 8
     seeds = bench.shard_seeds(0, 1, P)

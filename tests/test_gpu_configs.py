@@ -44,22 +44,26 @@ def test_config_fit_and_predict_match_oracle(family, m, d, its, npm, npv):
     assert float((pv - opv.detach()).abs().max()) <= 1e-8 * kxx
 
 
-@pytest.mark.parametrize("m,d,alpha", [(17, 3, 2), (18, 2, 1), (19, 5, 2), (20, 5, 2), (20, 2, 2), (21, 3, 2)])
+@pytest.mark.parametrize("m,d,alpha", [(17, 3, 2), (18, 2, 1), (19, 5, 2), (20, 5, 2), (20, 2, 2), (21, 3, 2),
+                                         (22, 3, 2), (24, 1, 2)])
 def test_half_length_fit_kernels_match_oracle(monkeypatch, m, d, alpha):
-    """The half-length (R2C) lattice fit kernels (n >= 2^17; csrc/fgp_nll.hip k_*_r2c) and the
-    full-length ones (FGP_R2C=0) on the same GP: eigenvalues (fgp_nll_lam) agree to 1e-12 relative;
-    MLL and gradient of both against the CPU oracle (torch.fft + autograd, the reference's op
-    sequence) to 2e-7 relative, the golden-fixture tolerance (tests/test_gpu_gp.py), with the nugget
-    raised to 1e-3 (at the default 1e-8 the MLL sums |y~|^2 / ev over eigenvalues at the nugget and
-    every implementation's O(eps log n) eigenvalue error -- the reference's own included -- moves it
-    by up to ~1e-5 relative at n = 2^21).  The R2C adjoint assumes dL/dlambda Hermitian; the kernel
-    makes it exactly so (each mirror pair evaluated once, conjugated for the partner) -- without that,
-    the rounding-level anti-Hermitian part, amplified by 1/ev^2 near the nugget, leaked 1e-5..1e-3
-    relative errors into the lengthscale gradient at n >= 2^19, d >= 3 (caught by this test)."""
+    """The lattice fit kernels for n >= 2^17 -- real-even (RE, regenerated parts; csrc/fgp_nll.hip
+    k_*_re, the default), half-length (R2C, FGP_R2C=1; k_*_r2c) and full-length (FGP_R2C=0) -- on the
+    same GP: eigenvalues (fgp_nll_lam) agree to 1e-12 relative; MLL and gradient of every variant
+    against the CPU oracle (torch.fft + autograd, the reference's op sequence) to 2e-7 relative, the
+    golden-fixture tolerance (tests/test_gpu_gp.py), with the nugget raised to 1e-3 (at the default
+    1e-8 the MLL sums |y~|^2 / ev over eigenvalues at the nugget and every implementation's
+    O(eps log n) eigenvalue error -- the reference's own included -- moves it by up to ~1e-5 relative at
+    n = 2^21).  The R2C adjoint assumes dL/dlambda Hermitian; the kernel makes it exactly so (each
+    mirror pair evaluated once, conjugated for the partner) -- without that, the rounding-level
+    anti-Hermitian part, amplified by 1/ev^2 near the nugget, leaked 1e-5..1e-3 relative errors into
+    the lengthscale gradient at n >= 2^19, d >= 3 (caught by this test).  The RE kernels treat lambda
+    as exactly real and even (folded loss over n/2 + 1 frequencies, the gradient through the
+    generated c_0 .. c_{n/2}); the oracle keeps the reference's complex arithmetic."""
     n = 2 ** m
     ls = torch.linspace(0.6, 1.8, d)
     res = {}
-    for mode in ("1", "0"):
+    for mode in ("2", "1", "0"):
         monkeypatch.setenv("FGP_R2C", mode)
         gp = F.FastGPLattice(F.Lattice(d, seed=11), alpha=alpha, lengthscales=ls, noise=1e-3, device=DEV)
         x = gp.get_x_next(n)
@@ -68,10 +72,13 @@ def test_half_length_fit_kernels_match_oracle(monkeypatch, m, d, alpha):
         with torch.no_grad():
             lam = gp.get_lam().clone()
         pb, G = gp._problem_batch()
-        eng = F.FusedMLL(gp._FAMILY, gp._k1parts(n), gp._ysq(pb, G), gp.raw_scale.detach().reshape(-1),
+        gen = gp._parts_gen(n) if mode == "2" else None
+        assert mode != "2" or gen is not None
+        eng = F.FusedMLL(gp._FAMILY, None if gen is not None else gp._k1parts(n), gp._ysq(pb, G),
+                         gp.raw_scale.detach().reshape(-1),
                          gp.raw_lengthscales.detach().reshape(-1, gp.raw_lengthscales.shape[-1]),
                          gp.raw_noise.detach().reshape(-1), logdet_weight=1.0,
-                         mll_const=F.fit_engine.mll_constant(1, n))
+                         mll_const=F.fit_engine.mll_constant(1, n), gen=gen)
         loss, t1, t2, grad = eng.evaluate()
         res[mode] = (lam, float(loss), grad.detach().cpu().clone())
     o = O.OracleFastGP("lattice", x.cpu(), None, y, alpha=alpha, lengthscales=ls, noise=1e-3)
@@ -80,9 +87,12 @@ def test_half_length_fit_kernels_match_oracle(monkeypatch, m, d, alpha):
     og = torch.cat([ogs.reshape(-1), ogl.reshape(-1)])
     (l1, f1, g1), (l0, f0, g0) = res["1"], res["0"]
     assert float((l1 - l0).abs().max()) <= 1e-12 * float(l0.abs().max())
-    errs = {mode: (abs(f - float(oloss)) / abs(float(oloss)), float((gr[:1 + d] - og).abs().max()) / float(og.abs().max()))
-            for mode, f, gr in (("r2c", f1, g1), ("full", f0, g0))}
+    errs = {name: (abs(res[mode][1] - float(oloss)) / abs(float(oloss)),
+                   float((res[mode][2][:1 + d] - og).abs().max()) / float(og.abs().max()))
+            for name, mode in (("re", "2"), ("r2c", "1"), ("full", "0"))}
     assert all(e[0] <= 2e-7 and e[1] <= 2e-7 for e in errs.values()), errs
+    # noise gradient (the third raw parameter block) against the full-length kernels
+    assert abs(float(res["2"][2][-1] - g0[-1])) <= 2e-7 * float(g0.abs().max()), (res["2"][2], g0)
 
 
 @pytest.mark.parametrize("m,d,alpha", [(17, 3, 2), (18, 2, 1), (19, 5, 2), (20, 3, 3)])
