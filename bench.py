@@ -270,13 +270,20 @@ def fit_variant(n, parts_array):
     return "re"
 
 
+def re_row_log2():
+    """Row length log2 of the real-even kernels' n/2-point transform (csrc/fgp_nll_re.hip, FGP_RE_P2, default 11)."""
+    return int(os.environ.get("FGP_RE_P2", "11") or 11)
+
+
 def fit_grid(n, P, variant):
-    """Workgroups per fit launch and threads per workgroup of each stage kernel."""
-    if variant == "re":
-        g = P * max(1, n // 16384)
-        return g, {"k_fwd_rows": 512, "k_fwd_cols": 256, "k_bwd_rows": 512}
+    """{stage kernel: (workgroups per fit launch, threads per workgroup)}."""
+    if variant == "re":     # N1 = n / (2 N2) rows of N2: N1/2 row-pair workgroups of N2/8, n/16384 column tiles
+        N2 = 2 ** re_row_log2()
+        N1 = n // (2 * N2)
+        return {"k_fwd_rows": (P * N1 // 2, N2 // 8), "k_fwd_cols": (P * n // 16384, 256),
+                "k_bwd_rows": (P * N1 // 2, N2 // 8)}
     g = P * max(1, (n // 2 if variant == "r2c" else n) // 4096)
-    return g, {k: 256 for k in STAGES}
+    return {k: (g, 256) for k in STAGES}
 
 
 def stage_bytes(n, d, P, parts_array, variant=None):
@@ -285,13 +292,13 @@ def stage_bytes(n, d, P, parts_array, variant=None):
       full (L = n):  rows 16L write (+ 8nd parts), cols 16L + 16L + Y 8n, bwd rows 16L (+ 8nd)
       r2c (L = n/2): as full with Y 4n (Y = |y~|^2 is even, Y_k = Y_{n-k}, and the kernel reads it only
                      at each mirror pair's primary element: the n/2 values Y_k, Y_{k+n/2})
-      re (L = n/4, columns [0, N2/2) of the n/2-point transform, N1 = n/8192 rows):
+      re (L = n/4, columns [0, N2/2) of the n/2-point transform, N1 = n/(2 N2) rows of N2 = 2^FGP_RE_P2):
                      rows 16L + the Nyquist column 16 N1; cols 16L + 16L + Y 4n (the pairs (Y_2k, Y_2k+1)
                      of its frequencies) + Nyquist 16 N1 read + 4 N1 written; bwd rows 16L + 4 N1"""
     variant = variant or fit_variant(n, parts_array)
     pb = 8 * n * d if parts_array else 0
     if variant == "re":
-        L, N1 = n // 4, n // 8192
+        L, N1 = n // 4, n // (2 * 2 ** re_row_log2())
         return {"k_fwd_rows": (16 * L + 16 * N1) * P, "k_fwd_cols": (32 * L + 4 * n + 20 * N1) * P,
                 "k_bwd_rows": (16 * L + 4 * N1) * P}
     L = n // 2 if variant == "r2c" else n
@@ -322,7 +329,8 @@ def roofline_fit_kernels(F, shifts, iters):
     eng.run(0, 2)
     torch.cuda.synchronize()
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(iters)]
-    grid, _ = fit_grid(n, eng.G, fit_variant(n, eng.gen is None))      # workgroups per fit launch
+    fg = fit_grid(n, eng.G, fit_variant(n, eng.gen is None))      # (workgroups, threads) per fit launch
+    grid = max(g for g, _ in fg.values())
     stamps = torch.zeros((iters, 3, grid, 5), dtype=torch.int64, device=dev)   # fgp_nll_desc.stamps
     torch.cuda._sleep(int(2.4e9 * 4e-4 * iters))
     for it in range(iters):
@@ -339,8 +347,13 @@ def roofline_fit_kernels(F, shifts, iters):
     eng._nll.stamps = None
     khz = wall_clock_khz(F, dev)
     st = stamps.cpu()
-    assert bool((st > 0).all()), "a fit launch did not write its device-clock stamps"
-    dur_us = (st[..., 1:].amax((2, 3)) - st[..., 0].amin(2)).double() * (1e3 / khz)     # [iters, 3]
+    dur = []
+    for k, name in enumerate(STAGES):    # records [workgroup][start, wave ends...] of this launch's grid
+        g, thr = fg[name]
+        sk = st[:, k, :g, :1 + thr // 64]
+        assert bool((sk > 0).all()), "a fit launch did not write its device-clock stamps"
+        dur.append((sk[..., 1:].amax((1, 2)) - sk[..., 0].amin(1)).double() * (1e3 / khz))
+    dur_us = torch.stack(dur, 1)     # [iters, 3]
     us_ev = {name: 1e3 * sum(e[k].elapsed_time(e[k + 1]) for e in ev) / iters for k, name in enumerate(STAGES)}
     us_ev["k_fit_reduce_step"] = 1e3 * sum(e[3].elapsed_time(e[4]) for e in ev) / iters
     us = {name: float(dur_us[:, k].mean()) for k, name in enumerate(STAGES)}
@@ -479,15 +492,15 @@ def main():
     dom = max(STAGES, key=lambda k: us[k])
     variant = fit_variant(n, parts_array)
     kname = dom + {"re": "_re", "r2c": "_r2c", "full": ""}[variant]
-    grid_wg, wg_threads = fit_grid(n, P, variant)
+    grid_wg, wg_thr = fit_grid(n, P, variant)[dom]
     # achieved / frac are priced on the rocprofv3 kernel-trace average of this same command (committed
     # under profiles/) when it is there -- the duration the profiler reports, including the dispatch
     # ramp; the live device-clock figure (first workgroup start to last wave end) is reported beside it
-    us_rp = rocprof_avg_us(kname, grid_wg * wg_threads[dom])
+    us_rp = rocprof_avg_us(kname, grid_wg * wg_thr)
     us_price = us_rp if us_rp is not None else us[dom]
     ach = sb[dom] / (us_price * 1e-6) / 1e9
     roof = {"bound": "hbm", "kernel": kname, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic(kname, grid_wg * wg_threads[dom]),
+            "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic(kname, grid_wg * wg_thr),
             "traffic_source": os.path.relpath(PMC_SUMMARY, ROOT),
             "algorithmic_bytes": sb[dom],
             "avg_us": us_price, "avg_us_source": ("rocprofv3 --kernel-trace average, %s" % os.path.relpath(

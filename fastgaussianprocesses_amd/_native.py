@@ -11,7 +11,7 @@ import threading
 import torch
 
 _LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
-LIB_PATH = os.path.join(_LIB_DIR, "libfgp_hip.so")
+LIB_PATH = os.environ.get("FGP_LIB_PATH") or os.path.join(_LIB_DIR, "libfgp_hip.so")   # override: experiments
 ABI_VERSION = 8
 MT_MAX_TASKS = 16
 MAX_D = 8

@@ -412,7 +412,125 @@ static void with_d(int d, Fn&& fn) {
   }
 }
 
+struct Fit {
+  int n_params;
+  double* raw;
+  double* prev;
+  double* step;
+  double* grad_out;
+  double* loss_hist;
+  double* raw_hist;
+  int scale_rg, ls_rg, noise_rg;
+  double mll_const, eta_minus, eta_plus, step_min, step_max;
+  int per_problem;
+};
+
+// Per-problem reduction + loss history + Rprop (torch.optim.Rprop single-tensor semantics) by one
+// workgroup of NT threads for problem g: k_fit_reduce_step, and the last row-pair workgroup of the
+// fused real-even backward kernel (SC1: the partials of that same launch are read with sc1 loads,
+// MI355X_MICROARCH.md hand-off row 1).  The kernel is a pure latency chain (it sits between two
+// iterations), so every load is issued up front: each thread's partials of all quantities at once, and
+// the parameter-owning threads' Rprop state before the reduction.  Per-quantity order of the sum is
+// fixed (deterministic).  red: [(4 + FGP_MAX_D) * NT / 64], vals: [4 + FGP_MAX_D] (LDS).
+template <int NT, bool SC1>
+__device__ __forceinline__ void reduce_step_wg(const Nll& a, const Fit& f, int g, int iter, int do_update, double* red,
+                                               double* vals) {
+  constexpr int NQ = 4 + FGP_MAX_D, NW = NT / 64;
+  const int k = threadIdx.x;
+  const int dl = a.ls_pd ? a.d : 1;
+  // the parameter thread k owns: 0 scale, 1..dl lengthscales, dl + 1 noise
+  int p = 0, rg = 0;
+  if (k == 0) {
+    p = a.scale_off + (a.scale_pp ? g : 0);
+    rg = f.scale_rg;
+  } else if (k <= dl) {
+    p = a.ls_off + (a.ls_pp ? g : 0) * dl + (k - 1);
+    rg = f.ls_rg;
+  } else {
+    p = a.noise_off + (a.noise_pp ? g : 0);
+    rg = f.noise_rg;
+  }
+  const bool owner = k < 2 + dl;
+  double raw_p = 0.0, prev_p = 0.0, step_p = 0.0;
+  if (owner) {
+    raw_p = f.raw[p];
+    prev_p = f.prev[p];
+    step_p = f.step[p];
+  }
+  double s[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) s[q] = 0.0;
+  for (int b = k; b < a.nb; b += NT) {
+    double v[NQ];   // quantities past nq re-read q = 0 (unused)
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      double* pp = part_ptr(a, g, q < a.nq ? q : 0, b);
+      v[q] = SC1 ? __hip_atomic_load(pp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *pp;
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) s[q] += v[q];
+  }
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    double v = s[q];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if ((k & 63) == 0) red[q * NW + (k >> 6)] = v;
+  }
+  __syncthreads();
+  if (k < NQ) {
+    double tot = 0.0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) tot += red[k * NW + w];
+    vals[k] = tot;
+  }
+  __syncthreads();
+  if (k == 0) {
+    const double term2 = a.logdet_weight * vals[1];
+    double* lh = f.loss_hist + ((int64_t)iter * a.G + g) * 3;
+    lh[0] = 0.5 * (vals[0] + term2 + f.mll_const);
+    lh[1] = vals[0];
+    lh[2] = term2;
+  }
+  if (!owner) return;
+  double gp;
+  if (k == 0) {
+    gp = vals[3];
+  } else if (k <= dl) {
+    if (a.ls_pd) {
+      gp = vals[4 + (k - 1)];
+    } else {
+      gp = 0.0;
+      for (int j = 0; j < a.d; ++j) gp += vals[4 + j];
+    }
+  } else {
+    gp = exp(raw_p) * vals[2];
+  }
+  f.raw_hist[(int64_t)iter * f.n_params + p] = raw_p;
+  f.grad_out[p] = gp;
+  if (!(do_update && rg)) return;
+  // torch.optim.Rprop single-tensor semantics (as rprop_update, on the prefetched state)
+  const double prod = gp * prev_p;
+  const double sgn = prod > 0.0 ? f.eta_plus : (prod < 0.0 ? f.eta_minus : 1.0);
+  const double st = fmin(fmax(step_p * sgn, f.step_min), f.step_max);
+  f.step[p] = st;
+  const double gg = (sgn == f.eta_minus) ? 0.0 : gp;
+  const double gs = gg > 0.0 ? 1.0 : (gg < 0.0 ? -1.0 : 0.0);
+  f.raw[p] = raw_p + (-1.0) * (gs * st);
+  f.prev[p] = gg;
+}
+
 // real-even lattice fit kernels (fgp_nll_re.hip): stage 0 forward rows, 1 columns, 2 adjoint rows
 int launch_re(const Nll& a, int stage, const Tables* tb, hipStream_t st);
+// fused backward + reduction + Rprop of one iteration (per-problem fits): the stage-2 kernel's last
+// row-pair workgroup of each problem runs reduce_step_wg.  counters: G zeroed 32-bit words.
+struct FitFuse {
+  Fit f;
+  int iter, do_update;
+  unsigned* counters;
+};
+int launch_re_bwd_fused(const Nll& a, const FitFuse& fz, const Tables* tb, hipStream_t st);
+// their row length log2 (FGP_RE_P2, default 10) for a transform of 2^log2n, or -1 when no split fits
+int re_row_log2(int log2n);
 
 }  // namespace fgp

@@ -25,6 +25,7 @@
 //               each) or, with the lattice generator (FGP_PARTS_LATTICE), regenerated in registers.
 //   then k_fit_step (one workgroup: deterministic reduction of the per-block partials, loss
 //   assembly, histories, Rprop update).
+#include <algorithm>
 #include <cstdlib>
 
 #include "fgp_nll.h"
@@ -760,18 +761,6 @@ __global__ __launch_bounds__(kWG) void k_bwd_rows_r2c(Nll a, const double2* __re
 }
 
 // ---------------------------------------------------------------- fit step (one workgroup)
-struct Fit {
-  int n_params;
-  double* raw;
-  double* prev;
-  double* step;
-  double* grad_out;
-  double* loss_hist;
-  double* raw_hist;
-  int scale_rg, ls_rg, noise_rg;
-  double mll_const, eta_minus, eta_plus, step_min, step_max;
-  int per_problem;
-};
 
 __device__ __forceinline__ void rprop_update(const Fit& f, int p, double gp) {
   const double prod = gp * f.prev[p];
@@ -842,94 +831,11 @@ __global__ __launch_bounds__(kWG) void k_fit_step(Nll a, Fit f, int iter, int do
 }
 
 // Independent problems (per_problem): one workgroup per GP reduces its partials, records its loss
-// and parameters and applies Rprop to the parameters it owns -- no cross-problem dependency.  The
-// kernel is a pure latency chain (it sits between two iterations), so every load is issued up front:
-// each thread's partials of all quantities at once, and the parameter-owning threads' Rprop state
-// before the reduction.  Per-quantity order of the sum is as block_sum's (fixed, deterministic).
+// and parameters and applies Rprop to the parameters it owns (reduce_step_wg, fgp_nll.h).
 __global__ __launch_bounds__(kWG) void k_fit_reduce_step(Nll a, Fit f, int iter, int do_update) {
-  constexpr int NQ = 4 + FGP_MAX_D, NW = kWG / 64;
-  __shared__ double red[NQ * NW];
-  __shared__ double vals[NQ];
-  const int g = blockIdx.x;
-  const int k = threadIdx.x;
-  const int dl = a.ls_pd ? a.d : 1;
-  // the parameter thread k owns: 0 scale, 1..dl lengthscales, dl + 1 noise
-  int p = 0, rg = 0;
-  if (k == 0) {
-    p = a.scale_off + (a.scale_pp ? g : 0);
-    rg = f.scale_rg;
-  } else if (k <= dl) {
-    p = a.ls_off + (a.ls_pp ? g : 0) * dl + (k - 1);
-    rg = f.ls_rg;
-  } else {
-    p = a.noise_off + (a.noise_pp ? g : 0);
-    rg = f.noise_rg;
-  }
-  const bool owner = k < 2 + dl;
-  double raw_p = 0.0, prev_p = 0.0, step_p = 0.0;
-  if (owner) {
-    raw_p = f.raw[p];
-    prev_p = f.prev[p];
-    step_p = f.step[p];
-  }
-  double s[NQ];
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) s[q] = 0.0;
-  for (int b = k; b < a.nb; b += kWG) {
-    double v[NQ];   // quantities past nq re-read q = 0 (unused)
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) v[q] = *part_ptr(a, g, q < a.nq ? q : 0, b);
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) s[q] += v[q];
-  }
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-    double v = s[q];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    if ((k & 63) == 0) red[q * NW + (k >> 6)] = v;
-  }
-  __syncthreads();
-  if (k < NQ) {
-    double tot = 0.0;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) tot += red[k * NW + w];
-    vals[k] = tot;
-  }
-  __syncthreads();
-  if (k == 0) {
-    const double term2 = a.logdet_weight * vals[1];
-    double* lh = f.loss_hist + ((int64_t)iter * a.G + g) * 3;
-    lh[0] = 0.5 * (vals[0] + term2 + f.mll_const);
-    lh[1] = vals[0];
-    lh[2] = term2;
-  }
-  if (!owner) return;
-  double gp;
-  if (k == 0) {
-    gp = vals[3];
-  } else if (k <= dl) {
-    if (a.ls_pd) {
-      gp = vals[4 + (k - 1)];
-    } else {
-      gp = 0.0;
-      for (int j = 0; j < a.d; ++j) gp += vals[4 + j];
-    }
-  } else {
-    gp = exp(raw_p) * vals[2];
-  }
-  f.raw_hist[(int64_t)iter * f.n_params + p] = raw_p;
-  f.grad_out[p] = gp;
-  if (!(do_update && rg)) return;
-  // torch.optim.Rprop single-tensor semantics (as rprop_update, on the prefetched state)
-  const double prod = gp * prev_p;
-  const double sgn = prod > 0.0 ? f.eta_plus : (prod < 0.0 ? f.eta_minus : 1.0);
-  const double st = fmin(fmax(step_p * sgn, f.step_min), f.step_max);
-  f.step[p] = st;
-  const double gg = (sgn == f.eta_minus) ? 0.0 : gp;
-  const double gs = gg > 0.0 ? 1.0 : (gg < 0.0 ? -1.0 : 0.0);
-  f.raw[p] = raw_p + (-1.0) * (gs * st);
-  f.prev[p] = gg;
+  __shared__ double red[(4 + FGP_MAX_D) * (kWG / 64)];
+  __shared__ double vals[4 + FGP_MAX_D];
+  reduce_step_wg<kWG, false>(a, f, blockIdx.x, iter, do_update, red, vals);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1001,8 +907,10 @@ static int to_nll(const fgp_nll_desc* d, Nll& a) {
   const char* r2c_env = getenv("FGP_R2C");
   const char mode = (r2c_env && r2c_env[0]) ? r2c_env[0] : '2';
   a.r2c = d->family == FGP_FAMILY_LATTICE && d->log2n >= 17 && mode != '0';
-  a.re = a.r2c && d->parts_gen == FGP_PARTS_LATTICE && mode != '1';
-  a.nb = d->log2n > 12 ? 1 << (d->log2n - 12 - (a.r2c ? 1 : 0) - (a.re ? 1 : 0)) : 1;
+  const int re_p2 = re_row_log2(d->log2n);
+  a.re = a.r2c && d->parts_gen == FGP_PARTS_LATTICE && re_p2 > 0 && mode != '1';
+  // per-block partials: one per row / row-pair workgroup (RE: N1/2 = n / 2^(P2 + 2) row pairs)
+  a.nb = d->log2n > 12 ? 1 << (a.re ? d->log2n - 2 - re_p2 : d->log2n - 12 - (a.r2c ? 1 : 0)) : 1;
   a.nq = 4 + d->d;
   a.parts = d->parts;
   a.parts_stride = d->parts_stride;
@@ -1360,10 +1268,31 @@ int fgp_fit_run(const fgp_nll_desc* nll, const fgp_fit_desc* fit, int iter0, int
   if (rc != kOk) return rc;
   const bool lat = nll->family == FGP_FAMILY_LATTICE;
   hipStream_t st = (hipStream_t)stream;
+  // real-even kernels, independent problems: the reduction + Rprop step runs in the backward kernel's
+  // last workgroup per problem, with G counters in the documented partials workspace past the
+  // G (4 + d) (nb + 1) doubles the kernels use (room while nb < n / 4096)
+  const int64_t nb_doc = std::max<int64_t>(1, ((int64_t)1 << a.log2n) >> 12);
+  const bool fuse = a.re && f.per_problem && a.nb < nb_doc && iters > 0;
+  FitFuse fz{};
+  const Tables* tb = nullptr;
+  if (fuse) {
+    fz.f = f;
+    fz.counters = reinterpret_cast<unsigned*>(a.partials + (int64_t)a.G * a.nq * (a.nb + 1));
+    tb = get_tables(st);
+    if (!tb) return set_error(kErrHip, "twiddle table initialisation failed");
+    if (hipMemsetAsync(fz.counters, 0, sizeof(unsigned) * (size_t)a.G, st) != hipSuccess)
+      return set_error(kErrHip, "fgp_fit_run: counter reset failed");
+  }
   for (int it = 0; it < iters; ++it) {
     if ((rc = nll_fwd(a, st, lat)) != kOk) return rc;
-    if ((rc = nll_bwd(a, st, lat)) != kOk) return rc;
     const int upd = !(final_no_update && it == iters - 1);
+    if (fuse) {
+      fz.iter = iter0 + it;
+      fz.do_update = upd;
+      if ((rc = launch_re_bwd_fused(a, fz, tb, st)) != kOk) return rc;
+      continue;
+    }
+    if ((rc = nll_bwd(a, st, lat)) != kOk) return rc;
     if ((rc = fit_step(a, f, iter0 + it, upd, st)) != kOk) return rc;
   }
   return kOk;
