@@ -28,7 +28,7 @@ def test_stage_bytes_half_length(monkeypatch):
 def test_stage_bytes_real_even(monkeypatch):
     monkeypatch.delenv("FGP_R2C", raising=False)
     n, d, P = 2 ** 20, 5, 8
-    N1 = n // 2048
+    N1 = n // (2 * 2 ** bench.re_row_log2())      # rows of the n/2-point transform (2048 by default)
     assert bench.fit_variant(n, parts_array=False) == "re"
     assert bench.fit_variant(n, parts_array=True) == "r2c"          # RE needs the parts generator
     assert bench.fit_variant(2 ** 16, parts_array=False) == "full"
@@ -37,8 +37,9 @@ def test_stage_bytes_real_even(monkeypatch):
     # frequencies (4n B); the Nyquist column (N1 complex) and its N1/2 adjoint values
     assert sb == {"k_fwd_rows": (4 * n + 16 * N1) * P, "k_fwd_cols": (12 * n + 20 * N1) * P,
                   "k_bwd_rows": (4 * n + 4 * N1) * P}
-    assert bench.fit_grid(n, P, "re") == {"k_fwd_rows": (P * N1 // 2, 128), "k_fwd_cols": (P * N1 // 8, 256),
-                                           "k_bwd_rows": (P * N1 // 2, 128)}
+    N2 = 2 ** bench.re_row_log2()
+    assert bench.fit_grid(n, P, "re") == {"k_fwd_rows": (P * N1 // 2, N2 // 8), "k_fwd_cols": (P * n // 16384, 256),
+                                           "k_bwd_rows": (P * N1 // 2, N2 // 8)}
 
 
 def test_pmc_traffic_lookup_matches_kernel_and_grid():
