@@ -12,7 +12,7 @@ import torch
 
 _LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
 LIB_PATH = os.environ.get("FGP_LIB_PATH") or os.path.join(_LIB_DIR, "libfgp_hip.so")   # override: experiments
-ABI_VERSION = 8
+ABI_VERSION = 9
 MT_MAX_TASKS = 16
 MAX_D = 8
 PARTS_ARRAY = 0
@@ -59,6 +59,7 @@ class FitDesc(ctypes.Structure):
         ("mll_const", _c_dbl), ("eta_minus", _c_dbl), ("eta_plus", _c_dbl),
         ("step_min", _c_dbl), ("step_max", _c_dbl),
         ("per_problem", _c_int),
+        ("hist_stride", _c_int), ("hist_offset", _c_int),
     ]
 
 

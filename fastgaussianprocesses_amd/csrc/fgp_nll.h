@@ -423,6 +423,7 @@ struct Fit {
   int scale_rg, ls_rg, noise_rg;
   double mll_const, eta_minus, eta_plus, step_min, step_max;
   int per_problem;
+  int hist_stride, hist_offset;   // loss_hist row stride in problems (0: G) and this desc's first problem
 };
 
 // Per-problem reduction + loss history + Rprop (torch.optim.Rprop single-tensor semantics) by one
@@ -487,7 +488,7 @@ __device__ __forceinline__ void reduce_step_wg(const Nll& a, const Fit& f, int g
   __syncthreads();
   if (k == 0) {
     const double term2 = a.logdet_weight * vals[1];
-    double* lh = f.loss_hist + ((int64_t)iter * a.G + g) * 3;
+    double* lh = f.loss_hist + ((int64_t)iter * (f.hist_stride ? f.hist_stride : a.G) + f.hist_offset + g) * 3;
     lh[0] = 0.5 * (vals[0] + term2 + f.mll_const);
     lh[1] = vals[0];
     lh[2] = term2;

@@ -1103,6 +1103,9 @@ static int to_fit(const fgp_fit_desc* d, Fit& f) {
   f.step_min = d->step_min;
   f.step_max = d->step_max;
   f.per_problem = d->per_problem;
+  f.hist_stride = d->hist_stride;
+  f.hist_offset = d->hist_offset;
+  if (f.hist_stride < 0 || f.hist_offset < 0) return set_error(kErrInvalid, "bad hist_stride / hist_offset");
   return kOk;
 }
 

@@ -131,6 +131,14 @@ __device__ __forceinline__ void wg_sums_t0(double* v, double* red /* [K][NW] */)
   }
 }
 
+// Phase stamps (experiment builds, -DFGP_EXP_PHASES): thread 0 of each workgroup records the wall clock
+// at phase k into stamps[blockIdx.x * 16 + k] (the launch's stamps buffer, sized by the experiment).
+#ifdef FGP_EXP_PHASES
+#define RE_PHASE(a, k) do { if ((a).stamps && threadIdx.x == 0) (a).stamps[(int64_t)blockIdx.x * 16 + (k)] = (unsigned long long)wall_clock64(); } while (0)
+#else
+#define RE_PHASE(a, k) do { } while (0)
+#endif
+
 // Row geometry of the length-n/2 transform for rows of N2 = 2^P2 (P2 = 10, 11, 12): TL = N2/16 threads
 // per row (one, two or four wavefronts), a row-pair workgroup of 2 TL threads.
 template <int P2>
@@ -211,12 +219,16 @@ __global__ __launch_bounds__(ReGeo<P2>::WG, 4) void k_fwd_rows_re(Nll a, const d
   const unsigned n = 1u << a.log2n, M = n >> 1, mask = n - 1;
   const double inv_n = ldexp(1.0, -a.log2n);
   const int q = rp.q;
+#ifndef FGP_EXP_PHASES
   stamp_begin(a);
+#endif
+  RE_PHASE(a, 0);
   Hyp h;
   load_hyp_wave(a, rp.g, h);
   fold_gen_coef<PG>(a, h);
   // element twiddles w_n^{i_e} = w_n^r w_{2 N2}^{brev(q)} w_32^{brev4(e)}
   const double2 wq = rp.wbase(twm_n, tw2);
+  RE_PHASE(a, 1);
   double2 v[16];
   double x0[16];
   double cM = 0.0;
@@ -264,14 +276,17 @@ __global__ __launch_bounds__(ReGeo<P2>::WG, 4) void k_fwd_rows_re(Nll a, const d
       v[e] = make_double2(__builtin_fma(-b, w.y, sa), b * w.x);
     });
   }
+  RE_PHASE(a, 2);
   double2 sum = make_double2(0.0, 0.0);
 #pragma unroll
   for (int t = 0; t < 16; ++t) sum += v[t];
   const double2 mean = group_sum<TL>(sum, red) * (1.0 / N2);   // per row (one wave: shuffles only)
 #pragma unroll
   for (int t = 0; t < 16; ++t) v[t] -= mean;
+  RE_PHASE(a, 3);
   fwd_reg_passes<P2, 0, true>(v, img + rp.hh * IMG, q, tw);
   if (q == 0) v[0] += mean * (double)N2;
+  RE_PHASE(a, 4);
   const RowTwRe<P2> rt(rp.r, q, rp.m1, tw, twm_t);
   double2* out = static_cast<double2*>(a.work) + (int64_t)rp.g * n;
 #pragma unroll
@@ -282,7 +297,10 @@ __global__ __launch_bounds__(ReGeo<P2>::WG, 4) void k_fwd_rows_re(Nll a, const d
       out[work_pos(rp.u, k1, rp.m1)] = tw_mul<double2>(v[j * R + t], rt.at(k1 - q, rp.m1, tw, twm_t), false);
     }
   if (q == 0) out[(n >> 2) + rp.u] = tw_mul<double2>(v[R / 2], rt.at(N2 / 2, rp.m1, tw, twm_t), false);   // column N2/2
+  RE_PHASE(a, 5);
+#ifndef FGP_EXP_PHASES
   stamp_end(a);
+#endif
 }
 
 // Column pass over columns [0, N2/2) (tile blk of C = 4096/N1 columns, all N1 rows), eigenvalue terms
@@ -428,7 +446,10 @@ __global__ __launch_bounds__(ReGeo<P2>::WG, 4) void k_bwd_rows_re(Nll a, const d
   const unsigned n = 1u << a.log2n, M = n >> 1, mask = n - 1;
   const double inv_n = ldexp(1.0, -a.log2n);
   const int q = rp.q, N1 = rp.N1;
+#ifndef FGP_EXP_PHASES
   stamp_begin(a);
+#endif
+  RE_PHASE(a, 0);
   const double2* in = static_cast<const double2*>(a.work) + (int64_t)rp.g * n;
   const double* vny = reinterpret_cast<const double*>(in + (n >> 2) + N1);
   const RowTwRe<P2> rt(rp.r, q, rp.m1, tw, twm_t);
@@ -461,8 +482,10 @@ __global__ __launch_bounds__(ReGeo<P2>::WG, 4) void k_bwd_rows_re(Nll a, const d
   const double2 mean = group_sum<TL>(sum, red) * (1.0 / N2);
 #pragma unroll
   for (int k = 0; k < 16; ++k) v[k] -= mean;
+  RE_PHASE(a, 1);
   adj_reg_passes<P2, LastPass<P2>::S, true>(v, img + rp.hh * IMG, q, tw);
   if (q == 0) v[0] += mean * (double)N2;
+  RE_PHASE(a, 2);
   // W at the mirror elements -- from the partner thread (regular), or the class-0 image (Re, then Im)
   // -- combined into dL/dc as they arrive (gv: the thread's 16 generated points, in loop order)
   double2* xw = reinterpret_cast<double2*>(img + rp.partner_h * IMG);
@@ -518,6 +541,7 @@ __global__ __launch_bounds__(ReGeo<P2>::WG, 4) void k_bwd_rows_re(Nll a, const d
     });
   }
   __syncthreads();
+  RE_PHASE(a, 3);
   // dL/dc values into private LDS slots (stride 17: conflict-free) for the rolled gradient loop
   double* gl = img + 17 * threadIdx.x;
 #pragma unroll
@@ -559,13 +583,17 @@ __global__ __launch_bounds__(ReGeo<P2>::WG, 4) void k_bwd_rows_re(Nll a, const d
     for (int j = 0; j < D; ++j) p[j] = lattice_gen_part<PG>(a.gz[j], M, mask, inv_n);
     grad_terms_p<D>(h, p, gM * gs, acc);
   }
+  RE_PHASE(a, 4);
   wg_sums_t0<Geo::WG / 64, 1 + D>(acc, redd);
   if (!fz.counters) {
     if (threadIdx.x == 0) {
 #pragma unroll
       for (int k = 0; k < 1 + D; ++k) *part_ptr(a, rp.g, 3 + k, rp.jp) = acc[k] * grad_factor(h, k);
     }
+    RE_PHASE(a, 5);
+#ifndef FGP_EXP_PHASES
     stamp_end(a);
+#endif
     return;
   }
   // Fused reduction + Rprop (fgp_fit_run, per-problem fits).  Hand-off (MI355X_MICROARCH.md row 1): the

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define FGP_ABI_VERSION 8
+#define FGP_ABI_VERSION 9
 
 #define FGP_OK 0
 #define FGP_ERR_INVALID (-1)     /* bad argument (shape, stride, null pointer) */
@@ -218,6 +218,9 @@ typedef struct fgp_fit_desc {
   double eta_minus, eta_plus, step_min, step_max; /* torch.optim.Rprop defaults 0.5, 1.2, 1e-6, 50 */
   int per_problem;            /* 1: the G problems are independent GPs (each owns its parameters, loss, Rprop
                                  state; every *_pp flag must be set when G > 1), one fused reduce+step kernel */
+  int hist_stride;            /* per_problem: problems per loss_hist row (0: G) -- a desc over problems
+                                 [hist_offset, hist_offset + G) of a larger batch writes its slice of the rows */
+  int hist_offset;
 } fgp_fit_desc;
 
 /* Reduce the partials of fgp_nll_fwd/bwd, assemble loss = 1/2 (term1 + term2 + mll_const), record
