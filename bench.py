@@ -363,8 +363,12 @@ def roofline_fit_kernels(F, shifts, iters):
 
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02_pmc_fit_kernels.json")
-ROCPROF_GRID_STATS = os.path.join(ROOT, "profiles", "r02_bench_kernel_grid_stats.txt")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02f_pmc_fit_kernels.json")
+PMC_SQ_SUMMARY = os.path.join(ROOT, "profiles", "r02f_pmc_sq_fit_kernels.json")
+ROCPROF_GRID_STATS = os.path.join(ROOT, "profiles", "r02f_bench_kernel_grid_stats.txt")
+# FP64 VALU lane-operations per second: 256 CUs x 4 SIMDs x 16 FP64 lanes per clock x 2.4 GHz = 3.93e13
+# (FP64 vector at half the FP32 vector rate of MI355X_MICROARCH.md, 157.3 TFLOP/s; 78.6 TFLOP/s FMA)
+FP64_LANE_OPS_PEAK = 256 * 4 * 16 * 2.4e9
 CPU_FIDELITY = os.path.join(ROOT, "profiles", "r02_cpu_fidelity.json")
 
 
@@ -380,6 +384,20 @@ def pmc_traffic(kernel, grid):
         name, _, g = k.partition("|grid=")
         if name.split("<")[0].split("::")[-1] == kernel and g == str(grid) and "traffic_bytes" in v:
             return v["traffic_bytes"]
+    return None
+
+
+def pmc_valu_insts(kernel, grid):
+    """VALU wave-instructions per launch (SQ_INSTS_VALU) of `kernel` at `grid` threads from the committed
+    SQ counter pass (tools/pmc_sq_summary.py over tools/fit_kernels.py), or None when absent."""
+    try:
+        summ = json.load(open(PMC_SQ_SUMMARY))
+    except (OSError, ValueError):
+        return None
+    for k, v in summ.items():
+        name, _, g = k.partition("|grid=")
+        if name.split("<")[0].split("::")[-1] == kernel and g == str(grid) and "SQ_INSTS_VALU" in v:
+            return v["SQ_INSTS_VALU"]
     return None
 
 
@@ -516,6 +534,15 @@ def main():
                             "GB/s": (sb[k] / (us[k] * 1e-6) / 1e9) if k in sb else None} for k in us},
             "parts": "array" if parts_array else "regenerated (FGP_PARTS_LATTICE)",
             "iteration_us": t_iter * 1e6}
+    vi = pmc_valu_insts(kname, grid_wg * wg_thr)
+    if vi is not None:
+        # the row kernels regenerate the kernel parts instead of reading them: their bound is the FP64
+        # VALU issue rate, not HBM.  Every VALU instruction priced as a 64-lane FP64 one (integer and
+        # FP32 ones issue faster), so `frac` here is an upper estimate of the issue-slot use.
+        lane_ops = vi * 64 / (us[dom] * 1e-6)
+        roof["valu"] = {"insts_per_launch": vi, "lane_ops_per_s": lane_ops, "peak_fp64_lane_ops_per_s": FP64_LANE_OPS_PEAK,
+                        "frac": lane_ops / FP64_LANE_OPS_PEAK, "time": "avg_us_device_clock",
+                        "source": os.path.relpath(PMC_SQ_SUMMARY, ROOT) + " (SQ_INSTS_VALU)"}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, n, d)

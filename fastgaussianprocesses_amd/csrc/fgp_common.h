@@ -477,6 +477,21 @@ __device__ __forceinline__ unsigned mul_u24(unsigned a, unsigned b) {
   return r;
 }
 
+// 16-byte write-through stores (cache policy sc1) into a buffer whose base is wave-uniform: the line
+// leaves the XCD's L2 with the store, so the kernel's end has no dirty bytes to write back before a
+// dependent launch can start (MI355X_MICROARCH.md price list, "boundary": + B / 6 TB/s for B dirty
+// bytes; "publish-large": write-through wins for tens of KB per workgroup).  Element offsets are
+// 32-bit byte offsets from the base (a buffer of < 2^28 double2 per base).
+struct WtStore {
+  __amdgpu_buffer_rsrc_t r;
+  __device__ __forceinline__ explicit WtStore(const void* base)
+      : r(__builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, -1, 0x00020000)) {}
+  __device__ __forceinline__ void put(unsigned idx, double2 v) const {
+    typedef int v4i __attribute__((ext_vector_type(4)));
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), r, (int)(idx << 4), 0, 16 /* sc1 */);
+  }
+};
+
 // Natural-order rank-1 lattice coordinate of point i (brev = brev_m(i), zm = z_j mod n):
 //   x = ((brev z_j mod n) / n + shift_j) % 1   -- the host generator's value (seqs.Lattice), bit for bit
 __device__ __forceinline__ double lattice_coord(unsigned brev, unsigned zm, unsigned mask, double inv_n, double sh) {

@@ -908,7 +908,11 @@ static int to_nll(const fgp_nll_desc* d, Nll& a) {
   const char mode = (r2c_env && r2c_env[0]) ? r2c_env[0] : '2';
   a.r2c = d->family == FGP_FAMILY_LATTICE && d->log2n >= 17 && mode != '0';
   const int re_p2 = re_row_log2(d->log2n);
-  a.re = a.r2c && d->parts_gen == FGP_PARTS_LATTICE && re_p2 > 0 && mode != '1';
+  // the real-even kernels form each mirror pair's parts from one lattice index, which needs every
+  // generating vector entry odd (M z_j = n/2 mod n); an even entry takes the R2C kernels
+  bool z_odd = true;
+  for (int j = 0; j < d->d && d->parts_gen == FGP_PARTS_LATTICE; ++j) z_odd = z_odd && (d->gen_z[j] & 1);
+  a.re = a.r2c && d->parts_gen == FGP_PARTS_LATTICE && re_p2 > 0 && mode != '1' && z_odd;
   // per-block partials: one per row / row-pair workgroup (RE: N1/2 = n / 2^(P2 + 2) row pairs)
   a.nb = d->log2n > 12 ? 1 << (a.re ? d->log2n - 2 - re_p2 : d->log2n - 12 - (a.r2c ? 1 : 0)) : 1;
   a.nq = 4 + d->d;

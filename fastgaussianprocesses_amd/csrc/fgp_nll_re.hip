@@ -71,19 +71,22 @@ __device__ __forceinline__ double bern_u(double u) {
   else return __builtin_fma(u * u, __builtin_fma(u, u - 4.0 / 3.0, 2.0 / 3.0), -1.0 / 30.0);
 }
 
-// The parts of the mirror pair (t, M - t) from ONE lattice index per dimension: with k = t z_j mod n and
-// x = min(k, n - k) / n (exact), u(t) = x^2 - x and, M z_j = n/2 mod n for odd z_j,
-// u(M - t) = u(frac(1/2 - delta)) = x^2 - 1/4 (even z_j: M - t has distance 1 - delta, u the same).
+// The parts of the mirror pair (t, M - t) from ONE lattice index per dimension (every z_j odd: the
+// real-even path is taken only then, see to_nll).  With k = t z_j mod n and y = k / n - 1/2 (exact):
+//   u(t)     = (k/n)^2 - k/n            = y^2 - 1/4
+//   u(M - t) = u(frac(1/2 - k/n))       = y^2 - |y|          (M z_j = n/2 mod n for odd z_j)
+// one fma each (|y| is a free source modifier).  Each is the exact value rounded once, so they equal the
+// forms x^2 - x / x^2 - 1/4 of x = min(k, n - k) / n bit for bit, at 3 VALU per dimension fewer.
 template <int PG, int D>
-__device__ __forceinline__ void parts_mirror_pair(const Nll& a, unsigned t, unsigned n, unsigned mask, double inv_n,
-                                                  double* p, double* pm) {
+__device__ __forceinline__ void parts_mirror_pair(const Nll& a, unsigned t, unsigned /*n*/, unsigned mask,
+                                                  double inv_n, double* p, double* pm) {
 #pragma unroll
   for (int j = 0; j < D; ++j) {
     const unsigned k = mul_u24(t, a.gz[j]) & mask;
-    const double x = (double)min(k, n - k) * inv_n;
-    const double u = __builtin_fma(x, x, -x);
-    p[j] = bern_u<PG>(u);
-    pm[j] = (a.gz[j] & 1u) ? bern_u<PG>(__builtin_fma(x, x, -0.25)) : p[j];
+    const double y = __builtin_fma((double)k, inv_n, -0.5);
+    const double ay = fabs(y);
+    p[j] = bern_u<PG>(__builtin_fma(y, y, -0.25));
+    pm[j] = bern_u<PG>(__builtin_fma(ay, ay, -ay));
   }
 }
 
@@ -289,12 +292,18 @@ __global__ __launch_bounds__(ReGeo<P2>::WG, 4) void k_fwd_rows_re(Nll a, const d
   RE_PHASE(a, 4);
   const RowTwRe<P2> rt(rp.r, q, rp.m1, tw, twm_t);
   double2* out = static_cast<double2*>(a.work) + (int64_t)rp.g * n;
+  const WtStore wo(out);   // write-through: the column kernel reads the intermediate from HBM / MALL
 #pragma unroll
   for (int j = 0; j < 16 / R; ++j)
 #pragma unroll
     for (int t = 0; t < R / 2; ++t) {
       const int k1 = pass_pos<P2, Geo::SL, Geo::RLL>(q, j, t);
-      out[work_pos(rp.u, k1, rp.m1)] = tw_mul<double2>(v[j * R + t], rt.at(k1 - q, rp.m1, tw, twm_t), false);
+      const double2 o = tw_mul<double2>(v[j * R + t], rt.at(k1 - q, rp.m1, tw, twm_t), false);
+#ifdef FGP_EXP_PLAIN_STORES
+      out[work_pos(rp.u, k1, rp.m1)] = o;
+#else
+      wo.put((unsigned)work_pos(rp.u, k1, rp.m1), o);
+#endif
     }
   if (q == 0) out[(n >> 2) + rp.u] = tw_mul<double2>(v[R / 2], rt.at(N2 / 2, rp.m1, tw, twm_t), false);   // column N2/2
   RE_PHASE(a, 5);
@@ -387,10 +396,21 @@ __global__ __launch_bounds__(kWG) void k_fwd_cols_re(Nll a, const double2* __res
   for (int k = 0; k < 16; ++k) v[k] -= mean;
   adj_reg_passes<P1, SL, false>(v, col, tt, tw);
   if (tt == 0) v[0] += mean * (double)N1;
+#ifdef FGP_EXP_PLAIN_STORES
 #pragma unroll
   for (int j = 0; j < 16 / R0; ++j)
 #pragma unroll
     for (int t = 0; t < R0; ++t) wk[pass_pos<P1, 0, RL0>(tt, j, t) * C] = v[j * R0 + t];
+#else
+  {
+    const WtStore wo(base);   // write-through, as the row kernel's stores
+    const unsigned o0 = (unsigned)(blk * kTile + c);
+#pragma unroll
+    for (int j = 0; j < 16 / R0; ++j)
+#pragma unroll
+      for (int t = 0; t < R0; ++t) wo.put(o0 + (unsigned)(pass_pos<P1, 0, RL0>(tt, j, t) * C), v[j * R0 + t]);
+  }
+#endif
   // Nyquist column (k1 = N2/2): Z_b = sum_u T_u w_N1^{brev(u) b} (mean-centred), real part, weight 2;
   // wave j < NQ of the workgroup takes b = NQ blk + j
   const double2* nyq = base + (n >> 2);

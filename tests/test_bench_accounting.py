@@ -44,8 +44,13 @@ def test_stage_bytes_real_even(monkeypatch):
 
 def test_pmc_traffic_lookup_matches_kernel_and_grid():
     n, P = 2 ** 20, 8
-    t = bench.pmc_traffic("k_fwd_cols_r2c", P * (n // 2) // 4096 * 256)
+    wg, thr = bench.fit_grid(n, P, "re")["k_fwd_cols"]
+    t = bench.pmc_traffic("k_fwd_cols_re", wg * thr)
     assert t is not None and t > 0
-    # the full-length kernel name must not match the R2C entry (exact name match, not a suffix)
-    assert bench.pmc_traffic("k_fwd_cols", P * (n // 2) // 4096 * 256) is None
-    assert bench.pmc_traffic("k_fwd_cols_r2c", 12345) is None
+    # the full-length kernel name must not match the RE entry (exact name match, not a suffix)
+    assert bench.pmc_traffic("k_fwd_cols", wg * thr) is None
+    assert bench.pmc_traffic("k_fwd_cols_re", 12345) is None
+    # the committed SQ pass holds the VALU instruction count of the dominant row kernel at the bench grid
+    wg, thr = bench.fit_grid(n, P, "re")["k_bwd_rows"]
+    assert bench.pmc_valu_insts("k_bwd_rows_re", wg * thr) > 0
+    assert bench.rocprof_avg_us("k_bwd_rows_re", wg * thr) > 0

@@ -95,6 +95,33 @@ def test_half_length_fit_kernels_match_oracle(monkeypatch, m, d, alpha):
     assert abs(float(res["2"][2][-1] - g0[-1])) <= 2e-7 * float(g0.abs().max()), (res["2"][2], g0)
 
 
+def test_even_generating_vector_entry_takes_r2c_and_matches_oracle():
+    """The real-even kernels form a mirror pair's parts from one lattice index, which needs every z_j odd
+    (M z_j = n/2 mod n); a generating vector with an even entry must take the R2C kernels (csrc/fgp_nll.hip
+    to_nll) and still match the oracle (loss and gradient, 2e-7 relative, nugget 1e-3 as above)."""
+    n, d = 2 ** 17, 2
+    gp = F.FastGPLattice(F.Lattice(d, seed=5, generating_vector=[1, 182668]), lengthscales=torch.tensor([0.7, 1.3]),
+                         noise=1e-3, device=DEV)
+    x = gp.get_x_next(n)
+    y = O.f_ackley(x.cpu())
+    gp.add_y_next(y.to(DEV))
+    pb, G = gp._problem_batch()
+    gen = gp._parts_gen(n)
+    assert gen is not None
+    eng = F.FusedMLL(gp._FAMILY, None, gp._ysq(pb, G), gp.raw_scale.detach().reshape(-1),
+                     gp.raw_lengthscales.detach().reshape(-1, gp.raw_lengthscales.shape[-1]),
+                     gp.raw_noise.detach().reshape(-1), logdet_weight=1.0,
+                     mll_const=F.fit_engine.mll_constant(1, n), gen=gen)
+    assert eng.partials.numel() >= G * (4 + d) * ((n >> 13) + 1)   # R2C block count fits the workspace
+    loss, _, _, grad = eng.evaluate()
+    o = O.OracleFastGP("lattice", x.cpu(), None, y, lengthscales=torch.tensor([0.7, 1.3]), noise=1e-3)
+    oloss = o.mll_loss()[0]
+    ogs, ogl = torch.autograd.grad(oloss, [o.raw_scale, o.raw_lengthscales])
+    og = torch.cat([ogs.reshape(-1), ogl.reshape(-1)])
+    assert abs(loss - float(oloss)) <= 2e-7 * abs(float(oloss))
+    assert float((grad.cpu()[:1 + d] - og).abs().max()) <= 2e-7 * float(og.abs().max())
+
+
 @pytest.mark.parametrize("m,d,alpha", [(17, 3, 2), (18, 2, 1), (19, 5, 2), (20, 3, 3)])
 def test_half_length_post_var_matches_full_length_and_oracle(monkeypatch, m, d, alpha):
     """Posterior variance through the half-length (R2C) quadratic-form kernels (csrc/fgp_predict.hip
