@@ -92,7 +92,8 @@ __global__ __launch_bounds__(kWG) void k_post_mean(const double* __restrict__ xt
                                                     int64_t n, PredSpec spec, int tbits,
                                                     const double* __restrict__ hyp, int Gk,
                                                     const double* __restrict__ coeffs, int64_t coeff_stride, int B,
-                                                    double* __restrict__ partial, int64_t nchunks, ProbStrides ps) {
+                                                    double* __restrict__ partial, int64_t nchunks, ProbStrides ps,
+                                                    int64_t chunk) {
   __shared__ double zs[D][kSlab];
   __shared__ double cs[NB][kSlab];
   const int tid = threadIdx.x;
@@ -146,8 +147,8 @@ __global__ __launch_bounds__(kWG) void k_post_mean(const double* __restrict__ xt
   double acc[NB];
 #pragma unroll
   for (int b = 0; b < NB; ++b) acc[b] = 0.0;
-  const int64_t i0 = (int64_t)blockIdx.x * kChunk;
-  const int64_t i1 = i0 + kChunk < n ? i0 + kChunk : n;
+  const int64_t i0 = (int64_t)blockIdx.x * chunk;
+  const int64_t i1 = i0 + chunk < n ? i0 + chunk : n;
   auto slabs = [&](auto fold_c) {
     constexpr bool FOLD = decltype(fold_c)::value;
     for (int64_t s0 = i0; s0 < i1; s0 += kSlab) {
@@ -720,17 +721,17 @@ __global__ __launch_bounds__(kWG) void k_inv_eig(const T* __restrict__ lam, cons
 template <int FAM, int D>
 static void post_mean_d(dim3 grid, hipStream_t st, bool uniform4, int B, const double* xt, int64_t N, const void* z,
                         int64_t n, const PredSpec& spec, int tbits, const double* hyp, int Gk, const double* coeffs,
-                        int64_t cstride, double* work, int64_t nchunks, const ProbStrides& ps) {
+                        int64_t cstride, double* work, int64_t nchunks, const ProbStrides& ps, int64_t chunk) {
   if (B == 1) {
     if (FAM == 1 || uniform4)
-      k_post_mean<FAM, D, 1, 4><<<grid, kWG, 0, st>>>(xt, N, z, n, spec, tbits, hyp, Gk, coeffs, cstride, B, work, nchunks, ps);
+      k_post_mean<FAM, D, 1, 4><<<grid, kWG, 0, st>>>(xt, N, z, n, spec, tbits, hyp, Gk, coeffs, cstride, B, work, nchunks, ps, chunk);
     else
-      k_post_mean<FAM, D, 1, 0><<<grid, kWG, 0, st>>>(xt, N, z, n, spec, tbits, hyp, Gk, coeffs, cstride, B, work, nchunks, ps);
+      k_post_mean<FAM, D, 1, 0><<<grid, kWG, 0, st>>>(xt, N, z, n, spec, tbits, hyp, Gk, coeffs, cstride, B, work, nchunks, ps, chunk);
   } else {
     if (FAM == 1 || uniform4)
-      k_post_mean<FAM, D, kPmB, 4><<<grid, kWG, 0, st>>>(xt, N, z, n, spec, tbits, hyp, Gk, coeffs, cstride, B, work, nchunks, ps);
+      k_post_mean<FAM, D, kPmB, 4><<<grid, kWG, 0, st>>>(xt, N, z, n, spec, tbits, hyp, Gk, coeffs, cstride, B, work, nchunks, ps, chunk);
     else
-      k_post_mean<FAM, D, kPmB, 0><<<grid, kWG, 0, st>>>(xt, N, z, n, spec, tbits, hyp, Gk, coeffs, cstride, B, work, nchunks, ps);
+      k_post_mean<FAM, D, kPmB, 0><<<grid, kWG, 0, st>>>(xt, N, z, n, spec, tbits, hyp, Gk, coeffs, cstride, B, work, nchunks, ps, chunk);
   }
 }
 
@@ -738,14 +739,14 @@ template <int FAM>
 static int launch_post_mean(int d, const double* xt, int64_t N, const void* z, int64_t n, const PredSpec& spec, int tbits,
                             const double* hyp, int Gk, const double* coeffs, int64_t cstride, int B, double* out,
                             int64_t out_stride, double* work, hipStream_t st, int P = 1,
-                            ProbStrides ps = ProbStrides{0, 0, 0, 0}) {
-  const int64_t nchunks = (n + kChunk - 1) / kChunk;
+                            ProbStrides ps = ProbStrides{0, 0, 0, 0}, int64_t chunk = kChunk) {
+  const int64_t nchunks = (n + chunk - 1) / chunk;
   const dim3 grid((unsigned)nchunks, (unsigned)((N + kWG - 1) / kWG), (unsigned)P);
   bool uniform4 = true;
   for (int j = 0; j < d; ++j) uniform4 = uniform4 && spec.order[j] == 4;
   switch (d) {
 #define FGP_C(DD) \
-  case DD: post_mean_d<FAM, DD>(grid, st, uniform4, B, xt, N, z, n, spec, tbits, hyp, Gk, coeffs, cstride, work, nchunks, ps); break;
+  case DD: post_mean_d<FAM, DD>(grid, st, uniform4, B, xt, N, z, n, spec, tbits, hyp, Gk, coeffs, cstride, work, nchunks, ps, chunk); break;
     FGP_C(1) FGP_C(2) FGP_C(3) FGP_C(4) FGP_C(5) FGP_C(6) FGP_C(7) FGP_C(8)
 #undef FGP_C
     default: return set_error(kErrUnsupported, "post_mean: d=%d unsupported", d);
@@ -806,10 +807,13 @@ int fgp_post_mean(int family, const double* xt, int64_t N, const void* z, int64_
   int rc = make_spec(family, d, order, coef, spec);
   if (rc != kOk) return rc;
   hipStream_t st = (hipStream_t)stream;
-  (void)chunk;   // fixed at kChunk; work must hold ceil(n / 1024) * B * N doubles
+  // chunk = training points per workgroup (work holds ceil(n / chunk) * B * N doubles): small chunks give
+  // small problems (n = 2^16, N = 256) enough workgroups to fill the chip
   if (family == FGP_FAMILY_LATTICE)
-    return launch_post_mean<0>(d, xt, N, z, n, spec, tbits, hyp, Gk, coeffs, coeff_stride, B, out, out_stride, work, st);
-  return launch_post_mean<1>(d, xt, N, z, n, spec, tbits, hyp, Gk, coeffs, coeff_stride, B, out, out_stride, work, st);
+    return launch_post_mean<0>(d, xt, N, z, n, spec, tbits, hyp, Gk, coeffs, coeff_stride, B, out, out_stride, work, st,
+                               1, ProbStrides{0, 0, 0, 0}, chunk);
+  return launch_post_mean<1>(d, xt, N, z, n, spec, tbits, hyp, Gk, coeffs, coeff_stride, B, out, out_stride, work, st,
+                             1, ProbStrides{0, 0, 0, 0}, chunk);
 }
 
 }  // extern "C"

@@ -311,11 +311,22 @@ def _pred_args(family, alphas, d):
     return N.int_array([int(a) for a in alphas] if alphas is not None else [1] * d), N.double_array([0.0] * d)
 
 
-def post_mean_matfree(family, xt, z_dn, hyp, coeffs, alphas=None, tbits=0, chunk=1024):
+def post_mean_chunk(n, Nt, target_wg=1024):
+    """Training points per fgp_post_mean workgroup: 1024, or fewer (down to 32, powers of two) so that the
+    launch (ceil(n / chunk) x ceil(N / 256) workgroups) has about `target_wg` workgroups -- 4 per CU; at
+    n = 2^16 and N = 256, 1024 points per workgroup would leave 3/4 of the chip idle."""
+    tiles = max(1, (Nt + 255) // 256)
+    chunk = 1024
+    while chunk > 32 and ((n + chunk - 1) // chunk) * tiles < target_wg:
+        chunk //= 2
+    return chunk
+
+
+def post_mean_matfree(family, xt, z_dn, hyp, coeffs, alphas=None, tbits=0, chunk=None):
     """out[b, t] = sum_i K_{b mod Gk}(xt[t], z[:, i]) coeffs[b, i] -> [B, N] (see fgp_post_mean).
 
     xt [N, d] float64, z_dn [d, n] (float64 lattice / int64 net), hyp [Gk, 1 + d] (scale, lengthscales),
-    coeffs [B, n]."""
+    coeffs [B, n]; chunk = training points per workgroup (default: post_mean_chunk)."""
     require_device(xt, "post_mean")
     xt = xt.to(torch.float64).contiguous()
     Nt, d = xt.shape
@@ -330,6 +341,8 @@ def post_mean_matfree(family, xt, z_dn, hyp, coeffs, alphas=None, tbits=0, chunk
         coeffs = coeffs.contiguous()
     out = torch.empty((B, Nt), dtype=torch.float64, device=xt.device)
     order, coef = _pred_args(family, alphas, d)
+    if chunk is None:
+        chunk = post_mean_chunk(n, Nt)
     nchunks = (n + chunk - 1) // chunk
     for b0 in range(0, B, 4):
         b1 = min(B, b0 + 4)

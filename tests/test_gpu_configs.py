@@ -152,3 +152,37 @@ def test_half_length_post_var_matches_full_length_and_oracle(monkeypatch, m, d, 
     assert float((b1 - b0).abs().max()) <= 1e-10 * kxx
     assert float((s1 - opv).abs().max()) <= 1e-8 * kxx
     assert float((b1[0] - opv).abs().max()) <= 1e-8 * kxx
+
+
+@pytest.mark.parametrize("family", ["lattice", "net"])
+def test_post_mean_chunk_sizes_agree(family):
+    """fgp_post_mean with 32 .. 1024 training points per workgroup (ops.post_mean_chunk picks fewer for
+    small problems, so that n = 2^16, N = 256 fills the chip): the same sum in a different order.  The sum
+    cancels heavily (|coeffs| ~ |y| / noise, noise = 1e-8), so the orders agree to the posterior-mean
+    tolerance (1e-7 relative; measured 5e-9), not to the rounding of one term; the automatic choice is
+    what FastGP*.post_mean runs and it matches the oracle."""
+    n, d = 2 ** 16, 3
+    if family == "lattice":
+        gp = F.FastGPLattice(F.Lattice(d, seed=3), device=DEV)
+    else:
+        gp = F.FastGPDigitalNetB2(F.DigitalNetB2(d, seed=3), device=DEV)
+    x = gp.get_x_next(n)
+    y = O.f_ackley(x.cpu())
+    gp.add_y_next(y.to(DEV))
+    xt = torch.rand((256, d), generator=torch.Generator().manual_seed(5)).to(DEV)
+    assert F.ops.post_mean_chunk(n, 256) == 64 and F.ops.post_mean_chunk(2 ** 20, 256) == 1024
+    with torch.no_grad():
+        coeffs = gp.coeffs.reshape(1, n)
+        z = gp._points_T(n)
+        hyp = gp._hyp_rows(gp._has_batch_params())
+        outs = [F.ops.post_mean_matfree(gp._FAMILY, xt, z, hyp, coeffs, alphas=gp._alphas, tbits=gp._tbits(), chunk=c)
+                for c in (1024, 256, 64, 32)]
+        pm = gp.post_mean(xt)
+    ref = outs[0]
+    for o in outs[1:]:
+        assert float((o - ref).abs().max()) <= 1e-7 * float(ref.abs().max())
+    assert torch.equal(pm.reshape(-1), outs[2].reshape(-1))    # the automatic chunk (64) bit for bit
+    o = O.OracleFastGP(family, x.cpu(), gp.get_xb().cpu() if family == "net" else None, y, alpha=gp._alphas[0],
+                       t=getattr(gp, "t", None))
+    opm = o.post_mean(xt.cpu())
+    assert float((pm.cpu() - opm).abs().max()) <= 1e-7 * float(opm.abs().max())
