@@ -641,9 +641,15 @@ __global__ __launch_bounds__(ReGeo<P2>::WG, 4) void k_bwd_rows_re(Nll a, const d
 
 // real-even lattice kernels: row pairs of the length-n/2 transform (G N1/2 workgroups of N2/8 threads),
 // column tiles of its columns [0, N2/2) (G n/16384 workgroups of 256); N1 = n / (2 N2).
+// Rows of 2^11 (measured best: profiles/r02d_exp_re_rows_*); experiment builds (-DFGP_EXP_RE_P2ALL) also
+// compile rows of 2^10 and 2^12, selected by FGP_RE_P2 (a third of the build time without them).
 int re_row_log2(int log2n) {
+#ifdef FGP_EXP_RE_P2ALL
   const char* e = getenv("FGP_RE_P2");
   const int p2 = e && e[0] ? atoi(e) : kP2reDefault;
+#else
+  const int p2 = kP2reDefault;
+#endif
   return (p2 >= 10 && p2 <= 12 && log2n - 1 - p2 <= 12 && log2n - 1 - p2 >= 4) ? p2 : -1;
 }
 
@@ -683,9 +689,11 @@ static int launch_re_p2(const Nll& a, int stage, const Tables* tb, hipStream_t s
 
 static int launch_re_any(const Nll& a, int stage, const Tables* tb, hipStream_t st, const FitFuse& fz) {
   switch (re_row_log2(a.log2n)) {
+#ifdef FGP_EXP_RE_P2ALL
     case 10: return launch_re_p2<10>(a, stage, tb, st, fz);
-    case 11: return launch_re_p2<11>(a, stage, tb, st, fz);
     case 12: return launch_re_p2<12>(a, stage, tb, st, fz);
+#endif
+    case 11: return launch_re_p2<11>(a, stage, tb, st, fz);
     default: return set_error(kErrInvalid, "real-even fit kernels: no row split for log2n=%d", a.log2n);
   }
 }
