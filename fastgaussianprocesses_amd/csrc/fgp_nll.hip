@@ -912,7 +912,9 @@ static int to_nll(const fgp_nll_desc* d, Nll& a) {
   // generating vector entry odd (M z_j = n/2 mod n); an even entry takes the R2C kernels
   bool z_odd = true;
   for (int j = 0; j < d->d && d->parts_gen == FGP_PARTS_LATTICE; ++j) z_odd = z_odd && (d->gen_z[j] & 1);
-  a.re = a.r2c && d->parts_gen == FGP_PARTS_LATTICE && re_p2 > 0 && mode != '1' && z_odd;
+  // (the real-even kernels also take n = 2^16, where the R2C ones do not run: rows of 2^11, 16 rows)
+  a.re = d->family == FGP_FAMILY_LATTICE && d->log2n >= 16 && mode != '0' && mode != '1' &&
+         d->parts_gen == FGP_PARTS_LATTICE && re_p2 > 0 && z_odd;
   // per-block partials: one per row / row-pair workgroup (RE: N1/2 = n / 2^(P2 + 2) row pairs)
   a.nb = d->log2n > 12 ? 1 << (a.re ? d->log2n - 2 - re_p2 : d->log2n - 12 - (a.r2c ? 1 : 0)) : 1;
   a.nq = 4 + d->d;
@@ -1061,7 +1063,7 @@ template <typename T>
 static int nll_stage_t(const Nll& a, int stage, const Tables* tb, hipStream_t st) {
   if (a.log2n <= 12) return stage == 0 ? launch_iter_single<T>(a, tb, st) : kOk;
   if constexpr (sizeof(T) == 16) {
-    if (a.r2c) {
+    if (a.r2c || a.re) {
       if (stage < 0 || stage > 2) return set_error(kErrInvalid, "bad stage %d", stage);
       return a.re ? launch_re(a, stage, tb, st) : launch_r2c(a, stage, tb, st, false);
     }
@@ -1224,6 +1226,10 @@ int fgp_nll_lam(const fgp_nll_desc* desc, void* stream) {
   int rc = to_nll(desc, a);
   if (rc != kOk) return rc;
   if (!desc->grad_lam) return set_error(kErrInvalid, "fgp_nll_lam: null grad_lam (the output)");
+  if (a.re && !a.r2c) {   // n = 2^16: lambda by the full-length kernels (their block count)
+    a.re = false;
+    a.nb = 1 << (a.log2n - 12);
+  }
   hipStream_t st = (hipStream_t)stream;
   const Tables* tb = get_tables(st);
   if (!tb) return set_error(kErrHip, "twiddle table initialisation failed");

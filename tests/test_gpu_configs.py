@@ -44,8 +44,8 @@ def test_config_fit_and_predict_match_oracle(family, m, d, its, npm, npv):
     assert float((pv - opv.detach()).abs().max()) <= 1e-8 * kxx
 
 
-@pytest.mark.parametrize("m,d,alpha", [(17, 3, 2), (18, 2, 1), (19, 5, 2), (20, 5, 2), (20, 2, 2), (21, 3, 2),
-                                         (22, 3, 2), (24, 1, 2)])
+@pytest.mark.parametrize("m,d,alpha", [(16, 3, 2), (16, 5, 3), (17, 3, 2), (18, 2, 1), (19, 5, 2), (20, 5, 2),
+                                         (20, 2, 2), (21, 3, 2), (22, 3, 2), (24, 1, 2)])
 def test_half_length_fit_kernels_match_oracle(monkeypatch, m, d, alpha):
     """The lattice fit kernels for n >= 2^17 -- real-even (RE, regenerated parts; csrc/fgp_nll.hip
     k_*_re, the default), half-length (R2C, FGP_R2C=1; k_*_r2c) and full-length (FGP_R2C=0) -- on the
@@ -60,7 +60,7 @@ def test_half_length_fit_kernels_match_oracle(monkeypatch, m, d, alpha):
     the lengthscale gradient at n >= 2^19, d >= 3 (caught by this test).  The RE kernels treat lambda
     as exactly real and even (folded loss over n/2 + 1 frequencies, the gradient through the
     generated c_0 .. c_{n/2}); the oracle keeps the reference's complex arithmetic."""
-    n = 2 ** m
+    n = 2 ** m      # (n = 2^16: real-even and full-length kernels; FGP_R2C=1 runs the full-length ones there)
     ls = torch.linspace(0.6, 1.8, d)
     res = {}
     for mode in ("2", "1", "0"):
