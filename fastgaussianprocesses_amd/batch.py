@@ -11,9 +11,7 @@ own methods return: the stopping rule is applied per GP on its own loss history,
 parameters are restored, and the GP objects hold the fitted parameters and data afterwards.
 """
 import collections
-import ctypes
 import math
-import os
 
 import torch
 
@@ -416,44 +414,10 @@ class GPBatch(object):
         for t0 in range(0, Nt, chunk):
             t1 = min(Nt, t0 + chunk)
             xc = x[..., t0:t1, :].contiguous()
-            nt = t1 - t0
-            pc = self._post_var_problems(nt)
-            # one [pc, nt, n] intermediate reused by every problem group: the row pass writes it and the
-            # column pass reads it back while it is still in the MALL (256 MB)
-            work = torch.empty((pc, nt, self.n), dtype=cdt, device=self.device)
-            partial = torch.empty((self.P, nt, self.n >> 12), dtype=torch.float64, device=self.device)
-            oc = torch.empty((self.P, nt), dtype=torch.float64, device=self.device)
-            for p0 in range(0, self.P, pc):
-                p1 = min(self.P, p0 + pc)
-                sub = self._sub_desc(desc, p0, p1)
-                xp = xc if xc.ndim == 2 else xc[p0:p1]
-                N.call("fgp_post_var_batched", sub, N.ptr(xp), (0 if xp.ndim == 2 else xp.stride(0)), nt, part0,
-                       N.ptr(oc[p0:p1]), N.ptr(work), N.ptr(partial[p0:p1]), N.stream_ptr(self.device))
+            work = torch.empty((self.P, t1 - t0, self.n), dtype=cdt, device=self.device)
+            partial = torch.empty((self.P, t1 - t0, self.n >> 12), dtype=torch.float64, device=self.device)
+            oc = torch.empty((self.P, t1 - t0), dtype=torch.float64, device=self.device)
+            N.call("fgp_post_var_batched", desc, N.ptr(xc), (0 if xc.ndim == 2 else xc.stride(0)), t1 - t0, part0,
+                   N.ptr(oc), N.ptr(work), N.ptr(partial), N.stream_ptr(self.device))
             out[:, t0:t1] = oc
         return out
-
-    def _post_var_problems(self, nt):
-        """Problems per fgp_post_var_batched call: the used part of the intermediate (n/2 complex per test
-        point for lattices with n >= 2^17, R2C; n values otherwise) kept to <= 128 MB (FGP_PV_MB), half the
-        MALL; all P at once when FGP_PV_MB=0."""
-        mb = int(os.environ.get("FGP_PV_MB", "128"))
-        if mb <= 0:
-            return self.P
-        per = nt * (self.n * 8 if self.family == ops.LATTICE and self.m >= 17 else self.n * 16 if
-                    self.family == ops.LATTICE else self.n * 8)
-        return max(1, min(self.P, (mb << 20) // per))
-
-    @staticmethod
-    def _sub_desc(desc, p0, p1):
-        """fgp_pred_desc over problems [p0, p1) of `desc` (pointers advanced by the per-problem strides)."""
-        if p0 == 0 and p1 == desc.P:
-            return desc
-        sub = N.PredDesc()
-        ctypes.pointer(sub)[0] = desc
-        sub.P = p1 - p0
-        for name, stride in (("z", "z_stride"), ("hyp", "hyp_stride"), ("coeffs", "coeff_stride"),
-                             ("wa", "wa_stride"), ("gen_shift", "gen_shift_stride")):
-            ptr = getattr(desc, name)
-            if ptr:
-                setattr(sub, name, ptr + 8 * p0 * getattr(desc, stride))
-        return sub
