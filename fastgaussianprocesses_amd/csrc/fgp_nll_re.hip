@@ -31,6 +31,11 @@ namespace fgp {
 // rows write n/4 complex (4n B), columns read 4n + Y 4n and write 4n, rows read 4n: 20n bytes
 // (R2C 40n), and half the eigenvalue terms and kernel parts.
 constexpr int kP2reDefault = 11;             // row length 2^P2 of the n/2-point transform (FGP_RE_P2)
+// unroll factor of the column kernel's eigen-term loop; experiment builds may also set one for the
+// backward kernel's gradient loop over the 8 mirror pairs (FGP_RE_GRAD_UNROLL; default: the compiler's)
+#ifndef FGP_RE_EIG_UNROLL
+#define FGP_RE_EIG_UNROLL 2
+#endif
 
 // v * exp(-2 pi i J / 32), J < 32 compile-time
 template <int J>
@@ -370,7 +375,7 @@ __global__ __launch_bounds__(kWG) void k_fwd_cols_re(Nll a, const double2* __res
   for (int j = 0; j < 16 / RLAST; ++j)
 #pragma unroll
     for (int t = 0; t < RLAST; ++t) col[pass_pos<P1, SL, RLL>(tt, j, t)] = v[j * RLAST + t];
-#pragma unroll 2
+#pragma unroll FGP_RE_EIG_UNROLL
   for (int k = 0; k < 16; ++k) {
     const int pos = pass_pos<P1, SL, RLL>(tt, k / RLAST, k % RLAST);
     const double2 yk = y2[k1 + N2 * pos];
@@ -588,6 +593,9 @@ __global__ __launch_bounds__(ReGeo<P2>::WG, 4) void k_bwd_rows_re(Nll a, const d
 #ifdef FGP_EXP_NOGEN
     for (int e = 0; e < 8; ++e) acc[0] += gl[2 * e] + gl[2 * e + 1];
     if (false)
+#endif
+#ifdef FGP_RE_GRAD_UNROLL
+#pragma unroll FGP_RE_GRAD_UNROLL
 #endif
     for (int e = 0; e < 8; ++e) {
       const unsigned i = (unsigned)rp.r + (unsigned)N1 * (((__builtin_bitreverse32((unsigned)e) >> 28) << (P2 - 4)) | sq);
