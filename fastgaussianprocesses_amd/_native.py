@@ -12,7 +12,7 @@ import torch
 
 _LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
 LIB_PATH = os.environ.get("FGP_LIB_PATH") or os.path.join(_LIB_DIR, "libfgp_hip.so")   # override: experiments
-ABI_VERSION = 9
+ABI_VERSION = 10
 MT_MAX_TASKS = 16
 MAX_D = 8
 PARTS_ARRAY = 0
@@ -91,6 +91,7 @@ _SIGNATURES = {
     "fgp_fftbr": [_c_vp, _c_i64, _c_int, _c_vp, _c_i64, _c_int, _c_int, _c_vp],
     "fgp_ifftbr": [_c_vp, _c_i64, _c_vp, _c_int, _c_vp, _c_i64, _c_int, _c_int, _c_vp],
     "fgp_fwht": [_c_vp, _c_i64, _c_vp, _c_i64, _c_int, _c_int, _c_vp],
+    "fgp_fftbr_real": [_c_vp, _c_i64, _c_vp, _c_vp, _c_i64, _c_int, _c_vp],
     "fgp_fftbr_c64": [_c_vp, _c_i64, _c_int, _c_vp, _c_i64, _c_int, _c_int, _c_vp],
     "fgp_ifftbr_c64": [_c_vp, _c_i64, _c_vp, _c_int, _c_vp, _c_i64, _c_int, _c_int, _c_vp],
     "fgp_fwht_f32": [_c_vp, _c_i64, _c_vp, _c_i64, _c_int, _c_int, _c_vp],

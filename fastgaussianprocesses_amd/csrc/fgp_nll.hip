@@ -486,6 +486,44 @@ __global__ __launch_bounds__(kWG) void k_fwd_rows_r2c(Nll a, const double2* __re
   stamp_end(a);
 }
 
+// The same row pass on a REAL input array (fgp_fftbr_real): x[:n/2] + i x[n/2:] of problem g read as
+// 16-byte pairs instead of generated k1.
+__global__ __launch_bounds__(kWG) void k_fwd_rows_r2c_in(const double* __restrict__ in, int64_t in_stride, int log2n,
+                                                         double2* __restrict__ work, const double2* __restrict__ tw,
+                                                         const double2* __restrict__ twm) {
+  constexpr int P2 = 12, N2 = 1 << P2;
+  __shared__ double ldsd[kTile + kTile / 16];
+  __shared__ double2 red[kWG / 64];
+  const int mt = log2n - 1, m1 = mt - P2;
+  const int64_t n = (int64_t)1 << log2n, nt = n >> 1;
+  const int64_t tiles = nt >> kTileLog;
+  const int64_t g = blockIdx.x / tiles;
+  const int row0 = (int)(blockIdx.x % tiles);
+  const int tid = threadIdx.x;
+  const double* x = in + g * in_stride + (int64_t)row0 * N2 + 16 * tid;
+  double2 v[16];
+  double2 sum = make_double2(0.0, 0.0);
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const double2 lo = *reinterpret_cast<const double2*>(x + 2 * u);
+    const double2 hi = *reinterpret_cast<const double2*>(x + nt + 2 * u);
+    v[2 * u] = make_double2(lo.x, hi.x);
+    v[2 * u + 1] = make_double2(lo.y, hi.y);
+  }
+#pragma unroll
+  for (int t = 0; t < 16; ++t) sum += v[t];
+  const double2 mean = block_sum_t(sum, red) * (1.0 / N2);
+#pragma unroll
+  for (int t = 0; t < 16; ++t) v[t] -= mean;
+  fwd_reg_passes<P2, 0, true>(v, ldsd, tid, tw);
+  if (tid == 0) v[0] += mean * (double)N2;
+  const RowTwiddle rt((unsigned)row0, tid, P2, m1, tw, twm);
+  double2* out = work + g * n;
+#pragma unroll
+  for (int k = 0; k < 16; ++k)
+    out[work_pos_pair(row0, tid + k * kWG, m1, N2)] = tw_mul<double2>(v[k], rt.at(k, P2, m1, tw, twm), false);
+}
+
 // Mirror-pair evaluation of the R2C column kernel.  The pair (k, nt - k) of the half-length spectrum Z
 // (primary Z_k = zk, partner Z_{nt-k} = zm, W = w_n^k) gives the length-n spectrum at k and k + n/2:
 //   A0, A1 = (S -/+ i W D) / 2,  S = Z_k + conj Z_{nt-k},  D = Z_k - conj Z_{nt-k}
@@ -1259,6 +1297,39 @@ int fgp_nll_bwd(const fgp_nll_desc* desc, void* stream) {
   int rc = to_nll(desc, a);
   if (rc != kOk) return rc;
   return nll_bwd(a, (hipStream_t)stream, desc->family == FGP_FAMILY_LATTICE);
+}
+
+int fgp_fftbr_real(const double* in, int64_t in_batch_stride, void* out, void* work, int64_t batch, int log2n,
+                   void* stream) {
+  if (log2n < 17 || log2n > 24 || batch < 0) return set_error(kErrInvalid, "fgp_fftbr_real: needs 17 <= log2n <= 24");
+  if (batch == 0) return kOk;
+  if (!in || !out || !work) return set_error(kErrInvalid, "fgp_fftbr_real: null pointer");
+  if (in_batch_stride < ((int64_t)1 << log2n) && batch > 1)
+    return set_error(kErrInvalid, "fgp_fftbr_real: batch stride below n");
+  if (((uintptr_t)in & 15) || (in_batch_stride & 1)) return set_error(kErrInvalid, "fgp_fftbr_real: in must be 16-byte aligned rows");
+  const int64_t tiles = (int64_t)1 << (log2n - 1 - kTileLog);
+  if (batch * tiles >= ((int64_t)1 << 31)) return set_error(kErrUnsupported, "fgp_fftbr_real: batch too large");
+  hipStream_t st = (hipStream_t)stream;
+  const Tables* tb = get_tables(st);
+  if (!tb) return set_error(kErrHip, "twiddle table initialisation failed");
+  const int mt = log2n - 1, p1 = mt - 12;
+  const unsigned grid = (unsigned)(batch * tiles);
+  k_fwd_rows_r2c_in<<<grid, kWG, 0, st>>>(in, in_batch_stride, log2n, static_cast<double2*>(work), tb->tw4096, tb->twm[mt]);
+  int rc = check_launch("k_fwd_rows_r2c_in");
+  if (rc != kOk) return rc;
+  Nll a{};
+  a.log2n = log2n;
+  a.G = (int)batch;
+  a.work = work;
+  a.grad_lam = out;
+  a.stamps = nullptr;
+  switch (p1) {
+#define FGP_C(PP) case PP: k_fwd_cols_r2c<PP, true><<<grid, kWG, 0, st>>>(a, tb->tw4096, tb->twm[log2n]); break;
+    FGP_C(4) FGP_C(5) FGP_C(6) FGP_C(7) FGP_C(8) FGP_C(9) FGP_C(10) FGP_C(11)
+#undef FGP_C
+    default: return set_error(kErrInvalid, "bad r2c m1");
+  }
+  return check_launch("k_fwd_cols_r2c");
 }
 
 int fgp_fit_step(const fgp_nll_desc* nll, const fgp_fit_desc* fit, int iter, int do_update, void* stream) {

@@ -13,6 +13,7 @@ all differentiable (backward = the exact adjoint transform, real part for real i
 With stable=True the mean-centring of AbstractFastGP.ft/ift happens inside the kernels.
 """
 import math
+import os
 
 import numpy as np
 
@@ -75,9 +76,24 @@ def fftbr_raw(x, stable=True):
     m = log2_exact(n)
     rows, bs = _as_rows(x)
     out = torch.empty(rows.shape, dtype=cdt, device=x.device)
+    if _real_half_length(x, m) and rows.data_ptr() % 16 == 0 and bs % 2 == 0:
+        # real float64 input, 2^17 <= n <= 2^24: the half-length transform (fgp_fftbr_real, 40n instead
+        # of 56n bytes per row)
+        work = torch.empty(rows.shape, dtype=cdt, device=x.device)
+        N.call("fgp_fftbr_real", N.ptr(rows), bs, N.ptr(out), N.ptr(work), rows.size(0), m, _stream(x))
+        return out.reshape(shape)
     N.call("fgp_fftbr_c64" if sp else "fgp_fftbr", N.ptr(rows), bs, 0 if x.is_complex() else 1, N.ptr(out),
            rows.size(0), m, int(stable), _stream(x))
     return out.reshape(shape)
+
+
+def _real_half_length(x, m):
+    """fgp_fftbr_real applies: float64 real input, 17 <= m <= 24 (FGP_R2C=0 keeps the full-length path)."""
+    return (x.dtype == torch.float64 and 17 <= m <= 24 and rows_ok_env())
+
+
+def rows_ok_env():
+    return os.environ.get("FGP_R2C", "2")[:1] != "0"
 
 
 def ifftbr_raw(x, stable=True, real_out=False):

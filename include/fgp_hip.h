@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define FGP_ABI_VERSION 9
+#define FGP_ABI_VERSION 10
 
 #define FGP_OK 0
 #define FGP_ERR_INVALID (-1)     /* bad argument (shape, stride, null pointer) */
@@ -62,6 +62,16 @@ int fgp_ifftbr(const void* in, int64_t in_batch_stride, void* out, int out_real,
  * when in_batch_stride == n. */
 int fgp_fwht(const double* in, int64_t in_batch_stride, double* out, int64_t batch, int log2n, int stable,
              void* stream);
+
+/* fftbr of REAL float64 input at half length (ABI 10), 17 <= log2n <= 24: the packed
+ * z = x[:n/2] + i x[n/2:] through an n/2-point transform and the split
+ *   out[k], out[k + n/2] = 1/2 (Z_k + conj Z_{n/2-k}) -/+ 1/2 i w_n^k (Z_k - conj Z_{n/2-k})
+ * in the column pass (the fit's R2C kernels, emitting the spectrum): 40n bytes moved per row instead of
+ * the full-length transform's 56n.  out: [batch][n] complex128 (the whole spectrum); work: device
+ * scratch of batch * n complex128.  Same values as fgp_fftbr(in_is_real = 1) up to rounding (the
+ * engine centres every row / column internally, so `stable` needs no separate pass). */
+int fgp_fftbr_real(const double* in, int64_t in_batch_stride, void* out, void* work, int64_t batch, int log2n,
+                   void* stream);
 
 /* Single-precision variants (complex64 / float32; SURVEY §8(b) fgp_fftbr_c64 / fgp_ifftbr_c64 /
  * fgp_fwht_f32): the same transforms, arguments and layouts with float / complex64 in place of

@@ -265,3 +265,20 @@ def test_device_point_generators_are_bit_identical(d, t):
         ref = net(n_min=n0, n_max=n1, return_binary=True).astype(np.int64)
         assert np.array_equal(xb.cpu().numpy(), ref)
         assert np.array_equal(x.cpu().numpy(), ref.astype(np.float64) * 2.0 ** (-t))
+
+
+@pytest.mark.parametrize("m,batch", [(17, 3), (18, 2), (20, 2), (22, 1), (24, 1)])
+def test_fftbr_real_half_length_matches_full_length(monkeypatch, m, batch):
+    """fgp_fftbr_real (real float64 input, n >= 2^17: the n/2-point packed transform with the split in
+    the column pass) against the full-length fgp_fftbr (FGP_R2C=0) on the same rows, batched and from a
+    strided view, to the transform tolerance; and against the oracle at m <= 20."""
+    n = 2 ** m
+    g = torch.Generator().manual_seed(300 + m)
+    x = (torch.randn((batch, n + 8), generator=g) + 1.5).to(DEV)
+    xs = x[:, :n]                                   # row stride n + 8 (view, even stride)
+    half = F.ops.fftbr_raw(xs, stable=True)
+    monkeypatch.setenv("FGP_R2C", "0")
+    full = F.ops.fftbr_raw(xs, stable=True)
+    _close(half, full, m)
+    if m <= 20:
+        _close(half, O.ft_stable(xs.cpu(), O.fftbr), m)
