@@ -92,6 +92,7 @@ _SIGNATURES = {
     "fgp_ifftbr": [_c_vp, _c_i64, _c_vp, _c_int, _c_vp, _c_i64, _c_int, _c_int, _c_vp],
     "fgp_fwht": [_c_vp, _c_i64, _c_vp, _c_i64, _c_int, _c_int, _c_vp],
     "fgp_fftbr_real": [_c_vp, _c_i64, _c_vp, _c_vp, _c_i64, _c_int, _c_vp],
+    "fgp_ifftbr_real": [_c_vp, _c_i64, _c_vp, _c_i64, _c_vp, _c_i64, _c_vp, _c_i64, _c_int, _c_vp],
     "fgp_fftbr_c64": [_c_vp, _c_i64, _c_int, _c_vp, _c_i64, _c_int, _c_int, _c_vp],
     "fgp_ifftbr_c64": [_c_vp, _c_i64, _c_vp, _c_int, _c_vp, _c_i64, _c_int, _c_int, _c_vp],
     "fgp_fwht_f32": [_c_vp, _c_i64, _c_vp, _c_i64, _c_int, _c_int, _c_vp],

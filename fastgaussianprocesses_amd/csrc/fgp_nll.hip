@@ -740,6 +740,154 @@ __global__ __launch_bounds__(kWG, 2) void k_fwd_cols_r2c(Nll a, const double2* _
   stamp_end(a);
 }
 
+// ---------------------------------------------------------------- half-length real-output inverse
+// x = Re ifftbr_n(X) (orthonormal) for a spectrum X [n] (fgp_ifftbr_real): the adjoint of the packed
+// forward above.  With X~ the Hermitian part of X (X~_k = (X_k + conj X_{n-k}) / 2: Re ifftbr(X) =
+// ifftbr(X~) exactly), V_k = E + i O, E = X~_k + X~_{k+n/2}, O = (X~_k - X~_{k+n/2}) conj(w_n^k), and
+//   x[:n/2] + i x[n/2:] = DFT_{n/2}^H(V) / sqrt(n)
+// (the fit kernels' V packing with X in place of dL/dlambda).  The column kernel takes each mirror pair
+// (k, k + n/2; n/2 - k, n - k) once -- reading the four values, so X~ is the exact Hermitian part --
+// writes V of both partners into the LDS image and runs the adjoint column pass; the row kernel runs the
+// conjugate-twiddled adjoint row pass and writes the real rows.  f (optional): X = in * f, fused into the
+// loads (the tilde-domain solve of gram_matrix_solve, util.py:341-343).
+template <int P1>
+__global__ __launch_bounds__(kWG, 2) void k_inv_cols_c2r(const double2* __restrict__ X, int64_t xs,
+                                                         const double2* __restrict__ f, int64_t fs,
+                                                         double2* __restrict__ work, int log2n,
+                                                         const double2* __restrict__ tw,
+                                                         const double2* __restrict__ twmf) {
+  constexpr int N1 = 1 << P1, C = kTile / N1, CS = N1 + 1, HC = C / 2;
+  constexpr int RL0 = PassRL<P1, 0>::value, R0 = 1 << RL0;
+  constexpr int SL = LastPass<P1>::S, RLL = PassRL<P1, SL>::value, RLAST = 1 << RLL;
+  constexpr int JOBS = kTile / 2 / kWG, RSTEP = kWG / HC;     // JOBS * RSTEP = N1
+  static_assert(JOBS * RSTEP == N1, "pair jobs cover the tile");
+  __shared__ double2 lds[C * CS];
+  __shared__ double2 part[ColPart<C>::size];
+  const int m = log2n;
+  const int64_t n = (int64_t)1 << m, nt = n >> 1, N2 = nt >> P1;
+  const int64_t tiles = nt >> kTileLog;
+  const int64_t g = blockIdx.x / tiles;
+  const int blk = (int)(blockIdx.x % tiles);
+  const int tid = threadIdx.x;
+  const int sl = tid % C, tt = tid / C;
+  double2* col = lds + sl * CS;
+  const int q = tid % HC, rr0 = tid / HC;
+  const bool col0 = blk == 0 && q == 0;                      // tile 0's self-mirrored columns
+  const int64_t cp_gen = (int64_t)blk * HC + q;
+  const double2* xg = X + g * xs;
+  const double2* fg = f ? f + g * fs : nullptr;
+  auto xv = [&](int64_t k) {
+    const double2 v = xg[k];
+    return fg ? cmul(v, fg[k]) : v;
+  };
+  // Hermitian part at (k, k + n/2) given the partner pair (n/2 - k, n - k): X~_k, X~_{k+n/2}
+  auto herm = [&](int64_t k, int64_t ks, double2& h0, double2& h1) {
+    const double2 a0 = xv(k), a1 = xv(k + nt), b0 = xv(ks), b1 = xv(ks + nt);   // X_k, X_{k+nt}, X_{nt-k}, X_{n-k}
+    h0 = make_double2(0.5 * (a0.x + b1.x), 0.5 * (a0.y - b1.y));
+    h1 = make_double2(0.5 * (a1.x + b0.x), 0.5 * (a1.y - b0.y));
+  };
+  auto vpack = [](double2 h0, double2 h1, double2 W, double2& vp, double2& vs) {
+    const double2 E = h0 + h1;
+    const double2 O = cmulc(h0 - h1, W);
+    vp = make_double2(E.x - O.y, E.y + O.x);                        // V = E + i O
+    vs = make_double2(E.x + O.y, O.x - E.y);                        // the partner's (conjugate arithmetic)
+  };
+  const double2 wcp = twmf[col0 ? 0 : cp_gen];
+#pragma unroll 2
+  for (int j = 0; j < JOBS; ++j) {
+    const int rr = rr0 + RSTEP * j;
+    int sp, rp, ss, rs;
+    int64_t cp;
+    if (!col0) {
+      sp = q; rp = rr; cp = cp_gen; ss = sp + HC; rs = N1 - 1 - rp;
+    } else if (rr < N1 / 2) {
+      sp = 0; rp = rr; cp = 0; ss = 0; rs = (N1 - rp) & (N1 - 1);
+    } else {
+      sp = HC; rp = rr - N1 / 2; cp = N2 >> 1; ss = HC; rs = N1 - 1 - rp;
+    }
+    const bool self = col0 && sp == 0 && rp == 0;   // frequencies 0, n/2 and (second element) n/4, 3n/4
+    const double2 wc = col0 ? twmf[cp] : wcp;
+    const double2 W = cmul(wc, tw[rp << (24 - m)]);                 // w_n^k, k = cp + N2 rp
+    const int64_t kp = cp + (int64_t)rp * N2;
+    double2 h0, h1, vp, vs;
+    herm(kp, self ? 0 : nt - kp, h0, h1);
+    if (self) {   // partners of 0 and n/2 are themselves: the real parts
+      h0 = make_double2(xv(0).x, 0.0);
+      h1 = make_double2(xv(nt).x, 0.0);
+    }
+    vpack(h0, h1, W, vp, vs);
+    lds[sp * CS + rp] = vp;
+    if (!self) lds[ss * CS + rs] = vs;
+    if (self) {   // column 0, row N1/2: frequencies n/4 and 3n/4, mirrors of each other
+      constexpr int rh = N1 / 2;
+      const int64_t kh = (int64_t)rh * N2;
+      const double2 a0 = xv(kh), a1 = xv(kh + nt);
+      const double2 hh0 = make_double2(0.5 * (a0.x + a1.x), 0.5 * (a0.y - a1.y));
+      const double2 hh1 = make_double2(hh0.x, -hh0.y);
+      double2 vh, unused;
+      vpack(hh0, hh1, tw[rh << (24 - m)], vh, unused);
+      lds[rh] = vh;
+    }
+  }
+  __syncthreads();
+  double2 v[16];
+  double2 sum = zero_v<double2>();
+#pragma unroll
+  for (int j = 0; j < 16 / RLAST; ++j)
+#pragma unroll
+    for (int t = 0; t < RLAST; ++t) {
+      v[j * RLAST + t] = col[pass_pos<P1, SL, RLL>(tt, j, t)];
+      sum += v[j * RLAST + t];
+    }
+  column_partials<C>(sum, part);
+  const double2 mean = column_total<C>(sl, part) * (1.0 / N1);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v[k] -= mean;
+  adj_reg_passes<P1, SL, false>(v, col, tt, tw);
+  if (tt == 0) v[0] += mean * (double)N1;
+  const WtStore wo(work + g * n);
+  const unsigned o0 = (unsigned)((int64_t)blk * kTile + sl);
+#pragma unroll
+  for (int j = 0; j < 16 / R0; ++j)
+#pragma unroll
+    for (int t = 0; t < R0; ++t) wo.put(o0 + (unsigned)(pass_pos<P1, 0, RL0>(tt, j, t) * C), v[j * R0 + t]);
+}
+
+__global__ __launch_bounds__(kWG) void k_inv_rows_c2r(const double2* __restrict__ work, int log2n, double* __restrict__ out,
+                                                      int64_t out_stride, const double2* __restrict__ tw,
+                                                      const double2* __restrict__ twm) {
+  constexpr int P2 = 12, N2 = 1 << P2;
+  __shared__ double ldsd[kTile + kTile / 16];
+  __shared__ double2 red[kWG / 64];
+  const int mt = log2n - 1, m1 = mt - P2;
+  const int64_t n = (int64_t)1 << log2n, nt = n >> 1;
+  const int64_t tiles = nt >> kTileLog;
+  const int64_t g = blockIdx.x / tiles;
+  const int row0 = (int)(blockIdx.x % tiles);
+  const int tid = threadIdx.x;
+  const double2* in = work + g * n;
+  double2 v[16];
+  double2 sum = zero_v<double2>();
+  const RowTwiddle rt((unsigned)row0, tid, P2, m1, tw, twm);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    v[k] = tw_mul<double2>(in[work_pos_pair(row0, tid + k * kWG, m1, N2)], rt.at(k, P2, m1, tw, twm), true);
+    sum += v[k];
+  }
+  const double2 mean = block_sum_t(sum, red) * (1.0 / N2);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v[k] -= mean;
+  adj_reg_passes<P2, LastPass<P2>::S, true>(v, ldsd, tid, tw);
+  if (tid == 0) v[0] += mean * (double)N2;
+  const double gs = 1.0 / sqrt((double)n);
+  double* xo = out + g * out_stride + (int64_t)row0 * N2 + 16 * tid;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    *reinterpret_cast<double2*>(xo + 2 * u) = make_double2(v[2 * u].x * gs, v[2 * u + 1].x * gs);
+    *reinterpret_cast<double2*>(xo + nt + 2 * u) = make_double2(v[2 * u].y * gs, v[2 * u + 1].y * gs);
+  }
+}
+
 // adjoint half-length row pass: Re -> gradient terms of x[:n/2], Im -> of x[n/2:]
 template <int PG, int D>
 __global__ __launch_bounds__(kWG) void k_bwd_rows_r2c(Nll a, const double2* __restrict__ tw, const double2* __restrict__ twm) {
@@ -1330,6 +1478,37 @@ int fgp_fftbr_real(const double* in, int64_t in_batch_stride, void* out, void* w
     default: return set_error(kErrInvalid, "bad r2c m1");
   }
   return check_launch("k_fwd_cols_r2c");
+}
+
+int fgp_ifftbr_real(const void* in, int64_t in_batch_stride, const void* f, int64_t f_batch_stride, double* out,
+                    int64_t out_batch_stride, void* work, int64_t batch, int log2n, void* stream) {
+  if (log2n < 17 || log2n > 24 || batch < 0) return set_error(kErrInvalid, "fgp_ifftbr_real: needs 17 <= log2n <= 24");
+  if (batch == 0) return kOk;
+  if (!in || !out || !work) return set_error(kErrInvalid, "fgp_ifftbr_real: null pointer");
+  const int64_t n = (int64_t)1 << log2n;
+  if (batch > 1 && (in_batch_stride < n || out_batch_stride < n))
+    return set_error(kErrInvalid, "fgp_ifftbr_real: batch stride below n");
+  if (((uintptr_t)out & 15) || (out_batch_stride & 1)) return set_error(kErrInvalid, "fgp_ifftbr_real: out must be 16-byte aligned rows");
+  const int64_t tiles = (int64_t)1 << (log2n - 1 - kTileLog);
+  if (batch * tiles >= ((int64_t)1 << 31)) return set_error(kErrUnsupported, "fgp_ifftbr_real: batch too large");
+  hipStream_t st = (hipStream_t)stream;
+  const Tables* tb = get_tables(st);
+  if (!tb) return set_error(kErrHip, "twiddle table initialisation failed");
+  const int mt = log2n - 1, p1 = mt - 12;
+  const unsigned grid = (unsigned)(batch * tiles);
+  const double2* X = static_cast<const double2*>(in);
+  const double2* F = static_cast<const double2*>(f);
+  double2* wk = static_cast<double2*>(work);
+  switch (p1) {
+#define FGP_C(PP) case PP: k_inv_cols_c2r<PP><<<grid, kWG, 0, st>>>(X, in_batch_stride, F, f_batch_stride, wk, log2n, tb->tw4096, tb->twm[log2n]); break;
+    FGP_C(4) FGP_C(5) FGP_C(6) FGP_C(7) FGP_C(8) FGP_C(9) FGP_C(10) FGP_C(11)
+#undef FGP_C
+    default: return set_error(kErrInvalid, "bad c2r m1");
+  }
+  int rc = check_launch("k_inv_cols_c2r");
+  if (rc != kOk) return rc;
+  k_inv_rows_c2r<<<grid, kWG, 0, st>>>(wk, log2n, out, out_batch_stride, tb->tw4096, tb->twm[mt]);
+  return check_launch("k_inv_rows_c2r");
 }
 
 int fgp_fit_step(const fgp_nll_desc* nll, const fgp_fit_desc* fit, int iter, int do_update, void* stream) {

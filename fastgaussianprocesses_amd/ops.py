@@ -107,6 +107,12 @@ def ifftbr_raw(x, stable=True, real_out=False):
     n = shape[-1]
     m = log2_exact(n)
     rows, bs = _as_rows(x)
+    if real_out and not sp and 17 <= m <= 24 and rows_ok_env():
+        # real part at half length (fgp_ifftbr_real): the Hermitian part through an n/2-point transform
+        out = torch.empty(rows.shape, dtype=rdt, device=x.device)
+        work = torch.empty(rows.shape, dtype=cdt, device=x.device)
+        N.call("fgp_ifftbr_real", N.ptr(rows), bs, None, 0, N.ptr(out), n, N.ptr(work), rows.size(0), m, _stream(x))
+        return out.reshape(shape)
     if real_out:
         out = torch.empty(rows.shape, dtype=rdt, device=x.device)
         work = torch.empty(rows.shape, dtype=cdt, device=x.device) if m > 12 else None
@@ -176,6 +182,13 @@ def inverse_mul(family, x, f, real_out=False, stable=True):
         prod = x * f
         return ifftbr_raw(prod, stable, real_out) if family == LATTICE else fwht_raw(prod, stable)
     f2 = f2.contiguous()
+    if family == LATTICE and real_out and not sp and 17 <= m <= 24 and rows_ok_env():
+        # Re ift(x * f) at half length (fgp_ifftbr_real, the product fused into the column loads)
+        out = torch.empty(rows.shape, dtype=torch.float64, device=x.device)
+        work = torch.empty(rows.shape, dtype=rows.dtype, device=x.device)
+        N.call("fgp_ifftbr_real", N.ptr(rows), bs, N.ptr(f2), fbs, N.ptr(out), n, N.ptr(work), rows.size(0), m,
+               _stream(x))
+        return out.reshape(x.shape)
     if family == LATTICE:
         odt = (torch.float32 if sp else torch.float64) if real_out else rows.dtype
         out = torch.empty(rows.shape, dtype=odt, device=x.device)

@@ -73,6 +73,14 @@ int fgp_fwht(const double* in, int64_t in_batch_stride, double* out, int64_t bat
 int fgp_fftbr_real(const double* in, int64_t in_batch_stride, void* out, void* work, int64_t batch, int log2n,
                    void* stream);
 
+/* Real part of the orthonormal ifftbr of complex128 rows at half length (ABI 10), 17 <= log2n <= 24:
+ *   out[b] = Re ifftbr(in[b] * f[b])      (f NULL: no product; f_batch_stride 0: one shared row)
+ * (gram_matrix_solve's ift(A * y~).real, util.py:341-343) through the adjoint of fgp_fftbr_real: the
+ * Hermitian part of each mirror pair packed into V = E + i O, an n/2-point adjoint transform, real rows
+ * out.  out: [batch][n] float64 (16-byte aligned rows); work: device scratch of batch * n complex128. */
+int fgp_ifftbr_real(const void* in, int64_t in_batch_stride, const void* f, int64_t f_batch_stride, double* out,
+                    int64_t out_batch_stride, void* work, int64_t batch, int log2n, void* stream);
+
 /* Single-precision variants (complex64 / float32; SURVEY §8(b) fgp_fftbr_c64 / fgp_ifftbr_c64 /
  * fgp_fwht_f32): the same transforms, arguments and layouts with float / complex64 in place of
  * double / complex128 (fgp_fftbr_c64: in float32 when in_is_real, else complex64; out complex64;

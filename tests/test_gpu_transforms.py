@@ -282,3 +282,26 @@ def test_fftbr_real_half_length_matches_full_length(monkeypatch, m, batch):
     _close(half, full, m)
     if m <= 20:
         _close(half, O.ft_stable(xs.cpu(), O.fftbr), m)
+
+
+@pytest.mark.parametrize("m,batch,shared_f", [(17, 3, False), (18, 2, True), (20, 2, False), (22, 1, True),
+                                              (24, 1, False)])
+def test_ifftbr_real_half_length_matches_full_length(monkeypatch, m, batch, shared_f):
+    """fgp_ifftbr_real (Re ifftbr at half length: the Hermitian part of every mirror pair packed into an
+    n/2-point adjoint transform) against the full-length real-output inverse (FGP_R2C=0), on arbitrary
+    (non-Hermitian) complex rows, without and with the fused product (inverse_mul, one shared row or one
+    per row), to the transform tolerance; and against the oracle at m <= 20."""
+    n = 2 ** m
+    g = torch.Generator().manual_seed(400 + m)
+    x = (torch.randn((batch, n), generator=g) + 1j * torch.randn((batch, n), generator=g) + 0.5).to(DEV)
+    f = (torch.rand((1 if shared_f else batch, n), generator=g) + 0.5 + 0.1j * torch.randn((1 if shared_f else batch, n), generator=g)).to(DEV)
+    half = F.ops.ifftbr_raw(x, stable=True, real_out=True)
+    half_mul = F.ops.inverse_mul(F.ops.LATTICE, x, f, real_out=True)
+    monkeypatch.setenv("FGP_R2C", "0")
+    full = F.ops.ifftbr_raw(x, stable=True, real_out=True)
+    full_mul = F.ops.inverse_mul(F.ops.LATTICE, x, f, real_out=True)
+    assert half.dtype == torch.float64 and half.shape == (batch, n)
+    _close(half, full, m)
+    _close(half_mul, full_mul, m)
+    if m <= 20:
+        _close(half, O.ft_stable(x.cpu(), O.ifftbr).real, m)
