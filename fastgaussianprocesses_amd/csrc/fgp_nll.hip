@@ -793,7 +793,10 @@ __global__ __launch_bounds__(kWG, 2) void k_inv_cols_c2r(const double2* __restri
     vs = make_double2(E.x + O.y, O.x - E.y);                        // the partner's (conjugate arithmetic)
   };
   const double2 wcp = twmf[col0 ? 0 : cp_gen];
-#pragma unroll 2
+#ifndef FGP_C2R_UNROLL
+#define FGP_C2R_UNROLL 8   // measured: 1501 vs 1533 us at 512 x 2^18 (profiles/r02i_exp_half_length_transforms.jsonl)
+#endif
+#pragma unroll FGP_C2R_UNROLL
   for (int j = 0; j < JOBS; ++j) {
     const int rr = rr0 + RSTEP * j;
     int sp, rp, ss, rs;
