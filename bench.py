@@ -363,9 +363,9 @@ def roofline_fit_kernels(F, shifts, iters):
 
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02j_pmc_fit_kernels.json")
-PMC_SQ_SUMMARY = os.path.join(ROOT, "profiles", "r02j_pmc_sq_fit_kernels.json")
-ROCPROF_GRID_STATS = os.path.join(ROOT, "profiles", "r02l_bench_kernel_grid_stats.txt")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02m_pmc_fit_kernels.json")
+PMC_SQ_SUMMARY = os.path.join(ROOT, "profiles", "r02m_pmc_sq_fit_kernels.json")
+ROCPROF_GRID_STATS = os.path.join(ROOT, "profiles", "r02m_bench_kernel_grid_stats.txt")
 # FP64 VALU lane-operations per second: 256 CUs x 4 SIMDs x 16 FP64 lanes per clock x 2.4 GHz = 3.93e13
 # (FP64 vector at half the FP32 vector rate of MI355X_MICROARCH.md, 157.3 TFLOP/s; 78.6 TFLOP/s FMA)
 FP64_LANE_OPS_PEAK = 256 * 4 * 16 * 2.4e9
