@@ -232,26 +232,42 @@ def secondary_configs(F, args, device):
 def phase_breakdown(sh, iters, xm, xv):
     """HIP-event timing of each phase of one batched step over the rank's shifts (torch's current
     stream)."""
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(7)]
     sh.reset()
     b = sh.batch
     ev[0].record()
     b.ysq()
     ev[1].record()
-    b.fit(iterations=iters, stop_crit_wait_iterations=iters + 1)
+    b.basis()          # part-product spectra (spectral fit path; None on the transform path)
     ev[2].record()
-    b.coeffs()
+    b.fit(iterations=iters, stop_crit_wait_iterations=iters + 1)
     ev[3].record()
-    b.post_mean(xm)
+    b.coeffs()
     ev[4].record()
-    b.post_var(xv)
+    b.post_mean(xm)
     ev[5].record()
+    b.post_var(xv)
+    ev[6].record()
     torch.cuda.synchronize()
-    names = ["ytilde", "fit", "coeffs", "post_mean", "post_var"]
-    return {names[i]: ev[i].elapsed_time(ev[i + 1]) for i in range(5)}
+    names = ["ytilde", "basis", "fit", "coeffs", "post_mean", "post_var"]
+    return {names[i]: ev[i].elapsed_time(ev[i + 1]) for i in range(6)}
 
 
 STAGES = ("k_fwd_rows", "k_fwd_cols", "k_bwd_rows")
+SPEC_BLOCKS = 512      # k blocks per problem of the spectral iteration (csrc/fgp_nll.h kSpecBlocks)
+
+
+def stage_names(variant):
+    """The fit-iteration kernels of a variant, in launch order (the reduce + Rprop step aside)."""
+    return ("k_spec_iter",) if variant == "spectral" else STAGES
+
+
+def spec_geometry(n, d, G, shared=True, family=0):
+    """(k blocks, problems per wave, problem groups) of k_spec_iter (csrc/fgp_spectral.hip spec_geometry)."""
+    main = n // 2 if family == 0 else n
+    nb = min(SPEC_BLOCKS, max(1, main // 64))
+    ppw = 2 if (G >= 2 and shared and d <= 5) else 1
+    return nb, ppw, (G + ppw - 1) // ppw
 
 
 def r2c_active(n):
@@ -275,8 +291,11 @@ def re_row_log2():
     return int(os.environ.get("FGP_RE_P2", "11") or 11)
 
 
-def fit_grid(n, P, variant):
+def fit_grid(n, P, variant, d=5):
     """{stage kernel: (workgroups per fit launch, threads per workgroup)}."""
+    if variant == "spectral":
+        nb, _, pg = spec_geometry(n, d, P)
+        return {"k_spec_iter": ((nb * pg + 3) // 4, 256)}
     if variant == "re":     # N1 = n / (2 N2) rows of N2: N1/2 row-pair workgroups of N2/8, n/16384 column tiles
         N2 = 2 ** re_row_log2()
         N1 = n // (2 * N2)
@@ -297,6 +316,12 @@ def stage_bytes(n, d, P, parts_array, variant=None):
                      of its frequencies) + Nyquist 16 N1 read + 4 N1 written; bwd rows 16L + 4 N1"""
     variant = variant or fit_variant(n, parts_array)
     pb = 8 * n * d if parts_array else 0
+    if variant == "spectral":
+        # one shared set of 2^d spectra of K = n/2 + 1 doubles read once per launch, Y[:K] of every
+        # problem, (4 + d) partials per problem and k block written
+        K = n // 2 + 1
+        nb, _, _ = spec_geometry(n, d, P)
+        return {"k_spec_iter": 8 * K * (2 ** d) + 8 * K * P + 8 * (4 + d) * nb * P}
     if variant == "re":
         L, N1 = n // 4, n // (2 * 2 ** re_row_log2())
         return {"k_fwd_rows": (16 * L + 16 * N1) * P, "k_fwd_cols": (32 * L + 4 * n + 20 * N1) * P,
@@ -328,38 +353,41 @@ def roofline_fit_kernels(F, shifts, iters):
     eng = F.batch.batched_engine(gps, iters)
     eng.run(0, 2)
     torch.cuda.synchronize()
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(iters)]
-    fg = fit_grid(n, eng.G, fit_variant(n, eng.gen is None))      # (workgroups, threads) per fit launch
+    variant = "spectral" if eng.basis is not None else fit_variant(n, eng.gen is None)
+    names = stage_names(variant)
+    ns = len(names)
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(ns + 2)] for _ in range(iters)]
+    fg = fit_grid(n, eng.G, variant, eng.d)      # (workgroups, threads) per fit launch
     grid = max(g for g, _ in fg.values())
-    stamps = torch.zeros((iters, 3, grid, 5), dtype=torch.int64, device=dev)   # fgp_nll_desc.stamps
+    stamps = torch.zeros((iters, ns, grid, 5), dtype=torch.int64, device=dev)   # fgp_nll_desc.stamps
     torch.cuda._sleep(int(2.4e9 * 4e-4 * iters))
     for it in range(iters):
         e = ev[it]
         e[0].record()
-        for k in range(3):
+        for k in range(ns):
             eng._nll.stamps = stamps[it, k].data_ptr()
             eng.stage(k)
             e[k + 1].record()
         eng._nll.stamps = None
         eng.fit_step(it)
-        e[4].record()
+        e[ns + 1].record()
     torch.cuda.synchronize()
     eng._nll.stamps = None
     khz = wall_clock_khz(F, dev)
     st = stamps.cpu()
     dur = []
-    for k, name in enumerate(STAGES):    # records [workgroup][start, wave ends...] of this launch's grid
+    for k, name in enumerate(names):    # records [workgroup][start, wave ends...] of this launch's grid
         g, thr = fg[name]
         sk = st[:, k, :g, :1 + thr // 64]
         assert bool((sk > 0).all()), "a fit launch did not write its device-clock stamps"
         dur.append((sk[..., 1:].amax((1, 2)) - sk[..., 0].amin(1)).double() * (1e3 / khz))
-    dur_us = torch.stack(dur, 1)     # [iters, 3]
-    us_ev = {name: 1e3 * sum(e[k].elapsed_time(e[k + 1]) for e in ev) / iters for k, name in enumerate(STAGES)}
-    us_ev["k_fit_reduce_step"] = 1e3 * sum(e[3].elapsed_time(e[4]) for e in ev) / iters
-    us = {name: float(dur_us[:, k].mean()) for k, name in enumerate(STAGES)}
+    dur_us = torch.stack(dur, 1)     # [iters, ns]
+    us_ev = {name: 1e3 * sum(e[k].elapsed_time(e[k + 1]) for e in ev) / iters for k, name in enumerate(names)}
+    us_ev["k_fit_reduce_step"] = 1e3 * sum(e[ns].elapsed_time(e[ns + 1]) for e in ev) / iters
+    us = {name: float(dur_us[:, k].mean()) for k, name in enumerate(names)}
     us["k_fit_reduce_step"] = us_ev["k_fit_reduce_step"]
     t_iter = sum(us_ev.values()) / 1e6
-    return n, eng.gen is None, us, us_ev, t_iter, khz
+    return n, variant, us, us_ev, t_iter, khz
 
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -504,13 +532,13 @@ def main():
     value = args.shifts * n * world / sec_step
 
     phases = phase_breakdown(shifts, args.fit_iters, xm, xv)
-    n_, parts_array, us, us_ev, t_iter, khz = roofline_fit_kernels(F, shifts, args.fit_iters)
+    n_, variant, us, us_ev, t_iter, khz = roofline_fit_kernels(F, shifts, args.fit_iters)
+    parts_array = variant not in ("spectral", "re")
     P = len(shifts.gps)
-    sb = stage_bytes(n, d, P, parts_array)
-    dom = max(STAGES, key=lambda k: us[k])
-    variant = fit_variant(n, parts_array)
-    kname = dom + {"re": "_re", "r2c": "_r2c", "full": ""}[variant]
-    grid_wg, wg_thr = fit_grid(n, P, variant)[dom]
+    sb = stage_bytes(n, d, P, parts_array, variant)
+    dom = max(stage_names(variant), key=lambda k: us[k])
+    kname = dom + {"re": "_re", "r2c": "_r2c", "full": "", "spectral": ""}[variant]
+    grid_wg, wg_thr = fit_grid(n, P, variant, d)[dom]
     # achieved / frac are priced on the rocprofv3 kernel-trace average of this same command (committed
     # under profiles/) when it is there -- the duration the profiler reports, including the dispatch
     # ramp; the live device-clock figure (first workgroup start to last wave end) is reported beside it
@@ -529,10 +557,12 @@ def main():
             "avg_us_events": us_ev[dom],
             "launch": "%d problems x n=2^%d (grid %d workgroups)" % (P, args.log2n, grid_wg),
             "transform": {"re": "real-even: n/2-point transform, columns [0, N2/2) (n/4 complex)",
-                          "r2c": "half-length R2C (n/2 complex)", "full": "full-length (n complex)"}[variant],
+                          "r2c": "half-length R2C (n/2 complex)", "full": "full-length (n complex)",
+                          "spectral": "none per iteration: lambda from the 2^d part-product spectra"}[variant],
             "kernels": {k: {"avg_us": us[k], "avg_us_events": us_ev[k], "bytes": sb.get(k),
                             "GB/s": (sb[k] / (us[k] * 1e-6) / 1e9) if k in sb else None} for k in us},
-            "parts": "array" if parts_array else "regenerated (FGP_PARTS_LATTICE)",
+            "parts": ("spectra (fgp_spec_basis, built in the step)" if variant == "spectral" else
+                      "array" if parts_array else "regenerated (FGP_PARTS_LATTICE)"),
             "iteration_us": t_iter * 1e6}
     vi = pmc_valu_insts(kname, grid_wg * wg_thr)
     if vi is not None:

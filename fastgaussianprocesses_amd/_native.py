@@ -12,7 +12,7 @@ import torch
 
 _LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
 LIB_PATH = os.environ.get("FGP_LIB_PATH") or os.path.join(_LIB_DIR, "libfgp_hip.so")   # override: experiments
-ABI_VERSION = 10
+ABI_VERSION = 11
 MT_MAX_TASKS = 16
 MAX_D = 8
 PARTS_ARRAY = 0
@@ -46,6 +46,7 @@ class NllDesc(ctypes.Structure):
         ("parts_gen", _c_int), ("gen_order", _c_int * 8), ("gen_coef", _c_dbl * 8), ("gen_z", _c_i64 * 8),
         ("gen_shift", _c_vp), ("gen_shift_stride", _c_i64),
         ("stamps", _c_vp),
+        ("basis", _c_vp), ("basis_stride", _c_i64),
     ]
 
 
@@ -125,6 +126,9 @@ _SIGNATURES = {
     "fgp_mt_solve": [_P_MT, _c_vp, _c_i64, _c_vp, _c_i64, _c_i64, _c_vp, _c_vp],
     "fgp_mt_selinv": [_P_MT, _c_vp, _c_i64, _c_vp, _c_vp],
     "fgp_mt_mll_grad": [_P_MT, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_i64, _c_vp, _c_vp],
+    "fgp_nll_partials_len": [_P_NLL, _c_pl],
+    "fgp_spec_basis": [_c_int, _c_vp, _c_i64, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_i64, _c_vp],
+    "fgp_spec_basis_work": [_c_int, _c_int, _c_int, _c_pl],
     "fgp_inv_eig": [_c_int, _c_vp, _c_vp, _c_i64, _c_vp, _c_i64, _c_i64, _c_int, _c_vp, _c_vp, _c_vp],
 }
 

@@ -17,7 +17,7 @@ import torch
 
 from . import _native as N
 from . import ops
-from .fit_engine import FusedMLL, LatticePartsGen, fused_lam, mll_constant
+from .fit_engine import FusedMLL, LatticePartsGen, fused_lam, mll_constant, spec_basis, spectral_wanted
 
 
 class _LossReader(object):
@@ -166,7 +166,23 @@ def _set_raw(gps, raw, dl):
         gp._snap = None
 
 
-def _engine(gps, n, ysq, parts, gen, lr, iterations):
+def _basis_for(gps, n, parts, gen):
+    """Part-product spectra of the batch (fit_engine.spec_basis) when the spectral fit path is the cheaper
+    one, else None: ONE [2^d, K] set for lattice GPs sharing a generating vector (the first-column
+    distances (brev(i) z mod n) / n do not depend on the shift), else [P, 2^d, K] from the stacked parts."""
+    g0 = gps[0]
+    P = len(gps)
+    shared = gen is not None or P == 1
+    if not spectral_wanted(g0._FAMILY, n, g0.d, P, 1 if shared else P):
+        return None
+    if gen is not None:
+        p = ops.lattice_parts_gen(gen.z, gen.shift[0], gen.alphas, n)
+    else:
+        p = parts[0] if P == 1 else parts
+    return spec_basis(g0._FAMILY, p, n)
+
+
+def _engine(gps, n, ysq, parts, gen, lr, iterations, basis=None):
     g0 = gps[0]
     dl = g0.raw_lengthscales.shape[-1]
     d_out = int(torch.tensor(g0.shape_batch).prod())
@@ -178,7 +194,8 @@ def _engine(gps, n, ysq, parts, gen, lr, iterations):
                     requires_grad=(g0.raw_scale.requires_grad, g0.raw_lengthscales.requires_grad,
                                    g0.raw_noise.requires_grad),
                     lr=1e-1 if lr is None else lr, max_iters=iterations + 1, parts_per_problem=True,
-                    per_problem=True, gen=gen)
+                    per_problem=True, gen=None if basis is not None else gen,
+                    basis=basis)
 
 
 def _fit_data(state, store):
@@ -216,7 +233,7 @@ def batched_engine(gps, iterations, lr=None):
     n = gps[0]._nh
     parts, gen = _parts_source(gps, n)
     ysq = torch.stack([gp._ysq(*gp._problem_batch())[0] for gp in gps])
-    return _engine(gps, n, ysq, parts, gen, lr, iterations)
+    return _engine(gps, n, ysq, parts, gen, lr, iterations, basis=_basis_for(gps, n, parts, gen))
 
 
 class GPBatch(object):
@@ -286,6 +303,14 @@ class GPBatch(object):
             self._src = _parts_source(self.gps, self.n)
         return self._src
 
+    def basis(self):
+        """The batch's part-product spectra (None: transform fit path); rebuilt after set_data, like every
+        other cache of a step."""
+        if "basis" not in self._st:
+            parts, gen = self._source()
+            self._st["basis"] = _basis_for(self.gps, self.n, parts, gen)
+        return self._st["basis"]
+
     def _put_ytilde(self):
         yt = self._st.get("yt")
         if yt is not None:
@@ -317,7 +342,7 @@ class GPBatch(object):
         """Every GP's AbstractGP.fit(loss_metric="MLL", verbose=0) in one device loop; returns the list of
         per-GP data dicts."""
         parts, gen = self._source()
-        eng = _engine(self.gps, self.n, self.ysq(), parts, gen, lr, iterations)
+        eng = _engine(self.gps, self.n, self.ysq(), parts, gen, lr, iterations, basis=self.basis())
         state = _fit_loop(eng, iterations, stop_crit_improvement_threshold, stop_crit_wait_iterations)
         best = _best_raw(eng, state, self.dl)
         self.set_raw(best)
@@ -332,7 +357,8 @@ class GPBatch(object):
             raw = self.raw()
             parts, gen = self._source()
             dl = self.dl
-            lam = fused_lam(self.family, parts, raw[:, 0], raw[:, 1:1 + dl], raw[:, 1 + dl], self.P, gen=gen, n=self.n)
+            lam = fused_lam(self.family, parts, raw[:, 0], raw[:, 1:1 + dl], raw[:, 1 + dl], self.P, gen=gen, n=self.n,
+                            basis=self.basis())
             yt = self.ytilde()
             ya = torch.empty_like(lam)
             wa = torch.empty((self.P, self.n), dtype=torch.float64, device=self.device)

@@ -14,7 +14,8 @@ CSRC = os.path.join(HERE, "csrc")
 LIB_DIR = os.path.join(HERE, "_lib")
 LIB = os.path.join(LIB_DIR, "libfgp_hip.so")
 OBJ_DIR = os.path.join(LIB_DIR, "obj")
-SOURCES = ["fgp_runtime.hip", "fgp_transforms.hip", "fgp_nll.hip", "fgp_nll_re.hip", "fgp_predict.hip", "fgp_multitask.hip", "fgp_points.hip"]
+SOURCES = ["fgp_runtime.hip", "fgp_transforms.hip", "fgp_nll.hip", "fgp_nll_re.hip", "fgp_predict.hip", "fgp_multitask.hip", "fgp_points.hip",
+           "fgp_spectral.hip"]
 HEADERS = ["fgp_common.h", "fgp_runtime.h", "fgp_nll.h"]
 ARCH = os.environ.get("FGP_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

@@ -32,6 +32,14 @@ struct Nll {
   int r2c;                       // lattice, n >= 2^17: half-length (R2C) fit kernels
   int re;                        // ... with regenerated parts: real-even (RE) fit kernels (default)
   unsigned long long* stamps;    // optional device-clock timing of the launch (fgp_nll_desc.stamps)
+  // spectral path (fgp_spectral.hip, ABI 11): part-product spectra [G?][2^d][spec_K]
+  const double* basis;
+  int64_t basis_stride;
+  int spec, spec_net;            // spectral fit path (basis != NULL); nets (weight 1, K = n)
+  int64_t spec_K, spec_KS, spec_main;  // frequencies per spectrum, its row stride, frequencies in k blocks
+  int spec_kpl, spec_ppw, spec_pg;   // frequencies per lane and block, problems per wave, problem groups
+  int spec_tile, spec_pgp, spec_ck;  // LDS-tiled kernel: problem-group slots, frequencies per chunk
+  int64_t spec_kw;                   // ... and per workgroup
 };
 
 // Device-clock kernel timing (fgp_nll_desc.stamps; off when NULL -- a uniform branch on a kernel
@@ -531,6 +539,16 @@ struct FitFuse {
   unsigned* counters;
 };
 int launch_re_bwd_fused(const Nll& a, const FitFuse& fz, const Tables* tb, hipStream_t st);
+
+// spectral fit path (fgp_spectral.hip): d <= kSpecMaxD, at most kSpecBlocks k blocks per problem
+constexpr int kSpecMaxD = 6;
+constexpr int kSpecBlocks = 512;
+void spec_geometry(Nll& a);                        // nb and the spec_* fields of a spectral desc
+int64_t spec_row_stride(bool net, int log2n);      // row stride of the spectra (fgp_spec_basis layout)
+// one fit iteration (loss + gradient partials); with fz (tile kernel only) also the reduction + Rprop
+int launch_spec_iter(const Nll& a, hipStream_t st, const FitFuse* fz = nullptr);
+int launch_spec_reduce_step(const Nll& a, const Fit& f, int iter, int do_update, hipStream_t st);
+int launch_spec_lam(const Nll& a, hipStream_t st);    // lambda of the current parameters into grad_lam
 // their row length log2 (FGP_RE_P2, default 10) for a transform of 2^log2n, or -1 when no split fits
 int re_row_log2(int log2n);
 

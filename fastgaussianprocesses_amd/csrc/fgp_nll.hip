@@ -1069,10 +1069,13 @@ static int to_nll(const fgp_nll_desc* d, Nll& a) {
   if (d->log2n < 4 || d->log2n > kMaxLog2N) return set_error(kErrUnsupported, "fused fit needs 4 <= log2n <= 24");
   if (d->d < 1 || d->d > FGP_MAX_D) return set_error(kErrUnsupported, "d=%d outside [1, %d]", d->d, FGP_MAX_D);
   if (d->G < 1) return set_error(kErrInvalid, "G < 1");
-  if (!d->ysq || !d->raw || !d->partials || (d->log2n > 12 && !d->work))
+  if (!d->ysq || !d->raw || !d->partials || (d->log2n > 12 && !d->work && !d->basis))
     return set_error(kErrInvalid, "null pointer in nll desc");
+  if (d->basis && d->d > kSpecMaxD)
+    return set_error(kErrUnsupported, "spectral fit path: d = %d > %d", d->d, kSpecMaxD);
+  if (d->basis && d->basis_stride < 0) return set_error(kErrInvalid, "negative basis_stride");
   if (d->parts_gen == FGP_PARTS_ARRAY) {
-    if (!d->parts) return set_error(kErrInvalid, "null parts in nll desc");
+    if (!d->parts && !d->basis) return set_error(kErrInvalid, "null parts in nll desc");
   } else if (d->parts_gen == FGP_PARTS_LATTICE) {
     if (d->family != FGP_FAMILY_LATTICE) return set_error(kErrInvalid, "lattice parts generator needs the lattice family");
     if (!d->gen_shift) return set_error(kErrInvalid, "null gen_shift in nll desc");
@@ -1135,6 +1138,17 @@ static int to_nll(const fgp_nll_desc* d, Nll& a) {
   a.gshift = d->gen_shift;
   a.gshift_stride = d->gen_shift_stride;
   a.stamps = reinterpret_cast<unsigned long long*>(d->stamps);
+  // spectral path: the eigenvalues from the part-product spectra, one kernel per iteration
+  a.basis = d->basis;
+  a.basis_stride = d->basis_stride;
+  a.spec = d->basis != nullptr;
+  a.spec_net = d->family == FGP_FAMILY_NET;
+  a.spec_K = a.spec_KS = a.spec_main = a.spec_kw = 0;
+  a.spec_kpl = a.spec_ppw = a.spec_pg = a.spec_tile = a.spec_pgp = a.spec_ck = 0;
+  if (a.spec) {
+    a.re = a.r2c = 0;
+    spec_geometry(a);
+  }
   return kOk;
 }
 
@@ -1266,6 +1280,10 @@ static int nll_stage_t(const Nll& a, int stage, const Tables* tb, hipStream_t st
 }
 
 static int nll_stage(const Nll& a, int stage, hipStream_t st, bool lattice) {
+  if (a.spec) {
+    if (stage < 0 || stage > 2) return set_error(kErrInvalid, "bad stage %d", stage);
+    return stage == 0 ? launch_spec_iter(a, st) : kOk;
+  }
   const Tables* tb = get_tables(st);
   if (!tb) return set_error(kErrHip, "twiddle table initialisation failed");
   return lattice ? nll_stage_t<double2>(a, stage, tb, st) : nll_stage_t<double>(a, stage, tb, st);
@@ -1311,6 +1329,7 @@ static int check_per_problem(const Nll& a, const Fit& f) {
 }
 
 static int fit_step(const Nll& a, const Fit& f, int iter, int do_update, hipStream_t st) {
+  if (f.per_problem && a.spec) return launch_spec_reduce_step(a, f, iter, do_update, st);
   if (f.per_problem) {
     k_fit_reduce_step<<<a.G, kWG, 0, st>>>(a, f, iter, do_update);
     return check_launch("k_fit_reduce_step");
@@ -1415,6 +1434,7 @@ int fgp_nll_lam(const fgp_nll_desc* desc, void* stream) {
   int rc = to_nll(desc, a);
   if (rc != kOk) return rc;
   if (!desc->grad_lam) return set_error(kErrInvalid, "fgp_nll_lam: null grad_lam (the output)");
+  if (a.spec) return launch_spec_lam(a, (hipStream_t)stream);
   if (a.re && !a.r2c) {   // n = 2^16: lambda by the full-length kernels (their block count)
     a.re = false;
     a.nb = 1 << (a.log2n - 12);
@@ -1434,6 +1454,22 @@ int fgp_nll_lam(const fgp_nll_desc* desc, void* stream) {
   }
   rc = launch_rows_fwd<double>(a, tb, st);
   return rc != kOk ? rc : launch_cols_fwd<double>(a, tb, st, true);
+}
+
+int fgp_nll_partials_len(const fgp_nll_desc* desc, int64_t* len) {
+  if (!desc) return set_error(kErrInvalid, "null nll desc");
+  fgp_nll_desc probe = *desc;   // the workspace is sized before it exists: placeholder pointers
+  static const double dummy = 0.0;
+  if (!probe.partials) probe.partials = const_cast<double*>(&dummy);
+  if (!probe.ysq) probe.ysq = &dummy;
+  if (!probe.raw) probe.raw = &dummy;
+  Nll a;
+  int rc = to_nll(&probe, a);
+  if (rc != kOk) return rc;
+  if (!len) return set_error(kErrInvalid, "fgp_nll_partials_len: null len");
+  const int64_t nb_doc = std::max<int64_t>(1, ((int64_t)1 << a.log2n) >> 12);
+  *len = (int64_t)a.G * a.nq * (std::max<int64_t>(a.nb, nb_doc) + 1) + a.G;
+  return kOk;
 }
 
 int fgp_nll_stage(const fgp_nll_desc* desc, int stage, void* stream) {
@@ -1538,20 +1574,28 @@ int fgp_fit_run(const fgp_nll_desc* nll, const fgp_fit_desc* fit, int iter0, int
   // last workgroup per problem, with G counters in the documented partials workspace past the
   // G (4 + d) (nb + 1) doubles the kernels use (room while nb < n / 4096)
   const int64_t nb_doc = std::max<int64_t>(1, ((int64_t)1 << a.log2n) >> 12);
-  const bool fuse = a.re && f.per_problem && a.nb < nb_doc && iters > 0;
+  // spectral tile kernel: the whole iteration (and the step, in its last workgroup) is one launch
+  const bool fuse_spec = a.spec && a.spec_tile && f.per_problem && a.G <= 8 && iters > 0;
+  const bool fuse = (a.re && f.per_problem && a.nb < nb_doc && iters > 0) || fuse_spec;
   FitFuse fz{};
   const Tables* tb = nullptr;
   if (fuse) {
     fz.f = f;
     fz.counters = reinterpret_cast<unsigned*>(a.partials + (int64_t)a.G * a.nq * (a.nb + 1));
-    tb = get_tables(st);
-    if (!tb) return set_error(kErrHip, "twiddle table initialisation failed");
+    if (!fuse_spec) tb = get_tables(st);
+    if (!fuse_spec && !tb) return set_error(kErrHip, "twiddle table initialisation failed");
     if (hipMemsetAsync(fz.counters, 0, sizeof(unsigned) * (size_t)a.G, st) != hipSuccess)
       return set_error(kErrHip, "fgp_fit_run: counter reset failed");
   }
   for (int it = 0; it < iters; ++it) {
-    if ((rc = nll_fwd(a, st, lat)) != kOk) return rc;
     const int upd = !(final_no_update && it == iters - 1);
+    if (fuse_spec) {
+      fz.iter = iter0 + it;
+      fz.do_update = upd;
+      if ((rc = launch_spec_iter(a, st, &fz)) != kOk) return rc;
+      continue;
+    }
+    if ((rc = nll_fwd(a, st, lat)) != kOk) return rc;
     if (fuse) {
       fz.iter = iter0 + it;
       fz.do_update = upd;

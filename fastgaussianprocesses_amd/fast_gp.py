@@ -27,7 +27,7 @@ import torch
 
 from . import ops
 from . import seqs as _seqs
-from .fit_engine import FusedMLL, LatticePartsGen, mll_constant
+from .fit_engine import FusedMLL, LatticePartsGen, mll_constant, spec_basis, spectral_wanted
 
 
 def _log(x):
@@ -417,14 +417,30 @@ class AbstractFastGP(torch.nn.Module):
                 and self._tfs["noise"][1] is _exp and self._problem_batch() is not None)
 
     def _lam_fused(self, n):
-        """lambda = ft(k1) by fgp_nll_lam (k1 formed on the fly from the cached parts)."""
+        """lambda = ft(k1) by fgp_nll_lam (k1 formed on the fly from the cached parts, or lambda from the
+        part-product spectra on the spectral path)."""
         from .fit_engine import fused_lam
         pb, G = self._problem_batch()
-        gen = self._parts_gen(n)
-        lam = fused_lam(self._FAMILY, self._k1parts(n) if gen is None else None, self.raw_scale.detach().reshape(-1),
+        basis = self._spec_basis(n, G)
+        gen = self._parts_gen(n) if basis is None else None
+        parts = self._k1parts(n) if (gen is None and basis is None) else None
+        lam = fused_lam(self._FAMILY, parts, self.raw_scale.detach().reshape(-1),
                         self.raw_lengthscales.detach().reshape(-1, self.raw_lengthscales.shape[-1]),
-                        self.raw_noise.detach().reshape(-1), G, gen=gen, n=n)
+                        self.raw_noise.detach().reshape(-1), G, gen=gen, n=n, basis=basis)
         return lam.reshape(tuple(pb) + (n,))
+
+    def _spec_basis(self, n, G=1):
+        """Part-product spectra Phi_S = ft(prod_{j in S} parts_j) of the first n points (fgp_spec_basis)
+        when the spectral fit path is the cheaper one for G eigen-problems (fit_engine.spectral_wanted),
+        else None.  Hyper-parameter independent; cached with the data (dropped by add_y_next)."""
+        if not spectral_wanted(self._FAMILY, n, self.d, G):
+            return None
+
+        def f():
+            gen = self._parts_gen(n)
+            parts = ops.lattice_parts_gen(gen.z, gen.shift[0], gen.alphas, n) if gen is not None else self._k1parts(n)
+            return spec_basis(self._FAMILY, parts, n)
+        return self._cached(("basis", n), f, grad_sensitive=False)
 
     def get_ytilde(self, task=0):
         """_YtildeCache (util.py:164-183): after add_y_next doubled n, ytilde_2n comes from the cached
@@ -573,8 +589,9 @@ class AbstractFastGP(torch.nn.Module):
         pb_shape, G = self._problem_batch()
         if d_out is None:
             d_out = int(torch.tensor(self.shape_batch).prod())
-        gen = self._parts_gen(n)
-        parts = self._k1parts(n) if gen is None else None
+        basis = self._spec_basis(n, G)
+        gen = self._parts_gen(n) if basis is None else None
+        parts = self._k1parts(n) if (gen is None and basis is None) else None
         ls_raw = self.raw_lengthscales.detach()
         ls2 = ls_raw.reshape(-1, ls_raw.shape[-1])
         eng = FusedMLL(self._FAMILY, parts, self._ysq(pb_shape, G) if ysq is None else ysq,
@@ -583,7 +600,7 @@ class AbstractFastGP(torch.nn.Module):
                        mll_const=mll_constant(d_out, n),
                        requires_grad=(self.raw_scale.requires_grad, self.raw_lengthscales.requires_grad,
                                       self.raw_noise.requires_grad),
-                       lr=lr, max_iters=min(iterations + 1, 64), gen=gen)
+                       lr=lr, max_iters=min(iterations + 1, 64), gen=gen, basis=basis)
         self._iters_for_log = iterations
         self._log_header(verbose, indent)
         best, save, waited = math.inf, math.inf, 0

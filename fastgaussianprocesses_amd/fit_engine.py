@@ -51,12 +51,73 @@ class LatticePartsGen(object):
         desc.gen_shift_stride = d if self.shift.shape[0] > 1 else 0
 
 
+SPEC_MAX_D = 6                 # fgp_spec_basis / the spectral fit kernels (include/fgp_hip.h, ABI 11)
+SPEC_WORK_CAP = 512 << 20      # scratch of one fgp_spec_basis call (subsets are transformed in chunks)
+
+
+def spec_k(family, n):
+    """Frequencies per part-product spectrum: n/2 + 1 (lattice, real even), n (net)."""
+    return n // 2 + 1 if family == 0 else n
+
+
+def spec_row(family, n):
+    """Row stride of the spectra (fgp_spec_basis): lattice n/2 + 16 (k = 0 .. n/2, zero padding to 128-byte
+    rows), net n."""
+    return n // 2 + 16 if family == 0 else n
+
+
+def spectral_wanted(family, n, d, G, nbases=1):
+    """Fit path choice: the part-product spectra (one streaming kernel per iteration, 8 2^d bytes per
+    frequency per distinct point set + Y) or the transform kernels (an FFT / FWHT of k1 and its adjoint per
+    iteration).  A per-iteration time model from the round-3 measurements:
+      spectral:  bytes / 6 TB/s + 6 us;
+      transform: max(40 us latency floor of three dependent launches, G n x 10.8 ps (real-even lattice
+                 kernels at saturation) / 30 ps (nets, full-length kernels)).
+    FGP_FIT_PATH=spectral / transform forces a path (the spectral one needs d <= 6)."""
+    if d > SPEC_MAX_D or n < 16:
+        return False
+    force = os.environ.get("FGP_FIT_PATH", "").lower()
+    if force.startswith("s"):
+        return True
+    if force.startswith("t"):
+        return False
+    K = spec_k(family, n)
+    bytes_it = 8 * K * ((2 ** d) * nbases + G)
+    t_spec = bytes_it / 6e12 + 6e-6
+    per_point = 10.8e-12 if (family == 0 and n >= 2 ** 16) else 30e-12
+    t_tr = max(40e-6, G * n * per_point)
+    return t_spec < t_tr and (2 ** d) * nbases * K * 8 <= (16 << 30)
+
+
+def spec_basis(family, parts, n):
+    """Part-product spectra (fgp_spec_basis): parts [d, n] -> [2^d, KS], or [P, d, n] -> [P, 2^d, KS] (row
+    stride KS = spec_row, the first spec_k entries of a row used); lambda = scale sum_S l^S basis[S] for
+    every hyper-parameter setting (include/fgp_hip.h)."""
+    require_device(parts, "spec_basis")
+    parts = parts.contiguous()
+    d = parts.shape[-2]
+    m = log2_exact(n)
+    P = parts.shape[0] if parts.dim() == 3 else 1
+    K = spec_row(family, n)
+    total = ctypes.c_int64(0)
+    N.call("fgp_spec_basis_work", int(family), m, int(d), ctypes.byref(total))
+    one = total.value >> d
+    wbytes = max(one, min(total.value, SPEC_WORK_CAP))
+    work = torch.empty((wbytes,), dtype=torch.uint8, device=parts.device)
+    out = torch.empty(((P,) if parts.dim() == 3 else ()) + (2 ** d, K), dtype=torch.float64, device=parts.device)
+    N.call("fgp_spec_basis", int(family), N.ptr(parts), d * n, P, m, int(d), N.ptr(out), N.ptr(work), wbytes,
+           N.stream_ptr(parts.device))
+    return out
+
+
 class FusedMLL(object):
     def __init__(self, family, parts, ysq, raw_scale, raw_lengthscales, raw_noise, logdet_weight, mll_const,
                  requires_grad=(True, True, False), lr=0.1, max_iters=1, parts_per_problem=False, per_problem=None,
-                 gen=None):
+                 gen=None, basis=None):
         """
         family: 0 lattice (FFT) / 1 net (FWHT)
+        basis:  part-product spectra (spec_basis) [2^d, K] shared or [G, 2^d, K]: the spectral fit path
+                (one kernel per iteration, no transform; parts / gen are then not used)
         parts:  [d, n] shared, or [G, d, n] when parts_per_problem; None with `gen` (LatticePartsGen)
         ysq:    [G, n]
         per_problem: the G problems are independent GPs with their own loss / Rprop (default: G == 1);
@@ -72,11 +133,16 @@ class FusedMLL(object):
         self.m = log2_exact(n)
         if self.m < 4:
             raise ValueError("fused fit needs n >= 16")
-        d = parts.shape[-2] if parts is not None else len(gen.z)
+        if basis is not None:
+            d = int(round(math.log2(basis.shape[-2])))
+            parts, gen = None, None
+        else:
+            d = parts.shape[-2] if parts is not None else len(gen.z)
         self.d = int(d)
         if d > 8:
             raise ValueError("fused fit supports d <= 8")
         self.gen = gen
+        self.basis = basis.contiguous() if basis is not None else None
         self.parts = parts.contiguous() if parts is not None else None
         if gen is not None and gen.shift.shape[0] not in (1, G):
             raise ValueError("generator shift rows must be 1 or G")
@@ -99,9 +165,7 @@ class FusedMLL(object):
         self.raw = torch.cat([raw_scale.reshape(-1), raw_lengthscales.reshape(-1), raw_noise.reshape(-1)]).to(
             device=self.device, dtype=torch.float64).contiguous()
         cdt = torch.complex128 if self.family == 0 else torch.float64
-        self.work = torch.empty((G, n), dtype=cdt, device=self.device) if self.m > 12 else None
-        nb = max(1, n >> 12)
-        self.partials = torch.empty((G * (4 + d) * (nb + 1),), dtype=torch.float64, device=self.device)
+        self.work = torch.empty((G, n), dtype=cdt, device=self.device) if (self.m > 12 and basis is None) else None
         self.prev = torch.zeros(self.n_params, dtype=torch.float64, device=self.device)
         self.step = torch.full((self.n_params,), float(lr), dtype=torch.float64, device=self.device)
         self.grad = torch.zeros(self.n_params, dtype=torch.float64, device=self.device)
@@ -116,9 +180,16 @@ class FusedMLL(object):
             ysq=self.ysq.data_ptr(), ysq_stride=n, raw=self.raw.data_ptr(),
             logdet_weight=float(logdet_weight),
             grad_lam=0, work=(self.work.data_ptr() if self.work is not None else 0),
-            partials=self.partials.data_ptr(), **self.layout)
+            partials=0, **self.layout)
         if gen is not None:
             gen.apply(self._nll, n)
+        if self.basis is not None:
+            self._nll.basis = self.basis.data_ptr()
+            self._nll.basis_stride = (self.basis.shape[-2] * self.basis.shape[-1]) if self.basis.dim() == 3 else 0
+        plen = ctypes.c_int64(0)
+        N.call("fgp_nll_partials_len", self._nll, ctypes.byref(plen))
+        self.partials = torch.empty((plen.value,), dtype=torch.float64, device=self.device)
+        self._nll.partials = self.partials.data_ptr()
         self.per_problem = bool(G == 1 if per_problem is None else per_problem)
         self.requires_grad = tuple(int(bool(r)) for r in requires_grad)
         self.mll_const = float(mll_const)
@@ -198,15 +269,16 @@ class FusedMLL(object):
         if getattr(self, "_streams", None) is None or len(self._streams) < groups:
             self._streams = [torch.cuda.Stream(self.device) for _ in range(groups)]
         G, n, d = self.G, self.n, self.d
-        nb = max(1, n >> 12)
         out = []
         for k in range(groups):
             g0, g1 = G * k // groups, G * (k + 1) // groups
             Gk = g1 - g0
-            part = torch.empty((Gk * (4 + d) * (nb + 1),), dtype=torch.float64, device=self.device)
             nll = N.NllDesc()
             ctypes.pointer(nll)[0] = self._nll
             nll.G = Gk
+            plen = ctypes.c_int64(0)
+            N.call("fgp_nll_partials_len", nll, ctypes.byref(plen))
+            part = torch.empty((plen.value,), dtype=torch.float64, device=self.device)
             nll.ysq = self.ysq[g0].data_ptr()
             if self.work is not None:
                 nll.work = self.work[g0].data_ptr()
@@ -215,6 +287,8 @@ class FusedMLL(object):
                 nll.parts = self.parts[g0].data_ptr()
             if self.gen is not None and self._nll.gen_shift_stride:
                 nll.gen_shift = self.gen.shift[g0].data_ptr()
+            if self.basis is not None and self._nll.basis_stride:
+                nll.basis = self.basis[g0].data_ptr()
             lay = self.layout
             dl = self.sizes[1] // (G if lay["ls_pp"] else 1)
             if lay["scale_pp"]:
@@ -262,11 +336,16 @@ def mll_constant(d_out, n):
     return d_out * n * math.log(2 * math.pi)
 
 
-def fused_lam(family, parts, raw_scale, raw_lengthscales, raw_noise, G, gen=None, n=None):
+def fused_lam(family, parts, raw_scale, raw_lengthscales, raw_noise, G, gen=None, n=None, basis=None):
     """lambda = ft(k1) for G eigen-problems sharing `parts` ([d, n]), with parts of their own
-    ([G, d, n]), or with the generator `gen` (size n), via fgp_nll_lam -> [G, n]."""
+    ([G, d, n]), with the generator `gen` (size n), or from part-product spectra `basis` ([2^d, K] shared,
+    [G, 2^d, K]), via fgp_nll_lam -> [G, n]."""
     parts_stride = 0
-    if parts is not None:
+    if basis is not None:
+        require_device(basis, "fused_lam")
+        d, dev = int(round(math.log2(basis.shape[-2]))), basis.device
+        parts, gen = None, None
+    elif parts is not None:
         require_device(parts, "fused_lam")
         d, n = parts.shape[-2:]
         dev = parts.device
@@ -283,7 +362,7 @@ def fused_lam(family, parts, raw_scale, raw_lengthscales, raw_noise, G, gen=None
         device=dev, dtype=torch.float64).contiguous()
     cdt = torch.complex128 if family == 0 else torch.float64
     out = torch.empty((G, n), dtype=cdt, device=dev)
-    work = torch.empty((G, n), dtype=cdt, device=dev) if m > 12 else None
+    work = torch.empty((G, n), dtype=cdt, device=dev) if (m > 12 and basis is None) else None
     desc = N.NllDesc(family=family, log2n=m, d=d, G=G, parts=(parts.data_ptr() if parts is not None else 0),
                      parts_stride=parts_stride,
                      ysq=out.data_ptr(), ysq_stride=0, raw=raw.data_ptr(),
@@ -293,5 +372,9 @@ def fused_lam(family, parts, raw_scale, raw_lengthscales, raw_noise, G, gen=None
                      partials=out.data_ptr())
     if gen is not None:
         gen.apply(desc, n)
+    if basis is not None:
+        basis = basis.contiguous()
+        desc.basis = basis.data_ptr()
+        desc.basis_stride = (basis.shape[-2] * basis.shape[-1]) if basis.dim() == 3 else 0
     N.call("fgp_nll_lam", desc, N.stream_ptr(dev))
     return out

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define FGP_ABI_VERSION 10
+#define FGP_ABI_VERSION 11
 
 #define FGP_OK 0
 #define FGP_ERR_INVALID (-1)     /* bad argument (shape, stride, null pointer) */
@@ -200,7 +200,38 @@ typedef struct fgp_nll_desc {
    * workgroups); max(ends) - min(starts) is the kernel's duration as rocprofv3 --kernel-trace sees it,
    * measured in-process without the dependent-launch gap that HIP events include. */
   uint64_t* stamps;
+  /* ABI 11 -- spectral fit path.  basis non-NULL: the part-product spectra of fgp_spec_basis
+   * ([G or 1][2^d][K], K = n/2 + 1 lattice / n net, problem g's at basis + g * basis_stride; stride 0 = one
+   * set shared by all G problems).  Every kernel of this desc then evaluates
+   *   lambda_g = scale_g sum_S (prod_{j in S} l_gj) Phi_S
+   * instead of transforming k1 (parts / parts_gen / work are not read; d <= 6): fgp_nll_fwd / fgp_fit_run
+   * run ONE kernel per iteration (stage 0: loss and gradient partials; stages 1, 2 are no-ops), fgp_nll_lam
+   * writes lambda (lattice: the even spectrum mirrored, imaginary parts 0).  The partials workspace must
+   * hold fgp_nll_partials_len doubles. */
+  const double* basis;
+  int64_t basis_stride;
 } fgp_nll_desc;
+
+/* Doubles the `partials` workspace of this desc needs (per-block partials + the fused fit's counters):
+ * G (4 + d) (max(nb, n / 4096) + 1) + G, nb the kernels' block count (spectral path: up to 512). */
+int fgp_nll_partials_len(const fgp_nll_desc* desc, int64_t* len);
+
+/* Part-product spectra (ABI 11) for the spectral fit path.  With b_S[i] = prod_{j in S} parts[j, i]
+ * (ascending j; b_{} = 1) for every subset S of the d dimensions (bit j of S = dimension j):
+ *   basis[p][S][k] = ft(b_S)[k],  k < K:
+ *   lattice: Re fftbr(b_S) (stable; the lattice b_S is even in the natural index, so the spectrum is real
+ *            and even and k = 0 .. n/2 carry it: K = n/2 + 1);  net: fwht(b_S) (stable), K = n.
+ * Then for every (scale, l) the eigenvalues are lambda = scale sum_S l^S basis[S] -- ft(k1) of the
+ * reference's _LamCaches (fastgps/util.py:95-112), k1 = scale prod_j (1 + l_j parts_j) of
+ * abstract_fast_gp.py:181-191, by linearity of ft.
+ * parts: [P][d][n] float64 (fgp_lattice_parts / fgp_lattice_parts_gen / fgp_net_parts layout; problem
+ * stride parts_stride elements); basis: [P][2^d][K] float64; 1 <= d <= 6.
+ * work: device scratch of work_bytes >= fgp_spec_basis_work bytes for ONE subset (the subsets are then
+ * transformed in chunks; the bytes for all 2^d at once make it one chunk). */
+int fgp_spec_basis(int family, const double* parts, int64_t parts_stride, int64_t P, int log2n, int d, double* basis,
+                   void* work, int64_t work_bytes, void* stream);
+/* Bytes of `work` for all 2^d subsets at once (divide by 2^d for the one-subset minimum). */
+int fgp_spec_basis_work(int family, int log2n, int d, int64_t* bytes);
 
 #define FGP_PARTS_ARRAY 0
 #define FGP_PARTS_LATTICE 1
