@@ -146,83 +146,133 @@ class SingleGP(object):
 
 
 class MultiOutputGP(SingleGP):
-    """BASELINE config C5: one FastGPLattice, n = 2^18, d = 3, shape_batch = [B] outputs sharing the
-    reference's default hyper-parameters (shape_scale = [1], shape_lengthscales = [d]):
-    y_b = f_ackley(x) (1 + b / B) + 0.01 randn (seeded).  fp64 (the reference's precision)."""
+    """BASELINE config C5: one FastGPLattice, n = 2^18, d = 3, shape_batch = [B] outputs,
+    y_b = f_ackley(x) (1 + b / B) + 0.01 randn (seeded; the [B, n] noise is drawn whole and sliced, so an
+    output's data do not depend on the rank that owns it).  Shared hyper-parameters (the reference's
+    default shape_scale = [1], shape_lengthscales = [d]), or per_output ones
+    (shape_scale = [B, 1], shape_lengthscales = [B, d]: B independent eigen-problems on one point set,
+    docs/examples/batch_multitask/fgp_lattice.ipynb cell 6).  `shard` = (start, stop): the outputs this
+    rank owns (bench.py under torchrun).  fp64 (the reference's precision) or fp32 observations."""
 
-    def __init__(self, F, log2n, d, outputs, device, data_dtype=torch.float64):
+    def __init__(self, F, log2n, d, outputs, device, data_dtype=torch.float64, shard=None, per_output=False):
         n = 2 ** log2n
-        self.gp = F.FastGPLattice(F.Lattice(d, seed=7), shape_batch=[outputs], device=device, data_dtype=data_dtype)
+        a, b = shard if shard is not None else (0, outputs)
+        B = b - a
+        extra = dict(shape_scale=[B, 1], shape_lengthscales=[B, d]) if per_output else {}
+        self.gp = F.FastGPLattice(F.Lattice(d, seed=7), shape_batch=[B], device=device, data_dtype=data_dtype, **extra)
         f = f_ackley(self.gp.get_x_next(n))
         g = torch.Generator(device=device).manual_seed(5)
-        b = torch.arange(outputs, device=device, dtype=torch.float64)[:, None]
-        self.y = (f[None, :] * (1 + b / outputs) + 0.01 * torch.randn((outputs, n), generator=g, device=device,
-                                                                         dtype=torch.float64)).to(data_dtype).contiguous()
+        bb = torch.arange(outputs, device=device, dtype=torch.float64)[:, None]
+        noise = torch.randn((outputs, n), generator=g, device=device, dtype=torch.float64)
+        self.y = (f[None, :] * (1 + bb / outputs) + 0.01 * noise)[a:b].to(data_dtype).contiguous()
+        del noise
         self.raw0 = [p.detach().clone() for p in (self.gp.raw_scale, self.gp.raw_lengthscales, self.gp.raw_noise)]
-        self.n, self.outputs = n, outputs
+        self.n, self.outputs, self.total = n, B, outputs
+        self.sharded = shard is not None and B < outputs and not per_output
 
 
 def step_single(sg, args, xm, xv):
+    """One step of a single GP (C2, C3) or of a multi-output GP (C5): fresh data, fit, post_mean, post_var.
+    A C5 GP whose outputs are sharded over the ranks fits with distributed.fit_sharded (ONE all-reduce of
+    Y = sum_b |ytilde_b|^2, then the identical fit on every rank)."""
     sg.reset()
-    sg.gp.fit(iterations=args.fit_iters, stop_crit_wait_iterations=args.fit_iters + 1, verbose=0)
+    its = dict(iterations=args.fit_iters, stop_crit_wait_iterations=args.fit_iters + 1)
+    if getattr(sg, "sharded", False):
+        from fastgaussianprocesses_amd.distributed import fit_sharded
+        fit_sharded(sg.gp, sg.total, **its)
+    else:
+        sg.gp.fit(verbose=0, **its)
     pm = sg.gp.post_mean(xm)
     pv = sg.gp.post_var(xv)
     return pm, pv
 
 
-def time_steps(fn, steps, warmup):
+def time_steps(fn, steps, warmup, device=None):
+    """Seconds per step: warmup, then `steps` steps bracketed by a barrier + device sync on both sides,
+    the max over the ranks when a process group is up."""
+    import torch.distributed as tdist
+    dist = tdist.is_available() and tdist.is_initialized() and tdist.get_world_size() > 1
     for _ in range(warmup):
         fn()
     torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
     t0 = time.perf_counter()
     for _ in range(steps):
         fn()
     torch.cuda.synchronize()
-    return (time.perf_counter() - t0) / steps
+    if dist:
+        tdist.barrier()
+    el = time.perf_counter() - t0
+    if dist:
+        el = max_over_ranks(el, device)
+    return el / steps
 
 
-def secondary_configs(F, args, device):
-    """The other BASELINE.json configs on this GPU (rank 0, N = 1), each timed as its own step
-    (fit K Rprop iterations without early stopping + post_mean N + post_var N):
-    C2 FastGPLattice n=2^16 d=3, C3 FastGPDigitalNetB2 n=2^16 d=3 (default alpha = 2),
-    C5 multi-output FastGPLattice n=2^18 d=3 x B outputs (fp64; the reference cannot run fp32)."""
+def c5_shard(outputs, rank, world):
+    from fastgaussianprocesses_amd.distributed import output_shard
+    return output_shard(outputs, rank, world) if world > 1 else None
+
+
+def secondary_configs(F, args, device, rank=0, world=1):
+    """The other BASELINE.json configs, each timed as its own step (fit K Rprop iterations without early
+    stopping + post_mean N + post_var N):
+      N = 1 only: C2 FastGPLattice n=2^16 d=3, C3 FastGPDigitalNetB2 n=2^16 d=3 (default alpha = 2), C5 with
+        fp32 observations;
+      every N (all ranks take part, max-over-ranks time, value = all outputs x n / s): C5 multi-output
+        FastGPLattice n=2^18 d=3 x B outputs, fp64, outputs sharded over the ranks (fit_sharded: one Y
+        all-reduce), and C5 with per-output hyper-parameters (B independent eigen-problems; replicas, no
+        collective)."""
     g = torch.Generator().manual_seed(17)
+    B = args.c5_outputs
+    sh = c5_shard(B, rank, world)
+    cases = []
+    if world == 1:
+        cases += [("C2: FastGPLattice n=2^16 d=3", lambda: SingleGP(F, "lattice", 16, 3, device), 3),
+                  ("C3: FastGPDigitalNetB2 n=2^16 d=3 alpha=2", lambda: SingleGP(F, "net", 16, 3, device), 3)]
+    cases.append(("C5: FastGPLattice n=2^18 d=3 x %d outputs (shared hyper-parameters), fp64%s"
+                  % (B, ", outputs sharded over %d ranks (one Y all-reduce)" % world if world > 1 else ""),
+                  lambda: MultiOutputGP(F, 18, 3, B, device, shard=sh), 3))
+    cases.append(("C5 per-output: FastGPLattice n=2^18 d=3 x %d outputs, per-output hyper-parameters "
+                  "(shape_scale=[%d,1], shape_lengthscales=[%d,3]), fp64%s"
+                  % (B, B, B, ", replicas over %d ranks" % world if world > 1 else ""),
+                  lambda: MultiOutputGP(F, 18, 3, B, device, shard=sh, per_output=True), 3))
+    if world == 1:
+        cases.append(("C5 mixed: FastGPLattice n=2^18 d=3 x %d outputs, fp32 observations + complex64 "
+                      "ytilde for the MLL, fp64 eigenvalues / coefficients / posteriors" % B,
+                      lambda: MultiOutputGP(F, 18, 3, B, device, torch.float32), 3))
     out = []
-    for name, make, log2n, d in (("C2: FastGPLattice n=2^16 d=3", lambda: SingleGP(F, "lattice", 16, 3, device), 16, 3),
-                                 ("C3: FastGPDigitalNetB2 n=2^16 d=3 alpha=2", lambda: SingleGP(F, "net", 16, 3, device),
-                                  16, 3),
-                                 ("C5: FastGPLattice n=2^18 d=3 x %d outputs (shared hyper-parameters), fp64"
-                                  % args.c5_outputs, lambda: MultiOutputGP(F, 18, 3, args.c5_outputs, device), 18, 3),
-                                 ("C5 mixed: FastGPLattice n=2^18 d=3 x %d outputs, fp32 observations + complex64 "
-                                  "ytilde for the MLL, fp64 eigenvalues / coefficients / posteriors" % args.c5_outputs,
-                                  lambda: MultiOutputGP(F, 18, 3, args.c5_outputs, device, torch.float32), 18, 3)):
+    for name, make, d in cases:
         sg = make()
         xm = torch.rand((args.n_mean, d), generator=g).to(device)
         xv = torch.rand((args.n_var, d), generator=g).to(device)
-        sec = time_steps(lambda: step_single(sg, args, xm, xv), max(1, args.steps), 1)
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
-        sg.reset()
-        ev[0].record()
-        sg.gp.fit(iterations=args.fit_iters, stop_crit_wait_iterations=args.fit_iters + 1, verbose=0)
-        ev[1].record()
-        with torch.no_grad():
-            sg.gp.coeffs                 # the graph-free coefficients post_mean uses
-        ev[2].record()
-        sg.gp.post_mean(xm)
-        ev[3].record()
-        sg.gp.post_var(xv)
-        ev[4].record()
-        torch.cuda.synchronize()
-        phases = {k: ev[i].elapsed_time(ev[i + 1]) for i, k in enumerate(("ytilde+fit", "coeffs", "post_mean",
-                                                                          "post_var"))}
-        out.append({"metric": "GP fit+predict points/sec" if sg.outputs == 1 else
+        sec = time_steps(lambda: step_single(sg, args, xm, xv), max(1, args.steps), 1, device)
+        phases = None
+        if world == 1:
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
+            sg.reset()
+            ev[0].record()
+            sg.gp.fit(iterations=args.fit_iters, stop_crit_wait_iterations=args.fit_iters + 1, verbose=0)
+            ev[1].record()
+            with torch.no_grad():
+                sg.gp.coeffs                 # the graph-free coefficients post_mean uses
+            ev[2].record()
+            sg.gp.post_mean(xm)
+            ev[3].record()
+            sg.gp.post_var(xv)
+            ev[4].record()
+            torch.cuda.synchronize()
+            phases = {k: ev[i].elapsed_time(ev[i + 1]) for i, k in enumerate(("ytilde+fit", "coeffs", "post_mean",
+                                                                              "post_var"))}
+        total = getattr(sg, "total", 1)
+        out.append({"metric": "GP fit+predict points/sec" if total == 1 else
                     "multi-output GP fit+predict output-points/sec",
-                    "value": sg.n * sg.outputs / sec, "unit": "points/s" if sg.outputs == 1 else "output-points/s",
-                    "ms_per_step": sec * 1e3, "steps": max(1, args.steps),
+                    "value": sg.n * total / sec, "unit": "points/s" if total == 1 else "output-points/s",
+                    "ms_per_step": sec * 1e3, "steps": max(1, args.steps), "n_gpus": world,
                     "dtype": "f64" if sg.gp.data_dtype == torch.float64 else "f32 data / f64 eigenvalues",
                     "config": {"workload": "%s: fit %d Rprop iters + post_mean N=%d + post_var N=%d"
                                            % (name, args.fit_iters, args.n_mean, args.n_var),
-                               "n": sg.n, "outputs": sg.outputs},
+                               "n": sg.n, "outputs": total},
                     "phases_ms": phases})
         del sg
         torch.cuda.empty_cache()
@@ -577,8 +627,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, n, d)
     secondary = None
-    if rank == 0 and world == 1 and args.secondary:
-        secondary = secondary_configs(F, args, device)
+    if args.secondary:
+        secondary = secondary_configs(F, args, device, rank, world)
     if rank == 0:
         out = {"metric": "GP fit+predict points/sec at n=2^20 fp64; achieved HBM GB/s vs roofline",
                "value": value, "unit": "points/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,

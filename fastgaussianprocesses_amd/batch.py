@@ -168,7 +168,7 @@ def _set_raw(gps, raw, dl):
 
 def _basis_for(gps, n, parts, gen):
     """Part-product spectra of the batch (fit_engine.spec_basis) when the spectral fit path is the cheaper
-    one, else None: ONE [2^d, K] set for lattice GPs sharing a generating vector (the first-column
+    one, else None: ONE set for lattice GPs sharing a generating vector (the first-column
     distances (brev(i) z mod n) / n do not depend on the shift), else [P, 2^d, K] from the stacked parts."""
     g0 = gps[0]
     P = len(gps)

@@ -36,7 +36,7 @@ struct Nll {
   const double* basis;
   int64_t basis_stride;
   int spec, spec_net;            // spectral fit path (basis != NULL); nets (weight 1, K = n)
-  int64_t spec_K, spec_KS, spec_main;  // frequencies per spectrum, its row stride, frequencies in k blocks
+  int64_t spec_K, spec_KS, spec_main;  // frequencies per spectrum, 64 x its chunks, frequencies in k blocks
   int spec_kpl, spec_ppw, spec_pg;   // frequencies per lane and block, problems per wave, problem groups
   int spec_tile, spec_pgp, spec_ck;  // LDS-tiled kernel: problem-group slots, frequencies per chunk
   int64_t spec_kw;                   // ... and per workgroup
@@ -543,8 +543,13 @@ int launch_re_bwd_fused(const Nll& a, const FitFuse& fz, const Tables* tb, hipSt
 // spectral fit path (fgp_spectral.hip): d <= kSpecMaxD, at most kSpecBlocks k blocks per problem
 constexpr int kSpecMaxD = 6;
 constexpr int kSpecBlocks = 512;
+#ifndef FGP_SPEC_RING
+#define FGP_SPEC_RING 4
+#endif
+constexpr int kSpecRing = FGP_SPEC_RING;         // LDS ring depth of the spectral tile kernel (chunks)
+constexpr int kSpecLdsMax = 80 * 1024;           // its dynamic LDS per workgroup, at most (2 per CU)
 void spec_geometry(Nll& a);                        // nb and the spec_* fields of a spectral desc
-int64_t spec_row_stride(bool net, int log2n);      // row stride of the spectra (fgp_spec_basis layout)
+int64_t spec_chunks(bool net, int log2n);          // 64-frequency chunks of the spectra (fgp_spec_basis layout)
 // one fit iteration (loss + gradient partials); with fz (tile kernel only) also the reduction + Rprop
 int launch_spec_iter(const Nll& a, hipStream_t st, const FitFuse* fz = nullptr);
 int launch_spec_reduce_step(const Nll& a, const Fit& f, int iter, int do_update, hipStream_t st);

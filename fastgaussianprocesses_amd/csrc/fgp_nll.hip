@@ -978,29 +978,64 @@ __global__ __launch_bounds__(kWG) void k_fit_reduce(Nll a) {
   }
 }
 
-// loss assembly, histories and the Rprop update (torch.optim.Rprop single-tensor semantics)
+// loss assembly, histories and the Rprop update (torch.optim.Rprop single-tensor semantics) of ONE loss
+// over the G problems (per-output hyper-parameters of one GP): thread t takes problems t, t + kWG, ...
+// (ascending): a per-problem parameter's gradient is written by the one thread owning that problem, the
+// loss terms and the gradients of shared parameters are per-thread sums reduced in a fixed order
+// (wave shuffles, then the waves in order) -- O(G / kWG) per thread instead of a serial pass over G.
 __global__ __launch_bounds__(kWG) void k_fit_step(Nll a, Fit f, int iter, int do_update) {
   extern __shared__ double grad[];   // [n_params]
+  constexpr int NV = 4 + FGP_MAX_D, NW = kWG / 64;
+  __shared__ double red[NV * NW];
   const int tid = threadIdx.x;
   for (int p = tid; p < f.n_params; p += kWG) {
     grad[p] = 0.0;
     f.raw_hist[(int64_t)iter * f.n_params + p] = f.raw[p];
   }
   __syncthreads();
-  if (tid == 0) {
-    double term1 = 0.0, logdet_sum = 0.0;
-    for (int g = 0; g < a.G; ++g) {
-      term1 += *red_ptr(a, g, 0);
-      logdet_sum += *red_ptr(a, g, 1);
-      const int ni = a.noise_off + (a.noise_pp ? g : 0);
-      grad[ni] += exp(a.raw[ni]) * *red_ptr(a, g, 2);
-      grad[a.scale_off + (a.scale_pp ? g : 0)] += *red_ptr(a, g, 3);
-      const int lb = a.ls_off + (a.ls_pp ? g : 0) * (a.ls_pd ? a.d : 1);
-      for (int j = 0; j < a.d; ++j) grad[lb + (a.ls_pd ? j : 0)] += *red_ptr(a, g, 4 + j);
+  double v[NV];   // term1, logdet, shared dnoise, shared dscale, shared dlengthscale[j]
+#pragma unroll
+  for (int q = 0; q < NV; ++q) v[q] = 0.0;
+  for (int g = tid; g < a.G; g += kWG) {
+    v[0] += *red_ptr(a, g, 0);
+    v[1] += *red_ptr(a, g, 1);
+    const int ni = a.noise_off + (a.noise_pp ? g : 0);
+    const double dn = exp(a.raw[ni]) * *red_ptr(a, g, 2);
+    if (a.noise_pp) grad[ni] += dn;
+    else v[2] += dn;
+    if (a.scale_pp) grad[a.scale_off + g] += *red_ptr(a, g, 3);
+    else v[3] += *red_ptr(a, g, 3);
+    const int lb = a.ls_off + (a.ls_pp ? g : 0) * (a.ls_pd ? a.d : 1);
+    for (int j = 0; j < a.d; ++j) {
+      const double r = *red_ptr(a, g, 4 + j);
+      if (a.ls_pp) grad[lb + (a.ls_pd ? j : 0)] += r;
+      else v[4 + (a.ls_pd ? j : 0)] += r;
     }
-    const double term2 = a.logdet_weight * logdet_sum;
-    f.loss_hist[(int64_t)iter * 3 + 0] = 0.5 * (term1 + term2 + f.mll_const);
-    f.loss_hist[(int64_t)iter * 3 + 1] = term1;
+  }
+#pragma unroll
+  for (int q = 0; q < NV; ++q) {
+    double x = v[q];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+    if ((tid & 63) == 0) red[q * NW + (tid >> 6)] = x;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double tot[NV];
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+      tot[q] = 0.0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) tot[q] += red[q * NW + w];
+    }
+    if (!a.noise_pp) grad[a.noise_off] += tot[2];
+    if (!a.scale_pp) grad[a.scale_off] += tot[3];
+    if (!a.ls_pp) {
+      for (int j = 0; j < (a.ls_pd ? a.d : 1); ++j) grad[a.ls_off + j] += tot[4 + j];
+    }
+    const double term2 = a.logdet_weight * tot[1];
+    f.loss_hist[(int64_t)iter * 3 + 0] = 0.5 * (tot[0] + term2 + f.mll_const);
+    f.loss_hist[(int64_t)iter * 3 + 1] = tot[0];
     f.loss_hist[(int64_t)iter * 3 + 2] = term2;
   }
   __syncthreads();

@@ -19,6 +19,7 @@
 // 0 < k < n/2), exactly as the real-even kernels fold it (fgp_nll_re.hip).  Nets: Phi_S (FWHT) real,
 // k = 0 .. n-1, weight 1.
 #include <algorithm>
+#include <cstdlib>
 
 #include "fgp_nll.h"
 
@@ -45,10 +46,21 @@ __device__ __forceinline__ double mlin(const double* phi, const double* l, doubl
   }
 }
 
-// Per-problem accumulators of one lane (its frequencies of one block).
+// Layout of the spectra (fgp_spec_basis): chunks of 64 frequencies, each holding the 2^d spectra of its
+// frequencies contiguously -- [chunk][S][64], frequency k of spectrum S at (k / 64) 2^d 64 + 64 S + k mod 64
+// (the lattice's k = n/2 in chunk n/128, zero padding after it).  A wave's 64 frequencies of every S, and
+// an LDS tile chunk, are then one contiguous 2^d x 512-byte run instead of 2^d rows n/2 apart.
+template <int NS>
+__device__ __forceinline__ int64_t spec_at(int64_t k, int s) {
+  return ((k >> 6) * NS + s) * 64 + (k & 63);
+}
+
+// Per-problem accumulators of one lane (its frequencies of one block): UNWEIGHTED sums over them --
+// the lattice's fold weights (2 for 0 < k < n/2, 1 at k = 0 and n/2) are applied once per block
+// (spec_block_partials), not per frequency.
 template <int D>
 struct SpecAcc {
-  double norm = 0.0, dnoise = 0.0, gs = 0.0, mant = 1.0;
+  double norm = 0.0, ge = 0.0, gs = 0.0, mant = 1.0;
   double gl[D];
   int ex = 0;
   __device__ __forceinline__ SpecAcc() {
@@ -57,27 +69,103 @@ struct SpecAcc {
   }
 };
 
-// One frequency k of problem p: eigenvalue ev = sqrt(n) scale P + noise and its terms (weight w = 1 or 2;
-// two: the folded pair k, n - k).  Loss terms as eig_terms (fgp_nll.h): norm += w Y / ev,
-// log|ev| (frexp mantissa product + exponent sum), dL/dev = w/2 (wl / ev - Y / ev^2).
+// 1 / e: v_rcp_f64 and two Newton steps (within an ulp of the quotient; 5 VALU instead of the ~11 of
+// the IEEE division sequence)
+__device__ __forceinline__ double rcp_nr(double e) {
+  double r = __builtin_amdgcn_rcp(e);
+  r = __builtin_fma(__builtin_fma(-e, r, 1.0), r, r);
+  return __builtin_fma(__builtin_fma(-e, r, 1.0), r, r);
+}
+
+// One frequency of one problem: ev = sqrt(n) scale P + noise and the loss terms of eig_terms (fgp_nll.h)
+// with weight 1: norm += Y / ev, log|ev| (frexp mantissa product + exponent sum), and g = wl / ev - Y / ev^2
+// (= 2 dL/dev) into dL/dnoise, the scale term g P and the lengthscale terms g dP/dl_j.
 template <int D>
-__device__ __forceinline__ void spec_terms(const double* phi, const Hyp& h, double rootn, double wl, double Y, bool two,
+__device__ __forceinline__ void spec_terms(const double* phi, const Hyp& h, double rootn, double wl, double Y,
                                            SpecAcc<D>& acc) {
   double dp[D];
   const double P = mlin<D>(phi, h.ls, dp);
   const double e = __builtin_fma(rootn, h.scale * P, h.noise);
-  const double r = 1.0 / e;
-  const double w = two ? 2.0 : 1.0;
-  acc.norm = __builtin_fma(w * Y, r, acc.norm);
+  const double r = rcp_nr(e);
+  acc.norm = __builtin_fma(Y, r, acc.norm);
   int ex;
   const double m = frexp(fabs(e), &ex);
-  acc.mant *= two ? m * m : m;
-  acc.ex += two ? 2 * ex : ex;
-  const double ge = (0.5 * w) * r * __builtin_fma(-Y, r, wl);   // dL/dev
-  acc.dnoise += ge;
-  acc.gs = __builtin_fma(ge, P, acc.gs);
+  acc.mant *= m;
+  acc.ex += ex;
+  const double g = r * __builtin_fma(-Y, r, wl);
+  acc.ge += g;
+  acc.gs = __builtin_fma(g, P, acc.gs);
 #pragma unroll
-  for (int j = 0; j < D; ++j) acc.gl[j] = __builtin_fma(ge, dp[j], acc.gl[j]);
+  for (int j = 0; j < D; ++j) acc.gl[j] = __builtin_fma(g, dp[j], acc.gl[j]);
+}
+
+// v[0..3+D] of one accumulator set: norm, log|ev| sum, g sum, g P sum, g dP/dl_j sums
+template <int D>
+__device__ __forceinline__ void spec_values(const SpecAcc<D>& acc, double* v) {
+  v[0] = acc.norm;
+  v[1] = log(acc.mant) + (double)acc.ex * 0.69314718055994530942;
+  v[2] = acc.ge;
+  v[3] = acc.gs;
+#pragma unroll
+  for (int j = 0; j < D; ++j) v[4 + j] = acc.gl[j];
+}
+
+// The block's partials of problem g from the lanes' unweighted sums: weights (lattice: 2 per frequency,
+// then k = 0 taken back to weight 1 in lane 0 of block 0 and k = n/2 added with weight 1 in lane 0 of the
+// last block; nets: 1), dL/dev = g / 2, wave sums (fixed shuffle order), the gradient factors
+// (dL/dlambda = sqrt(n) dL/dev; dlambda/draw_scale = lambda, dlambda/draw_l_j = scale l_j dP/dl_j) and
+// one store per quantity by lane 0 (sc1 when handed to a last-workgroup reduction).  The single-frequency
+// corrections reload their spectra and Y from global memory, so every kernel computes the same values.
+template <int D, bool NET>
+__device__ __forceinline__ void spec_block_partials(const Nll& a, const Hyp& h, int g, int blk, double rootn, double wl,
+                                                    const SpecAcc<D>& acc, bool sc1) {
+  constexpr int NS = 1 << D, NV = 4 + D;
+  const int lane = threadIdx.x & 63;
+  double v[NV];
+  spec_values<D>(acc, v);
+  const double wlin = NET ? 1.0 : 2.0;
+  v[0] *= wlin;
+  v[1] *= wlin;
+#pragma unroll
+  for (int q = 2; q < NV; ++q) v[q] *= 0.5 * wlin;
+  if (!NET && lane == 0 && (blk == 0 || blk == a.nb - 1)) {
+    const double* phib = a.basis + (int64_t)g * a.basis_stride;
+    const double* ys = a.ysq + (int64_t)g * a.ysq_stride;
+#pragma unroll
+    for (int side = 0; side < 2; ++side) {
+      const bool here = side == 0 ? blk == 0 : blk == a.nb - 1;
+      if (!here) continue;
+      const int64_t k = side == 0 ? 0 : a.spec_main;
+      double phi[NS];
+#pragma unroll
+      for (int s = 0; s < NS; ++s) phi[s] = phib[spec_at<NS>(k, s)];
+      SpecAcc<D> t;
+      spec_terms<D>(phi, h, rootn, wl, ys[k], t);
+      double tv[NV];
+      spec_values<D>(t, tv);
+      const double sg = side == 0 ? -1.0 : 1.0;   // k = 0: weight 2 -> 1; k = n/2: weight 1
+      v[0] = __builtin_fma(sg, tv[0], v[0]);
+      v[1] = __builtin_fma(sg, tv[1], v[1]);
+#pragma unroll
+      for (int q = 2; q < NV; ++q) v[q] = __builtin_fma(0.5 * sg, tv[q], v[q]);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < NV; ++q)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v[q] += __shfl_xor(v[q], o, 64);
+  if (lane == 0) {
+    const double gsc = rootn * h.scale;
+    v[3] *= gsc;
+#pragma unroll
+    for (int j = 0; j < D; ++j) v[4 + j] *= gsc * h.ls[j];
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+      double* dst = part_ptr(a, g, q, blk);
+      if (sc1) __hip_atomic_store(dst, v[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else *dst = v[q];
+    }
+  }
 }
 
 // One fit iteration over every problem and frequency: per-block partials of the norm, logdet, dL/dnoise
@@ -103,7 +191,7 @@ __global__ __launch_bounds__(kWG) void k_spec_iter(Nll a) {
       on[p] = g0 + p < a.G;
       load_hyp_wave(a, on[p] ? g0 + p : g0, h[p]);
     }
-    const int64_t KS = a.spec_KS, main = a.spec_main;
+    const int64_t main = a.spec_main;
     const double rootn = sqrt((double)((int64_t)1 << a.log2n)), wl = a.logdet_weight;
     const double* phib = a.basis + (int64_t)g0 * a.basis_stride;   // PPW = 2: shared spectra (stride 0)
     const double* ys[PPW];
@@ -111,48 +199,22 @@ __global__ __launch_bounds__(kWG) void k_spec_iter(Nll a) {
     for (int p = 0; p < PPW; ++p) ys[p] = a.ysq + (int64_t)(on[p] ? g0 + p : g0) * a.ysq_stride;
     SpecAcc<D> acc[PPW];
     const int64_t kbase = (int64_t)kb * 64 * a.spec_kpl;
-    auto step = [&](int64_t k, bool two) {
+    for (int i = 0; i < a.spec_kpl; ++i) {
+      const int64_t k = kbase + lane + 64 * i;
+      if (k >= main) break;
       double phi[NS];
 #pragma unroll
-      for (int s = 0; s < NS; ++s) phi[s] = phib[(int64_t)s * KS + k];
+      for (int s = 0; s < NS; ++s) phi[s] = phib[spec_at<NS>(k, s)];
       double Y[PPW];
 #pragma unroll
       for (int p = 0; p < PPW; ++p) Y[p] = ys[p][k];
 #pragma unroll
       for (int p = 0; p < PPW; ++p)
-        if (on[p]) spec_terms<D>(phi, h[p], rootn, wl, Y[p], two, acc[p]);
-    };
-    for (int i = 0; i < a.spec_kpl; ++i) {
-      const int64_t k = kbase + lane + 64 * i;
-      if (k >= main) break;
-      step(k, !NET && k != 0);
+        if (on[p]) spec_terms<D>(phi, h[p], rootn, wl, Y[p], acc[p]);
     }
-    if (!NET && kb == a.nb - 1 && lane == 0) step(main, false);   // k = n/2
-    // wave sums (fixed shuffle order: deterministic) and this block's partials
 #pragma unroll
-    for (int p = 0; p < PPW; ++p) {
-      if (!on[p]) continue;
-      double v[4 + D];
-      v[0] = acc[p].norm;
-      v[1] = log(acc[p].mant) + (double)acc[p].ex * 0.69314718055994530942;
-      v[2] = acc[p].dnoise;
-      v[3] = acc[p].gs;
-#pragma unroll
-      for (int j = 0; j < D; ++j) v[4 + j] = acc[p].gl[j];
-#pragma unroll
-      for (int q = 0; q < 4 + D; ++q)
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v[q] += __shfl_xor(v[q], o, 64);
-      if (lane == 0) {
-        const int g = g0 + p;
-        const double gsc = rootn * h[p].scale;   // dL/dlambda = sqrt(n) dL/dev; dlambda/draw_scale = lambda
-        v[3] *= gsc;
-#pragma unroll
-        for (int j = 0; j < D; ++j) v[4 + j] *= gsc * h[p].ls[j];
-#pragma unroll
-        for (int q = 0; q < 4 + D; ++q) *part_ptr(a, g, q, kb) = v[q];
-      }
-    }
+    for (int p = 0; p < PPW; ++p)
+      if (on[p]) spec_block_partials<D, NET>(a, h[p], g0 + p, kb, rootn, wl, acc[p], false);
   }
   stamp_end(a);
 }
@@ -162,9 +224,9 @@ __global__ __launch_bounds__(kWG) void k_spec_iter(Nll a) {
 // blocks summed lane-strided then by shuffles -- the one order used by both the stage launches
 // (k_spec_reduce_step) and the fused last-workgroup step of k_spec_tile, so the two are bit-identical.
 // SC1: the partials of the same launch are read with sc1 loads (the producers stored them sc1).
-template <bool SC1>
+template <bool SC1, int D>
 __device__ __forceinline__ void reduce_step_wave(const Nll& a, const Fit& f, int g, int iter, int do_update) {
-  constexpr int NQ = 4 + FGP_MAX_D;
+  constexpr int NQ = 4 + D, UB = 4;   // quantities; blocks per lane whose loads are issued together
   const int lane = threadIdx.x & 63;
   const int dl = a.ls_pd ? a.d : 1;
   int p = 0, rg = 0;
@@ -188,19 +250,23 @@ __device__ __forceinline__ void reduce_step_wave(const Nll& a, const Fit& f, int
   double v[NQ];
 #pragma unroll
   for (int q = 0; q < NQ; ++q) v[q] = 0.0;
-  for (int b = lane; b < a.nb; b += 64) {
-    double t[NQ];
+  // lane-strided blocks in ascending order, UB blocks' loads in flight at once (a dependent chain of
+  // round trips otherwise); out-of-range blocks read block 0 and add nothing
+  for (int b0 = lane; b0 < a.nb; b0 += 64 * UB) {
+    double t[UB][NQ];
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      if (q < a.nq) {
-        double* pp = part_ptr(a, g, q, b);
-        t[q] = SC1 ? __hip_atomic_load(pp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *pp;
-      } else {
-        t[q] = 0.0;
+    for (int u = 0; u < UB; ++u) {
+      const int b = b0 + 64 * u;
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        double* pp = part_ptr(a, g, q, b < a.nb ? b : 0);
+        t[u][q] = SC1 ? __hip_atomic_load(pp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *pp;
       }
     }
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) v[q] += t[q];
+    for (int u = 0; u < UB; ++u)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) v[q] += (b0 + 64 * u < a.nb) ? t[u][q] : 0.0;
   }
 #pragma unroll
   for (int q = 0; q < NQ; ++q)
@@ -221,11 +287,11 @@ __device__ __forceinline__ void reduce_step_wave(const Nll& a, const Fit& f, int
     if (a.ls_pd) {
       gp = 0.0;
 #pragma unroll
-      for (int j = 0; j < FGP_MAX_D; ++j) gp = (j == lane - 1) ? v[4 + j] : gp;
+      for (int j = 0; j < D; ++j) gp = (j == lane - 1) ? v[4 + j] : gp;
     } else {
       gp = 0.0;
 #pragma unroll
-      for (int j = 0; j < FGP_MAX_D; ++j) gp += (j < a.d) ? v[4 + j] : 0.0;
+      for (int j = 0; j < D; ++j) gp += v[4 + j];
     }
   } else {
     gp = exp(raw_p) * v[2];
@@ -245,33 +311,70 @@ __device__ __forceinline__ void reduce_step_wave(const Nll& a, const Fit& f, int
 
 // The per-problem step of the spectral path as its own launch (fgp_fit_step, stage-by-stage fits):
 // wave w of workgroup b reduces problem 4 b + w.
+template <int D>
 __global__ __launch_bounds__(kWG) void k_spec_reduce_step(Nll a, Fit f, int iter, int do_update) {
   const int g = (int)blockIdx.x * (kWG / 64) + (int)(threadIdx.x >> 6);
-  if (g < a.G) reduce_step_wave<false>(a, f, g, iter, do_update);
+  if (g < a.G) reduce_step_wave<false, D>(a, f, g, iter, do_update);
+}
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void glb_void;
+
+// s_waitcnt vmcnt(n) for a runtime n <= 15 (the immediate must be a constant)
+__device__ __forceinline__ void wait_vmcnt(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
+    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+  }
+}
+
+// workgroup barrier that lets LDS-DMA loads stay in flight across it (__syncthreads() would drain them
+// with vmcnt(0)): the waves' LDS accesses retired (lgkmcnt), the raw barrier, a compiler memory fence
+__device__ __forceinline__ void barrier_keep_vm() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
 }
 
 // One fit iteration when every problem shares ONE set of spectra and the problem groups fit in the four
 // waves of a workgroup (PG = ceil(G / PPW) <= 4; the C4 shifts, single GPs) and a chunk's tile is at most
-// 24 KB (two buffers: 48 KB of LDS, two workgroups per CU).  The k blocks are those of
+// 24 KB (a 3-deep ring: 72 KB of LDS, two workgroups per CU).  The k blocks are those of
 // k_spec_iter (nb blocks of B = 64 kpl frequencies, one partial per problem and block, lane l summing
 // k = block base + l + 64 i in ascending i): workgroup b owns NBW = 4 / PGP consecutive blocks (PGP = PG
 // rounded up to 1, 2 or 4), wave w the block w / PGP for problem group w mod PGP -- so every problem's
 // arithmetic, and its partials, are those of k_spec_iter whatever G is (a batch equals its GPs' own fits
-// bit for bit).  The spectra and Y stream through a double-buffered LDS tile in chunks of 64 frequencies
-// per block: the chunk's (2^d + G) rows x NBW segments are read ONCE from HBM by all 256 threads (16-byte
-// loads issued a chunk ahead into registers, so they fly under the previous chunk's compute) instead of
-// once per problem group, and each wave reads its segment from LDS (lane-consecutive 8-byte reads:
-// conflict-free).  With fz.counters the LAST workgroup to finish (sc1 partials, an agent-scope arrival
+// bit for bit).  The spectra and Y stream through a 3-deep LDS ring in chunks of 64 frequencies per
+// block: the chunk's (2^d + G) rows x NBW segments are read ONCE from HBM by all four waves (16-byte LDS-DMA
+// loads, global_load_lds_dwordx4, no register staging; two chunks in flight under each chunk's compute,
+// counted vmcnt waits and raw barriers so they stay in flight: cdna_hip_programming.md section 5
+// "Pipelining across barriers") instead of once per problem group, and each wave reads its segment from
+// LDS (lane-consecutive 8-byte reads: conflict-free).  With fz.counters the LAST workgroup to finish (sc1 partials, an agent-scope arrival
 // counter: MI355X_MICROARCH.md hand-off row 1, as the real-even backward kernel) runs every problem's
 // reduction + Rprop, wave w taking problems w, w + 4, ...
 template <int D, int PPW, bool NET>
 __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
-  constexpr int NS = 1 << D, MAXP = 8;              // 16-byte pieces per thread and chunk, at most
-  extern __shared__ double lds[];                   // [2][NS + G][NBW][64]
-  __shared__ int last_wg;
+  constexpr int NS = 1 << D;
+  constexpr int RING = kSpecRing;                   // chunks in LDS; RING - 1 in flight under a compute
+  extern __shared__ double lds[];                   // [RING][NBW][NS + G][64] ring
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int PGP = a.spec_pgp, NBW = 4 / PGP, G = a.G;
-  const int rows = NS + G, tile = rows * NBW * 64, npieces = tile / 2, rowp = 32 * NBW;
+  const int rows = NS + G, tile = rows * NBW * 64, npieces = tile / 2, segp = 32 * rows;
+  const int ninst = npieces / 64;                   // 1-KiB LDS-DMA wave-instructions per chunk (whole)
+  const int cnt_w = (ninst - w + 3) / 4;            // ... issued by this wave: j = w, w + 4, ...
   const int pg = w % PGP, bw = w / PGP;
   const int g0 = pg * PPW;
   const bool active = g0 < G;
@@ -285,99 +388,74 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
     on[p] = g0 + p < G;
     load_hyp_wave(a, on[p] ? g0 + p : 0, h[p]);
   }
-  const int64_t KS = a.spec_KS, main = a.spec_main;
   const double rootn = sqrt((double)((int64_t)1 << a.log2n)), wl = a.logdet_weight;
   const int64_t wg_base = (int64_t)blockIdx.x * NBW * B;
-  // piece i of chunk c: row i / rowp (spectrum rows, then Y rows), segment (i mod rowp) / 32, 16-byte
-  // column i mod 32; LDS offset 2 i (the image is [row][segment][64] in piece order)
-  auto src = [&](int i, int c) -> const double2* {
-    const int r = i / rowp, rem = i - r * rowp, sg = rem >> 5, col = rem & 31;
-    const double* row = r < NS ? a.basis + (int64_t)r * KS : a.ysq + (int64_t)(r - NS) * a.ysq_stride;
-    return reinterpret_cast<const double2*>(row + wg_base + sg * B + 64 * (int64_t)c) + col;
-  };
-  double2 stage[MAXP];
-  auto load_chunk = [&](int c) {
+  // chunk c into buffer buf: piece i (16 bytes) = segment i / (32 rows) (the workgroup's block), row
+  // (i mod 32 rows) / 32 (spectrum rows, then Y rows), column i mod 32, at LDS byte 16 i -- a wave's
+  // spectra and Y of a chunk are then at compile-time offsets from one base.  Wave-instruction j moves
+  // pieces [64 j, 64 j + 64); this wave's instructions j = w + 4 t (t < cnt_w <= kMaxDma): chunk-0 source
+  // and per-chunk step per lane, formed once (a chunk further is NS 64 doubles on in the chunked spectra,
+  // 64 in a Y row).
+  constexpr int kMaxDma = 6;                        // tile <= 3072 doubles: 24 instructions, 6 per wave
+  const double* src0[kMaxDma];
+  int64_t step[kMaxDma];
 #pragma unroll
-    for (int j = 0; j < MAXP; ++j) {
-      const int i = (int)threadIdx.x + kWG * j;
-      if (i < npieces) stage[j] = *src(i, c);
-    }
-  };
-  auto store_chunk = [&](double* buf) {
+  for (int t = 0; t < kMaxDma; ++t) {
+    const int jj = w + 4 * t;
+    const int i = (jj < ninst ? jj : 0) * 64 + lane;
+    const int sg = i / segp, rem = i - sg * segp, r = rem >> 5, col = rem & 31;
+    const int64_t k = wg_base + sg * B;             // the segment's first frequency in chunk 0
+    src0[t] = (r < NS ? a.basis + spec_at<NS>(k, r) : a.ysq + (int64_t)(r - NS) * a.ysq_stride + k) + 2 * col;
+    step[t] = r < NS ? NS * 64 : 64;
+  }
+  auto issue = [&](int c, double* buf) {
 #pragma unroll
-    for (int j = 0; j < MAXP; ++j) {
-      const int i = (int)threadIdx.x + kWG * j;
-      if (i < npieces) reinterpret_cast<double2*>(buf)[i] = stage[j];
+    for (int t = 0; t < kMaxDma; ++t) {
+      if (t < cnt_w) {
+        const double* src = src0[t] + step[t] * c;
+        __builtin_amdgcn_global_load_lds((glb_void*)src, (lds_void*)(buf + 128 * (w + 4 * t)), 16, 0, 0);
+      }
     }
   };
   SpecAcc<D> acc[PPW];
   const int nc = a.spec_kpl;
-  load_chunk(0);
-  store_chunk(lds);
-  __syncthreads();
+  const int wofs = bw * rows * 64 + lane;           // this lane's spectra in a buffer: wofs + 64 s
+  const int yofs = wofs + (NS + g0) * 64;           // ... its problems' Y: yofs + 64 p
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // only the chunk loads below are counted
+#pragma unroll
+  for (int c = 0; c < RING - 1; ++c)
+    if (c < nc) issue(c, lds + c * tile);
   for (int c = 0; c < nc; ++c) {
-    if (c + 1 < nc) load_chunk(c + 1);
-    const double* buf = lds + (c & 1) * tile;
+    // this wave's loads of chunk c have landed (chunks c + 1 .. c + RING - 2 may stay in flight)
+    wait_vmcnt(cnt_w * min(RING - 2, nc - 1 - c));
+    barrier_keep_vm();                              // ... every wave's; every wave done with chunk c - 1
+    if (c + RING - 1 < nc) issue(c + RING - 1, lds + ((c + RING - 1) % RING) * tile);
+    const double* buf = lds + (c % RING) * tile;
     if (active) {
       double phi[NS];
 #pragma unroll
-      for (int s = 0; s < NS; ++s) phi[s] = buf[(s * NBW + bw) * 64 + lane];
-      const bool two = !NET && (blk != 0 || c != 0 || lane != 0);
+      for (int s = 0; s < NS; ++s) phi[s] = buf[wofs + 64 * s];
 #pragma unroll
       for (int p = 0; p < PPW; ++p)
-        if (on[p]) spec_terms<D>(phi, h[p], rootn, wl, buf[((NS + g0 + p) * NBW + bw) * 64 + lane], two, acc[p]);
-    }
-    if (c + 1 < nc) store_chunk(lds + ((c + 1) & 1) * tile);
-    __syncthreads();
-  }
-  if (!NET && active && blk == a.nb - 1 && lane == 0) {   // k = n/2, weight 1 (as k_spec_iter)
-    double phi[NS];
-#pragma unroll
-    for (int s = 0; s < NS; ++s) phi[s] = a.basis[(int64_t)s * KS + main];
-#pragma unroll
-    for (int p = 0; p < PPW; ++p)
-      if (on[p]) spec_terms<D>(phi, h[p], rootn, wl, a.ysq[(int64_t)(g0 + p) * a.ysq_stride + main], false, acc[p]);
-  }
-  // the block's partials (k_spec_iter's values), one storing lane per problem (sc1 when fused)
-#pragma unroll
-  for (int p = 0; p < PPW; ++p) {
-    if (!on[p] || !active) continue;
-    double v[4 + D];
-    v[0] = acc[p].norm;
-    v[1] = log(acc[p].mant) + (double)acc[p].ex * 0.69314718055994530942;
-    v[2] = acc[p].dnoise;
-    v[3] = acc[p].gs;
-#pragma unroll
-    for (int j = 0; j < D; ++j) v[4 + j] = acc[p].gl[j];
-#pragma unroll
-    for (int q = 0; q < 4 + D; ++q)
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) v[q] += __shfl_xor(v[q], o, 64);
-    if (lane == 0) {
-      const int g = g0 + p;
-      const double gsc = rootn * h[p].scale;
-      v[3] *= gsc;
-#pragma unroll
-      for (int j = 0; j < D; ++j) v[4 + j] *= gsc * h[p].ls[j];
-#pragma unroll
-      for (int q = 0; q < 4 + D; ++q) {
-        double* dst = part_ptr(a, g, q, blk);
-        if (fz.counters) __hip_atomic_store(dst, v[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else *dst = v[q];
-      }
+        if (on[p]) spec_terms<D>(phi, h[p], rootn, wl, buf[yofs + 64 * p], acc[p]);
     }
   }
+  // the block's partials (k_spec_iter's values; sc1 when handed to the last workgroup)
+#pragma unroll
+  for (int p = 0; p < PPW; ++p)
+    if (on[p] && active) spec_block_partials<D, NET>(a, h[p], g0 + p, blk, rootn, wl, acc[p], fz.counters != nullptr);
   if (fz.counters) {
     // hand-off: every storing lane's sc1 stores retired (vmcnt) before the workgroup's arrival
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    int* last_wg = reinterpret_cast<int*>(lds);     // the ring is free now
     if (threadIdx.x == 0) {
       const unsigned prev = __hip_atomic_fetch_add(fz.counters, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      last_wg = prev == gridDim.x - 1;
+      *last_wg = prev == gridDim.x - 1;
     }
     __syncthreads();
-    if (last_wg) {
-      for (int g = w; g < G; g += kWG / 64) reduce_step_wave<true>(a, fz.f, g, fz.iter, fz.do_update);
+    if (*last_wg) {
+      for (int g = w; g < G; g += kWG / 64) reduce_step_wave<true, D>(a, fz.f, g, fz.iter, fz.do_update);
       if (threadIdx.x == 0) __hip_atomic_store(fz.counters, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
@@ -398,7 +476,7 @@ __global__ __launch_bounds__(kWG) void k_spec_lam(Nll a) {
   const double* phib = a.basis + (int64_t)g * a.basis_stride;
   double phi[NS], dp[D];
 #pragma unroll
-  for (int s = 0; s < NS; ++s) phi[s] = phib[(int64_t)s * a.spec_KS + k];
+  for (int s = 0; s < NS; ++s) phi[s] = phib[spec_at<NS>(k, s)];
   const double lam = h.scale * mlin<D>(phi, h.ls, dp);
   if constexpr (NET) {
     static_cast<double*>(a.grad_lam)[(int64_t)g * n + k] = lam;
@@ -431,7 +509,7 @@ void spec_geometry(Nll& a) {
   const bool net = a.spec_net;
   a.spec_main = net ? n : n / 2;
   a.spec_K = net ? n : n / 2 + 1;
-  a.spec_KS = spec_row_stride(net, a.log2n);
+  a.spec_KS = spec_chunks(net, a.log2n) * 64;
   a.spec_ppw = (a.G >= 2 && a.basis_stride == 0 && a.d <= 5) ? 2 : 1;
   a.spec_pg = (a.G + a.spec_ppw - 1) / a.spec_ppw;
   const int64_t lanes = std::max<int64_t>(1, a.spec_main / 64);
@@ -440,10 +518,16 @@ void spec_geometry(Nll& a) {
   a.spec_tile = 0;
   a.spec_pgp = a.spec_ck = 0;
   a.spec_kw = 0;
-  if (a.basis_stride == 0 && a.spec_pg <= 4 && a.d <= 5 && a.spec_main >= 256) {
+  const char* te = getenv("FGP_SPEC_TILE");   // 0: the per-wave kernel only (A/B experiments)
+  const bool tile_ok = !(te && te[0] == '0');
+  if (tile_ok && a.basis_stride == 0 && a.spec_pg <= 4 && a.d <= 5 && a.spec_main >= 256) {
     const int pgp = a.spec_pg <= 1 ? 1 : (a.spec_pg <= 2 ? 2 : 4);
     const int ck = 64 * (4 / pgp);   // frequencies per chunk (64 per block of the workgroup)
-    if (((1 << a.d) + a.G) * ck <= 3072 && a.nb % (4 / pgp) == 0 && a.spec_main % (64 * (int64_t)a.nb) == 0) {
+    // the ring <= kSpecLdsMax (two workgroups per CU), whole 1-KiB wave-instructions, <= 6 per wave
+    const int rows = (1 << a.d) + a.G;
+    if (rows * ck * 8 * kSpecRing <= kSpecLdsMax && rows * ck <= 3072 && (rows * ck) % 128 == 0 &&
+        a.nb % (4 / pgp) == 0 &&
+        a.spec_main % (64 * (int64_t)a.nb) == 0) {
       a.spec_tile = 1;
       a.spec_pgp = pgp;
       a.spec_ck = ck;
@@ -452,9 +536,9 @@ void spec_geometry(Nll& a) {
   }
 }
 
-int64_t spec_row_stride(bool net, int log2n) {
-  const int64_t n = (int64_t)1 << log2n;
-  return net ? n : n / 2 + 16;   // lattice: k = 0 .. n/2 and zero padding to a 128-byte row
+int64_t spec_chunks(bool net, int log2n) {
+  const int64_t n = (int64_t)1 << log2n, K = net ? n : n / 2 + 1;
+  return (K + 63) / 64;
 }
 
 int launch_spec_iter(const Nll& a, hipStream_t st, const FitFuse* fz) {
@@ -462,17 +546,27 @@ int launch_spec_iter(const Nll& a, hipStream_t st, const FitFuse* fz) {
     FitFuse none{};
     none.counters = nullptr;
     const FitFuse& f = fz ? *fz : none;
-    const size_t shm = sizeof(double) * 2 * (size_t)(((1 << a.d) + a.G) * a.spec_ck);
+    const size_t shm = sizeof(double) * (size_t)kSpecRing * (size_t)(((1 << a.d) + a.G) * a.spec_ck);
     const unsigned grid = (unsigned)(a.nb / (4 / a.spec_pgp));
     return with_spec_d(a.d, [&](auto dc) {
       constexpr int D = decltype(dc)::value;
       if constexpr (D <= 5) {
+        auto go = [&](auto kern) {
+          // the ring may exceed the 64 KB default of dynamic LDS: raise the kernel's limit once
+          static bool raised = false;
+          if (!raised) {
+            hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                kSpecLdsMax);
+            raised = true;
+          }
+          kern<<<grid, kWG, shm, st>>>(a, f);
+        };
         if (a.spec_net) {
-          if (a.spec_ppw == 2) k_spec_tile<D, 2, true><<<grid, kWG, shm, st>>>(a, f);
-          else k_spec_tile<D, 1, true><<<grid, kWG, shm, st>>>(a, f);
+          if (a.spec_ppw == 2) go(k_spec_tile<D, 2, true>);
+          else go(k_spec_tile<D, 1, true>);
         } else {
-          if (a.spec_ppw == 2) k_spec_tile<D, 2, false><<<grid, kWG, shm, st>>>(a, f);
-          else k_spec_tile<D, 1, false><<<grid, kWG, shm, st>>>(a, f);
+          if (a.spec_ppw == 2) go(k_spec_tile<D, 2, false>);
+          else go(k_spec_tile<D, 1, false>);
         }
         return check_launch("k_spec_tile");
       } else {
@@ -497,8 +591,11 @@ int launch_spec_iter(const Nll& a, hipStream_t st, const FitFuse* fz) {
 }
 
 int launch_spec_reduce_step(const Nll& a, const Fit& f, int iter, int do_update, hipStream_t st) {
-  k_spec_reduce_step<<<(unsigned)((a.G + kWG / 64 - 1) / (kWG / 64)), kWG, 0, st>>>(a, f, iter, do_update);
-  return check_launch("k_spec_reduce_step");
+  return with_spec_d(a.d, [&](auto dc) {
+    k_spec_reduce_step<decltype(dc)::value>
+        <<<(unsigned)((a.G + kWG / 64 - 1) / (kWG / 64)), kWG, 0, st>>>(a, f, iter, do_update);
+    return check_launch("k_spec_reduce_step");
+  });
 }
 
 int launch_spec_lam(const Nll& a, hipStream_t st) {
@@ -532,17 +629,25 @@ __global__ __launch_bounds__(kWG) void k_spec_products(const double* __restrict_
   }
 }
 
-// basis[s][k] = Re spec[s][k], k < K (the even spectrum's independent half), zeros to the row stride KS
-__global__ __launch_bounds__(kWG) void k_spec_extract(const double2* __restrict__ spec, int64_t n, int64_t K,
-                                                      int64_t KS, double* __restrict__ basis) {
-  const int64_t k = (int64_t)blockIdx.x * kWG + threadIdx.x;
-  const int s = blockIdx.y;
-  if (k < KS) basis[(int64_t)s * KS + k] = k < K ? spec[(int64_t)s * n + k].x : 0.0;
+// spectra of the subsets s0 .. s0 + cnt - 1 into the chunked layout (spec_at): Re of a complex [cnt][n]
+// spectrum (lattice: the even spectrum's independent half, k < K), or a real [cnt][n] one (net); zeros
+// past K.  Thread = (chunk, subset, frequency within the chunk): 512-byte runs on both sides.
+template <bool CX>
+__global__ __launch_bounds__(kWG) void k_spec_extract(const void* __restrict__ spec, int64_t n, int64_t K, int64_t qs,
+                                                      int ns, int s0, int cnt, double* __restrict__ basis) {
+  const int64_t t = (int64_t)blockIdx.x * kWG + threadIdx.x;
+  const int64_t e = t & 63, rest = t >> 6;
+  const int c = (int)(rest % cnt);
+  const int64_t q = rest / cnt, k = q * 64 + e;
+  if (q >= qs) return;
+  double v = 0.0;
+  if (k < K) v = CX ? static_cast<const double2*>(spec)[(int64_t)c * n + k].x : static_cast<const double*>(spec)[(int64_t)c * n + k];
+  basis[(q * ns + s0 + c) * 64 + e] = v;
 }
 
 static int64_t spec_subset_bytes(int family, int log2n) {
   const int64_t n = (int64_t)1 << log2n;
-  if (family == FGP_FAMILY_NET) return 8 * n;                 // products, transformed into the basis
+  if (family == FGP_FAMILY_NET) return 8 * n + 8 * n;         // products + their fwht
   return 8 * n + 16 * n + (log2n >= 17 ? 16 * n : 0);          // products + spectrum (+ fgp_fftbr_real scratch)
 }
 
@@ -571,7 +676,7 @@ int fgp_spec_basis(int family, const double* parts, int64_t parts_stride, int64_
   const int64_t n = (int64_t)1 << log2n;
   if (P > 1 && parts_stride < d * n) return set_error(kErrInvalid, "fgp_spec_basis: parts_stride below d n");
   const bool net = family == FGP_FAMILY_NET;
-  const int64_t K = net ? n : n / 2 + 1, KS = spec_row_stride(net, log2n);
+  const int64_t K = net ? n : n / 2 + 1, QS = spec_chunks(net, log2n);
   const int NS = 1 << d;
   const int64_t per = spec_subset_bytes(family, log2n);
   const int chunk = (int)std::min<int64_t>(NS, work_bytes / per);
@@ -584,7 +689,7 @@ int fgp_spec_basis(int family, const double* parts, int64_t parts_stride, int64_
   const unsigned gi = (unsigned)((n + kWG - 1) / kWG);
   for (int64_t p = 0; p < P; ++p) {
     const double* pp = parts + p * parts_stride;
-    double* bp = basis + p * (int64_t)NS * KS;
+    double* bp = basis + p * QS * NS * 64;
     for (int s0 = 0; s0 < NS; s0 += chunk) {
       const int cnt = std::min(chunk, NS - s0);
       int rc = with_spec_d(d, [&](auto dc) {
@@ -592,14 +697,19 @@ int fgp_spec_basis(int family, const double* parts, int64_t parts_stride, int64_
         return check_launch("k_spec_products");
       });
       if (rc != kOk) return rc;
+      const unsigned ge = (unsigned)((QS * 64 * cnt + kWG - 1) / kWG);
       if (net) {
-        rc = fgp_fwht(prod, n, bp + (int64_t)s0 * KS, cnt, log2n, 1, stream);
+        double* wht = reinterpret_cast<double*>(spec);
+        rc = fgp_fwht(prod, n, wht, cnt, log2n, 1, stream);
+        if (rc == kOk) {
+          k_spec_extract<false><<<ge, kWG, 0, st>>>(wht, n, K, QS, NS, s0, cnt, bp);
+          rc = check_launch("k_spec_extract");
+        }
       } else {
         rc = log2n >= 17 ? fgp_fftbr_real(prod, n, spec, scratch, cnt, log2n, stream)
                          : fgp_fftbr(prod, n, 1, spec, cnt, log2n, 1, stream);
         if (rc == kOk) {
-          k_spec_extract<<<dim3((unsigned)((KS + kWG - 1) / kWG), (unsigned)cnt), kWG, 0, st>>>(
-              spec, n, K, KS, bp + (int64_t)s0 * KS);
+          k_spec_extract<true><<<ge, kWG, 0, st>>>(spec, n, K, QS, NS, s0, cnt, bp);
           rc = check_launch("k_spec_extract");
         }
       }

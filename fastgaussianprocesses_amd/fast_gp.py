@@ -38,8 +38,12 @@ def _exp(x):
     return torch.exp(x)
 
 
+def _identity(x):
+    return x
+
+
 _DEFAULT_TFS = (_log, _exp)
-_IDENTITY_TFS = ((lambda x: x), (lambda x: x))
+_IDENTITY_TFS = (_identity, _identity)     # module-level functions: a GP pickles (torch.save) whole
 
 
 def _as_size(s):
@@ -490,7 +494,10 @@ class AbstractFastGP(torch.nn.Module):
     def _coeffs_now(self):
         n = self._nh
         if self._gradmode() or n < 2:
-            return self._solve(self._y[0], n)
+            # data_dtype=float32: the coefficients still come from an fp64 transform (as the graph-free
+            # branch below), so both modes give the same posterior mean
+            y = self._y[0]
+            return self._solve(y if y.dtype == torch.float64 else y.to(torch.float64), n)
         # graph-free: reuse the cached ytilde = ft(y); A * ytilde fused into the inverse transform's
         # first pass and its real part into the last (fgp_ifftbr_mul).  data_dtype=float32: the
         # coefficients still come from an fp64 transform of the (fp32) observations -- cond(K) ~ n /

@@ -60,10 +60,16 @@ def spec_k(family, n):
     return n // 2 + 1 if family == 0 else n
 
 
-def spec_row(family, n):
-    """Row stride of the spectra (fgp_spec_basis): lattice n/2 + 16 (k = 0 .. n/2, zero padding to 128-byte
-    rows), net n."""
-    return n // 2 + 16 if family == 0 else n
+def spec_chunks(family, n):
+    """64-frequency chunks of the spectra (fgp_spec_basis layout [Q][2^d][64])."""
+    return (spec_k(family, n) + 63) // 64
+
+
+def spec_dense(basis, family, n):
+    """[(P,) Q, 2^d, 64] chunked spectra -> [(P,) 2^d, K] (k-contiguous rows; tests / inspection)."""
+    t = basis.movedim(-3, -2)
+    t = t.reshape(t.shape[:-2] + (t.shape[-2] * 64,))
+    return t[..., :spec_k(family, n)]
 
 
 def spectral_wanted(family, n, d, G, nbases=1):
@@ -90,21 +96,21 @@ def spectral_wanted(family, n, d, G, nbases=1):
 
 
 def spec_basis(family, parts, n):
-    """Part-product spectra (fgp_spec_basis): parts [d, n] -> [2^d, KS], or [P, d, n] -> [P, 2^d, KS] (row
-    stride KS = spec_row, the first spec_k entries of a row used); lambda = scale sum_S l^S basis[S] for
-    every hyper-parameter setting (include/fgp_hip.h)."""
+    """Part-product spectra (fgp_spec_basis): parts [d, n] -> [Q, 2^d, 64], or [P, d, n] -> [P, Q, 2^d, 64]
+    (chunks of 64 frequencies; spec_dense gives [2^d, K]); lambda = scale sum_S l^S Phi_S for every
+    hyper-parameter setting (include/fgp_hip.h)."""
     require_device(parts, "spec_basis")
     parts = parts.contiguous()
     d = parts.shape[-2]
     m = log2_exact(n)
     P = parts.shape[0] if parts.dim() == 3 else 1
-    K = spec_row(family, n)
+    Q = spec_chunks(family, n)
     total = ctypes.c_int64(0)
     N.call("fgp_spec_basis_work", int(family), m, int(d), ctypes.byref(total))
     one = total.value >> d
     wbytes = max(one, min(total.value, SPEC_WORK_CAP))
     work = torch.empty((wbytes,), dtype=torch.uint8, device=parts.device)
-    out = torch.empty(((P,) if parts.dim() == 3 else ()) + (2 ** d, K), dtype=torch.float64, device=parts.device)
+    out = torch.empty(((P,) if parts.dim() == 3 else ()) + (Q, 2 ** d, 64), dtype=torch.float64, device=parts.device)
     N.call("fgp_spec_basis", int(family), N.ptr(parts), d * n, P, m, int(d), N.ptr(out), N.ptr(work), wbytes,
            N.stream_ptr(parts.device))
     return out
@@ -116,7 +122,7 @@ class FusedMLL(object):
                  gen=None, basis=None):
         """
         family: 0 lattice (FFT) / 1 net (FWHT)
-        basis:  part-product spectra (spec_basis) [2^d, K] shared or [G, 2^d, K]: the spectral fit path
+        basis:  part-product spectra (spec_basis) [Q, 2^d, 64] shared or [G, Q, 2^d, 64]: the spectral fit path
                 (one kernel per iteration, no transform; parts / gen are then not used)
         parts:  [d, n] shared, or [G, d, n] when parts_per_problem; None with `gen` (LatticePartsGen)
         ysq:    [G, n]
@@ -185,7 +191,7 @@ class FusedMLL(object):
             gen.apply(self._nll, n)
         if self.basis is not None:
             self._nll.basis = self.basis.data_ptr()
-            self._nll.basis_stride = (self.basis.shape[-2] * self.basis.shape[-1]) if self.basis.dim() == 3 else 0
+            self._nll.basis_stride = self.basis[0].numel() if self.basis.dim() == 4 else 0
         plen = ctypes.c_int64(0)
         N.call("fgp_nll_partials_len", self._nll, ctypes.byref(plen))
         self.partials = torch.empty((plen.value,), dtype=torch.float64, device=self.device)
@@ -338,8 +344,8 @@ def mll_constant(d_out, n):
 
 def fused_lam(family, parts, raw_scale, raw_lengthscales, raw_noise, G, gen=None, n=None, basis=None):
     """lambda = ft(k1) for G eigen-problems sharing `parts` ([d, n]), with parts of their own
-    ([G, d, n]), with the generator `gen` (size n), or from part-product spectra `basis` ([2^d, K] shared,
-    [G, 2^d, K]), via fgp_nll_lam -> [G, n]."""
+    ([G, d, n]), with the generator `gen` (size n), or from part-product spectra `basis` ([Q, 2^d, 64]
+    shared, [G, Q, 2^d, 64]), via fgp_nll_lam -> [G, n]."""
     parts_stride = 0
     if basis is not None:
         require_device(basis, "fused_lam")
@@ -375,6 +381,6 @@ def fused_lam(family, parts, raw_scale, raw_lengthscales, raw_noise, G, gen=None
     if basis is not None:
         basis = basis.contiguous()
         desc.basis = basis.data_ptr()
-        desc.basis_stride = (basis.shape[-2] * basis.shape[-1]) if basis.dim() == 3 else 0
+        desc.basis_stride = basis[0].numel() if basis.dim() == 4 else 0
     N.call("fgp_nll_lam", desc, N.stream_ptr(dev))
     return out

@@ -25,7 +25,7 @@ import numpy as np
 import torch
 
 from . import ops
-from .fast_gp import AbstractFastGP, _Hyper, _as_size
+from .fast_gp import _IDENTITY_TFS, AbstractFastGP, _Hyper, _as_size
 
 
 def _to_n_tensor(n):
@@ -127,7 +127,7 @@ class MultiTaskFastGP(AbstractFastGP):
         # derivatives (abstract_gp.py:58-72)
         if derivatives is not None or derivatives_coeffs is not None:
             rank_factor_task_kernel = 1
-            tfs_noise_task_kernel = ((lambda x: x), (lambda x: x))
+            tfs_noise_task_kernel = _IDENTITY_TFS
             noise_task_kernel = 0.
         if derivatives is None:
             derivatives = [torch.zeros((1, d), dtype=torch.int64, device=dev) for _ in range(T)]
@@ -633,11 +633,23 @@ class MultiTaskFastGP(AbstractFastGP):
         return numer, denom
 
     def _inv_diag(self):
-        """get_inv_diag (util.py:381-394): diag of K^-1 by solving the identity (O(n^2 log n))."""
-        nsum = sum(self._ns)
-        eye = torch.eye(nsum, device=self.device)
-        kinv = self.gram_matrix_solve(eye)
-        return kinv.diagonal(dim1=-2, dim2=-1)
+        """get_inv_diag (util.py:381-394).  One task: the reference's mean(1 / (sqrt(n) lam)) (:382-385; real
+        part on lattices, as the CV loss takes it).  Several: diag of K^-1 by solving the identity
+        (O(n^2 log n)), its rows laid out [nsum, 1 per parameter-batch dim, nsum] so they broadcast against the
+        hyper-parameter batch instead of pairing with it, then permuted batch-first (:387-393)."""
+        if self.num_tasks == 1:
+            lam = self.get_lam(0, 0)
+            inv = (1 / (lam * math.sqrt(lam.size(-1)))).mean(-1, keepdim=True)
+            return inv.real if inv.is_complex() else inv
+        ns = list(self._ns)
+        nsum = sum(ns)
+        gshape = tuple(self._factor(ns)[4])
+        nb = len(gshape)
+        eye = torch.eye(nsum, device=self.device).reshape((nsum,) + (1,) * nb + (nsum,))
+        kinv = self.gram_matrix_solve(eye)                    # [nsum, *batch, nsum]
+        kinv = kinv.permute(tuple(range(1, kinv.ndim - 1)) + (0, kinv.ndim - 1))
+        idx = torch.arange(nsum, device=self.device)
+        return kinv[..., idx, idx]
 
     def fit(self, loss_metric="MLL", iterations=5000, lr=None, optimizer=None, stop_crit_improvement_threshold=5e-2,
             stop_crit_wait_iterations=10, store_hists=False, store_loss_hist=False, store_scale_hist=False,
@@ -930,6 +942,18 @@ def multitask_class(family_cls):
     """MultiTask<Family>: the family's transforms / point conversion over the multitask machinery
     (one class per family, created once)."""
     if family_cls not in _CLASSES:
-        _CLASSES[family_cls] = type("MultiTask" + family_cls.__name__, (family_cls, MultiTaskFastGP),
-                                    {"__module__": __name__, "__doc__": MultiTaskFastGP.__doc__})
+        name = "MultiTask" + family_cls.__name__
+        cls = type(name, (family_cls, MultiTaskFastGP),
+                   {"__module__": __name__, "__qualname__": name, "__doc__": MultiTaskFastGP.__doc__})
+        _CLASSES[family_cls] = cls
+        globals()[name] = cls      # a module attribute, so pickle / torch.save find the class by name
     return _CLASSES[family_cls]
+
+
+def _bind_family_classes():
+    from .fast_gp import FastGPDigitalNetB2, FastGPLattice
+    for fam in (FastGPLattice, FastGPDigitalNetB2):
+        multitask_class(fam)
+
+
+_bind_family_classes()

@@ -76,9 +76,10 @@ def fftbr_raw(x, stable=True):
     m = log2_exact(n)
     rows, bs = _as_rows(x)
     out = torch.empty(rows.shape, dtype=cdt, device=x.device)
-    if _real_half_length(x, m) and rows.data_ptr() % 16 == 0 and bs % 2 == 0:
+    if stable and _real_half_length(x, m) and rows.data_ptr() % 16 == 0 and bs % 2 == 0:
         # real float64 input, 2^17 <= n <= 2^24: the half-length transform (fgp_fftbr_real, 40n instead
-        # of 56n bytes per row)
+        # of 56n bytes per row; it centres every row / column internally, so only for stable=True --
+        # stable=False keeps qmcpy.fftbr_torch's plain transform)
         work = torch.empty(rows.shape, dtype=cdt, device=x.device)
         N.call("fgp_fftbr_real", N.ptr(rows), bs, N.ptr(out), N.ptr(work), rows.size(0), m, _stream(x))
         return out.reshape(shape)
@@ -107,7 +108,7 @@ def ifftbr_raw(x, stable=True, real_out=False):
     n = shape[-1]
     m = log2_exact(n)
     rows, bs = _as_rows(x)
-    if real_out and not sp and 17 <= m <= 24 and rows_ok_env():
+    if real_out and stable and not sp and 17 <= m <= 24 and rows_ok_env():
         # real part at half length (fgp_ifftbr_real): the Hermitian part through an n/2-point transform
         out = torch.empty(rows.shape, dtype=rdt, device=x.device)
         work = torch.empty(rows.shape, dtype=cdt, device=x.device)
@@ -182,7 +183,7 @@ def inverse_mul(family, x, f, real_out=False, stable=True):
         prod = x * f
         return ifftbr_raw(prod, stable, real_out) if family == LATTICE else fwht_raw(prod, stable)
     f2 = f2.contiguous()
-    if family == LATTICE and real_out and not sp and 17 <= m <= 24 and rows_ok_env():
+    if family == LATTICE and real_out and stable and not sp and 17 <= m <= 24 and rows_ok_env():
         # Re ift(x * f) at half length (fgp_ifftbr_real, the product fused into the column loads)
         out = torch.empty(rows.shape, dtype=torch.float64, device=x.device)
         work = torch.empty(rows.shape, dtype=rows.dtype, device=x.device)

@@ -201,8 +201,8 @@ typedef struct fgp_nll_desc {
    * measured in-process without the dependent-launch gap that HIP events include. */
   uint64_t* stamps;
   /* ABI 11 -- spectral fit path.  basis non-NULL: the part-product spectra of fgp_spec_basis
-   * ([G or 1][2^d][K], K = n/2 + 1 lattice / n net, problem g's at basis + g * basis_stride; stride 0 = one
-   * set shared by all G problems).  Every kernel of this desc then evaluates
+   * ([G or 1][Q][2^d][64], problem g's at basis + g * basis_stride; stride 0 = one set shared by all G
+   * problems).  Every kernel of this desc then evaluates
    *   lambda_g = scale_g sum_S (prod_{j in S} l_gj) Phi_S
    * instead of transforming k1 (parts / parts_gen / work are not read; d <= 6): fgp_nll_fwd / fgp_fit_run
    * run ONE kernel per iteration (stage 0: loss and gradient partials; stages 1, 2 are no-ops), fgp_nll_lam
@@ -218,14 +218,18 @@ int fgp_nll_partials_len(const fgp_nll_desc* desc, int64_t* len);
 
 /* Part-product spectra (ABI 11) for the spectral fit path.  With b_S[i] = prod_{j in S} parts[j, i]
  * (ascending j; b_{} = 1) for every subset S of the d dimensions (bit j of S = dimension j):
- *   basis[p][S][k] = ft(b_S)[k],  k < K:
+ *   Phi_S[k] = ft(b_S)[k],  k < K:
  *   lattice: Re fftbr(b_S) (stable; the lattice b_S is even in the natural index, so the spectrum is real
  *            and even and k = 0 .. n/2 carry it: K = n/2 + 1);  net: fwht(b_S) (stable), K = n.
- * Then for every (scale, l) the eigenvalues are lambda = scale sum_S l^S basis[S] -- ft(k1) of the
+ * Then for every (scale, l) the eigenvalues are lambda = scale sum_S l^S Phi_S -- ft(k1) of the
  * reference's _LamCaches (fastgps/util.py:95-112), k1 = scale prod_j (1 + l_j parts_j) of
  * abstract_fast_gp.py:181-191, by linearity of ft.
  * parts: [P][d][n] float64 (fgp_lattice_parts / fgp_lattice_parts_gen / fgp_net_parts layout; problem
- * stride parts_stride elements); basis: [P][2^d][K] float64; 1 <= d <= 6.
+ * stride parts_stride elements); 1 <= d <= 6.
+ * basis: [P][Q][2^d][64] float64, Q = ceil(K / 64) chunks of 64 frequencies: Phi_S[k] at
+ *   basis[p][k / 64][S][k mod 64]  (zeros past K)
+ * -- the 2^d spectra of 64 consecutive frequencies are one contiguous 2^d x 512-byte run, the unit the fit
+ * kernels stream (a row-per-spectrum layout puts them n/2 apart).
  * work: device scratch of work_bytes >= fgp_spec_basis_work bytes for ONE subset (the subsets are then
  * transformed in chunks; the bytes for all 2^d at once make it one chunk). */
 int fgp_spec_basis(int family, const double* parts, int64_t parts_stride, int64_t P, int log2n, int d, double* basis,

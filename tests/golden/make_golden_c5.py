@@ -1,0 +1,133 @@
+"""Golden vectors for the BENCHED C5 regime (BASELINE config C5: multi-output FastGPLattice, n = 2^18,
+d = 3, 512 outputs, shared hyper-parameters, the default nugget 1e-8), from the REAL reference, and the
+reference's own FFT-backend sensitivity there (VERDICT r02 "Next round" item 1).
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_c5.py
+
+Writes tests/golden/c5_m18_d3_b512.npz (inputs: the point set's generating vector + shift and the data
+seed; outputs: the reference's fit(iterations=3) loss / parameter trajectory, post_mean at 16 test points,
+post_var at 2), tests/golden/c5_m18_d3_b512_f32data.npz (the same on the observations rounded to float32:
+the mixed-precision path's data) and profiles/r03_c5_backend_spread.json: the same run with the reference's qmcpy
+fftbr_torch / ifftbr_torch replaced by numpy's pocketfft (a differentiable wrapper, adjoints by the
+inverse transform) -- the spread a correct implementation of the reference can show at this size and
+nugget.  tests/test_gpu_multioutput.py allows 5x it.
+"""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, HERE)
+from oracle.refshim.load_reference import import_reference  # noqa: E402
+from make_golden import LATTICE_Z, f_ackley  # noqa: E402
+
+M, D, B, ITS, NM, NV = 18, 3, 512, 3, 16, 2
+
+
+def c5_data(x, B, seed=5):
+    """y_b = f_ackley(x) (1 + b / B) + 0.01 randn (CPU generator, seeded): bench.py's C5 shape."""
+    f = f_ackley(x)
+    g = torch.Generator().manual_seed(seed)
+    noise = torch.randn((B, x.shape[0]), generator=g, dtype=torch.float64)
+    b = torch.arange(B, dtype=torch.float64)[:, None]
+    return f[None, :] * (1 + b / B) + 0.01 * noise
+
+
+def _bitrev(n):
+    m = n.bit_length() - 1
+    i = np.arange(n)
+    r = np.zeros(n, dtype=np.int64)
+    for k in range(m):
+        r |= ((i >> k) & 1) << (m - 1 - k)
+    return torch.from_numpy(r)
+
+
+class _NpFFTBR(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        br = _bitrev(x.size(-1))
+        ctx.real = not x.is_complex()
+        return torch.from_numpy(np.fft.fft(x[..., br].detach().numpy(), norm="ortho"))
+
+    @staticmethod
+    def backward(ctx, g):
+        br = _bitrev(g.size(-1))
+        gx = torch.from_numpy(np.fft.ifft(g.detach().numpy(), norm="ortho"))[..., br]
+        return gx.real if ctx.real else gx
+
+
+class _NpIFFTBR(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        br = _bitrev(x.size(-1))
+        ctx.real = not x.is_complex()
+        return torch.from_numpy(np.fft.ifft(x.detach().numpy(), norm="ortho"))[..., br]
+
+    @staticmethod
+    def backward(ctx, g):
+        br = _bitrev(g.size(-1))
+        gx = torch.from_numpy(np.fft.fft(g[..., br].detach().numpy(), norm="ortho"))
+        return gx.real if ctx.real else gx
+
+
+def run(fg, qmcpy, backend, f32_data=False):
+    if backend == "numpy":
+        qmcpy.fftbr_torch, qmcpy.ifftbr_torch = _NpFFTBR.apply, _NpIFFTBR.apply
+    n = 2 ** M
+    shift = np.random.default_rng(7).uniform(size=D)
+    seq = qmcpy.Lattice(D, randomize="SHIFT", generating_vector=LATTICE_Z[:D], shift=shift)
+    gp = fg.FastGPLattice(seq, alpha=2, shape_batch=[B])
+    x = gp.get_x_next(n)
+    y = c5_data(x, B)
+    if f32_data:     # the mixed-precision C5 path's observations (data_dtype=float32), fp64 from there on
+        y = y.float().double()
+    gp.add_y_next(y)
+    data = gp.fit(iterations=ITS, store_hists=True, verbose=0, stop_crit_wait_iterations=ITS + 5)
+    xt = torch.rand((NM, D), generator=torch.Generator().manual_seed(17))
+    pm = gp.post_mean(xt)
+    pv = gp.post_var(xt[:NV])
+    return dict(z=np.array(LATTICE_Z[:D], dtype=np.int64), shift=shift, x_test=xt.numpy(),
+                loss_hist=data["loss_hist"].detach().numpy(),
+                raw_scale=gp.raw_scale.detach().numpy(), raw_lengthscales=gp.raw_lengthscales.detach().numpy(),
+                pmean=pm.detach().numpy(), pvar=pv.detach().numpy(),
+                kxx=float(gp.kernel(xt[:NV], xt[:NV]).detach().abs().max()))
+
+
+def main():
+    torch.set_default_dtype(torch.float64)
+    torch.set_num_threads(os.cpu_count() or 1)
+    fg = import_reference()
+    import qmcpy
+    keep = (qmcpy.fftbr_torch, qmcpy.ifftbr_torch)
+    ref = run(fg, qmcpy, "torch")
+    np.savez_compressed(os.path.join(HERE, "c5_m18_d3_b512.npz"), m=np.array(M), d=np.array(D), B=np.array(B),
+                        its=np.array(ITS), **{k: np.asarray(v) for k, v in ref.items()})
+    r32 = run(fg, qmcpy, "torch", f32_data=True)
+    np.savez_compressed(os.path.join(HERE, "c5_m18_d3_b512_f32data.npz"), m=np.array(M), d=np.array(D),
+                        B=np.array(B), its=np.array(ITS), **{k: np.asarray(v) for k, v in r32.items()})
+    alt = run(fg, qmcpy, "numpy")
+    qmcpy.fftbr_torch, qmcpy.ifftbr_torch = keep
+
+    def rel(a, b):
+        return float(np.max(np.abs(np.asarray(a) - np.asarray(b))) / np.max(np.abs(np.asarray(b))))
+    spread = {"config": "C5 lattice n=2^%d d=%d x %d outputs, nugget 1e-8, fit(iterations=%d), post_mean N=%d, "
+                        "post_var N=%d" % (M, D, B, ITS, NM, NV),
+              "what": "the REAL reference (tests/golden/make_golden_c5.py) with qmcpy.fftbr_torch/ifftbr_torch "
+                      "(torch.fft) vs numpy pocketfft",
+              "loss_hist_rel": rel(alt["loss_hist"], ref["loss_hist"]),
+              "raw_lengthscales_abs": float(np.max(np.abs(alt["raw_lengthscales"] - ref["raw_lengthscales"]))),
+              "raw_scale_abs": float(np.max(np.abs(alt["raw_scale"] - ref["raw_scale"]))),
+              "pmean_rel": rel(alt["pmean"], ref["pmean"]),
+              "pvar_abs_over_kxx": float(np.max(np.abs(alt["pvar"] - ref["pvar"])) / ref["kxx"])}
+    with open(os.path.join(ROOT, "profiles", "r03_c5_backend_spread.json"), "w") as f:
+        json.dump(spread, f, indent=1)
+    print(json.dumps(spread, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -31,6 +31,53 @@ def _data(x, B):
     return torch.stack([f * (1 + b / B) + 0.01 * torch.randn(f.shape, generator=g) for b in range(B)])
 
 
+def _c5_data(x, B, seed=5):
+    """bench.py's / tests/golden/make_golden_c5.py's C5 observations: f_ackley(x) (1 + b / B) + 0.01 randn."""
+    g = torch.Generator().manual_seed(seed)
+    noise = torch.randn((B, x.shape[0]), generator=g, dtype=torch.float64)
+    b = torch.arange(B, dtype=torch.float64)[:, None]
+    return O.f_ackley(x)[None, :] * (1 + b / B) + 0.01 * noise
+
+
+# Tolerances of the benched C5 regime (2^18 x 512 outputs, nugget 1e-8) = 5x the REAL reference's own
+# spread between its torch.fft and numpy-pocketfft backends at that configuration
+# (tests/golden/make_golden_c5.py -> profiles/r03_c5_backend_spread.json: loss history 4.9e-7 relative,
+# post_mean 1.08e-7 relative, post_var 1e-15 K(x,x), fitted parameters identical).
+C5_TOL = dict(loss=2.5e-6, pmean=5.4e-7, pvar_kxx=1e-8, params=1e-10)
+
+
+@pytest.mark.parametrize("mixed", [False, True])
+def test_benched_c5_regime_matches_reference(mixed):
+    """The C5 configuration bench.py times: n = 2^18, d = 3, 512 outputs sharing the default hyper-parameters,
+    the default nugget 1e-8, fit(iterations=3) (early stopping off), post_mean at 16 and post_var at 2 test
+    points -- against the REAL reference's results on the same points and data (tests/golden/
+    c5_m18_d3_b512*.npz).  mixed: float32 observations (complex64 ytilde for the MLL's Y, fp64 from there)
+    against the reference on the same float32-rounded data; its loss tolerance adds 1e-6 for the complex64
+    ytilde's rounding of Y (~1e-7 relative per frequency, test_mixed_precision_multi_output_matches_oracle)."""
+    import numpy as np
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden",
+                             "c5_m18_d3_b512%s.npz" % ("_f32data" if mixed else "")))
+    m, d, B, its = int(g["m"]), int(g["d"]), int(g["B"]), int(g["its"])
+    seq = F.Lattice(d, randomize="SHIFT", generating_vector=g["z"], shift=g["shift"])
+    gp = F.FastGPLattice(seq, alpha=2, shape_batch=[B], device=DEV,
+                         data_dtype=torch.float32 if mixed else torch.float64)
+    x = gp.get_x_next(2 ** m).cpu()
+    y = _c5_data(x, B)
+    gp.add_y_next((y.float() if mixed else y).to(DEV))
+    data = gp.fit(iterations=its, store_loss_hist=True, verbose=0, stop_crit_wait_iterations=its + 5)
+    lh = data["loss_hist"]
+    olh = torch.from_numpy(g["loss_hist"])
+    assert rel_err(lh, olh) <= C5_TOL["loss"] + (1e-6 if mixed else 0.0)
+    assert float((gp.raw_lengthscales.detach().cpu() - torch.from_numpy(g["raw_lengthscales"])).abs().max()) <= C5_TOL["params"]
+    assert float((gp.raw_scale.detach().cpu() - torch.from_numpy(g["raw_scale"])).abs().max()) <= C5_TOL["params"]
+    xt = torch.from_numpy(g["x_test"])
+    pm = gp.post_mean(xt.to(DEV)).cpu()
+    assert pm.shape == tuple(g["pmean"].shape)
+    assert rel_err(pm, g["pmean"]) <= C5_TOL["pmean"]
+    pv = gp.post_var(xt[:g["pvar"].shape[-1]].to(DEV)).cpu()
+    assert float((pv - torch.from_numpy(g["pvar"])).abs().max()) <= C5_TOL["pvar_kxx"] * float(g["kxx"])
+
+
 @pytest.mark.parametrize("per_output", [False, True])
 def test_multi_output_fit_and_predict_match_oracle(per_output):
     m, d, B, its = 18, 3, 16, 3
@@ -116,7 +163,7 @@ def _free_port():
     return p
 
 
-def _sharded_worker(rank, world, port, B, m, d, q):
+def _sharded_worker(rank, world, port, B, m, d, its, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch.distributed as dist
@@ -128,20 +175,23 @@ def _sharded_worker(rank, world, port, B, m, d, q):
         a, b = output_shard(B, rank, world)
         gp = F.FastGPLattice(F.Lattice(d, seed=7), shape_batch=[b - a], device="cuda:0")
         x = gp.get_x_next(n).cpu()
-        gp.add_y_next(_data(x, B)[a:b].to("cuda:0"))
-        data = fit_sharded(gp, B, iterations=6, store_loss_hist=True, stop_crit_wait_iterations=10)
+        gp.add_y_next(_c5_data(x, B)[a:b].to("cuda:0"))
+        data = fit_sharded(gp, B, iterations=its, store_loss_hist=True, stop_crit_wait_iterations=10)
         q.put((rank, data["iterations"], data["loss_hist"].clone(), gp.raw_lengthscales.detach().cpu().clone(),
                gp.raw_scale.detach().cpu().clone()))
     finally:
         dist.destroy_process_group()
 
 
-def test_fit_sharded_two_processes_equals_unsharded():
-    B, m, d, world = 10, 16, 3, 2
+@pytest.mark.parametrize("B,m,its", [(10, 16, 6), (512, 18, 3)])
+def test_fit_sharded_two_processes_equals_unsharded(B, m, its):
+    """distributed.fit_sharded over two processes (gloo, both on cuda:0), outputs split B/2 + B/2 -- also
+    at the benched C5 size (2^18 x 512: 256 + 256) -- equals the unsharded fit on one process."""
+    d, world = 3, 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, B, m, d, q)) for r in range(world)]
+    procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, B, m, d, its, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=100) for _ in range(world)], key=lambda r: r[0])
@@ -150,10 +200,27 @@ def test_fit_sharded_two_processes_equals_unsharded():
         assert p.exitcode == 0
     full = F.FastGPLattice(F.Lattice(d, seed=7), shape_batch=[B], device=DEV)
     x = full.get_x_next(2 ** m).cpu()
-    full.add_y_next(_data(x, B).to(DEV))
-    ref = full.fit(iterations=6, verbose=0, store_loss_hist=True, stop_crit_wait_iterations=10)
+    full.add_y_next(_c5_data(x, B).to(DEV))
+    ref = full.fit(iterations=its, verbose=0, store_loss_hist=True, stop_crit_wait_iterations=10)
     for _, its, lh, ls, sc in res:
         assert its == ref["iterations"]
         assert rel_err(lh, ref["loss_hist"]) < 1e-10           # Y summed in another order
         assert rel_err(ls, full.raw_lengthscales) < 1e-10
     assert torch.equal(res[0][3], res[1][3]) and torch.equal(res[0][4], res[1][4])   # identical on every rank
+
+
+def test_fp32_data_coefficients_same_with_and_without_graph():
+    """data_dtype=float32: the coefficients come from an fp64 transform of the observations in grad mode
+    too (it ran the fp32 transform there, O(1) relative error), so both modes agree to the
+    coefficient tolerance of test_gpu_gp.py (1e-6: K^-1 y at cond(K) ~ n / noise; the two modes form
+    lambda by different kernels, autograd ft(k1) vs the fused path)."""
+    d, n = 2, 2 ** 12
+    gp = F.FastGPLattice(F.Lattice(d, seed=7), shape_batch=[3], device=DEV, data_dtype=torch.float32)
+    x = gp.get_x_next(n)
+    y = torch.stack([O.f_ackley(x.cpu()) * (1 + b) for b in range(3)]).to(DEV).float()
+    gp.add_y_next(y)
+    with torch.no_grad():
+        c0 = gp.coeffs.clone()
+    gp._cache = {}
+    c1 = gp.coeffs.detach()
+    assert rel_err(c1, c0) <= 1e-6

@@ -214,3 +214,52 @@ def test_multitask_default_construction_and_shapes():
     xn = gp.get_x_next(n_new)
     gp.add_y_next([fs[i](xn[i]) for i in range(3)])
     assert torch.allclose(gp.post_var(x), pv_future)
+
+
+def test_multitask_inv_diag_broadcasts_against_the_parameter_batch():
+    """get_inv_diag (util.py:381-394) with a hyper-parameter batch: the identity's rows are laid out
+    [nsum, 1, nsum] so they broadcast against the batch (util.py:389-393); each batch element's diagonal
+    equals the unbatched GP's at that element's parameters (the bare eye paired identity row
+    b with parameter batch b)."""
+    g = load_golden("mt_net_d2_a2_T3")
+    T = len(g["ns"])
+    scales = [0.7, 1.9]
+
+    def make(batch):
+        extra = dict(shape_batch=[2], shape_scale=[2, 1]) if batch else {}
+        seqs = [F.DigitalNetB2(int(g["d"]), randomize="DS", generating_matrices=g["C"].astype(np.uint64), t=int(g["t"]),
+                               shift=g["shifts"][l].astype(np.uint64)) for l in range(T)]
+        gp = F.FastGPDigitalNetB2(seqs, num_tasks=T, alpha=int(g["alpha"]), device=DEV, **extra)
+        gp.get_x_next(n=[int(v) for v in g["ns"]])
+        ys = [torch.from_numpy(g["y_%d" % l]).to(DEV) for l in range(T)]
+        gp.add_y_next([y.expand(2, -1).contiguous() for y in ys] if batch else ys)
+        return gp
+
+    gb = make(True)
+    with torch.no_grad():
+        gb.raw_scale.copy_(torch.log(torch.tensor(scales, device=DEV)).reshape(2, 1))
+        db = gb._inv_diag()
+    assert tuple(db.shape) == (2, sum(int(v) for v in g["ns"]))
+    for b, sc in enumerate(scales):
+        g1 = make(False)
+        with torch.no_grad():
+            g1.raw_scale.fill_(float(np.log(sc)))
+            d1 = g1._inv_diag()
+        assert rel_err(db[b], d1) < 1e-12
+    d2 = make(True).fit(loss_metric="CV", iterations=2, verbose=0, store_loss_hist=True)
+    assert torch.isfinite(d2["loss_hist"]).all()
+
+
+def test_multitask_gp_pickles():
+    """The generated multitask classes are module attributes: pickle / torch.save round-trip a whole GP."""
+    import io
+    gp = F.FastGPLattice(2, seed_for_seq=7, num_tasks=2, device=DEV)
+    xs = gp.get_x_next(n=[2 ** 5, 2 ** 4])
+    gp.add_y_next([x.sum(1) for x in xs])
+    buf = io.BytesIO()
+    torch.save(gp, buf)
+    buf.seek(0)
+    gp2 = torch.load(buf, weights_only=False)   # our own object (not a reference file)
+    assert type(gp2) is type(gp)
+    x = torch.rand((8, 2), device=DEV)
+    assert torch.equal(gp2.post_mean(x), gp.post_mean(x))

@@ -20,7 +20,7 @@ import pytest
 import torch
 
 import fastgaussianprocesses_amd as F
-from fastgaussianprocesses_amd.fit_engine import fused_lam, mll_constant, spec_basis, spectral_wanted
+from fastgaussianprocesses_amd.fit_engine import fused_lam, mll_constant, spec_basis, spec_dense, spectral_wanted
 from oracle import fgp_oracle as O
 from tests.gpu_fixtures import DEV, rel_err
 
@@ -54,11 +54,13 @@ def test_basis_matches_oracle_transforms(family, m, d):
     n = 2 ** m
     fam = gp._FAMILY
     parts = gp._k1parts(n)
-    basis = spec_basis(fam, parts, n).cpu()
+    raw = spec_basis(fam, parts, n).cpu()
     K = n // 2 + 1 if family == "lattice" else n
-    KS = n // 2 + 16 if family == "lattice" else n
-    assert basis.shape == (2 ** d, KS)
-    assert not basis[:, K:].any()
+    Q = (K + 63) // 64
+    assert raw.shape == (Q, 2 ** d, 64)
+    full = raw.movedim(0, 1).reshape(2 ** d, Q * 64)
+    assert not full[:, K:].any()                      # zero padding past K
+    basis = spec_dense(raw, fam, n)
     pc = parts.cpu()
     tr = O.fftbr if family == "lattice" else O.fwht
     for S in range(2 ** d):
@@ -138,7 +140,7 @@ def test_spectral_batch_shares_one_basis_and_equals_individual_fits(monkeypatch)
     b = F.GPBatch(gps)
     b.set_data(torch.stack([gp._y[0] for gp in gps]))
     basis = b.basis()
-    assert basis is not None and basis.shape == (2 ** d, 2 ** (m - 1) + 16)
+    assert basis is not None and basis.shape == ((2 ** (m - 1) + 1 + 63) // 64, 2 ** d, 64)
     data = b.fit(iterations=8, stop_crit_wait_iterations=20, store_loss_hist=True)
     ind = make()
     for p, gp in enumerate(ind):
