@@ -46,7 +46,7 @@ class NllDesc(ctypes.Structure):
         ("parts_gen", _c_int), ("gen_order", _c_int * 8), ("gen_coef", _c_dbl * 8), ("gen_z", _c_i64 * 8),
         ("gen_shift", _c_vp), ("gen_shift_stride", _c_i64),
         ("stamps", _c_vp),
-        ("basis", _c_vp), ("basis_stride", _c_i64),
+        ("basis", _c_vp), ("basis_stride", _c_i64), ("ysq_chunked", _c_int),
     ]
 
 

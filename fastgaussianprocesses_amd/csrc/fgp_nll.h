@@ -40,6 +40,8 @@ struct Nll {
   int spec_kpl, spec_ppw, spec_pg;   // frequencies per lane and block, problems per wave, problem groups
   int spec_tile, spec_pgp, spec_ck;  // LDS-tiled kernel: problem-group slots, frequencies per chunk
   int64_t spec_kw;                   // ... and per workgroup
+  int spec_exp_nocompute;            // experiment (FGP_SPEC_EXP_NOCOMPUTE=1): stream the chunks, skip the terms
+  int ysq_chunked;                   // ysq in the chunked layout [k / 64][G][64] (spectral path)
 };
 
 // Device-clock kernel timing (fgp_nll_desc.stamps; off when NULL -- a uniform branch on a kernel
@@ -544,15 +546,20 @@ int launch_re_bwd_fused(const Nll& a, const FitFuse& fz, const Tables* tb, hipSt
 constexpr int kSpecMaxD = 6;
 constexpr int kSpecBlocks = 512;
 #ifndef FGP_SPEC_RING
-#define FGP_SPEC_RING 4
+#define FGP_SPEC_RING 2
 #endif
 constexpr int kSpecRing = FGP_SPEC_RING;         // LDS ring depth of the spectral tile kernel (chunks)
-constexpr int kSpecLdsMax = 80 * 1024;           // its dynamic LDS per workgroup, at most (2 per CU)
+#ifndef FGP_SPEC_LDS_KB
+#define FGP_SPEC_LDS_KB 80
+#endif
+constexpr int kSpecLdsMax = FGP_SPEC_LDS_KB * 1024;   // its dynamic LDS per workgroup, at most (80: 2 per CU)
 void spec_geometry(Nll& a);                        // nb and the spec_* fields of a spectral desc
 int64_t spec_chunks(bool net, int log2n);          // 64-frequency chunks of the spectra (fgp_spec_basis layout)
 // one fit iteration (loss + gradient partials); with fz (tile kernel only) also the reduction + Rprop
 int launch_spec_iter(const Nll& a, hipStream_t st, const FitFuse* fz = nullptr);
 int launch_spec_reduce_step(const Nll& a, const Fit& f, int iter, int do_update, hipStream_t st);
+// the fused spectral step's counters: doubles offset into partials and how many 32-bit counters
+int spec_counters_offset(const Nll& a, int64_t* off, int* count);
 int launch_spec_lam(const Nll& a, hipStream_t st);    // lambda of the current parameters into grad_lam
 // their row length log2 (FGP_RE_P2, default 10) for a transform of 2^log2n, or -1 when no split fits
 int re_row_log2(int log2n);

@@ -1176,6 +1176,8 @@ static int to_nll(const fgp_nll_desc* d, Nll& a) {
   // spectral path: the eigenvalues from the part-product spectra, one kernel per iteration
   a.basis = d->basis;
   a.basis_stride = d->basis_stride;
+  a.ysq_chunked = d->ysq_chunked;
+  if (a.ysq_chunked && !d->basis) return set_error(kErrInvalid, "ysq_chunked needs the spectral path (basis)");
   a.spec = d->basis != nullptr;
   a.spec_net = d->family == FGP_FAMILY_NET;
   a.spec_K = a.spec_KS = a.spec_main = a.spec_kw = 0;
@@ -1504,6 +1506,12 @@ int fgp_nll_partials_len(const fgp_nll_desc* desc, int64_t* len) {
   if (!len) return set_error(kErrInvalid, "fgp_nll_partials_len: null len");
   const int64_t nb_doc = std::max<int64_t>(1, ((int64_t)1 << a.log2n) >> 12);
   *len = (int64_t)a.G * a.nq * (std::max<int64_t>(a.nb, nb_doc) + 1) + a.G;
+  if (a.spec) {   // level-1 + level-2 partials + counters of the fused spectral step (fgp_spectral.hip)
+    int64_t off;
+    int cnt;
+    spec_counters_offset(a, &off, &cnt);
+    *len = std::max<int64_t>(*len, off + cnt + 1);
+  }
   return kOk;
 }
 
@@ -1616,10 +1624,17 @@ int fgp_fit_run(const fgp_nll_desc* nll, const fgp_fit_desc* fit, int iter0, int
   const Tables* tb = nullptr;
   if (fuse) {
     fz.f = f;
-    fz.counters = reinterpret_cast<unsigned*>(a.partials + (int64_t)a.G * a.nq * (a.nb + 1));
-    if (!fuse_spec) tb = get_tables(st);
-    if (!fuse_spec && !tb) return set_error(kErrHip, "twiddle table initialisation failed");
-    if (hipMemsetAsync(fz.counters, 0, sizeof(unsigned) * (size_t)a.G, st) != hipSuccess)
+    int ncnt = a.G;
+    if (fuse_spec) {
+      int64_t off;
+      spec_counters_offset(a, &off, &ncnt);
+      fz.counters = reinterpret_cast<unsigned*>(a.partials + off);
+    } else {
+      fz.counters = reinterpret_cast<unsigned*>(a.partials + (int64_t)a.G * a.nq * (a.nb + 1));
+      tb = get_tables(st);
+      if (!tb) return set_error(kErrHip, "twiddle table initialisation failed");
+    }
+    if (hipMemsetAsync(fz.counters, 0, sizeof(unsigned) * (size_t)ncnt, st) != hipSuccess)
       return set_error(kErrHip, "fgp_fit_run: counter reset failed");
   }
   for (int it = 0; it < iters; ++it) {

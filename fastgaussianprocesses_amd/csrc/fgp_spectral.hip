@@ -55,6 +55,12 @@ __device__ __forceinline__ int64_t spec_at(int64_t k, int s) {
   return ((k >> 6) * NS + s) * 64 + (k & 63);
 }
 
+// Y of problem g at frequency k: rows [G][ysq_stride], or (ysq_chunked, the spectral path's copy) the
+// chunked layout [k / 64][G][64] -- a chunk's Y of every problem then follows as one contiguous run
+__device__ __forceinline__ int64_t ysq_at(const Nll& a, int g, int64_t k) {
+  return a.ysq_chunked ? ((k >> 6) * a.G + g) * 64 + (k & 63) : (int64_t)g * a.ysq_stride + k;
+}
+
 // Per-problem accumulators of one lane (its frequencies of one block): UNWEIGHTED sums over them --
 // the lattice's fold weights (2 for 0 < k < n/2, 1 at k = 0 and n/2) are applied once per block
 // (spec_block_partials), not per frequency.
@@ -130,7 +136,6 @@ __device__ __forceinline__ void spec_block_partials(const Nll& a, const Hyp& h, 
   for (int q = 2; q < NV; ++q) v[q] *= 0.5 * wlin;
   if (!NET && lane == 0 && (blk == 0 || blk == a.nb - 1)) {
     const double* phib = a.basis + (int64_t)g * a.basis_stride;
-    const double* ys = a.ysq + (int64_t)g * a.ysq_stride;
 #pragma unroll
     for (int side = 0; side < 2; ++side) {
       const bool here = side == 0 ? blk == 0 : blk == a.nb - 1;
@@ -140,7 +145,7 @@ __device__ __forceinline__ void spec_block_partials(const Nll& a, const Hyp& h, 
 #pragma unroll
       for (int s = 0; s < NS; ++s) phi[s] = phib[spec_at<NS>(k, s)];
       SpecAcc<D> t;
-      spec_terms<D>(phi, h, rootn, wl, ys[k], t);
+      spec_terms<D>(phi, h, rootn, wl, a.ysq[ysq_at(a, g, k)], t);
       double tv[NV];
       spec_values<D>(t, tv);
       const double sg = side == 0 ? -1.0 : 1.0;   // k = 0: weight 2 -> 1; k = n/2: weight 1
@@ -194,9 +199,6 @@ __global__ __launch_bounds__(kWG) void k_spec_iter(Nll a) {
     const int64_t main = a.spec_main;
     const double rootn = sqrt((double)((int64_t)1 << a.log2n)), wl = a.logdet_weight;
     const double* phib = a.basis + (int64_t)g0 * a.basis_stride;   // PPW = 2: shared spectra (stride 0)
-    const double* ys[PPW];
-#pragma unroll
-    for (int p = 0; p < PPW; ++p) ys[p] = a.ysq + (int64_t)(on[p] ? g0 + p : g0) * a.ysq_stride;
     SpecAcc<D> acc[PPW];
     const int64_t kbase = (int64_t)kb * 64 * a.spec_kpl;
     for (int i = 0; i < a.spec_kpl; ++i) {
@@ -207,7 +209,7 @@ __global__ __launch_bounds__(kWG) void k_spec_iter(Nll a) {
       for (int s = 0; s < NS; ++s) phi[s] = phib[spec_at<NS>(k, s)];
       double Y[PPW];
 #pragma unroll
-      for (int p = 0; p < PPW; ++p) Y[p] = ys[p][k];
+      for (int p = 0; p < PPW; ++p) Y[p] = a.ysq[ysq_at(a, on[p] ? g0 + p : g0, k)];
 #pragma unroll
       for (int p = 0; p < PPW; ++p)
         if (on[p]) spec_terms<D>(phi, h[p], rootn, wl, Y[p], acc[p]);
@@ -219,83 +221,84 @@ __global__ __launch_bounds__(kWG) void k_spec_iter(Nll a) {
   stamp_end(a);
 }
 
-// Per-problem reduction + loss history + Rprop of problem g by ONE wave: the reduce_step_wg semantics
-// (fgp_nll.h: torch.optim.Rprop single-tensor, loss = 1/2 (norm + w logdet + const), histories) with the
-// blocks summed lane-strided then by shuffles -- the one order used by both the stage launches
-// (k_spec_reduce_step) and the fused last-workgroup step of k_spec_tile, so the two are bit-identical.
-// SC1: the partials of the same launch are read with sc1 loads (the producers stored them sc1).
-template <bool SC1, int D>
-__device__ __forceinline__ void reduce_step_wave(const Nll& a, const Fit& f, int g, int iter, int do_update) {
-  constexpr int NQ = 4 + D, UB = 4;   // quantities; blocks per lane whose loads are issued together
-  const int lane = threadIdx.x & 63;
+// ---------------------------------------------------------------- reduction + Rprop of the spectral path
+// The nb per-block partials of each (problem, quantity) are summed in two levels, in ONE order used by
+// both the stage launches (k_spec_reduce_step) and the fused step at the end of k_spec_tile, so the two
+// are bit-identical: level 1 sums the blocks of each group of kSpecGroup consecutive blocks (ascending),
+// level 2 sums the ng = ceil(nb / kSpecGroup) group sums (ascending).  One thread per (problem,
+// quantity): a group's block loads are issued together (one round trip, not a dependent chain).
+constexpr int kSpecGroup = 32;
+
+__device__ __forceinline__ int spec_groups(const Nll& a) { return (a.nb + kSpecGroup - 1) / kSpecGroup; }
+
+// level-2 partials [G][nq][ng] after the level-1 ones, then the fused step's counters (ng + 1)
+__device__ __forceinline__ double* part2_ptr(const Nll& a, int g, int q, int grp) {
+  return a.partials + (int64_t)a.G * a.nq * a.nb + ((int64_t)g * a.nq + q) * spec_groups(a) + grp;
+}
+
+template <bool SC1>
+__device__ __forceinline__ double ld_part(const double* p) {
+  return SC1 ? __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *p;
+}
+
+// level 1: sum of problem g's quantity q over the blocks of group grp
+template <bool SC1>
+__device__ __forceinline__ double spec_group_sum(const Nll& a, int g, int q, int grp) {
+  const int b0 = grp * kSpecGroup, nbg = min(kSpecGroup, a.nb - b0);
+  const double* pp = part_ptr(a, g, q, b0);
+  double t[kSpecGroup];
+#pragma unroll
+  for (int b = 0; b < kSpecGroup; ++b) t[b] = ld_part<SC1>(pp + (b < nbg ? b : 0));
+  double s = 0.0;
+#pragma unroll
+  for (int b = 0; b < kSpecGroup; ++b) s += b < nbg ? t[b] : 0.0;
+  return s;
+}
+
+// Loss history + Rprop of the problems g0 .. g0 + cnt - 1 (cnt <= kWG / 16) from their reduced totals
+// tot[(g - g0) * nq + q] (LDS): thread 16 i + k owns parameter slot k (0 scale, 1 .. dl lengthscales,
+// dl + 1 noise) of problem g0 + i -- the reduce_step_wg semantics (fgp_nll.h: torch.optim.Rprop
+// single-tensor, loss = 1/2 (norm + w logdet + const), histories).
+template <int D>
+__device__ __forceinline__ void spec_finish(const Nll& a, const Fit& f, const double* tot, int g0, int cnt, int iter,
+                                            int do_update) {
+  const int i = threadIdx.x >> 4, k = threadIdx.x & 15;
+  if (i >= cnt) return;
+  const int g = g0 + i;
+  const double* v = tot + i * a.nq;
   const int dl = a.ls_pd ? a.d : 1;
-  int p = 0, rg = 0;
-  if (lane == 0) {
-    p = a.scale_off + (a.scale_pp ? g : 0);
-    rg = f.scale_rg;
-  } else if (lane <= dl) {
-    p = a.ls_off + (a.ls_pp ? g : 0) * dl + (lane - 1);
-    rg = f.ls_rg;
-  } else {
-    p = a.noise_off + (a.noise_pp ? g : 0);
-    rg = f.noise_rg;
-  }
-  const bool owner = lane < 2 + dl;
-  double raw_p = 0.0, prev_p = 0.0, step_p = 0.0;
-  if (owner) {
-    raw_p = f.raw[p];
-    prev_p = f.prev[p];
-    step_p = f.step[p];
-  }
-  double v[NQ];
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) v[q] = 0.0;
-  // lane-strided blocks in ascending order, UB blocks' loads in flight at once (a dependent chain of
-  // round trips otherwise); out-of-range blocks read block 0 and add nothing
-  for (int b0 = lane; b0 < a.nb; b0 += 64 * UB) {
-    double t[UB][NQ];
-#pragma unroll
-    for (int u = 0; u < UB; ++u) {
-      const int b = b0 + 64 * u;
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        double* pp = part_ptr(a, g, q, b < a.nb ? b : 0);
-        t[u][q] = SC1 ? __hip_atomic_load(pp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *pp;
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < UB; ++u)
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) v[q] += (b0 + 64 * u < a.nb) ? t[u][q] : 0.0;
-  }
-#pragma unroll
-  for (int q = 0; q < NQ; ++q)
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v[q] += __shfl_xor(v[q], o, 64);
-  if (lane == 0) {
+  if (k == 0) {
     const double term2 = a.logdet_weight * v[1];
     double* lh = f.loss_hist + ((int64_t)iter * (f.hist_stride ? f.hist_stride : a.G) + f.hist_offset + g) * 3;
     lh[0] = 0.5 * (v[0] + term2 + f.mll_const);
     lh[1] = v[0];
     lh[2] = term2;
   }
-  if (!owner) return;
+  if (k >= 2 + dl) return;
+  int p, rg;
   double gp;
-  if (lane == 0) {
+  if (k == 0) {
+    p = a.scale_off + (a.scale_pp ? g : 0);
+    rg = f.scale_rg;
     gp = v[3];
-  } else if (lane <= dl) {
+  } else if (k <= dl) {
+    p = a.ls_off + (a.ls_pp ? g : 0) * dl + (k - 1);
+    rg = f.ls_rg;
+    gp = 0.0;
     if (a.ls_pd) {
-      gp = 0.0;
 #pragma unroll
-      for (int j = 0; j < D; ++j) gp = (j == lane - 1) ? v[4 + j] : gp;
+      for (int j = 0; j < D; ++j) gp = (j == k - 1) ? v[4 + j] : gp;
     } else {
-      gp = 0.0;
 #pragma unroll
       for (int j = 0; j < D; ++j) gp += v[4 + j];
     }
   } else {
-    gp = exp(raw_p) * v[2];
+    p = a.noise_off + (a.noise_pp ? g : 0);
+    rg = f.noise_rg;
+    gp = 0.0;
   }
+  const double raw_p = f.raw[p], prev_p = f.prev[p], step_p = f.step[p];
+  if (k == dl + 1) gp = exp(raw_p) * v[2];
   f.raw_hist[(int64_t)iter * f.n_params + p] = raw_p;
   f.grad_out[p] = gp;
   if (!(do_update && rg)) return;
@@ -310,11 +313,27 @@ __device__ __forceinline__ void reduce_step_wave(const Nll& a, const Fit& f, int
 }
 
 // The per-problem step of the spectral path as its own launch (fgp_fit_step, stage-by-stage fits):
-// wave w of workgroup b reduces problem 4 b + w.
+// workgroup b takes problems 16 b .. 16 b + 15, both levels per (problem, quantity) thread.
 template <int D>
 __global__ __launch_bounds__(kWG) void k_spec_reduce_step(Nll a, Fit f, int iter, int do_update) {
-  const int g = (int)blockIdx.x * (kWG / 64) + (int)(threadIdx.x >> 6);
-  if (g < a.G) reduce_step_wave<false, D>(a, f, g, iter, do_update);
+  constexpr int NQ = 4 + D, MAXG = kSpecBlocks / kSpecGroup;
+  __shared__ double gs[16 * NQ * MAXG];   // level-1 sums [pair][group]
+  __shared__ double tot[16 * NQ];
+  const int g0 = (int)blockIdx.x * 16, cnt = min(16, a.G - g0), ng = spec_groups(a);
+  // level 1: every (problem, quantity, group) triple by its own thread (the groups' loads in parallel)
+  for (int t = threadIdx.x; t < cnt * NQ * ng; t += kWG) {
+    const int pair = t / ng, grp = t % ng;
+    gs[pair * MAXG + grp] = spec_group_sum<false>(a, g0 + pair / NQ, pair % NQ, grp);
+  }
+  __syncthreads();
+  // level 2: ascending over the groups, as the fused step
+  if ((int)threadIdx.x < cnt * NQ) {
+    double s = 0.0;
+    for (int grp = 0; grp < ng; ++grp) s += gs[threadIdx.x * MAXG + grp];
+    tot[threadIdx.x] = s;
+  }
+  __syncthreads();
+  spec_finish<D>(a, f, tot, g0, cnt, iter, do_update);
 }
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -405,8 +424,8 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
     const int i = (jj < ninst ? jj : 0) * 64 + lane;
     const int sg = i / segp, rem = i - sg * segp, r = rem >> 5, col = rem & 31;
     const int64_t k = wg_base + sg * B;             // the segment's first frequency in chunk 0
-    src0[t] = (r < NS ? a.basis + spec_at<NS>(k, r) : a.ysq + (int64_t)(r - NS) * a.ysq_stride + k) + 2 * col;
-    step[t] = r < NS ? NS * 64 : 64;
+    src0[t] = (r < NS ? a.basis + spec_at<NS>(k, r) : a.ysq + ysq_at(a, r - NS, k)) + 2 * col;
+    step[t] = r < NS ? NS * 64 : (a.ysq_chunked ? (int64_t)G * 64 : 64);
   }
   auto issue = [&](int c, double* buf) {
 #pragma unroll
@@ -419,8 +438,8 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
   };
   SpecAcc<D> acc[PPW];
   const int nc = a.spec_kpl;
-  const int wofs = bw * rows * 64 + lane;           // this lane's spectra in a buffer: wofs + 64 s
-  const int yofs = wofs + (NS + g0) * 64;           // ... its problems' Y: yofs + 64 p
+  const unsigned wofs = (unsigned)(bw * rows * 64 + lane);   // this lane's spectra in a buffer: wofs + 64 s
+  const unsigned yofs = wofs + (unsigned)(NS + g0) * 64u;     // ... its problems' Y: yofs + 64 p
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // only the chunk loads below are counted
 #pragma unroll
   for (int c = 0; c < RING - 1; ++c)
@@ -430,14 +449,16 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
     wait_vmcnt(cnt_w * min(RING - 2, nc - 1 - c));
     barrier_keep_vm();                              // ... every wave's; every wave done with chunk c - 1
     if (c + RING - 1 < nc) issue(c + RING - 1, lds + ((c + RING - 1) % RING) * tile);
-    const double* buf = lds + (c % RING) * tile;
-    if (active) {
+    const double* buf = lds + (unsigned)(c % RING) * (unsigned)tile;
+    if (active && !a.spec_exp_nocompute) {
+      const double* wb = buf + wofs;
       double phi[NS];
 #pragma unroll
-      for (int s = 0; s < NS; ++s) phi[s] = buf[wofs + 64 * s];
+      for (int s = 0; s < NS; ++s) phi[s] = wb[64u * s];
+      const double* yb = buf + yofs;
 #pragma unroll
       for (int p = 0; p < PPW; ++p)
-        if (on[p]) spec_terms<D>(phi, h[p], rootn, wl, buf[yofs + 64 * p], acc[p]);
+        if (on[p]) spec_terms<D>(phi, h[p], rootn, wl, yb[64u * p], acc[p]);
     }
   }
   // the block's partials (k_spec_iter's values; sc1 when handed to the last workgroup)
@@ -445,18 +466,47 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
   for (int p = 0; p < PPW; ++p)
     if (on[p] && active) spec_block_partials<D, NET>(a, h[p], g0 + p, blk, rootn, wl, acc[p], fz.counters != nullptr);
   if (fz.counters) {
-    // hand-off: every storing lane's sc1 stores retired (vmcnt) before the workgroup's arrival
+    // Fused step, two hand-offs (MI355X_MICROARCH.md hand-off row 1: sc1 stores retired by every storing
+    // wave, then ONE lane's agent-scope add; the waiter reads with sc1 loads after a barrier):
+    //   1. the last workgroup of each group of kSpecGroup blocks sums the group (level 1, sc1 store);
+    //   2. the last of the ng group finishers sums the groups (level 2) and applies every problem's Rprop.
+    const int ng = spec_groups(a), grp = (int)blockIdx.x * NBW / kSpecGroup;
+    const int wg_in_grp = (min(kSpecGroup, a.nb - grp * kSpecGroup) + NBW - 1) / NBW;
+    unsigned* cnt_grp = fz.counters + grp;
+    unsigned* cnt_all = fz.counters + ng;
+    int* flag = reinterpret_cast<int*>(lds);        // the ring is free now
+    double* tot = lds + 2;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    int* last_wg = reinterpret_cast<int*>(lds);     // the ring is free now
-    if (threadIdx.x == 0) {
-      const unsigned prev = __hip_atomic_fetch_add(fz.counters, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *last_wg = prev == gridDim.x - 1;
-    }
+    if (threadIdx.x == 0) flag[0] = __hip_atomic_fetch_add(cnt_grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                                    (unsigned)(wg_in_grp - 1);
     __syncthreads();
-    if (*last_wg) {
-      for (int g = w; g < G; g += kWG / 64) reduce_step_wave<true, D>(a, fz.f, g, fz.iter, fz.do_update);
-      if (threadIdx.x == 0) __hip_atomic_store(fz.counters, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (flag[0]) {
+      const int t = threadIdx.x;
+      if (t < G * a.nq) {
+        const int g = t / a.nq, q = t % a.nq;
+        __hip_atomic_store(part2_ptr(a, g, q, grp), spec_group_sum<true>(a, g, q, grp), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        __hip_atomic_store(cnt_grp, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        flag[1] = __hip_atomic_fetch_add(cnt_all, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                  (unsigned)(ng - 1);
+      }
+      __syncthreads();
+      if (flag[1]) {
+        if (t < G * a.nq) {
+          const int g = t / a.nq, q = t % a.nq;
+          double s = 0.0;
+          for (int gr = 0; gr < ng; ++gr) s += ld_part<true>(part2_ptr(a, g, q, gr));
+          tot[t] = s;
+        }
+        __syncthreads();
+        spec_finish<D>(a, fz.f, tot, 0, G, fz.iter, fz.do_update);
+        if (threadIdx.x == 0) __hip_atomic_store(cnt_all, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
   }
   stamp_end(a);
@@ -518,6 +568,8 @@ void spec_geometry(Nll& a) {
   a.spec_tile = 0;
   a.spec_pgp = a.spec_ck = 0;
   a.spec_kw = 0;
+  const char* nx = getenv("FGP_SPEC_EXP_NOCOMPUTE");   // experiment: the tile kernel's streaming alone
+  a.spec_exp_nocompute = nx && nx[0] == '1';
   const char* te = getenv("FGP_SPEC_TILE");   // 0: the per-wave kernel only (A/B experiments)
   const bool tile_ok = !(te && te[0] == '0');
   if (tile_ok && a.basis_stride == 0 && a.spec_pg <= 4 && a.d <= 5 && a.spec_main >= 256) {
@@ -592,10 +644,16 @@ int launch_spec_iter(const Nll& a, hipStream_t st, const FitFuse* fz) {
 
 int launch_spec_reduce_step(const Nll& a, const Fit& f, int iter, int do_update, hipStream_t st) {
   return with_spec_d(a.d, [&](auto dc) {
-    k_spec_reduce_step<decltype(dc)::value>
-        <<<(unsigned)((a.G + kWG / 64 - 1) / (kWG / 64)), kWG, 0, st>>>(a, f, iter, do_update);
+    k_spec_reduce_step<decltype(dc)::value><<<(unsigned)((a.G + 15) / 16), kWG, 0, st>>>(a, f, iter, do_update);
     return check_launch("k_spec_reduce_step");
   });
+}
+
+int spec_counters_offset(const Nll& a, int64_t* off, int* count) {
+  const int ng = (a.nb + kSpecGroup - 1) / kSpecGroup;
+  *off = (int64_t)a.G * a.nq * (a.nb + ng);
+  *count = ng + 1;
+  return kOk;
 }
 
 int launch_spec_lam(const Nll& a, hipStream_t st) {

@@ -189,9 +189,19 @@ class FusedMLL(object):
             partials=0, **self.layout)
         if gen is not None:
             gen.apply(self._nll, n)
+        self.ysq_rows = self.ysq
         if self.basis is not None:
             self._nll.basis = self.basis.data_ptr()
             self._nll.basis_stride = self.basis[0].numel() if self.basis.dim() == 4 else 0
+            # Y in the spectra's chunk layout [Q][G][64] (include/fgp_hip.h ysq_chunked): a chunk's spectra
+            # and every problem's Y of it are two contiguous runs
+            Q = spec_chunks(self.family, n)
+            w = min(n, Q * 64)
+            yp = torch.zeros((G, Q * 64), dtype=torch.float64, device=self.device)
+            yp[:, :w] = self.ysq[:, :w]
+            self.ysq = yp.view(G, Q, 64).transpose(0, 1).contiguous()
+            self._nll.ysq = self.ysq.data_ptr()
+            self._nll.ysq_chunked = 1
         plen = ctypes.c_int64(0)
         N.call("fgp_nll_partials_len", self._nll, ctypes.byref(plen))
         self.partials = torch.empty((plen.value,), dtype=torch.float64, device=self.device)
@@ -282,10 +292,11 @@ class FusedMLL(object):
             nll = N.NllDesc()
             ctypes.pointer(nll)[0] = self._nll
             nll.G = Gk
+            nll.ysq = self.ysq_rows[g0].data_ptr()      # row layout for a problem range
+            nll.ysq_chunked = 0
             plen = ctypes.c_int64(0)
             N.call("fgp_nll_partials_len", nll, ctypes.byref(plen))
             part = torch.empty((plen.value,), dtype=torch.float64, device=self.device)
-            nll.ysq = self.ysq[g0].data_ptr()
             if self.work is not None:
                 nll.work = self.work[g0].data_ptr()
             nll.partials = part.data_ptr()

@@ -210,6 +210,10 @@ typedef struct fgp_nll_desc {
    * hold fgp_nll_partials_len doubles. */
   const double* basis;
   int64_t basis_stride;
+  /* 1: ysq is laid out in chunks of 64 frequencies, [Q][G][64] (Y of problem g at frequency k at
+   * ((k / 64) G + g) 64 + k mod 64; ysq_stride unused) -- every problem's Y of a chunk contiguous, read
+   * beside the chunk's spectra.  Spectral path only (basis non-NULL). */
+  int ysq_chunked;
 } fgp_nll_desc;
 
 /* Doubles the `partials` workspace of this desc needs (per-block partials + the fused fit's counters):

@@ -1,4 +1,4 @@
-"""Load golden fixtures (tests/golden/*.npz, produced by tests/golden/make_golden.py)."""
+"""Load golden fixtures (tests/golden/*.npz, produced by tests/golden/make_golden*.py)."""
 import glob
 import os
 
@@ -10,7 +10,9 @@ GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 def golden_names(family=None, multitask=False):
     """Single-task fixtures (make_golden.py) by default; multitask=True: the multitask /
     derivative-informed ones (make_golden_multitask.py, names mt_* / deriv_*)."""
-    names = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz")))
+    # (c5_*: the benched C5 regime of make_golden_c5.py, read by tests/test_gpu_multioutput.py only)
+    names = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz"))
+                   if not os.path.basename(p).startswith("c5_"))
     mt = [n for n in names if n.startswith("mt_") or n.startswith("deriv_")]
     names = mt if multitask else [n for n in names if n not in mt]
     if family is not None:

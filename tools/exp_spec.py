@@ -54,6 +54,12 @@ def main():
     from fastgaussianprocesses_amd.fit_engine import FusedMLL, mll_constant
     ysq1 = b.ysq()[:1].contiguous()
     raw = b.raw()
+    os.environ["FGP_SPEC_EXP_NOCOMPUTE"] = "1"
+    e8 = FusedMLL(0, None, b.ysq()[:8].contiguous(), raw[:8, 0], raw[:8, 1:1 + args.d], raw[:8, -1], 1.0,
+                  mll_constant(1, n), max_iters=4, per_problem=True, basis=bas)
+    print(json.dumps({"variant": "tile stage kernel, G=8, streaming only (no terms)",
+                      "us": 1e3 * ev_time(lambda: e8.stage(0), 20)}), flush=True)
+    os.environ.pop("FGP_SPEC_EXP_NOCOMPUTE")
     for G in (1, 2, 4, 8):
         e1 = FusedMLL(0, None, b.ysq()[:G].contiguous(), raw[:G, 0], raw[:G, 1:1 + args.d], raw[:G, -1], 1.0,
                       mll_constant(1, n), max_iters=4, per_problem=True, basis=bas)
