@@ -162,7 +162,7 @@ def _set_raw(gps, raw, dl):
         for name, v in vals.items():
             old = getattr(gp, name)
             setattr(gp, name, torch.nn.Parameter(v.reshape(old.shape), requires_grad=old.requires_grad))
-        gp._cache = {}
+        gp._cache = {k: v for k, v in gp._cache.items() if not k[2]}
         gp._snap = None
 
 

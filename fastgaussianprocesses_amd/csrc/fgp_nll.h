@@ -545,6 +545,8 @@ int launch_re_bwd_fused(const Nll& a, const FitFuse& fz, const Tables* tb, hipSt
 // spectral fit path (fgp_spectral.hip): d <= kSpecMaxD, at most kSpecBlocks k blocks per problem
 constexpr int kSpecMaxD = 6;
 constexpr int kSpecBlocks = 512;
+// frequency k of subset 0 in the chunked spectra of ns subsets ([chunk][subset][64]; subset s at + 64 s)
+__host__ __device__ __forceinline__ int64_t spec_pos(int64_t k, int ns) { return (((k >> 6) * ns) << 6) + (k & 63); }
 #ifndef FGP_SPEC_RING
 #define FGP_SPEC_RING 2
 #endif
@@ -561,6 +563,9 @@ int launch_spec_reduce_step(const Nll& a, const Fit& f, int iter, int do_update,
 // the fused spectral step's counters: doubles offset into partials and how many 32-bit counters
 int spec_counters_offset(const Nll& a, int64_t* off, int* count);
 int launch_spec_lam(const Nll& a, hipStream_t st);    // lambda of the current parameters into grad_lam
+// lattice spectra of the subsets s0 .. s0 + cnt - 1 (log2n >= 17) by the fused R2C pair: products formed in
+// the row kernel, real parts k <= n/2 written by the column kernel (work: 16 n cnt bytes)
+int spec_basis_r2c(const double* parts, int d, int log2n, int s0, int cnt, double* basis, void* work, hipStream_t st);
 // their row length log2 (FGP_RE_P2, default 10) for a transform of 2^log2n, or -1 when no split fits
 int re_row_log2(int log2n);
 

@@ -524,6 +524,58 @@ __global__ __launch_bounds__(kWG) void k_fwd_rows_r2c_in(const double* __restric
     out[work_pos_pair(row0, tid + k * kWG, m1, N2)] = tw_mul<double2>(v[k], rt.at(k, P2, m1, tw, twm), false);
 }
 
+// The same row pass on the products of a subset of the kernel parts (the spectral basis, fgp_spec_basis):
+// workgroup (row, c) forms b_S = prod_{j in S} parts_j (S = s0 + c, ascending j from 1.0 -- the products
+// of k_spec_products bit for bit) for its row in registers, instead of a products array written and read
+// back.  Subsets fastest in the grid: a row's parts are read from L2 by every subset's workgroup.
+template <int D>
+__global__ __launch_bounds__(kWG) void k_fwd_rows_r2c_prod(const double* __restrict__ parts, int log2n, int s0,
+                                                           int cnt, double2* __restrict__ work,
+                                                           const double2* __restrict__ tw,
+                                                           const double2* __restrict__ twm) {
+  constexpr int P2 = 12, N2 = 1 << P2;
+  __shared__ double ldsd[kTile + kTile / 16];
+  __shared__ double2 red[kWG / 64];
+  const int mt = log2n - 1, m1 = mt - P2;
+  const int64_t n = (int64_t)1 << log2n, nt = n >> 1;
+  const int c = (int)(blockIdx.x % (unsigned)cnt);
+  const int row0 = (int)(blockIdx.x / (unsigned)cnt);
+  const int S = s0 + c;
+  const int tid = threadIdx.x;
+  const double* x = parts + (int64_t)row0 * N2 + 16 * tid;
+  double2 v[16];
+#pragma unroll
+  for (int t = 0; t < 16; ++t) v[t] = make_double2(1.0, 1.0);
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+    if ((S >> j) & 1) {                      // uniform over the workgroup
+      const double* xj = x + (int64_t)j * n;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const double2 lo = *reinterpret_cast<const double2*>(xj + 2 * u);
+        const double2 hi = *reinterpret_cast<const double2*>(xj + nt + 2 * u);
+        v[2 * u].x *= lo.x;
+        v[2 * u + 1].x *= lo.y;
+        v[2 * u].y *= hi.x;
+        v[2 * u + 1].y *= hi.y;
+      }
+    }
+  }
+  double2 sum = make_double2(0.0, 0.0);
+#pragma unroll
+  for (int t = 0; t < 16; ++t) sum += v[t];
+  const double2 mean = block_sum_t(sum, red) * (1.0 / N2);
+#pragma unroll
+  for (int t = 0; t < 16; ++t) v[t] -= mean;
+  fwd_reg_passes<P2, 0, true>(v, ldsd, tid, tw);
+  if (tid == 0) v[0] += mean * (double)N2;
+  const RowTwiddle rt((unsigned)row0, tid, P2, m1, tw, twm);
+  double2* out = work + (int64_t)c * n;
+#pragma unroll
+  for (int k = 0; k < 16; ++k)
+    out[work_pos_pair(row0, tid + k * kWG, m1, N2)] = tw_mul<double2>(v[k], rt.at(k, P2, m1, tw, twm), false);
+}
+
 // Mirror-pair evaluation of the R2C column kernel.  The pair (k, nt - k) of the half-length spectrum Z
 // (primary Z_k = zk, partner Z_{nt-k} = zm, W = w_n^k) gives the length-n spectrum at k and k + n/2:
 //   A0, A1 = (S -/+ i W D) / 2,  S = Z_k + conj Z_{nt-k},  D = Z_k - conj Z_{nt-k}
@@ -564,7 +616,7 @@ __device__ __forceinline__ void pair_eval(double2 zk, double2 zm, double2 W, dou
 // self pairs), rr >= N1/2 a column-N2/2 pair.
 // Lanes run over q (consecutive columns: coalesced Y reads; the image reads of consecutive lanes fall
 // on distinct bank quads).  Y for the thread's jobs is loaded before the forward passes.
-template <int P1, bool EMIT>
+template <int P1, int OUT>
 __global__ __launch_bounds__(kWG, 2) void k_fwd_cols_r2c(Nll a, const double2* __restrict__ tw,
                                                           const double2* __restrict__ twmf) {
   constexpr int N1 = 1 << P1, C = kTile / N1, CS = N1 + 1, HC = C / 2;
@@ -602,7 +654,7 @@ __global__ __launch_bounds__(kWG, 2) void k_fwd_cols_r2c(Nll a, const double2* _
     }
   };
   double y0[JOBS], y1[JOBS];
-  if constexpr (!EMIT) {
+  if constexpr (OUT == 0) {
 #pragma unroll
     for (int j = 0; j < JOBS; ++j) {
       int sp, rp;
@@ -636,9 +688,11 @@ __global__ __launch_bounds__(kWG, 2) void k_fwd_cols_r2c(Nll a, const double2* _
   __syncthreads();
   const double rootn = sqrt((double)n), inv_rootn = 1.0 / rootn;
   Hyp h;
-  if constexpr (!EMIT) load_hyp_wave(a, g, h);
+  if constexpr (OUT == 0) load_hyp_wave(a, g, h);
   EigAcc acc2, acc1;          // regular pairs (weight 2), self-mirrored frequencies (weight 1)
-  double2* gl = EMIT ? static_cast<double2*>(a.grad_lam) + (int64_t)g * n : nullptr;
+  double2* gl = OUT == 1 ? static_cast<double2*>(a.grad_lam) + (int64_t)g * n : nullptr;
+  double* gb = OUT == 2 ? static_cast<double*>(a.grad_lam) + (int64_t)g * 64 : nullptr;   // basis + (s0 + g) 64
+  const int ns = 1 << a.d;
   const double2 wcp = twmf[col0 ? 0 : cp_gen];
 #pragma unroll 2
   for (int j = 0; j < JOBS; ++j) {
@@ -661,13 +715,13 @@ __global__ __launch_bounds__(kWG, 2) void k_fwd_cols_r2c(Nll a, const double2* _
     const double2 zk = *ip, zm = *is;
     double2 g0, g1, A0, A1;
     double ya = 0.0, yb = 0.0;
-    if constexpr (!EMIT) {
+    if constexpr (OUT == 0) {
       ya = y0[j];
       yb = y1[j];
     }
     EigAcc& ac = self ? acc1 : acc2;
     pair_eval(zk, zm, W, ya, yb, rootn, inv_rootn, h.noise, a.logdet_weight, ac, g0, g1, A0, A1);
-    if constexpr (EMIT) {   // lambda at k, k + n/2 and (conjugates, swapped) at the partner's nt - k, n - k
+    if constexpr (OUT == 1) {   // lambda at k, k + n/2 and (conjugates, swapped) at the partner's nt - k, n - k
       const int64_t kp = cp + (int64_t)rp * N2;
       gl[kp] = A0 * inv_rootn;
       gl[kp + nt] = A1 * inv_rootn;
@@ -676,6 +730,11 @@ __global__ __launch_bounds__(kWG, 2) void k_fwd_cols_r2c(Nll a, const double2* _
         gl[ks] = make_double2(A1.x, -A1.y) * inv_rootn;
         gl[ks + nt] = make_double2(A0.x, -A0.y) * inv_rootn;
       }
+    } else if constexpr (OUT == 2) {   // the real parts at k <= n/2 only, into the chunked spectra
+      const int64_t kp = cp + (int64_t)rp * N2;
+      gb[spec_pos(kp, ns)] = A0.x * inv_rootn;
+      if (kp == 0) gb[spec_pos(nt, ns)] = A1.x * inv_rootn;                 // the Nyquist frequency n/2
+      if (!self) gb[spec_pos((col0 ? cp : N2 - cp) + (int64_t)rs * N2, ns)] = A1.x * inv_rootn;
     } else {
       const double2 E = g0 + g1;
       const double2 O = cmulc(g0 - g1, W);
@@ -688,14 +747,16 @@ __global__ __launch_bounds__(kWG, 2) void k_fwd_cols_r2c(Nll a, const double2* _
       const double2 zh = *ih;
       const double2 Wh = tw[rh << (24 - m)];
       double yc = 0.0, yd = 0.0;
-      if constexpr (!EMIT) {
+      if constexpr (OUT == 0) {
         yc = yg[(int64_t)rh * N2];
         yd = yg[(int64_t)rh * N2 + nt];
       }
       pair_eval(zh, zh, Wh, yc, yd, rootn, inv_rootn, h.noise, a.logdet_weight, acc1, g0, g1, A0, A1);
-      if constexpr (EMIT) {
+      if constexpr (OUT == 1) {
         gl[(int64_t)rh * N2] = A0 * inv_rootn;
         gl[(int64_t)rh * N2 + nt] = A1 * inv_rootn;
+      } else if constexpr (OUT == 2) {
+        gb[spec_pos((int64_t)rh * N2, ns)] = A0.x * inv_rootn;              // n/4 (3n/4 is past n/2)
       } else {
         const double2 E = g0 + g1;
         const double2 O = cmulc(g0 - g1, Wh);
@@ -703,7 +764,7 @@ __global__ __launch_bounds__(kWG, 2) void k_fwd_cols_r2c(Nll a, const double2* _
       }
     }
   }
-  if constexpr (EMIT) {
+  if constexpr (OUT != 0) {
     stamp_end(a);
     return;
   }
@@ -1287,8 +1348,8 @@ static int launch_r2c(const Nll& a, int stage, const Tables* tb, hipStream_t st,
   switch (p1) {
 #define FGP_C(PP)                                                                              \
   case PP:                                                                                     \
-    if (emit) k_fwd_cols_r2c<PP, true><<<grid, kWG, 0, st>>>(a, tb->tw4096, tb->twm[m]);       \
-    else k_fwd_cols_r2c<PP, false><<<grid, kWG, 0, st>>>(a, tb->tw4096, tb->twm[m]);           \
+    if (emit) k_fwd_cols_r2c<PP, 1><<<grid, kWG, 0, st>>>(a, tb->tw4096, tb->twm[m]);       \
+    else k_fwd_cols_r2c<PP, 0><<<grid, kWG, 0, st>>>(a, tb->tw4096, tb->twm[m]);           \
     break;
     FGP_C(4) FGP_C(5) FGP_C(6) FGP_C(7) FGP_C(8) FGP_C(9) FGP_C(10) FGP_C(11)
 #undef FGP_C
@@ -1554,7 +1615,7 @@ int fgp_fftbr_real(const double* in, int64_t in_batch_stride, void* out, void* w
   a.grad_lam = out;
   a.stamps = nullptr;
   switch (p1) {
-#define FGP_C(PP) case PP: k_fwd_cols_r2c<PP, true><<<grid, kWG, 0, st>>>(a, tb->tw4096, tb->twm[log2n]); break;
+#define FGP_C(PP) case PP: k_fwd_cols_r2c<PP, 1><<<grid, kWG, 0, st>>>(a, tb->tw4096, tb->twm[log2n]); break;
     FGP_C(4) FGP_C(5) FGP_C(6) FGP_C(7) FGP_C(8) FGP_C(9) FGP_C(10) FGP_C(11)
 #undef FGP_C
     default: return set_error(kErrInvalid, "bad r2c m1");
@@ -1592,6 +1653,50 @@ int fgp_ifftbr_real(const void* in, int64_t in_batch_stride, const void* f, int6
   k_inv_rows_c2r<<<grid, kWG, 0, st>>>(wk, log2n, out, out_batch_stride, tb->tw4096, tb->twm[mt]);
   return check_launch("k_inv_rows_c2r");
 }
+
+}  // extern "C"
+
+namespace fgp {
+
+int spec_basis_r2c(const double* parts, int d, int log2n, int s0, int cnt, double* basis, void* work, hipStream_t st) {
+  if (log2n < 17 || log2n > 24 || d < 1 || d > kSpecMaxD || cnt < 1 || s0 < 0 || s0 + cnt > (1 << d))
+    return set_error(kErrInvalid, "spec_basis_r2c: bad shape");
+  const int64_t n = (int64_t)1 << log2n, nt = n >> 1;
+  const int64_t tiles = nt >> kTileLog;
+  const Tables* tb = get_tables(st);
+  if (!tb) return set_error(kErrHip, "twiddle table initialisation failed");
+  const int ns = 1 << d, mt = log2n - 1, p1 = mt - 12;
+  // the last chunk holds n/2 and 63 zeros of padding: zero the subsets' runs before the kernel writes n/2
+  if (hipMemsetAsync(basis + spec_pos(nt, ns) + 64 * (int64_t)s0, 0, sizeof(double) * 64 * (size_t)cnt, st) != hipSuccess)
+    return set_error(kErrHip, "spec_basis_r2c: memset failed");
+  const unsigned grid = (unsigned)(tiles * cnt);
+  double2* wk = static_cast<double2*>(work);
+  switch (d) {
+#define FGP_R(DD) case DD: k_fwd_rows_r2c_prod<DD><<<grid, kWG, 0, st>>>(parts, log2n, s0, cnt, wk, tb->tw4096, tb->twm[mt]); break;
+    FGP_R(1) FGP_R(2) FGP_R(3) FGP_R(4) FGP_R(5) FGP_R(6)
+#undef FGP_R
+  }
+  int rc = check_launch("k_fwd_rows_r2c_prod");
+  if (rc != kOk) return rc;
+  Nll a{};
+  a.log2n = log2n;
+  a.G = cnt;
+  a.d = d;
+  a.work = work;
+  a.grad_lam = basis + 64 * (int64_t)s0;
+  a.stamps = nullptr;
+  switch (p1) {
+#define FGP_C(PP) case PP: k_fwd_cols_r2c<PP, 2><<<grid, kWG, 0, st>>>(a, tb->tw4096, tb->twm[log2n]); break;
+    FGP_C(4) FGP_C(5) FGP_C(6) FGP_C(7) FGP_C(8) FGP_C(9) FGP_C(10) FGP_C(11)
+#undef FGP_C
+    default: return set_error(kErrInvalid, "bad r2c m1");
+  }
+  return check_launch("k_fwd_cols_r2c");
+}
+
+}  // namespace fgp
+
+extern "C" {
 
 int fgp_fit_step(const fgp_nll_desc* nll, const fgp_fit_desc* fit, int iter, int do_update, void* stream) {
   Nll a;

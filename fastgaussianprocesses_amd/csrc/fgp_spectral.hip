@@ -498,9 +498,17 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
       __syncthreads();
       if (flag[1]) {
         if (t < G * a.nq) {
+          // every group's sum in flight at once (a serial chain of ng agent-scope loads costs ~1 us
+          // each), then added ascending -- k_spec_reduce_step's order
+          constexpr int MAXG = kSpecBlocks / kSpecGroup;
           const int g = t / a.nq, q = t % a.nq;
+          double v[MAXG];
+#pragma unroll
+          for (int gr = 0; gr < MAXG; ++gr) v[gr] = ld_part<true>(part2_ptr(a, g, q, gr < ng ? gr : 0));
           double s = 0.0;
-          for (int gr = 0; gr < ng; ++gr) s += ld_part<true>(part2_ptr(a, g, q, gr));
+#pragma unroll
+          for (int gr = 0; gr < MAXG; ++gr)
+            if (gr < ng) s += v[gr];
           tot[t] = s;
         }
         __syncthreads();
@@ -706,7 +714,8 @@ __global__ __launch_bounds__(kWG) void k_spec_extract(const void* __restrict__ s
 static int64_t spec_subset_bytes(int family, int log2n) {
   const int64_t n = (int64_t)1 << log2n;
   if (family == FGP_FAMILY_NET) return 8 * n + 8 * n;         // products + their fwht
-  return 8 * n + 16 * n + (log2n >= 17 ? 16 * n : 0);          // products + spectrum (+ fgp_fftbr_real scratch)
+  if (log2n >= 17) return 16 * n;                              // the fused R2C pair's intermediate (spec_basis_r2c)
+  return 8 * n + 16 * n;                                       // products + spectrum
 }
 
 }  // namespace fgp
@@ -743,13 +752,17 @@ int fgp_spec_basis(int family, const double* parts, int64_t parts_stride, int64_
   char* wb = static_cast<char*>(work);
   double* prod = reinterpret_cast<double*>(wb);
   double2* spec = reinterpret_cast<double2*>(wb + 8 * n * (int64_t)chunk);
-  void* scratch = wb + 24 * n * (int64_t)chunk;
   const unsigned gi = (unsigned)((n + kWG - 1) / kWG);
   for (int64_t p = 0; p < P; ++p) {
     const double* pp = parts + p * parts_stride;
     double* bp = basis + p * QS * NS * 64;
     for (int s0 = 0; s0 < NS; s0 += chunk) {
       const int cnt = std::min(chunk, NS - s0);
+      if (!net && log2n >= 17) {   // products in the row kernel, real parts k <= n/2 from the column kernel
+        const int rc = spec_basis_r2c(pp, d, log2n, s0, cnt, bp, work, st);
+        if (rc != kOk) return rc;
+        continue;
+      }
       int rc = with_spec_d(d, [&](auto dc) {
         k_spec_products<decltype(dc)::value><<<gi, kWG, 0, st>>>(pp, n, s0, cnt, prod);
         return check_launch("k_spec_products");
@@ -764,8 +777,7 @@ int fgp_spec_basis(int family, const double* parts, int64_t parts_stride, int64_
           rc = check_launch("k_spec_extract");
         }
       } else {
-        rc = log2n >= 17 ? fgp_fftbr_real(prod, n, spec, scratch, cnt, log2n, stream)
-                         : fgp_fftbr(prod, n, 1, spec, cnt, log2n, 1, stream);
+        rc = fgp_fftbr(prod, n, 1, spec, cnt, log2n, 1, stream);
         if (rc == kOk) {
           k_spec_extract<true><<<ge, kWG, 0, st>>>(spec, n, K, QS, NS, s0, cnt, bp);
           rc = check_launch("k_spec_extract");

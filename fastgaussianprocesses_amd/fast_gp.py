@@ -615,6 +615,21 @@ class AbstractFastGP(torch.nn.Module):
         total = iterations + 1
         done = False
         losses = []
+        if wait_max > iterations:
+            # no early stop is possible: every iteration runs, the best iterate is the first minimum of
+            # the loss history (the host rule `lv < best`; NaN never best), found on the device -- one
+            # enqueue, no host sync unless losses are logged or returned
+            eng.run(0, total, final_no_update=True)
+            lh_dev = eng.loss_hist[:total, 0]
+            l0 = lh_dev[:, 0]
+            best_i = torch.where(torch.isnan(l0), torch.full_like(l0, math.inf), l0).argmin()
+            i = iterations
+            done = True
+            if verbose or hists["loss"]:
+                losses = [tuple(r) for r in lh_dev.cpu().tolist()]
+                for r in range(total):
+                    if verbose and (r % verbose == 0 or r == iterations):
+                        self._log_row(r, losses[r][0], losses[r][1], losses[r][2], indent)
         while not done:
             k = min(chunk, total - i0)
             eng.run(i0, k, final_no_update=(i0 + k == total))
@@ -645,7 +660,7 @@ class AbstractFastGP(torch.nn.Module):
             for name, val in (("raw_scale", b_s), ("raw_lengthscales", b_l), ("raw_noise", b_n)):
                 old = getattr(self, name)
                 setattr(self, name, torch.nn.Parameter(val.reshape(old.shape).clone(), requires_grad=old.requires_grad))
-        self._cache = {}
+        self._cache = {k: v for k, v in self._cache.items() if not k[2]}    # keep data-only entries (ytilde, spectra)
         self._snap = None
         data = {"iterations": i}
         if hists["loss"]:
@@ -712,7 +727,7 @@ class AbstractFastGP(torch.nn.Module):
         best, save, waited = math.inf, math.inf, 0
         best_params = None
         for i in range(iterations + 1):
-            self._cache = {}
+            self._cache = {k: v for k, v in self._cache.items() if not k[2]}
             loss, t1, t2, metric = self._loss_generic(loss_metric, masks, cv_weights, d_out)
             lv = loss.item()
             if lv < best:
@@ -744,7 +759,7 @@ class AbstractFastGP(torch.nn.Module):
             optimizer.zero_grad()
         for k, v in best_params.items():
             setattr(self, k, torch.nn.Parameter(v, requires_grad=getattr(self, k).requires_grad))
-        self._cache = {}
+        self._cache = {k: v for k, v in self._cache.items() if not k[2]}
         self._snap = None
         data = {"iterations": i}
         if hists["loss"]:

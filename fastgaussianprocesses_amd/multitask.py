@@ -693,7 +693,7 @@ class MultiTaskFastGP(AbstractFastGP):
         best_params = None
         rec = {k: [] for k in ("loss", "scale", "lengthscales", "noise", "task_kernel")}
         for i in range(iterations + 1):
-            self._cache = {}
+            self._cache = {k: v for k, v in self._cache.items() if not k[2]}
             if loss_metric == "GCV":
                 numer, denom = self._gcv_numer_denom()
                 if masks is None:
@@ -750,7 +750,7 @@ class MultiTaskFastGP(AbstractFastGP):
             optimizer.zero_grad()
         for k, v in best_params.items():
             setattr(self, k, torch.nn.Parameter(v, requires_grad=getattr(self, k).requires_grad))
-        self._cache = {}
+        self._cache = {k: v for k, v in self._cache.items() if not k[2]}
         self._snap = None
         data = {"iterations": i}
         if h_loss:
