@@ -307,8 +307,14 @@ STAGES = ("k_fwd_rows", "k_fwd_cols", "k_bwd_rows")
 SPEC_BLOCKS = 512      # k blocks per problem of the spectral iteration (csrc/fgp_nll.h kSpecBlocks)
 
 
+SPEC_RING, SPEC_LDS_MAX = 2, 80 * 1024     # csrc/fgp_nll.h kSpecRing / kSpecLdsMax
+
+
 def stage_names(variant):
-    """The fit-iteration kernels of a variant, in launch order (the reduce + Rprop step aside)."""
+    """The fit-iteration kernels of a variant, in launch order (the reduce + Rprop step aside; the fused
+    spectral kernel includes it)."""
+    if variant == "spectral_fused":
+        return ("k_spec_tile",)
     return ("k_spec_iter",) if variant == "spectral" else STAGES
 
 
@@ -317,7 +323,30 @@ def spec_geometry(n, d, G, shared=True, family=0):
     main = n // 2 if family == 0 else n
     nb = min(SPEC_BLOCKS, max(1, main // 64))
     ppw = 2 if (G >= 2 and shared and d <= 5) else 1
+    if ppw == 2 and G > 8 and d <= 3:
+        ppw = 4
     return nb, ppw, (G + ppw - 1) // ppw
+
+
+def spec_tile_grid(n, d, G, shared=True, family=0):
+    """Workgroups of the LDS-ring tile kernel k_spec_tile, or None when spec_geometry picks the per-wave
+    k_spec_iter (the conditions of csrc/fgp_spectral.hip spec_geometry)."""
+    main = n // 2 if family == 0 else n
+    nb, ppw, pg = spec_geometry(n, d, G, shared, family)
+    if not (shared and ppw <= 2 and pg <= 4 and d <= 5 and main >= 256) or os.environ.get("FGP_SPEC_TILE", "1")[:1] == "0":
+        return None
+    pgp = 1 if pg <= 1 else (2 if pg <= 2 else 4)
+    ck = 64 * (4 // pgp)
+    rows = 2 ** d + G
+    ok = (rows * ck * 8 * SPEC_RING <= SPEC_LDS_MAX and rows * ck <= 3072 and (rows * ck) % 128 == 0 and
+          nb % (4 // pgp) == 0 and main % (64 * nb) == 0)
+    return nb // (4 // pgp) if ok else None
+
+
+def spec_fused(n, d, G):
+    """fgp_fit_run runs the whole iteration (streaming + reduction + Rprop) as ONE k_spec_tile launch:
+    tile geometry, per-problem parameters, G <= 8 (csrc/fgp_nll.hip fgp_fit_run)."""
+    return spec_tile_grid(n, d, G) is not None and G <= 8
 
 
 def r2c_active(n):
@@ -343,6 +372,8 @@ def re_row_log2():
 
 def fit_grid(n, P, variant, d=5):
     """{stage kernel: (workgroups per fit launch, threads per workgroup)}."""
+    if variant == "spectral_fused":
+        return {"k_spec_tile": (spec_tile_grid(n, d, P), 256)}
     if variant == "spectral":
         nb, _, pg = spec_geometry(n, d, P)
         return {"k_spec_iter": ((nb * pg + 3) // 4, 256)}
@@ -366,12 +397,13 @@ def stage_bytes(n, d, P, parts_array, variant=None):
                      of its frequencies) + Nyquist 16 N1 read + 4 N1 written; bwd rows 16L + 4 N1"""
     variant = variant or fit_variant(n, parts_array)
     pb = 8 * n * d if parts_array else 0
-    if variant == "spectral":
+    if variant in ("spectral", "spectral_fused"):
         # one shared set of 2^d spectra of K = n/2 + 1 doubles read once per launch, Y[:K] of every
-        # problem, (4 + d) partials per problem and k block written
+        # problem, (4 + d) partials per problem and k block written (the fused kernel's level-1 group
+        # sums, reads of the partials and the parameter / history updates are < 0.1% on top)
         K = n // 2 + 1
         nb, _, _ = spec_geometry(n, d, P)
-        return {"k_spec_iter": 8 * K * (2 ** d) + 8 * K * P + 8 * (4 + d) * nb * P}
+        return {stage_names(variant)[0]: 8 * K * (2 ** d) + 8 * K * P + 8 * (4 + d) * nb * P}
     if variant == "re":
         L, N1 = n // 4, n // (2 * 2 ** re_row_log2())
         return {"k_fwd_rows": (16 * L + 16 * N1) * P, "k_fwd_cols": (32 * L + 4 * n + 20 * N1) * P,
@@ -404,6 +436,8 @@ def roofline_fit_kernels(F, shifts, iters):
     eng.run(0, 2)
     torch.cuda.synchronize()
     variant = "spectral" if eng.basis is not None else fit_variant(n, eng.gen is None)
+    if variant == "spectral" and spec_fused(n, eng.d, eng.G):
+        variant = "spectral_fused"
     names = stage_names(variant)
     ns = len(names)
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(ns + 2)] for _ in range(iters)]
@@ -411,9 +445,16 @@ def roofline_fit_kernels(F, shifts, iters):
     grid = max(g for g, _ in fg.values())
     stamps = torch.zeros((iters, ns, grid, 5), dtype=torch.int64, device=dev)   # fgp_nll_desc.stamps
     torch.cuda._sleep(int(2.4e9 * 4e-4 * iters))
+    fused = variant == "spectral_fused"
     for it in range(iters):
         e = ev[it]
         e[0].record()
+        if fused:     # the step's own launch: one kernel per iteration (fgp_fit_run), stamped
+            eng._nll.stamps = stamps[it, 0].data_ptr()
+            eng.run(it, 1)
+            e[1].record()
+            e[2].record()
+            continue
         for k in range(ns):
             eng._nll.stamps = stamps[it, k].data_ptr()
             eng.stage(k)
@@ -421,6 +462,7 @@ def roofline_fit_kernels(F, shifts, iters):
         eng._nll.stamps = None
         eng.fit_step(it)
         e[ns + 1].record()
+    eng._nll.stamps = None
     torch.cuda.synchronize()
     eng._nll.stamps = None
     khz = wall_clock_khz(F, dev)
@@ -433,9 +475,20 @@ def roofline_fit_kernels(F, shifts, iters):
         dur.append((sk[..., 1:].amax((1, 2)) - sk[..., 0].amin(1)).double() * (1e3 / khz))
     dur_us = torch.stack(dur, 1)     # [iters, ns]
     us_ev = {name: 1e3 * sum(e[k].elapsed_time(e[k + 1]) for e in ev) / iters for k, name in enumerate(names)}
-    us_ev["k_fit_reduce_step"] = 1e3 * sum(e[ns].elapsed_time(e[ns + 1]) for e in ev) / iters
+    if fused:
+        # the per-launch events above include one counter reset per fgp_fit_run call; the step makes ONE
+        # call for all its iterations -- time that (events around eng.run(0, iters)) for the iteration
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda._sleep(int(2.4e9 * 2e-4))
+        e0.record()
+        eng.run(0, iters)
+        e1.record()
+        torch.cuda.synchronize()
+        us_ev = {names[0]: 1e3 * e0.elapsed_time(e1) / iters}
     us = {name: float(dur_us[:, k].mean()) for k, name in enumerate(names)}
-    us["k_fit_reduce_step"] = us_ev["k_fit_reduce_step"]
+    if not fused:
+        us_ev["k_fit_reduce_step"] = 1e3 * sum(e[ns].elapsed_time(e[ns + 1]) for e in ev) / iters
+        us["k_fit_reduce_step"] = us_ev["k_fit_reduce_step"]
     t_iter = sum(us_ev.values()) / 1e6
     return n, variant, us, us_ev, t_iter, khz
 
@@ -583,11 +636,11 @@ def main():
 
     phases = phase_breakdown(shifts, args.fit_iters, xm, xv)
     n_, variant, us, us_ev, t_iter, khz = roofline_fit_kernels(F, shifts, args.fit_iters)
-    parts_array = variant not in ("spectral", "re")
+    parts_array = variant not in ("spectral", "spectral_fused", "re")
     P = len(shifts.gps)
     sb = stage_bytes(n, d, P, parts_array, variant)
     dom = max(stage_names(variant), key=lambda k: us[k])
-    kname = dom + {"re": "_re", "r2c": "_r2c", "full": "", "spectral": ""}[variant]
+    kname = dom + {"re": "_re", "r2c": "_r2c", "full": "", "spectral": "", "spectral_fused": ""}[variant]
     grid_wg, wg_thr = fit_grid(n, P, variant, d)[dom]
     # achieved / frac are priced on the rocprofv3 kernel-trace average of this same command (committed
     # under profiles/) when it is there -- the duration the profiler reports, including the dispatch
@@ -608,10 +661,13 @@ def main():
             "launch": "%d problems x n=2^%d (grid %d workgroups)" % (P, args.log2n, grid_wg),
             "transform": {"re": "real-even: n/2-point transform, columns [0, N2/2) (n/4 complex)",
                           "r2c": "half-length R2C (n/2 complex)", "full": "full-length (n complex)",
-                          "spectral": "none per iteration: lambda from the 2^d part-product spectra"}[variant],
+                          "spectral": "none per iteration: lambda from the 2^d part-product spectra",
+                          "spectral_fused": "none per iteration: lambda from the 2^d part-product spectra; "
+                                            "the kernel also reduces the partials (two deterministic levels) "
+                                            "and applies every problem's Rprop step"}[variant],
             "kernels": {k: {"avg_us": us[k], "avg_us_events": us_ev[k], "bytes": sb.get(k),
                             "GB/s": (sb[k] / (us[k] * 1e-6) / 1e9) if k in sb else None} for k in us},
-            "parts": ("spectra (fgp_spec_basis, built in the step)" if variant == "spectral" else
+            "parts": ("spectra (fgp_spec_basis, built in the step)" if variant.startswith("spectral") else
                       "array" if parts_array else "regenerated (FGP_PARTS_LATTICE)"),
             "iteration_us": t_iter * 1e6}
     vi = pmc_valu_insts(kname, grid_wg * wg_thr)

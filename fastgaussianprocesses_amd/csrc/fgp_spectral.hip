@@ -201,15 +201,24 @@ __global__ __launch_bounds__(kWG) void k_spec_iter(Nll a) {
     const double* phib = a.basis + (int64_t)g0 * a.basis_stride;   // PPW = 2: shared spectra (stride 0)
     SpecAcc<D> acc[PPW];
     const int64_t kbase = (int64_t)kb * 64 * a.spec_kpl;
+    // software-pipelined: the next frequency's spectra and Y are in flight while this one is evaluated
+    double phn[NS], Yn[PPW];
+    auto fetch = [&](int64_t k) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s) phn[s] = phib[spec_at<NS>(k, s)];
+#pragma unroll
+      for (int p = 0; p < PPW; ++p) Yn[p] = a.ysq[ysq_at(a, on[p] ? g0 + p : g0, k)];
+    };
+    if (kbase + lane < main) fetch(kbase + lane);
     for (int i = 0; i < a.spec_kpl; ++i) {
       const int64_t k = kbase + lane + 64 * i;
       if (k >= main) break;
-      double phi[NS];
+      double phi[NS], Y[PPW];
 #pragma unroll
-      for (int s = 0; s < NS; ++s) phi[s] = phib[spec_at<NS>(k, s)];
-      double Y[PPW];
+      for (int s = 0; s < NS; ++s) phi[s] = phn[s];
 #pragma unroll
-      for (int p = 0; p < PPW; ++p) Y[p] = a.ysq[ysq_at(a, on[p] ? g0 + p : g0, k)];
+      for (int p = 0; p < PPW; ++p) Y[p] = Yn[p];
+      if (i + 1 < a.spec_kpl && k + 64 < main) fetch(k + 64);
 #pragma unroll
       for (int p = 0; p < PPW; ++p)
         if (on[p]) spec_terms<D>(phi, h[p], rootn, wl, Y[p], acc[p]);
@@ -568,7 +577,12 @@ void spec_geometry(Nll& a) {
   a.spec_main = net ? n : n / 2;
   a.spec_K = net ? n : n / 2 + 1;
   a.spec_KS = spec_chunks(net, a.log2n) * 64;
+  // problems per wave sharing one read of the spectra: 2 (the tile kernel's, G <= 8), and for many
+  // problems (k_spec_iter, e.g. per-output hyper-parameters) 4 -- the spectra are then re-read from L2
+  // G / 4 times instead of G / 2 and each wave's loads serve 4 evaluations.  d <= 3 only: 156 VGPRs,
+  // 3 waves / SIMD there; at d = 4, 5 the four accumulator sets spill (8 per wave spills at d = 3)
   a.spec_ppw = (a.G >= 2 && a.basis_stride == 0 && a.d <= 5) ? 2 : 1;
+  if (a.spec_ppw == 2 && a.G > 8 && a.d <= 3) a.spec_ppw = 4;
   a.spec_pg = (a.G + a.spec_ppw - 1) / a.spec_ppw;
   const int64_t lanes = std::max<int64_t>(1, a.spec_main / 64);
   a.nb = (int)std::min<int64_t>(kSpecBlocks, lanes);
@@ -580,7 +594,7 @@ void spec_geometry(Nll& a) {
   a.spec_exp_nocompute = nx && nx[0] == '1';
   const char* te = getenv("FGP_SPEC_TILE");   // 0: the per-wave kernel only (A/B experiments)
   const bool tile_ok = !(te && te[0] == '0');
-  if (tile_ok && a.basis_stride == 0 && a.spec_pg <= 4 && a.d <= 5 && a.spec_main >= 256) {
+  if (tile_ok && a.basis_stride == 0 && a.spec_ppw <= 2 && a.spec_pg <= 4 && a.d <= 5 && a.spec_main >= 256) {
     const int pgp = a.spec_pg <= 1 ? 1 : (a.spec_pg <= 2 ? 2 : 4);
     const int ck = 64 * (4 / pgp);   // frequencies per chunk (64 per block of the workgroup)
     // the ring <= kSpecLdsMax (two workgroups per CU), whole 1-KiB wave-instructions, <= 6 per wave
@@ -603,6 +617,7 @@ int64_t spec_chunks(bool net, int log2n) {
 
 int launch_spec_iter(const Nll& a, hipStream_t st, const FitFuse* fz) {
   if (a.spec_tile) {
+    if (a.spec_ppw > 2) return set_error(kErrInvalid, "spectral tile kernel: %d problems per wave", a.spec_ppw);
     FitFuse none{};
     none.counters = nullptr;
     const FitFuse& f = fz ? *fz : none;
@@ -639,13 +654,16 @@ int launch_spec_iter(const Nll& a, hipStream_t st, const FitFuse* fz) {
   const unsigned grid = (unsigned)((tasks + kWG / 64 - 1) / (kWG / 64));
   return with_spec_d(a.d, [&](auto dc) {
     constexpr int D = decltype(dc)::value;
-    if (a.spec_net) {
-      if (a.spec_ppw == 2) k_spec_iter<D, 2, true><<<grid, kWG, 0, st>>>(a);
-      else k_spec_iter<D, 1, true><<<grid, kWG, 0, st>>>(a);
-    } else {
-      if (a.spec_ppw == 2) k_spec_iter<D, 2, false><<<grid, kWG, 0, st>>>(a);
-      else k_spec_iter<D, 1, false><<<grid, kWG, 0, st>>>(a);
-    }
+    auto go = [&](auto net) {
+      constexpr bool NET = decltype(net)::value;
+      switch (a.spec_ppw) {
+        case 4: if constexpr (D <= 3) { k_spec_iter<D, 4, NET><<<grid, kWG, 0, st>>>(a); break; } [[fallthrough]];
+        case 2: k_spec_iter<D, 2, NET><<<grid, kWG, 0, st>>>(a); break;
+        default: k_spec_iter<D, 1, NET><<<grid, kWG, 0, st>>>(a); break;
+      }
+    };
+    if (a.spec_net) go(std::true_type{});
+    else go(std::false_type{});
     return check_launch("k_spec_iter");
   });
 }

@@ -25,6 +25,7 @@ import numpy as np
 import scipy.stats
 import torch
 
+from . import _native
 from . import ops
 from . import seqs as _seqs
 from .fit_engine import FusedMLL, LatticePartsGen, mll_constant, spec_basis, spectral_wanted
@@ -275,13 +276,20 @@ class AbstractFastGP(torch.nn.Module):
             self._cache[k] = fn()
         return self._cache[k]
 
+    def _task_unit(self):
+        """gram_matrix_tasks == 1 (a single-task GP's unit task kernel).  Checked again only when the
+        task-kernel parameters change: the check synchronises with the device."""
+        key = tuple((id(p), p._version, p.data_ptr()) for p in (self.raw_factor_task_kernel, self.raw_noise_task_kernel))
+        hit = getattr(self, "_task_unit_memo", None)
+        if hit is None or hit[0] != key:
+            kt = self.gram_matrix_tasks.detach()
+            hit = self._task_unit_memo = (key, bool(torch.equal(kt, torch.ones_like(kt))))
+        return hit[1]
+
     def _task_scalar(self):
-        def check():
-            kt = self.gram_matrix_tasks
-            if not torch.equal(kt.detach(), torch.ones_like(kt)):
-                raise NotImplementedError("single-task GPs with a non-unit task kernel are not supported")
-            return 1.0
-        return self._cached(("task_unit", 0), check)
+        if not self._task_unit():
+            raise NotImplementedError("single-task GPs with a non-unit task kernel are not supported")
+        return 1.0
 
     # ------------------------------------------------------------------ points and data
     def _ensure_points(self, n):
@@ -347,8 +355,9 @@ class AbstractFastGP(torch.nn.Module):
             self._yt_state = None           # only an append keeps the cached prefix transform valid
         self._y[0] = torch.cat([self._y[0].to(self.data_dtype), y], -1)
         self._nh = int(self._y[0].size(-1))
-        self.n = torch.tensor([self._nh], dtype=torch.int64, device=self.device)
-        self.m = torch.tensor([self._nh.bit_length() - 1 if self._nh > 0 else -1], dtype=torch.int64, device=self.device)
+        # device fills, not host->device copies (a pageable copy blocks the host)
+        self.n = torch.full((1,), self._nh, dtype=torch.int64, device=self.device)
+        self.m = torch.full((1,), self._nh.bit_length() - 1 if self._nh > 0 else -1, dtype=torch.int64, device=self.device)
         self._cache = {}
         assert self._nh == 0 or (self._nh & (self._nh - 1)) == 0, "total samples must be power of 2"
 
@@ -507,6 +516,25 @@ class AbstractFastGP(torch.nn.Module):
         if self.data_dtype != torch.float64:
             y = self._y[0].to(torch.float64)
             yt = ops.fftbr_raw(y, stable=True) if self._FAMILY == ops.LATTICE else ops.fwht_raw(y, stable=True)
+        pb = self._problem_batch() if (self._lam_fusable(n) and not self.adaptive_nugget) else None
+        if pb is not None and yt.numel() == pb[1] * n:
+            # one output per eigen-problem: A = 1/ev and ytilde * A in ONE launch (fgp_inv_eig) instead of
+            # the torch chain of get_inv_log_det; Re(A) kept for post_var's quadratic form
+            self._task_scalar()
+            lam = self.get_lam(0, 0, n).reshape(pb[1], n).contiguous()
+            rows = yt.reshape(pb[1], n)
+            want = torch.complex128 if self._FAMILY == ops.LATTICE else torch.float64
+            assert lam.dtype == want and rows.dtype == want and rows.stride(-1) == 1, (lam.dtype, rows.dtype)
+            ya = torch.empty_like(lam)
+            wa = torch.empty((pb[1], n), dtype=torch.float64, device=self.device)
+            raw = self.raw_noise.detach().reshape(-1)
+            _native.call("fgp_inv_eig", self._FAMILY, _native.ptr(lam), _native.ptr(rows), rows.stride(0),
+                         _native.ptr(raw), 1 if raw.numel() > 1 else 0, pb[1], n.bit_length() - 1,
+                         _native.ptr(ya), _native.ptr(wa), _native.stream_ptr(self.device))
+            self._cached(("inv_real", n), lambda: wa.reshape(tuple(pb[0]) + (n,)))
+            if self._FAMILY == ops.LATTICE:
+                return ops.ifftbr_raw(ya, stable=True, real_out=True).reshape(yt.shape)
+            return ops.fwht_raw(ya, stable=True).reshape(yt.shape)
         return ops.inverse_mul(self._FAMILY, yt, self._inv(n), real_out=True)
 
     @property
@@ -520,7 +548,7 @@ class AbstractFastGP(torch.nn.Module):
             verbose_indent=4, masks=None, cv_weights=1):
         """Hyper-parameter optimisation with the reference's semantics (abstract_gp.py:152-306)."""
         assert isinstance(loss_metric, str) and loss_metric.upper() in ["MLL", "GCV", "CV"]
-        assert (self.n > 0).any(), "cannot fit without data"
+        assert self._nh > 0, "cannot fit without data"      # (self.n > 0).any() on the host mirror: no sync
         assert isinstance(iterations, int) and iterations >= 0
         assert (isinstance(verbose, int) or isinstance(verbose, bool)) and verbose >= 0, \
             "require verbose is a non-negative int"
@@ -557,8 +585,7 @@ class AbstractFastGP(torch.nn.Module):
             return False
         if self.raw_factor_task_kernel.requires_grad or self.raw_noise_task_kernel.requires_grad:
             return False
-        kt = self.gram_matrix_tasks.detach()
-        if not torch.equal(kt, torch.ones_like(kt)):
+        if not self._task_unit():
             return False
         pb = self._problem_batch()
         return pb is not None
@@ -567,9 +594,9 @@ class AbstractFastGP(torch.nn.Module):
         """G and the per-problem flags for the fused layout (None when shapes need broadcasting)."""
         shapes = [self.raw_scale.shape[:-1], self.raw_lengthscales.shape[:-1], self.raw_noise.shape[:-1]]
         big = max(shapes, key=len)
-        G = int(torch.tensor(big).prod()) if len(big) else 1
+        G = math.prod(big)
         for s in shapes:
-            cnt = int(torch.tensor(s).prod()) if len(s) else 1
+            cnt = math.prod(s)
             if cnt != 1 and s != big:
                 return None
         return big, G
@@ -595,7 +622,7 @@ class AbstractFastGP(torch.nn.Module):
         n = self._nh
         pb_shape, G = self._problem_batch()
         if d_out is None:
-            d_out = int(torch.tensor(self.shape_batch).prod())
+            d_out = math.prod(self.shape_batch)
         basis = self._spec_basis(n, G)
         gen = self._parts_gen(n) if basis is None else None
         parts = self._k1parts(n) if (gen is None and basis is None) else None
@@ -655,7 +682,9 @@ class AbstractFastGP(torch.nn.Module):
             chunk = min(64, chunk * 2)
         raw_hist = eng.raw_hist[:i + 1]
         s_raw, l_raw, nz_raw = eng.split_raw(raw_hist)
-        b_s, b_l, b_n = eng.split_raw(raw_hist[best_i])
+        # (a device index tensor: index_select, not raw_hist[t] -- a 0-d index tensor is read back to the host)
+        best_row = raw_hist.index_select(0, best_i.reshape(1))[0] if torch.is_tensor(best_i) else raw_hist[best_i]
+        b_s, b_l, b_n = eng.split_raw(best_row)
         with torch.no_grad():
             for name, val in (("raw_scale", b_s), ("raw_lengthscales", b_l), ("raw_noise", b_n)):
                 old = getattr(self, name)
@@ -857,6 +886,38 @@ class AbstractFastGP(torch.nn.Module):
                                                             tbits=self._tbits())
         return out
 
+    def _post_var_problems(self, x, n, work_bytes=1 << 30):
+        """Per-problem hyper-parameters (G eigen-problems on one point set, e.g. C5 per-output): every
+        problem's quadratic form sum_k Re(A_gk) |ft(K_g(x_t, .))_k|^2 and K_g(x, x) by
+        fgp_post_var_batched (shared points, z_stride 0), problems in chunks of <= work_bytes scratch --
+        instead of G x N kernel rows solved by full-length transforms."""
+        pb, G = self._problem_batch()
+        wa = self._cached(("inv_real", n), lambda: (lambda a: (a.real if a.is_complex() else a))(self._inv(n)))
+        wa = wa.reshape(G, n).contiguous()
+        hyp = self._hyp_rows(True).contiguous()                   # [G, 1 + d]
+        z = self._points_T(n)
+        order, coef = ops._pred_args(self._FAMILY, self._alphas, self.d)
+        x = x.contiguous()
+        Nt = x.size(0)
+        cdt = torch.complex128 if self._FAMILY == ops.LATTICE else torch.float64
+        per = Nt * n * (16 if self._FAMILY == ops.LATTICE else 8)
+        pc = max(1, min(G, work_bytes // per))
+        work = torch.empty((pc, Nt, n), dtype=cdt, device=self.device)
+        partial = torch.empty((pc, Nt, max(1, n >> 12)), dtype=torch.float64, device=self.device)
+        out = torch.empty((G, Nt), dtype=torch.float64, device=self.device)
+        part0 = _native.double_array([float(v) for v in self._part_at_zero()])
+        for p0 in range(0, G, pc):
+            p1 = min(G, p0 + pc)
+            desc = _native.PredDesc(family=self._FAMILY, d=self.d, tbits=int(self._tbits()), P=p1 - p0, n=n,
+                                    z=z.data_ptr(), z_stride=0, hyp=hyp[p0].data_ptr(), hyp_stride=hyp.stride(0),
+                                    coeffs=wa[p0].data_ptr(), coeff_stride=n, wa=wa[p0].data_ptr(), wa_stride=n)
+            for j in range(self.d):
+                desc.order[j] = order[j]
+                desc.coef[j] = coef[j]
+            _native.call("fgp_post_var_batched", desc, _native.ptr(x), 0, Nt, part0, _native.ptr(out[p0:p1]),
+                         _native.ptr(work), _native.ptr(partial), _native.stream_ptr(self.device))
+        return out.reshape(tuple(self.shape_batch) + (Nt,))
+
     def _kdiag(self, x):
         """K(x, x) (zero distance parts)."""
         part0 = getattr(self, "_part0_dev", None)
@@ -908,8 +969,11 @@ class AbstractFastGP(torch.nn.Module):
             x = x.to(device=self.device, dtype=torch.float64)
             self._defer_unit(x)
             bp = self._has_batch_params()
-            if not self._gradmode() and not bp and n > 4096 and self.d <= 8 and self._lam_fusable(n):
+            qf_ok = not self._gradmode() and 4096 < n <= 2 ** 24 and self.d <= 8 and self._lam_fusable(n)
+            if qf_ok and not bp:
                 diag = self._kdiag(x) - self._post_var_qf(x, n)
+            elif qf_ok and not self.adaptive_nugget and tuple(self._problem_batch()[0]) == tuple(self.shape_batch):
+                diag = self._post_var_problems(x, n)
             else:
                 rows = self._cross_rows(x, n, bp)                      # [Gk, N, n]
                 kmat = rows[0] if not bp else rows.reshape(tuple(self.shape_batch) + rows.shape[1:])

@@ -12,6 +12,7 @@ fast_gp_digital_net_b2.py:226):
 all differentiable (backward = the exact adjoint transform, real part for real inputs).
 With stable=True the mean-centring of AbstractFastGP.ft/ift happens inside the kernels.
 """
+import functools
 import math
 import os
 
@@ -258,8 +259,13 @@ def fwht(x, stable=False):
 # ------------------------------------------------------------------------------------- kernel parts
 def lattice_coefficient(alpha):
     """(-1)^(alpha+1) (2 pi)^(2 alpha) / (2 alpha)!  evaluated exactly as fast_gp_lattice.py:272."""
-    order = torch.tensor(2 * int(alpha), dtype=torch.int64)
-    return ((-1) ** (int(alpha) + 1) * torch.exp(2 * int(alpha) * math.log(2 * math.pi) - torch.lgamma(order + 1.0))).item()
+    return _lattice_coefficient(int(alpha))
+
+
+@functools.lru_cache(maxsize=None)
+def _lattice_coefficient(alpha):
+    order = torch.tensor(2 * alpha, dtype=torch.int64)
+    return ((-1) ** (alpha + 1) * torch.exp(2 * alpha * math.log(2 * math.pi) - torch.lgamma(order + 1.0))).item()
 
 
 def lattice_parts(x, z, alphas, out=None):
@@ -374,10 +380,16 @@ def post_mean_matfree(family, xt, z_dn, hyp, coeffs, alphas=None, tbits=0, chunk
     if chunk is None:
         chunk = post_mean_chunk(n, Nt)
     nchunks = (n + chunk - 1) // chunk
+    work_all = torch.empty((nchunks * min(B, 4) * Nt,), dtype=torch.float64, device=xt.device)
     for b0 in range(0, B, 4):
         b1 = min(B, b0 + 4)
-        hyp_b = hyp if Gk == 1 else hyp[torch.arange(b0, b1, device=hyp.device) % Gk]
-        work = torch.empty((nchunks, b1 - b0, Nt), dtype=torch.float64, device=xt.device)
+        if Gk == 1:
+            hyp_b = hyp
+        elif Gk == B:
+            hyp_b = hyp[b0:b1]        # a view: no gather launch per block of 4 outputs
+        else:
+            hyp_b = hyp[torch.arange(b0, b1, device=hyp.device) % Gk]
+        work = work_all[:nchunks * (b1 - b0) * Nt]
         cb = coeffs[b0:b1]
         N.call("fgp_post_mean", family, N.ptr(xt), Nt, N.ptr(z_dn), n, d, int(tbits), order, coef, N.ptr(hyp_b),
                hyp_b.shape[0], N.ptr(cb), cb.stride(0) if cb.shape[0] > 1 else n, b1 - b0, N.ptr(out[b0:b1]),

@@ -6,7 +6,6 @@
 """
 import cProfile
 import csv
-import io
 import os
 import pstats
 import sys
@@ -90,9 +89,11 @@ def main():
     torch.cuda.synchronize()
     t2 = time.perf_counter()
     print("%s: host enqueue %.3f ms, until GPU done %.3f ms" % (cfg, (t1 - t0) * 1e3, (t2 - t0) * 1e3))
-    s = io.StringIO()
-    pstats.Stats(pr, stream=s).sort_stats("cumtime").print_stats(40)
-    print(s.getvalue()[:5000])
+    st = pstats.Stats(pr).stats          # {(file, line, fn): (cc, nc, tottime, cumtime, callers)}
+    rows = sorted(st.items(), key=lambda kv: -kv[1][3])[:45]
+    print("%9s %9s %6s  %s" % ("cum_us", "self_us", "calls", "function"))
+    for (fn, ln, name), (cc, nc, tt, ct, _) in rows:
+        print("%9.1f %9.1f %6d  %s:%d(%s)" % (ct * 1e6, tt * 1e6, nc, os.path.basename(fn), ln, name))
 
 
 if __name__ == "__main__":
