@@ -366,8 +366,8 @@ def fit_variant(n, parts_array):
 
 
 def re_row_log2():
-    """Row length log2 of the real-even kernels' n/2-point transform (csrc/fgp_nll_re.hip, FGP_RE_P2, default 11)."""
-    return int(os.environ.get("FGP_RE_P2", "11") or 11)
+    """Row length log2 of the real-even kernels' n/2-point transform (csrc/fgp_nll_re.hip kP2reDefault)."""
+    return 11
 
 
 def fit_grid(n, P, variant, d=5):
@@ -392,7 +392,7 @@ def stage_bytes(n, d, P, parts_array, variant=None):
       full (L = n):  rows 16L write (+ 8nd parts), cols 16L + 16L + Y 8n, bwd rows 16L (+ 8nd)
       r2c (L = n/2): as full with Y 4n (Y = |y~|^2 is even, Y_k = Y_{n-k}, and the kernel reads it only
                      at each mirror pair's primary element: the n/2 values Y_k, Y_{k+n/2})
-      re (L = n/4, columns [0, N2/2) of the n/2-point transform, N1 = n/(2 N2) rows of N2 = 2^FGP_RE_P2):
+      re (L = n/4, columns [0, N2/2) of the n/2-point transform, N1 = n/(2 N2) rows of N2 = 2^11):
                      rows 16L + the Nyquist column 16 N1; cols 16L + 16L + Y 4n (the pairs (Y_2k, Y_2k+1)
                      of its frequencies) + Nyquist 16 N1 read + 4 N1 written; bwd rows 16L + 4 N1"""
     variant = variant or fit_variant(n, parts_array)

@@ -40,7 +40,6 @@ struct Nll {
   int spec_kpl, spec_ppw, spec_pg;   // frequencies per lane and block, problems per wave, problem groups
   int spec_tile, spec_pgp, spec_ck;  // LDS-tiled kernel: problem-group slots, frequencies per chunk
   int64_t spec_kw;                   // ... and per workgroup
-  int spec_exp_nocompute;            // experiment (FGP_SPEC_EXP_NOCOMPUTE=1): stream the chunks, skip the terms
   int ysq_chunked;                   // ysq in the chunked layout [k / 64][G][64] (spectral path)
 };
 
@@ -566,7 +565,7 @@ int launch_spec_lam(const Nll& a, hipStream_t st);    // lambda of the current p
 // lattice spectra of the subsets s0 .. s0 + cnt - 1 (log2n >= 17) by the fused R2C pair: products formed in
 // the row kernel, real parts k <= n/2 written by the column kernel (work: 16 n cnt bytes)
 int spec_basis_r2c(const double* parts, int d, int log2n, int s0, int cnt, double* basis, void* work, hipStream_t st);
-// their row length log2 (FGP_RE_P2, default 10) for a transform of 2^log2n, or -1 when no split fits
+// their row length log2 (11) for a transform of 2^log2n, or -1 when no split fits
 int re_row_log2(int log2n);
 
 }  // namespace fgp

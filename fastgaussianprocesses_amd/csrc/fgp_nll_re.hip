@@ -30,9 +30,8 @@ namespace fgp {
 // [0, N2/2), zero elsewhere, the Nyquist column's V by direct sums in the row kernel.  Per iteration:
 // rows write n/4 complex (4n B), columns read 4n + Y 4n and write 4n, rows read 4n: 20n bytes
 // (R2C 40n), and half the eigenvalue terms and kernel parts.
-constexpr int kP2reDefault = 11;             // row length 2^P2 of the n/2-point transform (FGP_RE_P2)
-// unroll factor of the column kernel's eigen-term loop; experiment builds may also set one for the
-// backward kernel's gradient loop over the 8 mirror pairs (FGP_RE_GRAD_UNROLL; default: the compiler's)
+constexpr int kP2reDefault = 11;             // row length 2^P2 of the n/2-point transform
+// unroll factor of the column kernel's eigen-term loop
 #ifndef FGP_RE_EIG_UNROLL
 #define FGP_RE_EIG_UNROLL 2
 #endif
@@ -139,13 +138,6 @@ __device__ __forceinline__ void wg_sums_t0(double* v, double* red /* [K][NW] */)
   }
 }
 
-// Phase stamps (experiment builds, -DFGP_EXP_PHASES): thread 0 of each workgroup records the wall clock
-// at phase k into stamps[blockIdx.x * 16 + k] (the launch's stamps buffer, sized by the experiment).
-#ifdef FGP_EXP_PHASES
-#define RE_PHASE(a, k) do { if ((a).stamps && threadIdx.x == 0) (a).stamps[(int64_t)blockIdx.x * 16 + (k)] = (unsigned long long)wall_clock64(); } while (0)
-#else
-#define RE_PHASE(a, k) do { } while (0)
-#endif
 
 // Row geometry of the length-n/2 transform for rows of N2 = 2^P2 (P2 = 10, 11, 12): TL = N2/16 threads
 // per row (one, two or four wavefronts), a row-pair workgroup of 2 TL threads.
@@ -206,11 +198,7 @@ struct RowTwRe {
   // twiddle of output k1 = q + off (off uniform)
   __device__ __forceinline__ double2 at(unsigned off, int m1, const double2* __restrict__ tw,
                                         const double2* __restrict__ twm) const {
-#ifdef FGP_EXP_NOTW
-    return base;
-#else
     return cmul(base, inter_tw(j1 * off, P2, m1, tw, twm));
-#endif
   }
 };
 
@@ -227,16 +215,12 @@ __global__ __launch_bounds__(ReGeo<P2>::WG, 4) void k_fwd_rows_re(Nll a, const d
   const unsigned n = 1u << a.log2n, M = n >> 1, mask = n - 1;
   const double inv_n = ldexp(1.0, -a.log2n);
   const int q = rp.q;
-#ifndef FGP_EXP_PHASES
   stamp_begin(a);
-#endif
-  RE_PHASE(a, 0);
   Hyp h;
   load_hyp_wave(a, rp.g, h);
   fold_gen_coef<PG>(a, h);
   // element twiddles w_n^{i_e} = w_n^r w_{2 N2}^{brev(q)} w_32^{brev4(e)}
   const double2 wq = rp.wbase(twm_n, tw2);
-  RE_PHASE(a, 1);
   double2 v[16];
   double x0[16];
   double cM = 0.0;
@@ -248,14 +232,10 @@ __global__ __launch_bounds__(ReGeo<P2>::WG, 4) void k_fwd_rows_re(Nll a, const d
     static_for<0, 8>([&](auto ec) {
       constexpr int e = decltype(ec)::value;
       const unsigned i = rp.nat(Brev4<e>::value);
-#ifdef FGP_EXP_NOGEN
-      const double x = (double)(i & 7) * h.scale, y = (double)(i & 3) * h.scale;
-#else
       double pi[D], pmi[D];
       parts_mirror_pair<PG, D>(a, i, n, mask, inv_n, pi, pmi);
       const double x = k1_of_parts<D>(h, pi);
       const double y = k1_of_parts<D>(h, pmi);
-#endif
       const double2 w = mul_root32<Brev4<e>::value>(wq);
       const double s = x + y, b = x - y;
       v[e] = make_double2(__builtin_fma(-b, w.y, s), b * w.x);                          // a + i b w
@@ -284,17 +264,14 @@ __global__ __launch_bounds__(ReGeo<P2>::WG, 4) void k_fwd_rows_re(Nll a, const d
       v[e] = make_double2(__builtin_fma(-b, w.y, sa), b * w.x);
     });
   }
-  RE_PHASE(a, 2);
   double2 sum = make_double2(0.0, 0.0);
 #pragma unroll
   for (int t = 0; t < 16; ++t) sum += v[t];
   const double2 mean = group_sum<TL>(sum, red) * (1.0 / N2);   // per row (one wave: shuffles only)
 #pragma unroll
   for (int t = 0; t < 16; ++t) v[t] -= mean;
-  RE_PHASE(a, 3);
   fwd_reg_passes<P2, 0, true>(v, img + rp.hh * IMG, q, tw);
   if (q == 0) v[0] += mean * (double)N2;
-  RE_PHASE(a, 4);
   const RowTwRe<P2> rt(rp.r, q, rp.m1, tw, twm_t);
   double2* out = static_cast<double2*>(a.work) + (int64_t)rp.g * n;
   const WtStore wo(out);   // write-through: the column kernel reads the intermediate from HBM / MALL
@@ -304,17 +281,10 @@ __global__ __launch_bounds__(ReGeo<P2>::WG, 4) void k_fwd_rows_re(Nll a, const d
     for (int t = 0; t < R / 2; ++t) {
       const int k1 = pass_pos<P2, Geo::SL, Geo::RLL>(q, j, t);
       const double2 o = tw_mul<double2>(v[j * R + t], rt.at(k1 - q, rp.m1, tw, twm_t), false);
-#ifdef FGP_EXP_PLAIN_STORES
-      out[work_pos(rp.u, k1, rp.m1)] = o;
-#else
       wo.put((unsigned)work_pos(rp.u, k1, rp.m1), o);
-#endif
     }
   if (q == 0) out[(n >> 2) + rp.u] = tw_mul<double2>(v[R / 2], rt.at(N2 / 2, rp.m1, tw, twm_t), false);   // column N2/2
-  RE_PHASE(a, 5);
-#ifndef FGP_EXP_PHASES
   stamp_end(a);
-#endif
 }
 
 // Column pass over columns [0, N2/2) (tile blk of C = 4096/N1 columns, all N1 rows), eigenvalue terms
@@ -401,12 +371,6 @@ __global__ __launch_bounds__(kWG) void k_fwd_cols_re(Nll a, const double2* __res
   for (int k = 0; k < 16; ++k) v[k] -= mean;
   adj_reg_passes<P1, SL, false>(v, col, tt, tw);
   if (tt == 0) v[0] += mean * (double)N1;
-#ifdef FGP_EXP_PLAIN_STORES
-#pragma unroll
-  for (int j = 0; j < 16 / R0; ++j)
-#pragma unroll
-    for (int t = 0; t < R0; ++t) wk[pass_pos<P1, 0, RL0>(tt, j, t) * C] = v[j * R0 + t];
-#else
   {
     const WtStore wo(base);   // write-through, as the row kernel's stores
     const unsigned o0 = (unsigned)(blk * kTile + c);
@@ -415,7 +379,6 @@ __global__ __launch_bounds__(kWG) void k_fwd_cols_re(Nll a, const double2* __res
 #pragma unroll
       for (int t = 0; t < R0; ++t) wo.put(o0 + (unsigned)(pass_pos<P1, 0, RL0>(tt, j, t) * C), v[j * R0 + t]);
   }
-#endif
   // Nyquist column (k1 = N2/2): Z_b = sum_u T_u w_N1^{brev(u) b} (mean-centred), real part, weight 2;
   // wave j < NQ of the workgroup takes b = NQ blk + j
   const double2* nyq = base + (n >> 2);
@@ -471,10 +434,7 @@ __global__ __launch_bounds__(ReGeo<P2>::WG, 4) void k_bwd_rows_re(Nll a, const d
   const unsigned n = 1u << a.log2n, M = n >> 1, mask = n - 1;
   const double inv_n = ldexp(1.0, -a.log2n);
   const int q = rp.q, N1 = rp.N1;
-#ifndef FGP_EXP_PHASES
   stamp_begin(a);
-#endif
-  RE_PHASE(a, 0);
   const double2* in = static_cast<const double2*>(a.work) + (int64_t)rp.g * n;
   const double* vny = reinterpret_cast<const double*>(in + (n >> 2) + N1);
   const RowTwRe<P2> rt(rp.r, q, rp.m1, tw, twm_t);
@@ -507,10 +467,8 @@ __global__ __launch_bounds__(ReGeo<P2>::WG, 4) void k_bwd_rows_re(Nll a, const d
   const double2 mean = group_sum<TL>(sum, red) * (1.0 / N2);
 #pragma unroll
   for (int k = 0; k < 16; ++k) v[k] -= mean;
-  RE_PHASE(a, 1);
   adj_reg_passes<P2, LastPass<P2>::S, true>(v, img + rp.hh * IMG, q, tw);
   if (q == 0) v[0] += mean * (double)N2;
-  RE_PHASE(a, 2);
   // W at the mirror elements -- from the partner thread (regular), or the class-0 image (Re, then Im)
   // -- combined into dL/dc as they arrive (gv: the thread's 16 generated points, in loop order)
   double2* xw = reinterpret_cast<double2*>(img + rp.partner_h * IMG);
@@ -566,7 +524,6 @@ __global__ __launch_bounds__(ReGeo<P2>::WG, 4) void k_bwd_rows_re(Nll a, const d
     });
   }
   __syncthreads();
-  RE_PHASE(a, 3);
   // dL/dc values into private LDS slots (stride 17: conflict-free) for the rolled gradient loop
   double* gl = img + 17 * threadIdx.x;
 #pragma unroll
@@ -590,13 +547,6 @@ __global__ __launch_bounds__(ReGeo<P2>::WG, 4) void k_bwd_rows_re(Nll a, const d
     }
   } else {
     // the mirror pairs (i, M - i): both points' parts from one lattice index per dimension
-#ifdef FGP_EXP_NOGEN
-    for (int e = 0; e < 8; ++e) acc[0] += gl[2 * e] + gl[2 * e + 1];
-    if (false)
-#endif
-#ifdef FGP_RE_GRAD_UNROLL
-#pragma unroll FGP_RE_GRAD_UNROLL
-#endif
     for (int e = 0; e < 8; ++e) {
       const unsigned i = (unsigned)rp.r + (unsigned)N1 * (((__builtin_bitreverse32((unsigned)e) >> 28) << (P2 - 4)) | sq);
       double p[D], pm[D];
@@ -611,17 +561,13 @@ __global__ __launch_bounds__(ReGeo<P2>::WG, 4) void k_bwd_rows_re(Nll a, const d
     for (int j = 0; j < D; ++j) p[j] = lattice_gen_part<PG>(a.gz[j], M, mask, inv_n);
     grad_terms_p<D>(h, p, gM * gs, acc);
   }
-  RE_PHASE(a, 4);
   wg_sums_t0<Geo::WG / 64, 1 + D>(acc, redd);
   if (!fz.counters) {
     if (threadIdx.x == 0) {
 #pragma unroll
       for (int k = 0; k < 1 + D; ++k) *part_ptr(a, rp.g, 3 + k, rp.jp) = acc[k] * grad_factor(h, k);
     }
-    RE_PHASE(a, 5);
-#ifndef FGP_EXP_PHASES
     stamp_end(a);
-#endif
     return;
   }
   // Fused reduction + Rprop (fgp_fit_run, per-problem fits).  Hand-off (MI355X_MICROARCH.md row 1): the
@@ -649,15 +595,9 @@ __global__ __launch_bounds__(ReGeo<P2>::WG, 4) void k_bwd_rows_re(Nll a, const d
 
 // real-even lattice kernels: row pairs of the length-n/2 transform (G N1/2 workgroups of N2/8 threads),
 // column tiles of its columns [0, N2/2) (G n/16384 workgroups of 256); N1 = n / (2 N2).
-// Rows of 2^11 (measured best: profiles/r02d_exp_re_rows_*); experiment builds (-DFGP_EXP_RE_P2ALL) also
-// compile rows of 2^10 and 2^12, selected by FGP_RE_P2 (a third of the build time without them).
+// Rows of 2^11 (measured best of 2^10 / 2^11 / 2^12: profiles/r02d_exp_re_rows_*).
 int re_row_log2(int log2n) {
-#ifdef FGP_EXP_RE_P2ALL
-  const char* e = getenv("FGP_RE_P2");
-  const int p2 = e && e[0] ? atoi(e) : kP2reDefault;
-#else
   const int p2 = kP2reDefault;
-#endif
   return (p2 >= 10 && p2 <= 12 && log2n - 1 - p2 <= 12 && log2n - 1 - p2 >= 4) ? p2 : -1;
 }
 
@@ -697,10 +637,6 @@ static int launch_re_p2(const Nll& a, int stage, const Tables* tb, hipStream_t s
 
 static int launch_re_any(const Nll& a, int stage, const Tables* tb, hipStream_t st, const FitFuse& fz) {
   switch (re_row_log2(a.log2n)) {
-#ifdef FGP_EXP_RE_P2ALL
-    case 10: return launch_re_p2<10>(a, stage, tb, st, fz);
-    case 12: return launch_re_p2<12>(a, stage, tb, st, fz);
-#endif
     case 11: return launch_re_p2<11>(a, stage, tb, st, fz);
     default: return set_error(kErrInvalid, "real-even fit kernels: no row split for log2n=%d", a.log2n);
   }

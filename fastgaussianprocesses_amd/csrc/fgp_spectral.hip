@@ -459,7 +459,7 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
     barrier_keep_vm();                              // ... every wave's; every wave done with chunk c - 1
     if (c + RING - 1 < nc) issue(c + RING - 1, lds + ((c + RING - 1) % RING) * tile);
     const double* buf = lds + (unsigned)(c % RING) * (unsigned)tile;
-    if (active && !a.spec_exp_nocompute) {
+    if (active) {
       const double* wb = buf + wofs;
       double phi[NS];
 #pragma unroll
@@ -590,8 +590,6 @@ void spec_geometry(Nll& a) {
   a.spec_tile = 0;
   a.spec_pgp = a.spec_ck = 0;
   a.spec_kw = 0;
-  const char* nx = getenv("FGP_SPEC_EXP_NOCOMPUTE");   // experiment: the tile kernel's streaming alone
-  a.spec_exp_nocompute = nx && nx[0] == '1';
   const char* te = getenv("FGP_SPEC_TILE");   // 0: the per-wave kernel only (A/B experiments)
   const bool tile_ok = !(te && te[0] == '0');
   if (tile_ok && a.basis_stride == 0 && a.spec_ppw <= 2 && a.spec_pg <= 4 && a.d <= 5 && a.spec_main >= 256) {

@@ -1,4 +1,6 @@
-"""Spectral fit path timing on one GPU (C4 shape by default: 8 shifted lattice GPs, n = 2^20, d = 5):
+"""(Historical: the FGP_SPEC_EXP_NOCOMPUTE switch these runs used was removed from the product kernel
+after the round-3 measurements; its 'stream' rows need a build of commit e26f9e6.)
+Spectral fit path timing on one GPU (C4 shape by default: 8 shifted lattice GPs, n = 2^20, d = 5):
 basis build, the iteration kernel alone (stage launches) and the fused fit loop per iteration, for the
 tile kernel, the per-wave kernel (FGP_SPEC_TILE=0) and the transform path (FGP_FIT_PATH=transform).
 Prints one JSON line per variant.  HIP events on torch's current stream.

@@ -1,4 +1,6 @@
-"""Tile-kernel ring-depth / LDS variants (experiment builds, tools/build_exp.sh into _lib/exp/): for each
+"""(Historical: the FGP_SPEC_EXP_NOCOMPUTE switch these runs used was removed from the product kernel
+after the round-3 measurements; its 'stream' rows need a build of commit e26f9e6.)
+Tile-kernel ring-depth / LDS variants (experiment builds, tools/build_exp.sh into _lib/exp/): for each
 library, the C4-shaped iteration kernel (8 GPs sharing one set of spectra, n = 2^20, d = 5) streaming only
 (FGP_SPEC_EXP_NOCOMPUTE=1) and complete, HIP events.  One JSON line per variant.
 

@@ -3,8 +3,9 @@
   python tools/fit_kernels.py [--log2n 20] [--d 5] [--shifts 8] [--iters 5] [--parts-array]
 
 Builds the same batched engine as bench.py's step (bench.Shifts + fastgaussianprocesses_amd.batch)
-and runs `--iters` iterations of stage 0/1/2 + fit step, so a counter pass sees a few dispatches of
-k_fwd_rows / k_fwd_cols / k_bwd_rows at the bench's grid.
+and runs `--iters` iterations as the step launches them (spectral path: one fused k_spec_tile per
+iteration; transform path: stage 0/1/2 + fit step), so a counter pass sees a few dispatches at the
+bench's grid.
 """
 import argparse
 import os
@@ -34,10 +35,13 @@ def main():
     shifts = bench.Shifts(F, a.d, 2 ** a.log2n, [1000 + s for s in range(a.shifts)], dev)
     shifts.reset()
     eng = F.batch.batched_engine(shifts.gps, a.iters)
-    for it in range(a.iters):
-        for k in range(3):
-            eng.stage(k)
-        eng.fit_step(it)
+    if eng.basis is not None:       # spectral path: the step's own launches (one fused kernel per iteration)
+        eng.run(0, a.iters)
+    else:
+        for it in range(a.iters):
+            for k in range(3):
+                eng.stage(k)
+            eng.fit_step(it)
     torch.cuda.synchronize()
     print("ran %d fit iterations over %d problems, n=2^%d, d=%d, parts=%s" %
           (a.iters, a.shifts, a.log2n, a.d, "array" if eng.gen is None else "regenerated"))
