@@ -56,6 +56,8 @@ def parse():
     p.add_argument("--no-secondary", dest="secondary", action="store_false",
                    help="skip the secondary BASELINE configs (C2, C3, C5) reported under 'secondary'")
     p.add_argument("--c5-outputs", type=int, default=512)
+    p.add_argument("--no-paper", dest="paper", action="store_false",
+                   help="skip the probnum25 paper's n=2^10 per-step timings reported under 'paper'")
     return p.parse_args()
 
 
@@ -276,6 +278,94 @@ def secondary_configs(F, args, device, rank=0, world=1):
                     "phases_ms": phases})
         del sg
         torch.cuda.empty_cache()
+    return out
+
+
+# ---------------------------------------------------------------- the probnum25 paper's timing table
+# docs/examples/probnum25_paper/benchmarks_accuracy_time.tex:6-10 ("time per optimization step", seconds; the
+# paper's hardware is unstated): {benchmark: (SI lattice f, SI lattice (f, grad f), DSI net f, DSI net (f, grad f))}
+PAPER_S_PER_STEP = {"Ackley": (5.6e-4, 1.3e-3, 7.7e-4, 1.9e-3), "Branin": (5.3e-4, 2.1e-3, 7.0e-4, 3.4e-3),
+                    "Camel": (5.0e-4, 2.2e-3, 6.8e-4, 3.4e-3), "StyTang": (5.2e-4, 2.2e-3, 7.7e-4, 3.4e-3),
+                    "Hartmann": (5.1e-4, 8.3e-3, 7.1e-4, 1.6e-2)}
+
+
+def paper_functions():
+    """The paper's benchmark functions (probnum25_paper.ipynb cell 7; the standard test-function
+    definitions) as (name, d, f, Baker transform for the lattice's (f, grad f) fit) -- cell 15's `funcs`."""
+    def branin(x):
+        a, b, c, r, s, t = 1.0, 5.1 / (4 * np.pi ** 2), 5 / np.pi, 6.0, 10.0, 1 / (8 * np.pi)
+        x1, x2 = 15 * x[:, 0] - 5, 15 * x[:, 1]
+        return a * (x2 - b * x1 ** 2 + c * x1 - r) ** 2 + s * (1 - t) * torch.cos(x1) + s
+
+    def camel(x):
+        x1, x2 = 6 * x[:, 0] - 3, 4 * x[:, 1] - 2
+        return (4 - 2.1 * x1 ** 2 + x1 ** 4 / 3) * x1 ** 2 + x1 * x2 + (-4 + 4 * x2 ** 2) * x2 ** 2
+
+    def styblinski_tang(x):
+        x = 10 * x - 5
+        return 0.5 * torch.sum(x ** 4 - 16 * x ** 2 + 5 * x, 1)
+
+    def hartmann(x):
+        al = torch.tensor([1.0, 1.2, 3.0, 3.2], device=x.device)
+        A = torch.tensor([[10, 3, 17, 3.5, 1.7, 8], [0.05, 10, 17, 0.1, 8, 14], [3, 3.5, 1.7, 10, 17, 8],
+                          [17, 8, 0.05, 10, 0.1, 14]], device=x.device)
+        P = 1e-4 * torch.tensor([[1312, 1696, 5569, 124, 8283, 5886], [2329, 4135, 8307, 3736, 1004, 9991],
+                                 [2348, 1451, 3522, 2883, 3047, 6650], [4047, 8828, 8732, 5743, 1091, 381]],
+                                device=x.device, dtype=torch.float64)
+        inner = (A[None] * (x[:, None, :] - P[None]) ** 2).sum(-1)
+        return -(2.58 + (al * torch.exp(-inner)).sum(1)) / 1.94
+
+    return [("Ackley", 1, f_ackley, False), ("Branin", 2, branin, True), ("Camel", 2, camel, False),
+            ("StyTang", 2, styblinski_tang, False), ("Hartmann", 6, hartmann, True)]
+
+
+def f_grad_f(f, x):
+    """(f, df/dx_1, ..., df/dx_d) at x [n, d] -> [n, 1 + d] (probnum25_paper.ipynb cell 7)."""
+    xs = [x[:, j].clone().requires_grad_() for j in range(x.shape[1])]
+    y = f(torch.stack(xs, 1))
+    grads = torch.autograd.grad(y, xs, grad_outputs=torch.ones_like(y))
+    return torch.stack([y] + list(grads), 1).detach()
+
+
+def paper_configs(F, device, log2n=10, iterations=5000):
+    """The paper's timing protocol (probnum25_paper.ipynb cell 15): n = 2^10 points per task, SI lattice
+    alpha = 2 / DSI digital net alpha = 4, f alone (derivatives = [0]) and (f, grad f) (1 + d derivative
+    tasks), fit() with the reference's defaults (Rprop lr 0.1, early stopping: improvement 5e-2 over 10
+    iterations, at most 5000), store_loss_hist; time per optimisation step = fit wall time / iterations."""
+    n = 2 ** log2n
+    out = []
+    for name, d, f, bake_grad in paper_functions():
+        for fam in ("lattice", "net"):
+            for grad in (False, True):
+                lbetas = [torch.zeros((1, d), dtype=torch.int64)]
+                if grad:
+                    lbetas += [e[None] for e in torch.eye(d, dtype=torch.int64)]
+                T = len(lbetas)
+                if fam == "lattice":
+                    gp = F.FastGPLattice([F.Lattice(d, seed=7) for _ in range(T)], derivatives=lbetas, alpha=2,
+                                         num_tasks=T, device=device)
+                else:
+                    gp = F.FastGPDigitalNetB2([F.DigitalNetB2(d, seed=7, randomize="DS") for _ in range(T)],
+                                              derivatives=lbetas, alpha=4, num_tasks=T, device=device)
+                xs = gp.get_x_next(n * torch.ones(T, dtype=torch.int64))
+                ff = (lambda x, f=f: f(1 - 2 * torch.abs(x - 0.5))) if (fam == "lattice" and grad and bake_grad) else f
+                if grad:
+                    gp.add_y_next([f_grad_f(ff, xs[i])[:, i] for i in range(T)])
+                else:
+                    gp.add_y_next([f(xs[0])])
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                data = gp.fit(iterations=iterations, verbose=0, store_loss_hist=True)
+                torch.cuda.synchronize()
+                el = time.perf_counter() - t0
+                its = max(1, int(data["iterations"]))
+                col = (0 if fam == "lattice" else 2) + (1 if grad else 0)
+                out.append({"benchmark": name, "d": d, "gp": "SI lattice alpha=2" if fam == "lattice" else
+                            "DSI digital net alpha=4", "data": "(f, grad f)" if grad else "f", "tasks": T,
+                            "n_per_task": n, "iterations": its, "s_per_step": el / its,
+                            "paper_s_per_step": PAPER_S_PER_STEP[name][col],
+                            "class": type(gp).__name__})
+                del gp
     return out
 
 
@@ -685,6 +775,12 @@ def main():
     secondary = None
     if args.secondary:
         secondary = secondary_configs(F, args, device, rank, world)
+    paper = None
+    if args.paper and world == 1:
+        paper = {"source": "docs/examples/probnum25_paper/benchmarks_accuracy_time.tex:6-10 (time per optimization "
+                           "step, s; the paper's hardware is unstated) with the protocol of probnum25_paper.ipynb "
+                           "cell 15 (fit wall time / iterations, reference fit defaults)",
+                 "configs": paper_configs(F, device)}
     if rank == 0:
         out = {"metric": "GP fit+predict points/sec at n=2^20 fp64; achieved HBM GB/s vs roofline",
                "value": value, "unit": "points/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -694,7 +790,8 @@ def main():
                                       "post_mean N=%d + post_var N=%d per shift" %
                                       (args.log2n, d, args.shifts, args.fit_iters, args.n_mean, args.n_var),
                           "global_shifts": args.shifts * world, "parallelism": "replicas%d" % world},
-               "roofline": roof, "cpu_baseline": cpu, "phases_ms": phases, "secondary": secondary}
+               "roofline": roof, "cpu_baseline": cpu, "phases_ms": phases, "secondary": secondary,
+               "paper": paper}
         print(json.dumps(out))
     if dist:
         tdist.destroy_process_group()

@@ -75,13 +75,35 @@ class _Hyper(object):
         return value
 
 
+def _trivial_derivatives(derivatives, derivatives_coeffs):
+    """derivatives / derivatives_coeffs that leave a one-task GP's kernel unchanged: ONE all-zero derivative
+    row (beta = 0) with coefficient 1 -- e.g. the probnum25 paper's `derivatives=[torch.zeros((1, d))]`
+    ($f$ columns of benchmarks_accuracy_time.tex).  None counts as trivial."""
+    if derivatives is not None:
+        v = derivatives[0] if isinstance(derivatives, (list, tuple)) and len(derivatives) == 1 else derivatives
+        if not isinstance(v, torch.Tensor):
+            return False
+        v = v.reshape(-1, v.shape[-1]) if v.ndim else v
+        if v.ndim != 2 or v.shape[0] != 1 or bool((v != 0).any()):
+            return False
+    if derivatives_coeffs is not None:
+        c = derivatives_coeffs[0] if isinstance(derivatives_coeffs, (list, tuple)) and len(derivatives_coeffs) == 1 \
+            else derivatives_coeffs
+        if not isinstance(c, torch.Tensor) or c.numel() != 1 or float(c.reshape(-1)[0]) != 1.0:
+            return False
+    return True
+
+
 def _wants_multitask(cls, args, kwargs):
-    """num_tasks > 1, or derivative information, in a family constructor's arguments."""
+    """num_tasks > 1, or non-trivial derivative information, in a family constructor's arguments.  One task
+    with trivial derivatives (_trivial_derivatives) is the single-task GP: the reference's general path gives
+    it the same loss and predictions (rank-1 task factor 1, task noise 0: gram_matrix_tasks == 1,
+    abstract_gp.py:58-72), so it takes the single-task fused kernels."""
     import inspect
     bound = inspect.signature(cls.__init__).bind_partial(None, *args, **kwargs).arguments
     nt = bound.get("num_tasks")
-    return (nt is not None and nt != 1) or bound.get("derivatives") is not None or \
-        bound.get("derivatives_coeffs") is not None
+    return (nt is not None and nt != 1) or not _trivial_derivatives(bound.get("derivatives"),
+                                                                    bound.get("derivatives_coeffs"))
 
 
 class AbstractFastGP(torch.nn.Module):
@@ -116,9 +138,14 @@ class AbstractFastGP(torch.nn.Module):
         else:
             assert isinstance(num_tasks, int) and num_tasks > 0
             self.solo_task, self.default_task = False, torch.arange(num_tasks)
-        if num_tasks != 1 or derivatives is not None or derivatives_coeffs is not None:
+        if num_tasks != 1 or not _trivial_derivatives(derivatives, derivatives_coeffs):
             raise AssertionError("multitask / derivative-informed GPs are built through FastGPLattice / "
                                  "FastGPDigitalNetB2 (multitask.py)")
+        if derivatives is not None or derivatives_coeffs is not None:
+            # the reference's derivative settings (abstract_gp.py:58-62): rank-1 task factor, task noise 0
+            rank_factor_task_kernel = 1
+            tfs_noise_task_kernel = _IDENTITY_TFS
+            noise_task_kernel = 0.
         self.num_tasks = 1
         # Extension (not in the reference, which is fp64-only, abstract_gp.py:46): data_dtype=float32
         # stores the observations in fp32 and forms the MLL's data term from a complex64 ytilde
@@ -133,6 +160,9 @@ class AbstractFastGP(torch.nn.Module):
         self.seq = self._resolve_seq(seqs, seed_for_seq)
         self.seqs = np.array([self.seq], dtype=object)
         self.d = int(self.seq.d)
+        # the (trivial) derivative specification (abstract_gp.py:63-72)
+        self.derivatives = [torch.zeros((1, self.d), dtype=torch.int64, device=self.device)]
+        self.derivatives_coeffs = [torch.ones(1, device=self.device)]
         # shape_batch / hyper-parameters (abstract_gp.py:73-139)
         shape_batch = _as_size(shape_batch)
         assert isinstance(shape_batch, torch.Size)

@@ -1,0 +1,115 @@
+"""Where the time of the spectral fit iteration goes (C4 shape: 8 shifted lattice GPs, n = 2^20, d = 5):
+device-clock stamps of every workgroup (start, each wave's end) over `--iters` launches of the fused
+k_spec_tile (the step's own launch: streaming + partials + the two-level reduction + Rprop) and of the
+stage launch (streaming + partials only), reported as offsets from the launch's first workgroup start:
+start spread, workgroup durations, end-time percentiles, and the tail = last end - the end of the
+last workgroup that does no reduction work.  One JSON line per variant; FGP_LIB_PATH selects an
+experiment build (tools/build_exp.sh).
+
+    python tools/exp_spec_stamps.py [--iters 20] [--log2n 20] [--d 5] [--shifts 8]
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+torch.set_default_dtype(torch.float64)
+
+
+def summarize(st, grid, khz, name, extra=None):
+    """st [iters, grid, 5] raw wall-clock stamps -> offsets in us"""
+    st = st[:, :grid].double()
+    t0 = st[:, :, 0].amin(1, keepdim=True)
+    start = (st[:, :, 0] - t0) * (1e3 / khz)
+    end = (st[:, :, 1:].amax(2) - t0) * (1e3 / khz)
+    dur = end - start
+    se, _ = end.sort(1)
+    q = lambda x, p: float(x.quantile(p))
+    out = {"variant": name, "grid": grid, "launches": st.shape[0],
+           "span_us": float(se[:, -1].mean()),
+           "start_p50_us": q(start, 0.5), "start_p99_us": q(start, 0.99), "start_max_us": float(start.amax(1).mean()),
+           "dur_p10_us": q(dur, 0.1), "dur_p50_us": q(dur, 0.5), "dur_p90_us": q(dur, 0.9),
+           "end_p50_us": q(end, 0.5), "end_p90_us": q(end, 0.9),
+           # the 17 latest workgroups include the 16 level-1 group finishers and the level-2 finisher
+           "end_18th_latest_us": float(se[:, -18].mean()), "end_2nd_latest_us": float(se[:, -2].mean())}
+    out["tail_us"] = out["span_us"] - out["end_18th_latest_us"]
+    if extra:
+        out.update(extra)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--log2n", type=int, default=20)
+    ap.add_argument("--d", type=int, default=5)
+    ap.add_argument("--shifts", type=int, default=8)
+    args = ap.parse_args()
+    import bench
+    import fastgaussianprocesses_amd as F
+    dev = torch.device("cuda", 0)
+    n = 2 ** args.log2n
+    sh = bench.Shifts(F, args.d, n, bench.shard_seeds(0, 1, args.shifts), dev)
+    sh.reset()
+    eng = F.batch.batched_engine(sh.gps, args.iters + 4)
+    eng.run(0, 2)
+    torch.cuda.synchronize()
+    assert eng.basis is not None, "the spectral path is not selected"
+    grid = bench.spec_tile_grid(n, eng.d, eng.G)
+    khz = bench.wall_clock_khz(F, dev)
+    it = args.iters
+    stamps = torch.zeros((it, max(grid, 1), 5), dtype=torch.int64, device=dev)
+    # fused launches (the step's own: fgp_fit_run, one iteration each)
+    torch.cuda._sleep(int(2.4e9 * 2e-4 * it))
+    for i in range(it):
+        eng._nll.stamps = stamps[i].data_ptr()
+        eng.run(i, 1)
+    eng._nll.stamps = None
+    torch.cuda.synchronize()
+    print(json.dumps(summarize(stamps.cpu(), grid, khz, "fused k_spec_tile")), flush=True)
+    # events around one enqueue of all iterations (the step's form)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda._sleep(int(2.4e9 * 2e-4))
+    a.record()
+    eng.run(0, it)
+    b.record()
+    torch.cuda.synchronize()
+    print(json.dumps({"variant": "fused fgp_fit_run, events", "us_per_iter": 1e3 * a.elapsed_time(b) / it}),
+          flush=True)
+    # stage launches (streaming + partials, no reduction)
+    stamps.zero_()
+    torch.cuda._sleep(int(2.4e9 * 2e-4 * it))
+    for i in range(it):
+        eng._nll.stamps = stamps[i].data_ptr()
+        eng.stage(0)
+    eng._nll.stamps = None
+    torch.cuda.synchronize()
+    print(json.dumps(summarize(stamps.cpu(), grid, khz, "stage k_spec_tile")), flush=True)
+    a.record()
+    for i in range(it):
+        eng.stage(0)
+    b.record()
+    torch.cuda.synchronize()
+    print(json.dumps({"variant": "stage launches, events", "us_per_iter": 1e3 * a.elapsed_time(b) / it}), flush=True)
+    # streaming calibration: a plain read of the spectra + Y (torch sum)
+    bas = eng.basis
+    ys = eng.ysq
+    for _ in range(2):
+        bas.sum()
+    a.record()
+    for _ in range(10):
+        bas.sum()
+        ys.sum()
+    b.record()
+    torch.cuda.synchronize()
+    us = 1e3 * a.elapsed_time(b) / 10
+    mb = (bas.numel() + ys.numel()) * 8 / 1e6
+    print(json.dumps({"variant": "torch sum of spectra + Y", "us": us, "MB": mb, "GBps": mb * 1e3 / us}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
