@@ -78,19 +78,22 @@ __device__ __forceinline__ double read_lane(double v, int lane) {
 // load_hyp for a problem index g that is uniform over the wave: one exp per parameter, evaluated
 // lane-parallel (lane 0 scale, 1 noise, 2 + j lengthscale j) and broadcast, instead of 2 + d
 // exps in every lane.  Same libm exp, so the same values as load_hyp.
-__device__ __forceinline__ void load_hyp_wave(const Nll& a, int g, Hyp& h) {
+// hyper-parameters of problem g from the raw vector `raw` (a.raw, or an LDS copy of the parameters a fused
+// launch has just stepped): exp per lane, broadcast by v_readlane
+__device__ __forceinline__ void load_hyp_wave(const Nll& a, int g, Hyp& h, const double* raw) {
   const int lane = threadIdx.x & 63;
   const int lb = a.ls_off + (a.ls_pp ? g : 0) * (a.ls_pd ? a.d : 1);
   int idx = -1;
   if (lane == 0) idx = a.scale_off + (a.scale_pp ? g : 0);
   else if (lane == 1) idx = a.noise_off + (a.noise_pp ? g : 0);
   else if (lane < 2 + a.d) idx = lb + (a.ls_pd ? lane - 2 : 0);
-  const double e = exp(idx >= 0 ? a.raw[idx] : 0.0);
+  const double e = exp(idx >= 0 ? raw[idx] : 0.0);
   h.scale = read_lane(e, 0);
   h.noise = read_lane(e, 1);
 #pragma unroll
   for (int j = 0; j < FGP_MAX_D; ++j) h.ls[j] = (j < a.d) ? read_lane(e, 2 + j) : 0.0;
 }
+__device__ __forceinline__ void load_hyp_wave(const Nll& a, int g, Hyp& h) { load_hyp_wave(a, g, h, a.raw); }
 
 // ------------------------------------------------------------------ parts source (array / generated)
 // Per-problem source of the kernel parts: the parts array, or (FGP_PARTS_LATTICE) the lattice point
@@ -534,10 +537,22 @@ __device__ __forceinline__ void reduce_step_wg(const Nll& a, const Fit& f, int g
 int launch_re(const Nll& a, int stage, const Tables* tb, hipStream_t st);
 // fused backward + reduction + Rprop of one iteration (per-problem fits): the stage-2 kernel's last
 // row-pair workgroup of each problem runs reduce_step_wg.  counters: G zeroed 32-bit words.
+// Rprop state (raw parameters, previous gradient, step sizes) of every problem: the fit's own vectors, or one
+// of the spectral fused run's two scratch copies (fgp_spectral.hip, deferred step)
+struct RpState {
+  double* raw;
+  double* prev;
+  double* step;
+};
 struct FitFuse {
   Fit f;
   int iter, do_update;
   unsigned* counters;
+  // spectral tile kernel (fgp_spectral.hip): the step of iteration iter - 1 is deferred into this launch
+  // (pending: every workgroup reduces that iteration's level-1 sums of parity par ^ 1 and steps the
+  // parameters from sin; workgroup 0 writes histories and sout); this launch's level-1 sums go to parity par
+  int pending, par;
+  RpState sin, sout;
 };
 int launch_re_bwd_fused(const Nll& a, const FitFuse& fz, const Tables* tb, hipStream_t st);
 
@@ -554,13 +569,18 @@ constexpr int kSpecRing = FGP_SPEC_RING;         // LDS ring depth of the spectr
 #define FGP_SPEC_LDS_KB 80
 #endif
 constexpr int kSpecLdsMax = FGP_SPEC_LDS_KB * 1024;   // its dynamic LDS per workgroup, at most (80: 2 per CU)
+constexpr int kSpecScratch = 256;                  // doubles after the ring: the deferred step's totals / parameters
 void spec_geometry(Nll& a);                        // nb and the spec_* fields of a spectral desc
 int64_t spec_chunks(bool net, int log2n);          // 64-frequency chunks of the spectra (fgp_spec_basis layout)
 // one fit iteration (loss + gradient partials); with fz (tile kernel only) also the reduction + Rprop
 int launch_spec_iter(const Nll& a, hipStream_t st, const FitFuse* fz = nullptr);
 int launch_spec_reduce_step(const Nll& a, const Fit& f, int iter, int do_update, hipStream_t st);
-// the fused spectral step's counters: doubles offset into partials and how many 32-bit counters
+// the fused spectral run's counters: doubles offset into partials and how many 32-bit counters
 int spec_counters_offset(const Nll& a, int64_t* off, int* count);
+// the fused spectral run's scratch copies of the Rprop state (parity 0, 1) in the partials workspace
+RpState spec_scratch_state(const Nll& a, int par);
+// the deferred step of a fused spectral run's last iteration (after its last k_spec_tile launch)
+int launch_spec_finish_step(const Nll& a, const FitFuse& fz, hipStream_t st);
 int launch_spec_lam(const Nll& a, hipStream_t st);    // lambda of the current parameters into grad_lam
 // lattice spectra of the subsets s0 .. s0 + cnt - 1 (log2n >= 17) by the fused R2C pair: products formed in
 // the row kernel, real parts k <= n/2 written by the column kernel (work: 16 n cnt bytes)

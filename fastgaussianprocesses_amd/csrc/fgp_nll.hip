@@ -1742,14 +1742,28 @@ int fgp_fit_run(const fgp_nll_desc* nll, const fgp_fit_desc* fit, int iter0, int
     if (hipMemsetAsync(fz.counters, 0, sizeof(unsigned) * (size_t)ncnt, st) != hipSuccess)
       return set_error(kErrHip, "fgp_fit_run: counter reset failed");
   }
+  if (fuse_spec) {
+    // one k_spec_tile launch per iteration; the step of iteration i runs in launch i + 1's prologue (its
+    // state read from the fit's vectors for the first step, else from the scratch copy of parity i,
+    // written to parity i + 1) and the last one in k_spec_finish_step, back into the fit's vectors
+    const RpState own{f.raw, f.prev, f.step};
+    for (int it = 0; it <= iters; ++it) {
+      const int i = iter0 + it;
+      fz.iter = i;
+      fz.par = i & 1;
+      fz.pending = it > 0;
+      fz.sin = it <= 1 ? own : spec_scratch_state(a, (i - 1) & 1);
+      fz.sout = it == iters ? own : spec_scratch_state(a, i & 1);
+      if (it == iters) {
+        fz.do_update = !final_no_update;
+        return launch_spec_finish_step(a, fz, st);
+      }
+      if ((rc = launch_spec_iter(a, st, &fz)) != kOk) return rc;
+    }
+    return kOk;
+  }
   for (int it = 0; it < iters; ++it) {
     const int upd = !(final_no_update && it == iters - 1);
-    if (fuse_spec) {
-      fz.iter = iter0 + it;
-      fz.do_update = upd;
-      if ((rc = launch_spec_iter(a, st, &fz)) != kOk) return rc;
-      continue;
-    }
     if ((rc = nll_fwd(a, st, lat)) != kOk) return rc;
     if (fuse) {
       fz.iter = iter0 + it;

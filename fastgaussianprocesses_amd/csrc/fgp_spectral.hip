@@ -240,9 +240,20 @@ constexpr int kSpecGroup = 32;
 
 __device__ __forceinline__ int spec_groups(const Nll& a) { return (a.nb + kSpecGroup - 1) / kSpecGroup; }
 
-// level-2 partials [G][nq][ng] after the level-1 ones, then the fused step's counters (ng + 1)
-__device__ __forceinline__ double* part2_ptr(const Nll& a, int g, int q, int grp) {
-  return a.partials + (int64_t)a.G * a.nq * a.nb + ((int64_t)g * a.nq + q) * spec_groups(a) + grp;
+// The fused run's workspace after the level-1 partials [G][nq][nb]: level-2 inputs (the group sums) of two
+// iterations [2][G][nq][ng] (parity of the iteration: a launch writes its own while it reads the previous
+// one's), two Rprop state copies [2][3][np], then the group counters (ng)
+__host__ __device__ __forceinline__ int spec_nparams(const Nll& a) { return a.noise_off + (a.noise_pp ? a.G : 1); }
+__host__ __device__ __forceinline__ int64_t spec_part2_off(const Nll& a, int par) {
+  return (int64_t)a.G * a.nq * a.nb + (int64_t)par * a.G * a.nq * ((a.nb + kSpecGroup - 1) / kSpecGroup);
+}
+__device__ __forceinline__ double* part2_ptr(const Nll& a, int par, int g, int q, int grp) {
+  return a.partials + spec_part2_off(a, par) + ((int64_t)g * a.nq + q) * spec_groups(a) + grp;
+}
+__host__ __device__ __forceinline__ RpState spec_state(const Nll& a, int par) {
+  const int np = spec_nparams(a);
+  double* b = a.partials + spec_part2_off(a, 2) + (int64_t)par * 3 * np;
+  return RpState{b, b + np, b + 2 * np};
 }
 
 template <bool SC1>
@@ -264,19 +275,42 @@ __device__ __forceinline__ double spec_group_sum(const Nll& a, int g, int q, int
   return s;
 }
 
+// level 2 of the fused run: tot[g nq + q] = the ascending sum over the groups of the level-1 sums of parity
+// par (k_spec_reduce_step's order); every group's sum in flight at once (a serial chain of loads costs ~1 us
+// each).  Threads t < G nq; plain loads (the sums were stored by an earlier launch).
+template <int D>
+__device__ __forceinline__ void spec_level2(const Nll& a, int par, double* tot) {
+  constexpr int MAXG = kSpecBlocks / kSpecGroup;
+  const int t = threadIdx.x, ng = spec_groups(a);
+  if (t < a.G * a.nq) {
+    const int g = t / a.nq, q = t % a.nq;
+    double v[MAXG];
+#pragma unroll
+    for (int gr = 0; gr < MAXG; ++gr) v[gr] = *part2_ptr(a, par, g, q, gr < ng ? gr : 0);
+    double s = 0.0;
+#pragma unroll
+    for (int gr = 0; gr < MAXG; ++gr)
+      if (gr < ng) s += v[gr];
+    tot[t] = s;
+  }
+}
+
 // Loss history + Rprop of the problems g0 .. g0 + cnt - 1 (cnt <= kWG / 16) from their reduced totals
 // tot[(g - g0) * nq + q] (LDS): thread 16 i + k owns parameter slot k (0 scale, 1 .. dl lengthscales,
 // dl + 1 noise) of problem g0 + i -- the reduce_step_wg semantics (fgp_nll.h: torch.optim.Rprop
-// single-tensor, loss = 1/2 (norm + w logdet + const), histories).
+// single-tensor, loss = 1/2 (norm + w logdet + const), histories).  The state is read from `in`; with
+// `write` the histories, the gradient and the new state (to `out`, which may be `in`) are stored; the new
+// raw parameters also go to newraw[p] when given (the deferred step of k_spec_tile, in every workgroup).
 template <int D>
 __device__ __forceinline__ void spec_finish(const Nll& a, const Fit& f, const double* tot, int g0, int cnt, int iter,
-                                            int do_update) {
+                                            int do_update, const RpState& in, const RpState& out, bool write,
+                                            double* newraw) {
   const int i = threadIdx.x >> 4, k = threadIdx.x & 15;
   if (i >= cnt) return;
   const int g = g0 + i;
   const double* v = tot + i * a.nq;
   const int dl = a.ls_pd ? a.d : 1;
-  if (k == 0) {
+  if (k == 0 && write) {
     const double term2 = a.logdet_weight * v[1];
     double* lh = f.loss_hist + ((int64_t)iter * (f.hist_stride ? f.hist_stride : a.G) + f.hist_offset + g) * 3;
     lh[0] = 0.5 * (v[0] + term2 + f.mll_const);
@@ -306,19 +340,27 @@ __device__ __forceinline__ void spec_finish(const Nll& a, const Fit& f, const do
     rg = f.noise_rg;
     gp = 0.0;
   }
-  const double raw_p = f.raw[p], prev_p = f.prev[p], step_p = f.step[p];
+  const double raw_p = in.raw[p], prev_p = in.prev[p], step_p = in.step[p];
   if (k == dl + 1) gp = exp(raw_p) * v[2];
-  f.raw_hist[(int64_t)iter * f.n_params + p] = raw_p;
-  f.grad_out[p] = gp;
-  if (!(do_update && rg)) return;
-  const double prod = gp * prev_p;
-  const double sgn = prod > 0.0 ? f.eta_plus : (prod < 0.0 ? f.eta_minus : 1.0);
-  const double st = fmin(fmax(step_p * sgn, f.step_min), f.step_max);
-  f.step[p] = st;
-  const double gg = (sgn == f.eta_minus) ? 0.0 : gp;
-  const double gs = gg > 0.0 ? 1.0 : (gg < 0.0 ? -1.0 : 0.0);
-  f.raw[p] = raw_p + (-1.0) * (gs * st);
-  f.prev[p] = gg;
+  if (write) {
+    f.raw_hist[(int64_t)iter * f.n_params + p] = raw_p;
+    f.grad_out[p] = gp;
+  }
+  double nraw = raw_p, nstep = step_p, nprev = prev_p;
+  if (do_update && rg) {
+    const double prod = gp * prev_p;
+    const double sgn = prod > 0.0 ? f.eta_plus : (prod < 0.0 ? f.eta_minus : 1.0);
+    nstep = fmin(fmax(step_p * sgn, f.step_min), f.step_max);
+    nprev = (sgn == f.eta_minus) ? 0.0 : gp;
+    const double gs = nprev > 0.0 ? 1.0 : (nprev < 0.0 ? -1.0 : 0.0);
+    nraw = raw_p + (-1.0) * (gs * nstep);
+  }
+  if (write) {
+    out.raw[p] = nraw;
+    out.step[p] = nstep;
+    out.prev[p] = nprev;
+  }
+  if (newraw) newraw[p] = nraw;
 }
 
 // The per-problem step of the spectral path as its own launch (fgp_fit_step, stage-by-stage fits):
@@ -342,7 +384,19 @@ __global__ __launch_bounds__(kWG) void k_spec_reduce_step(Nll a, Fit f, int iter
     tot[threadIdx.x] = s;
   }
   __syncthreads();
-  spec_finish<D>(a, f, tot, g0, cnt, iter, do_update);
+  const RpState st{f.raw, f.prev, f.step};
+  spec_finish<D>(a, f, tot, g0, cnt, iter, do_update, st, st, true, nullptr);
+}
+
+// The deferred step of a fused spectral run's LAST iteration (its own launch, one workgroup): the level-2 sum
+// of that iteration's group sums (parity fz.par ^ 1 as k_spec_tile's prologue reads them) and the step from
+// fz.sin to fz.sout (the fit's own state vectors)
+template <int D>
+__global__ __launch_bounds__(kWG) void k_spec_finish_step(Nll a, FitFuse fz) {
+  __shared__ double tot[16 * (4 + D)];
+  spec_level2<D>(a, fz.par ^ 1, tot);
+  __syncthreads();
+  spec_finish<D>(a, fz.f, tot, 0, a.G, fz.iter - 1, fz.do_update, fz.sin, fz.sout, true, nullptr);
 }
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -409,13 +463,9 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
   const int64_t B = 64 * (int64_t)a.spec_kpl;       // frequencies per block
   const int blk = (int)blockIdx.x * NBW + bw;
   stamp_begin(a);
-  Hyp h[PPW];
   bool on[PPW];
 #pragma unroll
-  for (int p = 0; p < PPW; ++p) {
-    on[p] = g0 + p < G;
-    load_hyp_wave(a, on[p] ? g0 + p : 0, h[p]);
-  }
+  for (int p = 0; p < PPW; ++p) on[p] = g0 + p < G;
   const double rootn = sqrt((double)((int64_t)1 << a.log2n)), wl = a.logdet_weight;
   const int64_t wg_base = (int64_t)blockIdx.x * NBW * B;
   // chunk c into buffer buf: piece i (16 bytes) = segment i / (32 rows) (the workgroup's block), row
@@ -453,6 +503,24 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
 #pragma unroll
   for (int c = 0; c < RING - 1; ++c)
     if (c < nc) issue(c, lds + c * tile);
+  // The parameters of this iteration.  With fz.pending the previous iteration's step was deferred into
+  // this launch: every workgroup sums its group sums (level 2, fixed order) and applies the Rprop step
+  // (identical arithmetic, identical results), workgroup 0 alone storing histories and the new state,
+  // while the first chunks are in flight; the parameters then come from LDS (scratch after the ring).
+  Hyp h[PPW];
+  if (fz.counters && fz.pending) {
+    double* tot = lds + RING * tile;                // [G nq] level-2 totals, then [np] new raw parameters
+    double* nraw = tot + G * a.nq;
+    spec_level2<D>(a, fz.par ^ 1, tot);
+    __syncthreads();
+    spec_finish<D>(a, fz.f, tot, 0, G, fz.iter - 1, 1, fz.sin, fz.sout, blockIdx.x == 0, nraw);
+    __syncthreads();
+#pragma unroll
+    for (int p = 0; p < PPW; ++p) load_hyp_wave(a, on[p] ? g0 + p : 0, h[p], nraw);
+  } else {
+#pragma unroll
+    for (int p = 0; p < PPW; ++p) load_hyp_wave(a, on[p] ? g0 + p : 0, h[p]);
+  }
   for (int c = 0; c < nc; ++c) {
     // this wave's loads of chunk c have landed (chunks c + 1 .. c + RING - 2 may stay in flight)
     wait_vmcnt(cnt_w * min(RING - 2, nc - 1 - c));
@@ -475,16 +543,14 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
   for (int p = 0; p < PPW; ++p)
     if (on[p] && active) spec_block_partials<D, NET>(a, h[p], g0 + p, blk, rootn, wl, acc[p], fz.counters != nullptr);
   if (fz.counters) {
-    // Fused step, two hand-offs (MI355X_MICROARCH.md hand-off row 1: sc1 stores retired by every storing
-    // wave, then ONE lane's agent-scope add; the waiter reads with sc1 loads after a barrier):
-    //   1. the last workgroup of each group of kSpecGroup blocks sums the group (level 1, sc1 store);
-    //   2. the last of the ng group finishers sums the groups (level 2) and applies every problem's Rprop.
-    const int ng = spec_groups(a), grp = (int)blockIdx.x * NBW / kSpecGroup;
+    // Level 1 of the fused reduction (MI355X_MICROARCH.md hand-off row 1: sc1 stores retired by every
+    // storing wave, then ONE lane's agent-scope add; the waiter reads with sc1 loads after a barrier): the
+    // last workgroup of each group of kSpecGroup blocks sums the group into the level-2 inputs of parity
+    // fz.par.  Level 2 and the step follow in the next launch's prologue (or k_spec_finish_step).
+    const int grp = (int)blockIdx.x * NBW / kSpecGroup;
     const int wg_in_grp = (min(kSpecGroup, a.nb - grp * kSpecGroup) + NBW - 1) / NBW;
     unsigned* cnt_grp = fz.counters + grp;
-    unsigned* cnt_all = fz.counters + ng;
     int* flag = reinterpret_cast<int*>(lds);        // the ring is free now
-    double* tot = lds + 2;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) flag[0] = __hip_atomic_fetch_add(cnt_grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
@@ -494,36 +560,10 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
       const int t = threadIdx.x;
       if (t < G * a.nq) {
         const int g = t / a.nq, q = t % a.nq;
-        __hip_atomic_store(part2_ptr(a, g, q, grp), spec_group_sum<true>(a, g, q, grp), __ATOMIC_RELAXED,
+        __hip_atomic_store(part2_ptr(a, fz.par, g, q, grp), spec_group_sum<true>(a, g, q, grp), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        __hip_atomic_store(cnt_grp, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        flag[1] = __hip_atomic_fetch_add(cnt_all, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                  (unsigned)(ng - 1);
-      }
-      __syncthreads();
-      if (flag[1]) {
-        if (t < G * a.nq) {
-          // every group's sum in flight at once (a serial chain of ng agent-scope loads costs ~1 us
-          // each), then added ascending -- k_spec_reduce_step's order
-          constexpr int MAXG = kSpecBlocks / kSpecGroup;
-          const int g = t / a.nq, q = t % a.nq;
-          double v[MAXG];
-#pragma unroll
-          for (int gr = 0; gr < MAXG; ++gr) v[gr] = ld_part<true>(part2_ptr(a, g, q, gr < ng ? gr : 0));
-          double s = 0.0;
-#pragma unroll
-          for (int gr = 0; gr < MAXG; ++gr)
-            if (gr < ng) s += v[gr];
-          tot[t] = s;
-        }
-        __syncthreads();
-        spec_finish<D>(a, fz.f, tot, 0, G, fz.iter, fz.do_update);
-        if (threadIdx.x == 0) __hip_atomic_store(cnt_all, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+      if (threadIdx.x == 0) __hip_atomic_store(cnt_grp, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   stamp_end(a);
@@ -597,7 +637,7 @@ void spec_geometry(Nll& a) {
     const int ck = 64 * (4 / pgp);   // frequencies per chunk (64 per block of the workgroup)
     // the ring <= kSpecLdsMax (two workgroups per CU), whole 1-KiB wave-instructions, <= 6 per wave
     const int rows = (1 << a.d) + a.G;
-    if (rows * ck * 8 * kSpecRing <= kSpecLdsMax && rows * ck <= 3072 && (rows * ck) % 128 == 0 &&
+    if (rows * ck * 8 * kSpecRing + kSpecScratch * 8 <= kSpecLdsMax && rows * ck <= 3072 && (rows * ck) % 128 == 0 &&
         a.nb % (4 / pgp) == 0 &&
         a.spec_main % (64 * (int64_t)a.nb) == 0) {
       a.spec_tile = 1;
@@ -619,7 +659,7 @@ int launch_spec_iter(const Nll& a, hipStream_t st, const FitFuse* fz) {
     FitFuse none{};
     none.counters = nullptr;
     const FitFuse& f = fz ? *fz : none;
-    const size_t shm = sizeof(double) * (size_t)kSpecRing * (size_t)(((1 << a.d) + a.G) * a.spec_ck);
+    const size_t shm = sizeof(double) * ((size_t)kSpecRing * (size_t)(((1 << a.d) + a.G) * a.spec_ck) + kSpecScratch);
     const unsigned grid = (unsigned)(a.nb / (4 / a.spec_pgp));
     return with_spec_d(a.d, [&](auto dc) {
       constexpr int D = decltype(dc)::value;
@@ -675,9 +715,18 @@ int launch_spec_reduce_step(const Nll& a, const Fit& f, int iter, int do_update,
 
 int spec_counters_offset(const Nll& a, int64_t* off, int* count) {
   const int ng = (a.nb + kSpecGroup - 1) / kSpecGroup;
-  *off = (int64_t)a.G * a.nq * (a.nb + ng);
-  *count = ng + 1;
+  *off = spec_part2_off(a, 2) + 2 * 3 * (int64_t)spec_nparams(a);
+  *count = ng;
   return kOk;
+}
+
+RpState spec_scratch_state(const Nll& a, int par) { return spec_state(a, par); }
+
+int launch_spec_finish_step(const Nll& a, const FitFuse& fz, hipStream_t st) {
+  return with_spec_d(a.d, [&](auto dc) {
+    k_spec_finish_step<decltype(dc)::value><<<1, kWG, 0, st>>>(a, fz);
+    return check_launch("k_spec_finish_step");
+  });
 }
 
 int launch_spec_lam(const Nll& a, hipStream_t st) {
