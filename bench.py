@@ -400,7 +400,7 @@ STAGES = ("k_fwd_rows", "k_fwd_cols", "k_bwd_rows")
 SPEC_BLOCKS = 512      # k blocks per problem of the spectral iteration (csrc/fgp_nll.h kSpecBlocks)
 
 
-SPEC_RING, SPEC_LDS_MAX = 2, 80 * 1024     # csrc/fgp_nll.h kSpecRing / kSpecLdsMax
+SPEC_RING, SPEC_LDS_MAX, SPEC_MAX_DMA = 2, 80 * 1024, 10     # csrc/fgp_nll.h kSpecRing / kSpecLdsMax / kSpecMaxDma
 
 
 def stage_names(variant):
@@ -411,10 +411,31 @@ def stage_names(variant):
     return ("k_spec_iter",) if variant == "spectral" else STAGES
 
 
-def spec_geometry(n, d, G, shared=True, family=0):
-    """(k blocks, problems per wave, problem groups) of k_spec_iter (csrc/fgp_spectral.hip spec_geometry)."""
+def spec_tile_geometry(n, d, G, shared=True, family=0):
+    """(workgroups, problems per wave, problem groups) of the LDS-ring tile kernel k_spec_tile, or None when
+    spec_geometry picks the per-wave k_spec_iter (the conditions of csrc/fgp_spectral.hip spec_geometry)."""
     main = n // 2 if family == 0 else n
     nb = min(SPEC_BLOCKS, max(1, main // 64))
+    if not (shared and d <= 5 and main >= 256) or os.environ.get("FGP_SPEC_TILE", "1")[:1] == "0":
+        return None
+    ppw = 2 if G >= 2 else 1
+    pg = (G + ppw - 1) // ppw
+    pgp = 1 if pg <= 1 else (2 if pg <= 2 else 4)
+    ck = 64 * (4 // pgp)
+    rows = 2 ** d + G
+    ok = (pg <= 4 and rows * ck * 8 * SPEC_RING <= SPEC_LDS_MAX and rows * ck <= 512 * SPEC_MAX_DMA and
+          (rows * ck) % 128 == 0 and rows * ck >= 256 and nb % (4 // pgp) == 0 and main % (64 * nb) == 0)
+    return (nb // (4 // pgp), ppw, pg) if ok else None
+
+
+def spec_geometry(n, d, G, shared=True, family=0):
+    """(k blocks, problems per wave, problem groups) of the spectral iteration (csrc/fgp_spectral.hip
+    spec_geometry): the tile kernel's when it applies, else k_spec_iter's."""
+    main = n // 2 if family == 0 else n
+    nb = min(SPEC_BLOCKS, max(1, main // 64))
+    t = spec_tile_geometry(n, d, G, shared, family)
+    if t is not None:
+        return nb, t[1], t[2]
     ppw = 2 if (G >= 2 and shared and d <= 5) else 1
     if ppw == 2 and G > 8 and d <= 3:
         ppw = 4
@@ -422,18 +443,9 @@ def spec_geometry(n, d, G, shared=True, family=0):
 
 
 def spec_tile_grid(n, d, G, shared=True, family=0):
-    """Workgroups of the LDS-ring tile kernel k_spec_tile, or None when spec_geometry picks the per-wave
-    k_spec_iter (the conditions of csrc/fgp_spectral.hip spec_geometry)."""
-    main = n // 2 if family == 0 else n
-    nb, ppw, pg = spec_geometry(n, d, G, shared, family)
-    if not (shared and ppw <= 2 and pg <= 4 and d <= 5 and main >= 256) or os.environ.get("FGP_SPEC_TILE", "1")[:1] == "0":
-        return None
-    pgp = 1 if pg <= 1 else (2 if pg <= 2 else 4)
-    ck = 64 * (4 // pgp)
-    rows = 2 ** d + G
-    ok = (rows * ck * 8 * SPEC_RING <= SPEC_LDS_MAX and rows * ck <= 3072 and (rows * ck) % 128 == 0 and
-          nb % (4 // pgp) == 0 and main % (64 * nb) == 0)
-    return nb // (4 // pgp) if ok else None
+    """Workgroups of the LDS-ring tile kernel k_spec_tile, or None (per-wave k_spec_iter)."""
+    t = spec_tile_geometry(n, d, G, shared, family)
+    return None if t is None else t[0]
 
 
 def spec_fused(n, d, G):

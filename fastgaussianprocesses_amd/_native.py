@@ -12,7 +12,7 @@ import torch
 
 _LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
 LIB_PATH = os.environ.get("FGP_LIB_PATH") or os.path.join(_LIB_DIR, "libfgp_hip.so")   # override: experiments
-ABI_VERSION = 11
+ABI_VERSION = 12
 MT_MAX_TASKS = 16
 MAX_D = 8
 PARTS_ARRAY = 0
@@ -47,6 +47,7 @@ class NllDesc(ctypes.Structure):
         ("gen_shift", _c_vp), ("gen_shift_stride", _c_i64),
         ("stamps", _c_vp),
         ("basis", _c_vp), ("basis_stride", _c_i64), ("ysq_chunked", _c_int),
+        ("mt_tasks", _c_int), ("mt_basis", _c_vp), ("mt_ytilde", _c_vp), ("mt_kt", _c_vp),
     ]
 
 

@@ -107,7 +107,7 @@ __device__ __forceinline__ double2 cmul_cj(double2 a, double2 b) {   // conj(a) 
 // so Lambda = L D L^H with L[(l, q mod q_l), (k, q)] = conj(u_kl[q]), and the factor lives in the packed
 // layout of the lams themselves: D on the diagonal entries, u on the coupling entries.  Work per
 // frequency class is R T^2 / 2 instead of the R^3 / 3 of a dense factorisation (and the reference's
-// bordering, util.py:301-323, which grows a dense [R, R] inverse).  logdet_j = sum log D.
+// bordering, util.py:301-323, which grows a dense [R, R] inverse).  logdet_j = sum log |D|.
 __global__ __launch_bounds__(kWG) void k_mt_ldl(const double2* __restrict__ lp, int64_t G, MtLay lay,
                                                 double2* __restrict__ fac, double* __restrict__ logdet,
                                                 int* __restrict__ info) {
@@ -126,7 +126,7 @@ __global__ __launch_bounds__(kWG) void k_mt_ldl(const double2* __restrict__ lp, 
     for (int q = 0; q < qk; ++q) {
       double dq = Dk[(int64_t)q * nm].x;
       if (!(dq > 0.0)) bad = true;
-      ld += log(dq);
+      ld += log(fabs(dq));      // log|S| as the reference's recursion takes it (util.py:299,310)
       Dk[(int64_t)q * nm] = make_double2(dq, 0.0);
       const double idq = 1.0 / dq;
       // updates of the later tasks' blocks (from the unscaled couplings c = D u), then u = c / D
@@ -146,7 +146,7 @@ __global__ __launch_bounds__(kWG) void k_mt_ldl(const double2* __restrict__ lp, 
       }
     }
   }
-  logdet[e] = bad ? __builtin_nan("") : ld;
+  logdet[e] = ld;            // a non-positive pivot still counts as log|pivot| (the reference's log|S|); info flags it
   if (bad) info[0] = 1;
 }
 

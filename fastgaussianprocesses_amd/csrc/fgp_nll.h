@@ -41,6 +41,12 @@ struct Nll {
   int spec_tile, spec_pgp, spec_ck;  // LDS-tiled kernel: problem-group slots, frequencies per chunk
   int64_t spec_kw;                   // ... and per workgroup
   int ysq_chunked;                   // ysq in the chunked layout [k / 64][G][64] (spectral path)
+  // multitask spectral fit (ABI 12, fgp_spectral.hip k_mt_spec_iter): T tasks (0: off), pair spectra,
+  // ytilde, task kernel; mt_F frequencies per chunk, mt_cpb chunks per block
+  int mt, mt_F, mt_cpb;
+  const void* mt_basis;
+  const void* mt_ytilde;
+  const double* mt_kt;
 };
 
 // Device-clock kernel timing (fgp_nll_desc.stamps; off when NULL -- a uniform branch on a kernel
@@ -569,7 +575,8 @@ constexpr int kSpecRing = FGP_SPEC_RING;         // LDS ring depth of the spectr
 #define FGP_SPEC_LDS_KB 80
 #endif
 constexpr int kSpecLdsMax = FGP_SPEC_LDS_KB * 1024;   // its dynamic LDS per workgroup, at most (80: 2 per CU)
-constexpr int kSpecScratch = 256;                  // doubles after the ring: the deferred step's totals / parameters
+constexpr int kSpecScratch = 256;                  // doubles of the deferred step's totals / parameters (ring slot RING-1)
+constexpr int kSpecMaxDma = 10;                    // LDS-DMA wave-instructions per wave and chunk (tile <= 5120 doubles)
 void spec_geometry(Nll& a);                        // nb and the spec_* fields of a spectral desc
 int64_t spec_chunks(bool net, int log2n);          // 64-frequency chunks of the spectra (fgp_spec_basis layout)
 // one fit iteration (loss + gradient partials); with fz (tile kernel only) also the reduction + Rprop
@@ -582,6 +589,10 @@ RpState spec_scratch_state(const Nll& a, int par);
 // the deferred step of a fused spectral run's last iteration (after its last k_spec_tile launch)
 int launch_spec_finish_step(const Nll& a, const FitFuse& fz, hipStream_t st);
 int launch_spec_lam(const Nll& a, hipStream_t st);    // lambda of the current parameters into grad_lam
+// multitask spectral fit (ABI 12): at most kMtMaxT tasks, kMtF frequencies per chunk
+constexpr int kMtMaxT = 8;
+constexpr int kMtF = 32;
+int launch_mt_spec_iter(const Nll& a, hipStream_t st);   // loss / gradient partials of one iteration
 // lattice spectra of the subsets s0 .. s0 + cnt - 1 (log2n >= 17) by the fused R2C pair: products formed in
 // the row kernel, real parts k <= n/2 written by the column kernel (work: 16 n cnt bytes)
 int spec_basis_r2c(const double* parts, int d, int log2n, int s0, int cnt, double* basis, void* work, hipStream_t st);

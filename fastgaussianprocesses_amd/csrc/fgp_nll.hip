@@ -1165,13 +1165,18 @@ static int to_nll(const fgp_nll_desc* d, Nll& a) {
   if (d->log2n < 4 || d->log2n > kMaxLog2N) return set_error(kErrUnsupported, "fused fit needs 4 <= log2n <= 24");
   if (d->d < 1 || d->d > FGP_MAX_D) return set_error(kErrUnsupported, "d=%d outside [1, %d]", d->d, FGP_MAX_D);
   if (d->G < 1) return set_error(kErrInvalid, "G < 1");
-  if (!d->ysq || !d->raw || !d->partials || (d->log2n > 12 && !d->work && !d->basis))
+  const bool mt = d->mt_tasks != 0;
+  if (!d->ysq || !d->raw || !d->partials || (d->log2n > 12 && !d->work && !d->basis && !mt))
     return set_error(kErrInvalid, "null pointer in nll desc");
+  if (mt && (d->mt_tasks < 1 || d->mt_tasks > kMtMaxT || d->G != 1 || d->d > kSpecMaxD || d->basis))
+    return set_error(kErrUnsupported, "multitask spectral fit: needs 1 <= T <= %d, G = 1, d <= %d, no basis",
+                     kMtMaxT, kSpecMaxD);
+  if (mt && (!d->mt_basis || !d->mt_ytilde || !d->mt_kt)) return set_error(kErrInvalid, "null pointer in nll desc (mt)");
   if (d->basis && d->d > kSpecMaxD)
     return set_error(kErrUnsupported, "spectral fit path: d = %d > %d", d->d, kSpecMaxD);
   if (d->basis && d->basis_stride < 0) return set_error(kErrInvalid, "negative basis_stride");
   if (d->parts_gen == FGP_PARTS_ARRAY) {
-    if (!d->parts && !d->basis) return set_error(kErrInvalid, "null parts in nll desc");
+    if (!d->parts && !d->basis && !mt) return set_error(kErrInvalid, "null parts in nll desc");
   } else if (d->parts_gen == FGP_PARTS_LATTICE) {
     if (d->family != FGP_FAMILY_LATTICE) return set_error(kErrInvalid, "lattice parts generator needs the lattice family");
     if (!d->gen_shift) return set_error(kErrInvalid, "null gen_shift in nll desc");
@@ -1246,6 +1251,23 @@ static int to_nll(const fgp_nll_desc* d, Nll& a) {
   if (a.spec) {
     a.re = a.r2c = 0;
     spec_geometry(a);
+  }
+  a.mt = 0;
+  a.mt_F = a.mt_cpb = 0;
+  a.mt_basis = d->mt_basis;
+  a.mt_ytilde = d->mt_ytilde;
+  a.mt_kt = d->mt_kt;
+  if (mt) {
+    // one chunk of kMtF frequencies per step, up to kSpecBlocks blocks (the spectral reduction's limit)
+    const int64_t n = (int64_t)1 << d->log2n;
+    a.mt = d->mt_tasks;
+    a.spec = 1;                      // the per-problem step is the spectral path's (k_spec_reduce_step)
+    a.spec_net = d->family == FGP_FAMILY_NET;
+    a.re = a.r2c = 0;
+    a.mt_F = (int)std::min<int64_t>(kMtF, n);
+    const int64_t chunks = n / a.mt_F;
+    a.nb = (int)std::min<int64_t>(kSpecBlocks, chunks);
+    a.mt_cpb = (int)(chunks / a.nb);
   }
   return kOk;
 }
@@ -1378,6 +1400,10 @@ static int nll_stage_t(const Nll& a, int stage, const Tables* tb, hipStream_t st
 }
 
 static int nll_stage(const Nll& a, int stage, hipStream_t st, bool lattice) {
+  if (a.mt) {
+    if (stage < 0 || stage > 2) return set_error(kErrInvalid, "bad stage %d", stage);
+    return stage == 0 ? launch_mt_spec_iter(a, st) : kOk;
+  }
   if (a.spec) {
     if (stage < 0 || stage > 2) return set_error(kErrInvalid, "bad stage %d", stage);
     return stage == 0 ? launch_spec_iter(a, st) : kOk;
@@ -1532,6 +1558,7 @@ int fgp_nll_lam(const fgp_nll_desc* desc, void* stream) {
   int rc = to_nll(desc, a);
   if (rc != kOk) return rc;
   if (!desc->grad_lam) return set_error(kErrInvalid, "fgp_nll_lam: null grad_lam (the output)");
+  if (a.mt) return set_error(kErrUnsupported, "fgp_nll_lam: not available for the multitask spectral fit");
   if (a.spec) return launch_spec_lam(a, (hipStream_t)stream);
   if (a.re && !a.r2c) {   // n = 2^16: lambda by the full-length kernels (their block count)
     a.re = false;

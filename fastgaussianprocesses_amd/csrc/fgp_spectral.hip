@@ -1,4 +1,4 @@
-// Part-product spectra: the spectral fit path (ABI 11).  See DESIGN.md section 3 "Spectral fit".
+// Part-product spectra: the spectral fit path (ABI 11; multitask ABI 12).  See DESIGN.md section 3 "Spectral fit".
 //
 // The first-column kernel of both families is a multilinear polynomial in the lengthscales:
 //   k1 = scale prod_j (1 + l_j part_j) = scale sum_{S subset of {0..d-1}} l^S b_S,
@@ -474,7 +474,8 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
   // pieces [64 j, 64 j + 64); this wave's instructions j = w + 4 t (t < cnt_w <= kMaxDma): chunk-0 source
   // and per-chunk step per lane, formed once (a chunk further is NS 64 doubles on in the chunked spectra,
   // 64 in a Y row).
-  constexpr int kMaxDma = 6;                        // tile <= 3072 doubles: 24 instructions, 6 per wave
+  constexpr int kMaxDma = kSpecMaxDma;              // tile <= 512 kMaxDma doubles: 1-KiB instructions, kMaxDma per wave
+  static_assert(kSpecRing >= 2, "the deferred step's scratch lives in ring slot RING - 1");
   const double* src0[kMaxDma];
   int64_t step[kMaxDma];
 #pragma unroll
@@ -509,7 +510,8 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
   // while the first chunks are in flight; the parameters then come from LDS (scratch after the ring).
   Hyp h[PPW];
   if (fz.counters && fz.pending) {
-    double* tot = lds + RING * tile;                // [G nq] level-2 totals, then [np] new raw parameters
+    double* tot = lds + (RING - 1) * tile;          // [G nq] level-2 totals, then [np] new raw parameters, in the
+                                                    // ring slot no chunk is loaded into before the loop
     double* nraw = tot + G * a.nq;
     spec_level2<D>(a, fz.par ^ 1, tot);
     __syncthreads();
@@ -594,6 +596,200 @@ __global__ __launch_bounds__(kWG) void k_spec_lam(Nll a) {
   }
 }
 
+// ---------------------------------------------------------------- multitask spectral fit (ABI 12)
+// One multitask / derivative-informed GP of T tasks with equal n (include/fgp_hip.h mt_tasks): the reference
+// inverts, per frequency j, the T x T Hermitian block Lambda_j of its lams (util.py:277-337) and forms
+// norm = Re sum_j y_j^H Lambda_j^-1 y_j and logdet = sum_j log|det Lambda_j| (util.py:364-370), y_j = (ytilde_k[j])_k;
+// autograd then differentiates through the block recursion and the transforms.  Here the pair eigenvalues
+// come from the pair spectra (lambda_kl = scale sum_S l^S Phi^{kl}_S, the part-product spectra of the
+// single-task path, per task pair), the block is factored LDL^H in LDS, and the gradient is the closed form
+//   dL = 1/2 tr(W dLambda),  W = Lambda^-1 - z z^H,  z = Lambda^-1 y:
+//   dL/draw_scale = sum_j sum_{k<=l} w_kl Re(W[l,k] dLambda[k,l]/draw_scale),  w = 1/2 (k = l) or 1,
+//   dLambda[k,l]/draw_scale = Kt[k,l] sqrt(n) scale P_kl,
+//   dLambda[k,l]/draw_l_m   = Kt[k,l] sqrt(n) scale sum_{S contains m} l^S Phi^{kl}_S   (l_m dP/dl_m),
+//   dL/dnoise = 1/2 sum_k Re W[k,k] Kt[k,k]
+// -- the quantities of the single-task partials (norm, logdet, dL/dnoise, dL/draw_scale, dL/draw_l), so
+// k_spec_reduce_step reduces them and applies the Rprop step (G = 1).  Workgroup = block of mt_cpb chunks of
+// F frequencies: (1) threads over (pair, frequency) evaluate the pair polynomials into the blocks (LDS),
+// (2) one thread per frequency factors its block, solves, and forms W (LDS), (3) threads over (pair,
+// frequency) contract W with the spectra; fixed per-thread orders and a fixed block reduction.
+__device__ __forceinline__ double2 mt_phi(const Nll& a, int64_t idx) {
+  if (a.spec_net) return make_double2(static_cast<const double*>(a.mt_basis)[idx], 0.0);
+  return static_cast<const double2*>(a.mt_basis)[idx];
+}
+
+__device__ __forceinline__ void mt_pair_kl(int p, int T, int& k, int& l) {
+  k = 0;
+  while (p >= T - k) {
+    p -= T - k;
+    ++k;
+  }
+  l = k + p;
+}
+
+template <int D>
+__global__ __launch_bounds__(kWG) void k_mt_spec_iter(Nll a) {
+  constexpr int NS = 1 << D, NQ = 4 + D;
+  __shared__ double ls_pow[NS];                          // l^S
+  __shared__ double kt[kMtMaxT * kMtMaxT];
+  __shared__ double2 blk[kMtF][kMtMaxT * kMtMaxT];       // Lambda_j (full), factored in place
+  __shared__ double2 wv[kMtF][kMtMaxT * (kMtMaxT + 1) / 2];   // W[l, k] of pair (k, l)
+  __shared__ double red[kWG / 64];
+  const int T = a.mt, NP = T * (T + 1) / 2, F = a.mt_F, tid = threadIdx.x;
+  const int64_t n = (int64_t)1 << a.log2n;
+  stamp_begin(a);
+  Hyp h;
+  load_hyp_wave(a, 0, h);
+  if (tid < NS) {
+    double pw = 1.0;
+#pragma unroll
+    for (int j = 0; j < D; ++j)
+      if ((tid >> j) & 1) pw *= h.ls[j];
+    ls_pow[tid] = pw;
+  }
+  if (tid < T * T) kt[tid] = a.mt_kt[tid];
+  const double rootn = sqrt((double)n), sn = rootn * h.scale;
+  double acc_norm = 0.0, acc_ld = 0.0, acc_noise = 0.0, acc_sc = 0.0, acc_l[D];
+#pragma unroll
+  for (int m = 0; m < D; ++m) acc_l[m] = 0.0;
+  for (int c = 0; c < a.mt_cpb; ++c) {
+    const int64_t j0 = ((int64_t)blockIdx.x * a.mt_cpb + c) * F;
+    __syncthreads();                                     // ls_pow / kt ready; previous chunk's wv consumed
+    // (1) Lambda[k, l] = Kt[k, l] (sqrt(n) scale P_kl + noise [k == l]) (the reference's order of operations)
+    for (int it = tid; it < NP * F; it += kWG) {
+      const int p = it / F, f = it - p * F;
+      int k, l;
+      mt_pair_kl(p, T, k, l);
+      const int64_t base = (int64_t)p * NS * n + j0 + f;
+      double2 P = make_double2(0.0, 0.0);
+#pragma unroll
+      for (int S = 0; S < NS; ++S) {
+        const double2 ph = mt_phi(a, base + (int64_t)S * n);
+        P.x = __builtin_fma(ls_pow[S], ph.x, P.x);
+        P.y = __builtin_fma(ls_pow[S], ph.y, P.y);
+      }
+      const double q = kt[k * T + l];
+      double2 v = make_double2(sn * P.x, sn * P.y);
+      if (k == l) v.x += h.noise;
+      v = make_double2(v.x * q, v.y * q);
+      blk[f][k * T + l] = v;
+      if (k != l) blk[f][l * T + k] = make_double2(v.x, -v.y);
+    }
+    __syncthreads();
+    // (2) per frequency: LDL^H (L strictly below the diagonal of blk, pivots Dg), logdet, z = Lambda^-1 y,
+    // norm, X = L^-1 (strictly lower, stored transposed in the upper triangle), W = Lambda^-1 - z z^H
+    if (tid < F) {
+      double2* A = blk[tid];
+      const int64_t j = j0 + tid;
+      double Dg[kMtMaxT];
+      double2 y[kMtMaxT], z[kMtMaxT];
+      for (int k = 0; k < T; ++k) {
+        double dk = A[k * T + k].x;
+        for (int m = 0; m < k; ++m) {
+          const double2 L = A[k * T + m];
+          dk -= (L.x * L.x + L.y * L.y) * Dg[m];
+        }
+        Dg[k] = dk;
+        for (int i = k + 1; i < T; ++i) {
+          double2 s = A[i * T + k];
+          for (int m = 0; m < k; ++m) {
+            const double2 t = cmulc(A[i * T + m], A[k * T + m]);   // L[i][m] conj(L[k][m])
+            s.x -= t.x * Dg[m];
+            s.y -= t.y * Dg[m];
+          }
+          A[i * T + k] = make_double2(s.x / dk, s.y / dk);
+        }
+        acc_ld += log(fabs(dk));
+      }
+      for (int k = 0; k < T; ++k) {
+        if (a.spec_net) y[k] = make_double2(static_cast<const double*>(a.mt_ytilde)[(int64_t)k * n + j], 0.0);
+        else y[k] = static_cast<const double2*>(a.mt_ytilde)[(int64_t)k * n + j];
+      }
+      // forward: w = L^-1 y (in z), norm = sum |w_k|^2 / D_k, then u = w / D, backward L^H z = u
+      for (int i = 0; i < T; ++i) {
+        double2 s = y[i];
+        for (int m = 0; m < i; ++m) {
+          const double2 t = cmul(A[i * T + m], z[m]);
+          s.x -= t.x;
+          s.y -= t.y;
+        }
+        z[i] = s;
+        acc_norm += (s.x * s.x + s.y * s.y) / Dg[i];
+      }
+      for (int i = 0; i < T; ++i) z[i] = make_double2(z[i].x / Dg[i], z[i].y / Dg[i]);
+      for (int i = T - 1; i >= 0; --i) {
+        double2 s = z[i];
+        for (int m = i + 1; m < T; ++m) {
+          const double2 t = cmulc(z[m], A[m * T + i]);            // conj(L[m][i]) z[m]
+          s.x -= t.x;
+          s.y -= t.y;
+        }
+        z[i] = s;
+      }
+      // X = L^-1: X[i][jj] = -(L[i][jj] + sum_{jj < m < i} L[i][m] X[m][jj]), stored at A[jj T + i]
+      for (int jj = 0; jj < T; ++jj)
+        for (int i = jj + 1; i < T; ++i) {
+          double2 s = A[i * T + jj];
+          for (int m = jj + 1; m < i; ++m) {
+            const double2 t = cmul(A[i * T + m], A[jj * T + m]);
+            s.x += t.x;
+            s.y += t.y;
+          }
+          A[jj * T + i] = make_double2(-s.x, -s.y);
+        }
+      // Lambda^-1[l][k] = sum_{m >= l} conj(X[m][l]) X[m][k] / D_m  (l >= k, X[m][m] = 1)
+      for (int p = 0, k = 0; k < T; ++k)
+        for (int l = k; l < T; ++l, ++p) {
+          double2 s = make_double2(0.0, 0.0);
+          for (int m = l; m < T; ++m) {
+            const double2 xl = m == l ? make_double2(1.0, 0.0) : A[l * T + m];
+            const double2 xk = m == k ? make_double2(1.0, 0.0) : A[k * T + m];
+            const double2 t = cmulc(xk, xl);                      // conj(X[m][l]) X[m][k]
+            s.x += t.x / Dg[m];
+            s.y += t.y / Dg[m];
+          }
+          const double2 zz = cmulc(z[l], z[k]);                  // z_l conj(z_k)
+          const double2 w = make_double2(s.x - zz.x, s.y - zz.y);
+          wv[tid][p] = w;
+          if (k == l) acc_noise += 0.5 * w.x * kt[k * T + k];
+        }
+    }
+    __syncthreads();
+    // (3) gradient: c = w_kl sqrt(n) scale Kt[k, l] W[l, k]; r_S = l^S Re(c Phi^{kl}_S)
+    for (int it = tid; it < NP * F; it += kWG) {
+      const int p = it / F, f = it - p * F;
+      int k, l;
+      mt_pair_kl(p, T, k, l);
+      const double wgt = (k == l ? 0.5 : 1.0) * sn * kt[k * T + l];
+      const double2 w = wv[f][p];
+      const double cx = wgt * w.x, cy = wgt * w.y;
+      const int64_t base = (int64_t)p * NS * n + j0 + f;
+#pragma unroll
+      for (int S = 0; S < NS; ++S) {
+        const double2 ph = mt_phi(a, base + (int64_t)S * n);
+        const double r = ls_pow[S] * (cx * ph.x - cy * ph.y);
+        acc_sc += r;
+#pragma unroll
+        for (int m = 0; m < D; ++m)
+          if ((S >> m) & 1) acc_l[m] += r;
+      }
+    }
+  }
+  double v[NQ];
+  v[0] = acc_norm;
+  v[1] = acc_ld;
+  v[2] = acc_noise;
+  v[3] = acc_sc;
+#pragma unroll
+  for (int m = 0; m < D; ++m) v[4 + m] = acc_l[m];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const double s = block_sum(v[q], red);
+    if (tid == 0) *part_ptr(a, 0, q, blockIdx.x) = s;
+  }
+  stamp_end(a);
+}
+
 template <typename Fn>
 static int with_spec_d(int d, Fn&& fn) {
   switch (d) {
@@ -621,9 +817,6 @@ void spec_geometry(Nll& a) {
   // problems (k_spec_iter, e.g. per-output hyper-parameters) 4 -- the spectra are then re-read from L2
   // G / 4 times instead of G / 2 and each wave's loads serve 4 evaluations.  d <= 3 only: 156 VGPRs,
   // 3 waves / SIMD there; at d = 4, 5 the four accumulator sets spill (8 per wave spills at d = 3)
-  a.spec_ppw = (a.G >= 2 && a.basis_stride == 0 && a.d <= 5) ? 2 : 1;
-  if (a.spec_ppw == 2 && a.G > 8 && a.d <= 3) a.spec_ppw = 4;
-  a.spec_pg = (a.G + a.spec_ppw - 1) / a.spec_ppw;
   const int64_t lanes = std::max<int64_t>(1, a.spec_main / 64);
   a.nb = (int)std::min<int64_t>(kSpecBlocks, lanes);
   a.spec_kpl = (int)((a.spec_main + 64 * (int64_t)a.nb - 1) / (64 * (int64_t)a.nb));
@@ -632,20 +825,35 @@ void spec_geometry(Nll& a) {
   a.spec_kw = 0;
   const char* te = getenv("FGP_SPEC_TILE");   // 0: the per-wave kernel only (A/B experiments)
   const bool tile_ok = !(te && te[0] == '0');
-  if (tile_ok && a.basis_stride == 0 && a.spec_ppw <= 2 && a.spec_pg <= 4 && a.d <= 5 && a.spec_main >= 256) {
-    const int pgp = a.spec_pg <= 1 ? 1 : (a.spec_pg <= 2 ? 2 : 4);
+  // Tile kernel (one shared set of spectra, d <= 5): 2 problems per wave (1 for G = 1), problem groups
+  // PG <= 4 in the 4 waves of a workgroup.  (4 problems per wave at G = 8 -- 233 VGPRs, 2 blocks per
+  // workgroup, 1024 blocks -- measured slower: 51.7 vs 42.0 us per C4 iteration, profiles/r03x_*.)
+  if (tile_ok && a.basis_stride == 0 && a.d <= 5 && a.spec_main >= 256) {
+    const int ppw = a.G >= 2 ? 2 : 1;
+    const int pg = (a.G + ppw - 1) / ppw;
+    const int pgp = pg <= 1 ? 1 : (pg <= 2 ? 2 : 4);
     const int ck = 64 * (4 / pgp);   // frequencies per chunk (64 per block of the workgroup)
-    // the ring <= kSpecLdsMax (two workgroups per CU), whole 1-KiB wave-instructions, <= 6 per wave
+    // the ring <= kSpecLdsMax (two workgroups per CU), whole 1-KiB wave-instructions, <= kSpecMaxDma per wave
     const int rows = (1 << a.d) + a.G;
-    if (rows * ck * 8 * kSpecRing + kSpecScratch * 8 <= kSpecLdsMax && rows * ck <= 3072 && (rows * ck) % 128 == 0 &&
-        a.nb % (4 / pgp) == 0 &&
+    if (pg <= 4 && rows * ck * 8 * kSpecRing <= kSpecLdsMax && rows * ck <= 512 * kSpecMaxDma &&
+        (rows * ck) % 128 == 0 && rows * ck >= kSpecScratch && a.nb % (4 / pgp) == 0 &&
         a.spec_main % (64 * (int64_t)a.nb) == 0) {
       a.spec_tile = 1;
+      a.spec_ppw = ppw;
+      a.spec_pg = pg;
       a.spec_pgp = pgp;
       a.spec_ck = ck;
       a.spec_kw = (int64_t)(4 / pgp) * 64 * a.spec_kpl;
+      return;
     }
   }
+  // per-wave kernel k_spec_iter: problems per wave sharing one read of the spectra, 2, and for many
+  // problems (e.g. per-output hyper-parameters) 4 -- the spectra are then re-read from L2 G / 4 times
+  // instead of G / 2 and each wave's loads serve 4 evaluations.  d <= 3 only: 156 VGPRs, 3 waves / SIMD
+  // there; at d = 4, 5 the four accumulator sets spill (8 per wave spills at d = 3)
+  a.spec_ppw = (a.G >= 2 && a.basis_stride == 0 && a.d <= 5) ? 2 : 1;
+  if (a.spec_ppw == 2 && a.G > 8 && a.d <= 3) a.spec_ppw = 4;
+  a.spec_pg = (a.G + a.spec_ppw - 1) / a.spec_ppw;
 }
 
 int64_t spec_chunks(bool net, int log2n) {
@@ -655,11 +863,11 @@ int64_t spec_chunks(bool net, int log2n) {
 
 int launch_spec_iter(const Nll& a, hipStream_t st, const FitFuse* fz) {
   if (a.spec_tile) {
-    if (a.spec_ppw > 2) return set_error(kErrInvalid, "spectral tile kernel: %d problems per wave", a.spec_ppw);
+    if (a.spec_ppw > 4) return set_error(kErrInvalid, "spectral tile kernel: %d problems per wave", a.spec_ppw);
     FitFuse none{};
     none.counters = nullptr;
     const FitFuse& f = fz ? *fz : none;
-    const size_t shm = sizeof(double) * ((size_t)kSpecRing * (size_t)(((1 << a.d) + a.G) * a.spec_ck) + kSpecScratch);
+    const size_t shm = sizeof(double) * (size_t)kSpecRing * (size_t)(((1 << a.d) + a.G) * a.spec_ck);
     const unsigned grid = (unsigned)(a.nb / (4 / a.spec_pgp));
     return with_spec_d(a.d, [&](auto dc) {
       constexpr int D = decltype(dc)::value;
@@ -675,10 +883,12 @@ int launch_spec_iter(const Nll& a, hipStream_t st, const FitFuse* fz) {
           kern<<<grid, kWG, shm, st>>>(a, f);
         };
         if (a.spec_net) {
-          if (a.spec_ppw == 2) go(k_spec_tile<D, 2, true>);
+          if (a.spec_ppw == 4) go(k_spec_tile<D, 4, true>);
+          else if (a.spec_ppw == 2) go(k_spec_tile<D, 2, true>);
           else go(k_spec_tile<D, 1, true>);
         } else {
-          if (a.spec_ppw == 2) go(k_spec_tile<D, 2, false>);
+          if (a.spec_ppw == 4) go(k_spec_tile<D, 4, false>);
+          else if (a.spec_ppw == 2) go(k_spec_tile<D, 2, false>);
           else go(k_spec_tile<D, 1, false>);
         }
         return check_launch("k_spec_tile");
@@ -703,6 +913,13 @@ int launch_spec_iter(const Nll& a, hipStream_t st, const FitFuse* fz) {
     if (a.spec_net) go(std::true_type{});
     else go(std::false_type{});
     return check_launch("k_spec_iter");
+  });
+}
+
+int launch_mt_spec_iter(const Nll& a, hipStream_t st) {
+  return with_spec_d(a.d, [&](auto dc) {
+    k_mt_spec_iter<decltype(dc)::value><<<(unsigned)a.nb, kWG, 0, st>>>(a);
+    return check_launch("k_mt_spec_iter");
   });
 }
 

@@ -645,10 +645,10 @@ class AbstractFastGP(torch.nn.Module):
     def _log_row(self, i, loss, t1, t2, indent):
         print(" " * indent + "%16.2e | %-10.2e | %-10.2e | %-10.2e" % (i, loss, t1, t2))
 
-    def _fit_fused(self, iterations, lr, stop, hists, verbose, indent, ysq=None, d_out=None):
-        """Device-resident MLL fit.  `ysq` / `d_out` override Y = sum_b |ytilde_b|^2 and the output
+    def _fused_engine(self, iterations, lr, ysq=None, d_out=None):
+        """The FusedMLL of this GP's fit: G eigen-problems from the part-product spectra, the regenerated
+        lattice parts or the parts array; `ysq` / `d_out` override Y = sum_b |ytilde_b|^2 and the output
         count (distributed.fit_sharded: Y all-reduced over the ranks' output shards)."""
-        logtol, wait_max = stop
         n = self._nh
         pb_shape, G = self._problem_batch()
         if d_out is None:
@@ -658,13 +658,19 @@ class AbstractFastGP(torch.nn.Module):
         parts = self._k1parts(n) if (gen is None and basis is None) else None
         ls_raw = self.raw_lengthscales.detach()
         ls2 = ls_raw.reshape(-1, ls_raw.shape[-1])
-        eng = FusedMLL(self._FAMILY, parts, self._ysq(pb_shape, G) if ysq is None else ysq,
-                       self.raw_scale.detach().reshape(-1), ls2,
-                       self.raw_noise.detach().reshape(-1), logdet_weight=d_out / G,
-                       mll_const=mll_constant(d_out, n),
-                       requires_grad=(self.raw_scale.requires_grad, self.raw_lengthscales.requires_grad,
-                                      self.raw_noise.requires_grad),
-                       lr=lr, max_iters=min(iterations + 1, 64), gen=gen, basis=basis)
+        return FusedMLL(self._FAMILY, parts, self._ysq(pb_shape, G) if ysq is None else ysq,
+                        self.raw_scale.detach().reshape(-1), ls2,
+                        self.raw_noise.detach().reshape(-1), logdet_weight=d_out / G,
+                        mll_const=mll_constant(d_out, n),
+                        requires_grad=(self.raw_scale.requires_grad, self.raw_lengthscales.requires_grad,
+                                       self.raw_noise.requires_grad),
+                        lr=lr, max_iters=min(iterations + 1, 64), gen=gen, basis=basis)
+
+    def _fit_fused(self, iterations, lr, stop, hists, verbose, indent, ysq=None, d_out=None):
+        """Device-resident MLL fit (the engine of _fused_engine; the reference's loop semantics: loss
+        history, early stopping, best iterate)."""
+        logtol, wait_max = stop
+        eng = self._fused_engine(iterations, lr, ysq, d_out)
         self._iters_for_log = iterations
         self._log_header(verbose, indent)
         best, save, waited = math.inf, math.inf, 0

@@ -119,7 +119,7 @@ def spec_basis(family, parts, n):
 class FusedMLL(object):
     def __init__(self, family, parts, ysq, raw_scale, raw_lengthscales, raw_noise, logdet_weight, mll_const,
                  requires_grad=(True, True, False), lr=0.1, max_iters=1, parts_per_problem=False, per_problem=None,
-                 gen=None, basis=None):
+                 gen=None, basis=None, mt=None):
         """
         family: 0 lattice (FFT) / 1 net (FWHT)
         basis:  part-product spectra (spec_basis) [Q, 2^d, 64] shared or [G, Q, 2^d, 64]: the spectral fit path
@@ -130,6 +130,8 @@ class FusedMLL(object):
                 otherwise one loss sums over the G problems (per-output hyper-parameters of one GP)
         raw_scale [S] with S in {1, G}; raw_lengthscales [S_l, D_l] with S_l in {1, G}, D_l in {1, d};
         raw_noise [S_n] with S_n in {1, G}
+        mt:     multitask spectral fit (include/fgp_hip.h mt_tasks; G = 1, ysq only gives n): dict with
+                `basis` the pair spectra [T (T+1)/2, 2^d, n], `ytilde` [T, n], `kt` the task kernel [T, T]
         """
         require_device(ysq, "FusedMLL")
         self.device = ysq.device
@@ -139,7 +141,10 @@ class FusedMLL(object):
         self.m = log2_exact(n)
         if self.m < 4:
             raise ValueError("fused fit needs n >= 16")
-        if basis is not None:
+        if mt is not None:
+            d = int(round(math.log2(mt["basis"].shape[1])))
+            parts, gen, basis = None, None, None
+        elif basis is not None:
             d = int(round(math.log2(basis.shape[-2])))
             parts, gen = None, None
         else:
@@ -171,7 +176,8 @@ class FusedMLL(object):
         self.raw = torch.cat([raw_scale.reshape(-1), raw_lengthscales.reshape(-1), raw_noise.reshape(-1)]).to(
             device=self.device, dtype=torch.float64).contiguous()
         cdt = torch.complex128 if self.family == 0 else torch.float64
-        self.work = torch.empty((G, n), dtype=cdt, device=self.device) if (self.m > 12 and basis is None) else None
+        self.work = torch.empty((G, n), dtype=cdt, device=self.device) if (self.m > 12 and basis is None and
+                                                                           mt is None) else None
         self.prev = torch.zeros(self.n_params, dtype=torch.float64, device=self.device)
         self.step = torch.full((self.n_params,), float(lr), dtype=torch.float64, device=self.device)
         self.grad = torch.zeros(self.n_params, dtype=torch.float64, device=self.device)
@@ -202,6 +208,16 @@ class FusedMLL(object):
             self.ysq = yp.view(G, Q, 64).transpose(0, 1).contiguous()
             self._nll.ysq = self.ysq.data_ptr()
             self._nll.ysq_chunked = 1
+        self.mt = None
+        if mt is not None:
+            T = int(mt["ytilde"].shape[0])
+            self.mt = dict(basis=mt["basis"].contiguous(), ytilde=mt["ytilde"].contiguous(),
+                           kt=mt["kt"].to(device=self.device, dtype=torch.float64).contiguous())
+            assert tuple(self.mt["basis"].shape) == (T * (T + 1) // 2, 1 << d, n)
+            self._nll.mt_tasks = T
+            self._nll.mt_basis = self.mt["basis"].data_ptr()
+            self._nll.mt_ytilde = self.mt["ytilde"].data_ptr()
+            self._nll.mt_kt = self.mt["kt"].data_ptr()
         plen = ctypes.c_int64(0)
         N.call("fgp_nll_partials_len", self._nll, ctypes.byref(plen))
         self.partials = torch.empty((plen.value,), dtype=torch.float64, device=self.device)

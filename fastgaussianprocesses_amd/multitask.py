@@ -20,12 +20,14 @@ statement of the same blocks (torch.linalg on the device) -- they need gradients
 the whole inverse that the structured kernels do not provide.  There is no CPU fallback.
 """
 import math
+import os
 
 import numpy as np
 import torch
 
 from . import ops
-from .fast_gp import _IDENTITY_TFS, AbstractFastGP, _Hyper, _as_size
+from .fast_gp import _IDENTITY_TFS, AbstractFastGP, _Hyper, _as_size, _exp
+from .fit_engine import FusedMLL, mll_constant
 
 
 def _to_n_tensor(n):
@@ -328,6 +330,65 @@ class MultiTaskFastGP(AbstractFastGP):
 
     def _fused_ok(self):
         return False
+
+    # ------------------------------------------------------------------ fused multitask fit
+    def _mt_fused_ok(self):
+        """The device-resident multitask MLL fit (k_mt_spec_iter + the spectral reduction / Rprop step,
+        include/fgp_hip.h mt_tasks) covers: every task with the same n >= 16, at most 8 tasks, d <= 6, no
+        parameter batch, the task kernel fixed (derivative-informed GPs fix it at 1, abstract_gp.py:146-150),
+        exp parameter transforms, no adaptive nugget.  FGP_MT_FUSED=0 takes the generic autograd loop."""
+        if os.environ.get("FGP_MT_FUSED", "1")[:1] == "0":
+            return False
+        ns = self._ns
+        n = ns[0]
+        if not (n >= 16 and all(v == n for v in ns) and self.num_tasks <= 8 and self.d <= 6):
+            return False
+        if self.adaptive_nugget or len(self.shape_batch) or self.raw_factor_task_kernel.requires_grad or \
+                self.raw_noise_task_kernel.requires_grad:
+            return False
+        if any(self._tfs[k][1] is not _exp for k in ("scale", "lengthscales", "noise")):
+            return False
+        return tuple(self.raw_scale.shape) == (1,) and tuple(self.raw_noise.shape) == (1,) and \
+            tuple(self.raw_lengthscales.shape) in ((1,), (self.d,))
+
+    def _mt_spectra(self, n):
+        """Pair spectra Phi^{kl}_S = ft(B^{kl}_S) [T (T+1)/2, 2^d, n] (pairs k <= l row-major): with the
+        derivative parts of get_k1parts(k, l) (abstract_fast_gp.py:173-180) and _kernel_from_parts'
+        k1_kl = scale sum_{b0, b1} c0 c1 prod_j (ind_j + l_j parts_j) (:181-191) expanded over the subsets S of
+        the dimensions, B^{kl}_S = sum over the (b0, b1) whose derivative dimensions lie in S of
+        c0 c1 prod_{j in S} parts_j -- so lam_kl = ft(k1_kl) = scale sum_S l^S Phi^{kl}_S (ft linear)."""
+        def f():
+            T, d, dev = self.num_tasks, self.d, self.device
+            NS = 1 << d
+            rows = []
+            for k in range(T):
+                for l in range(k, T):
+                    parts = self.get_k1parts(k, l, n)                         # [n, p0, p1, d]
+                    b0, b1 = self._derivs_h[k], self._derivs_h[l]
+                    need = (b0[:, None, :] + b1[None, :, :]) > 0              # [p0, p1, d]
+                    cc = self.derivatives_coeffs[k][:, None] * self.derivatives_coeffs[l][None, :]
+                    for S in range(NS):
+                        dims = [j for j in range(d) if (S >> j) & 1]
+                        ins = torch.tensor([bool((S >> j) & 1) for j in range(d)])
+                        valid = (~need | ins).all(-1).to(device=dev, dtype=torch.float64)
+                        prod = parts[..., dims].prod(-1) if dims else torch.ones(parts.shape[:-1], device=dev)
+                        rows.append((prod * (cc * valid)).sum((-1, -2)))
+            B = torch.stack(rows).reshape(T * (T + 1) // 2, NS, n)
+            return self.ft(B).contiguous()
+        return self._cached(("mt_spec", n), f, grad_sensitive=False)
+
+    def _fused_engine(self, iterations, lr, ysq=None, d_out=None):
+        """FusedMLL in multitask spectral mode (G = 1)."""
+        n, T = self._ns[0], self.num_tasks
+        yt = torch.stack([self.get_ytilde(k).reshape(n) for k in range(T)])
+        ls = self.raw_lengthscales.detach()
+        return FusedMLL(self._FAMILY, None, torch.zeros((1, n), device=self.device),
+                        self.raw_scale.detach().reshape(-1), ls.reshape(1, -1), self.raw_noise.detach().reshape(-1),
+                        logdet_weight=1.0, mll_const=mll_constant(1, T * n),
+                        requires_grad=(self.raw_scale.requires_grad, self.raw_lengthscales.requires_grad,
+                                       self.raw_noise.requires_grad),
+                        lr=lr, max_iters=min(iterations + 1, 64),
+                        mt=dict(basis=self._mt_spectra(n), ytilde=yt, kt=self.gram_matrix_tasks.detach()))
 
     # ------------------------------------------------------------------ kernel parts and kernels
     def _pair_spec(self, beta0, beta1):
@@ -659,6 +720,7 @@ class MultiTaskFastGP(AbstractFastGP):
         assert isinstance(loss_metric, str) and loss_metric.upper() in ["MLL", "GCV", "CV"]
         assert sum(self._ns) > 0, "cannot fit without data"
         assert isinstance(iterations, int) and iterations >= 0
+        default_optimizer = optimizer is None
         if optimizer is None:
             optimizer = self.get_default_optimizer(lr)
         assert isinstance(optimizer, torch.optim.Optimizer)
@@ -671,6 +733,15 @@ class MultiTaskFastGP(AbstractFastGP):
         assert isinstance(stop_crit_wait_iterations, int) and stop_crit_wait_iterations > 0
         assert masks is None or isinstance(masks, torch.Tensor)
         loss_metric = loss_metric.upper()
+        if loss_metric == "MLL" and default_optimizer and masks is None and self._mt_fused_ok():
+            hists = dict(loss=store_hists or store_loss_hist,
+                         scale=store_hists or (store_scale_hist and self.raw_scale.requires_grad),
+                         lengthscales=store_hists or (store_lengthscales_hist and self.raw_lengthscales.requires_grad),
+                         noise=store_hists or (store_noise_hist and self.raw_noise.requires_grad),
+                         task_kernel=store_hists)       # the task kernel is fixed on this path
+            return self._fit_fused(iterations, 1e-1 if lr is None else lr,
+                                   (np.log(1 + stop_crit_improvement_threshold), stop_crit_wait_iterations), hists,
+                                   verbose, verbose_indent)
         logtol = np.log(1 + stop_crit_improvement_threshold)
         h_loss = store_hists or store_loss_hist
         h_scale = store_hists or (store_scale_hist and self.raw_scale.requires_grad)

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define FGP_ABI_VERSION 11
+#define FGP_ABI_VERSION 12
 
 #define FGP_OK 0
 #define FGP_ERR_INVALID (-1)     /* bad argument (shape, stride, null pointer) */
@@ -214,6 +214,22 @@ typedef struct fgp_nll_desc {
    * ((k / 64) G + g) 64 + k mod 64; ysq_stride unused) -- every problem's Y of a chunk contiguous, read
    * beside the chunk's spectra.  Spectral path only (basis non-NULL). */
   int ysq_chunked;
+  /* ABI 12 -- multitask spectral fit.  mt_tasks = T > 0 (with G = 1): ONE multitask / derivative-informed GP
+   * of T tasks, every task with the same n = 2^log2n points, the task kernel Kt = gram_matrix_tasks fixed
+   * (not learned), the MLL of util.py:364-370 / abstract_gp.py:252-261.  With the pair spectra (k <= l)
+   *   Phi^{kl}_S = ft( sum_{b0 in beta_k, b1 in beta_l: S holds every j with b0_j + b1_j > 0}
+   *                    c0 c1 prod_{j in S} parts^{b0 b1}_j )
+   * (ft = fftbr, complex128 (lattice) / fwht, float64 (net); the parts and coefficients of _kernel_parts /
+   * _kernel_from_parts, abstract_fast_gp.py:173-191), each iteration forms per frequency the T x T Hermitian
+   * block of the reference's lams (util.py:277-298)
+   *   Lambda[k, l] = Kt[k, l] (sqrt(n) scale sum_S l^S Phi^{kl}_S + noise [k == l])
+   * factors it (LDL^H, real pivots), and writes the norm / logdet / gradient partials that fgp_fit_step /
+   * fgp_fit_run reduce and step (per_problem fit desc).  parts, basis and ysq are not read (ysq: any non-NULL
+   * pointer); fgp_nll_lam is not available.  1 <= T <= 8, d <= 6. */
+  int mt_tasks;
+  const void* mt_basis;       /* [T (T + 1) / 2][2^d][n] pair spectra, pairs (k, l), k <= l, row-major */
+  const void* mt_ytilde;      /* [T][n] ytilde of every task (complex128 lattice / float64 net) */
+  const double* mt_kt;        /* device [T][T] task kernel */
 } fgp_nll_desc;
 
 /* Doubles the `partials` workspace of this desc needs (per-block partials + the fused fit's counters):
@@ -422,8 +438,9 @@ int fgp_mt_parts(int family, const void* x, int64_t x_row_stride, int64_t N, con
 
 /* Factor the transform-domain Gram blocks of G problems (replaces _FastInverseLogDetCache.__call__,
  * util.py:275-337): structured LDL^H per frequency class in the packed layout (factor [G][L]),
- * logdet [G][nmin] per class (sum over the classes = the reference's logdet), *info set to 1 (device
- * int, zeroed by the caller) if a pivot is not positive. */
+ * logdet [G][nmin] per class (sum over the classes = the reference's logdet, sum log|pivot| as its
+ * recursion's log|S|, util.py:299,310), *info set to 1 (device int, zeroed by the caller) if a pivot is not
+ * positive (a numerically indefinite block). */
 int fgp_mt_factor(const fgp_mt_layout* layout, const void* lams, int64_t G, void* factor, double* logdet, int* info,
                   void* stream);
 

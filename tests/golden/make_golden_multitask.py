@@ -159,7 +159,16 @@ CASES = [
     ("deriv_lattice_d2_a2", "lattice", "deriv", 2, 2, [64, 8, 256], 0),
     ("deriv_net_d2_a4", "net", "deriv", 2, 4, [64, 8, 256], 0),
     ("deriv_lattice_d2_a3_equal", "lattice", "deriv", 2, 3, [128, 128, 128], 0),
+    # equal n per task: the probnum25 paper's (f, grad f) setting (docs/examples/probnum25_paper cell 15,
+    # SI lattice alpha = 2 / DSI net alpha = 4), the device-resident multitask fit's domain (8 iterations)
+    ("deriv_lattice_d2_a2_equal", "lattice", "deriv", 2, 2, [256, 256, 256], 0),
+    ("deriv_net_d2_a4_equal", "net", "deriv", 2, 4, [128, 128, 128], 0),
+    # the paper's n = 2^10 per task (12-iteration trajectories)
+    ("deriv_lattice_d2_a2_equal_n1024", "lattice", "deriv", 2, 2, [1024, 1024, 1024], 0),
+    ("deriv_net_d2_a4_equal_n1024", "net", "deriv", 2, 4, [1024, 1024, 1024], 0),
 ]
+FIT_ITS = {"deriv_lattice_d2_a2_equal": 8, "deriv_net_d2_a4_equal": 8, "deriv_lattice_d2_a2_equal_n1024": 12,
+           "deriv_net_d2_a4_equal_n1024": 12}
 
 
 def main():
@@ -170,7 +179,7 @@ def main():
     for name, family, kind, d, alpha, ns, B in CASES:
         if only and name not in only:
             continue
-        out = gen_case(fg, qmcpy, family, kind, d, alpha, ns, B)
+        out = gen_case(fg, qmcpy, family, kind, d, alpha, ns, B, fit_its=FIT_ITS.get(name, 3))
         np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
         print("wrote", name, "loss=%.10e" % float(out["loss"]), "fit loss", out["fit_loss_hist"])
 
