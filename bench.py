@@ -599,9 +599,12 @@ def roofline_fit_kernels(F, shifts, iters):
 
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02m_pmc_fit_kernels.json")
-PMC_SQ_SUMMARY = os.path.join(ROOT, "profiles", "r02m_pmc_sq_fit_kernels.json")
-ROCPROF_GRID_STATS = os.path.join(ROOT, "profiles", "r02m_bench_kernel_grid_stats.txt")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r03f_pmc_fit_kernels.json")
+PMC_SQ_SUMMARY = os.path.join(ROOT, "profiles", "r03f_pmc_sq_fit_kernels.json")
+ROCPROF_GRID_STATS = os.path.join(ROOT, "profiles", "r03f_bench_kernel_grid_stats.txt")
+# the read floor of the spectral iteration's footprint: tools/stream_microbench.hip over the same 168 MB,
+# re-read back to back, 24.0-24.3 us per pass (7.0 TB/s; profiles/r03v_stream_and_stamps.jsonl)
+STREAM_FLOOR_US = 24.0
 # FP64 VALU lane-operations per second: 256 CUs x 4 SIMDs x 16 FP64 lanes per clock x 2.4 GHz = 3.93e13
 # (FP64 vector at half the FP32 vector rate of MI355X_MICROARCH.md, 157.3 TFLOP/s; 78.6 TFLOP/s FMA)
 FP64_LANE_OPS_PEAK = 256 * 4 * 16 * 2.4e9
@@ -777,13 +780,24 @@ def main():
             "iteration_us": t_iter * 1e6}
     vi = pmc_valu_insts(kname, grid_wg * wg_thr)
     if vi is not None:
-        # the row kernels regenerate the kernel parts instead of reading them: their bound is the FP64
-        # VALU issue rate, not HBM.  Every VALU instruction priced as a 64-lane FP64 one (integer and
-        # FP32 ones issue faster), so `frac` here is an upper estimate of the issue-slot use.
-        lane_ops = vi * 64 / (us[dom] * 1e-6)
+        # the same kernel against the FP64 VALU issue peak, on the SAME duration as `frac` (avg_us).  Every
+        # VALU instruction priced as a 64-lane FP64 one (integer / FP32 ones issue faster): an upper
+        # estimate of the issue-slot use.
+        lane_ops = vi * 64 / (us_price * 1e-6)
         roof["valu"] = {"insts_per_launch": vi, "lane_ops_per_s": lane_ops, "peak_fp64_lane_ops_per_s": FP64_LANE_OPS_PEAK,
-                        "frac": lane_ops / FP64_LANE_OPS_PEAK, "time": "avg_us_device_clock",
+                        "frac": lane_ops / FP64_LANE_OPS_PEAK, "time": "avg_us",
                         "source": os.path.relpath(PMC_SQ_SUMMARY, ROOT) + " (SQ_INSTS_VALU)"}
+    if variant.startswith("spectral"):
+        # what the dataflow of the reference would move per iteration (B_iter = 16nd + 32n +
+        # 32n bytes per GP -- parts read twice, lambda written and re-read, ytilde read twice) is NOT a bound
+        # for this path: the spectral iteration reads only the shared spectra and Y (algorithmic_bytes)
+        b_iter = (16 * n * d + 64 * n) * P
+        roof["survey_byte_model"] = {
+            "bytes_per_iteration": b_iter, "effective_GBps": b_iter / (us_price * 1e-6) / 1e9,
+            "note": "SURVEY 8(d) reference-dataflow bytes over the kernel's duration; not a bound of the spectral "
+                    "path, which reads only the 2^d shared spectra and Y per iteration"}
+        roof["read_floor"] = {"us": STREAM_FLOOR_US, "frac": STREAM_FLOOR_US / us_price,
+                              "source": "tools/stream_microbench.hip, profiles/r03v_stream_and_stamps.jsonl"}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, n, d)

@@ -360,20 +360,21 @@ class MultiTaskFastGP(AbstractFastGP):
         def f():
             T, d, dev = self.num_tasks, self.d, self.device
             NS = 1 << d
+            ins = torch.tensor([[bool((S >> j) & 1) for j in range(d)] for S in range(NS)])   # [NS, d]
+            insd = ins.to(dev)
             rows = []
             for k in range(T):
                 for l in range(k, T):
                     parts = self.get_k1parts(k, l, n)                         # [n, p0, p1, d]
                     b0, b1 = self._derivs_h[k], self._derivs_h[l]
                     need = (b0[:, None, :] + b1[None, :, :]) > 0              # [p0, p1, d]
+                    valid = (~need[None] | ins[:, None, None, :]).all(-1)    # [NS, p0, p1]
                     cc = self.derivatives_coeffs[k][:, None] * self.derivatives_coeffs[l][None, :]
-                    for S in range(NS):
-                        dims = [j for j in range(d) if (S >> j) & 1]
-                        ins = torch.tensor([bool((S >> j) & 1) for j in range(d)])
-                        valid = (~need | ins).all(-1).to(device=dev, dtype=torch.float64)
-                        prod = parts[..., dims].prod(-1) if dims else torch.ones(parts.shape[:-1], device=dev)
-                        rows.append((prod * (cc * valid)).sum((-1, -2)))
-            B = torch.stack(rows).reshape(T * (T + 1) // 2, NS, n)
+                    # prod_{j in S} parts_j for every subset at once (ascending j), [NS, n, p0, p1]
+                    prod = torch.where(insd[:, None, None, None, :], parts[None], 1.0).prod(-1)
+                    w = cc[None] * valid.to(device=dev, dtype=torch.float64)                 # [NS, p0, p1]
+                    rows.append((prod * w[:, None]).sum((-1, -2)))           # [NS, n]
+            B = torch.stack(rows)                                            # [T (T+1) / 2, NS, n]
             return self.ft(B).contiguous()
         return self._cached(("mt_spec", n), f, grad_sensitive=False)
 

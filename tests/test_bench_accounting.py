@@ -44,17 +44,20 @@ def test_stage_bytes_real_even(monkeypatch):
 
 
 def test_pmc_traffic_lookup_matches_kernel_and_grid():
-    n, P = 2 ** 20, 8
-    wg, thr = bench.fit_grid(n, P, "re")["k_fwd_cols"]
-    t = bench.pmc_traffic("k_fwd_cols_re", wg * thr)
+    """The committed profiles the bench line prices on (profiles/r03f_*): PMC traffic, VALU instructions
+    and the rocprofv3 average of the dominant kernel k_spec_tile at the bench grid; exact name match."""
+    n, P, d = 2 ** 20, 8, 5
+    wg = bench.spec_tile_grid(n, d, P)
+    assert wg == 512
+    t = bench.pmc_traffic("k_spec_tile", wg * 256)
     assert t is not None and t > 0
-    # the full-length kernel name must not match the RE entry (exact name match, not a suffix)
-    assert bench.pmc_traffic("k_fwd_cols", wg * thr) is None
-    assert bench.pmc_traffic("k_fwd_cols_re", 12345) is None
-    # the committed SQ pass holds the VALU instruction count of the dominant row kernel at the bench grid
-    wg, thr = bench.fit_grid(n, P, "re")["k_bwd_rows"]
-    assert bench.pmc_valu_insts("k_bwd_rows_re", wg * thr) > 0
-    assert bench.rocprof_avg_us("k_bwd_rows_re", wg * thr) > 0
+    # PMC traffic within 2 % of the algorithmic bytes: the spectra and Y read once, no re-reads
+    sb = bench.stage_bytes(n, d, P, parts_array=False, variant="spectral_fused")["k_spec_tile"]
+    assert abs(t - sb) <= 0.02 * sb
+    assert bench.pmc_traffic("k_spec", wg * 256) is None           # exact name match, not a prefix
+    assert bench.pmc_traffic("k_spec_tile", 12345) is None
+    assert bench.pmc_valu_insts("k_spec_tile", wg * 256) > 0
+    assert bench.rocprof_avg_us("k_spec_tile", wg * 256) > 0
 
 
 def test_path_choice():
