@@ -400,7 +400,7 @@ STAGES = ("k_fwd_rows", "k_fwd_cols", "k_bwd_rows")
 SPEC_BLOCKS = 512      # k blocks per problem of the spectral iteration (csrc/fgp_nll.h kSpecBlocks)
 
 
-SPEC_RING, SPEC_LDS_MAX, SPEC_MAX_DMA = 2, 80 * 1024, 10     # csrc/fgp_nll.h kSpecRing / kSpecLdsMax / kSpecMaxDma
+SPEC_RING, SPEC_LDS_MAX, SPEC_MAX_DMA = 2, 80 * 1024, 6      # csrc/fgp_nll.h kSpecRing / kSpecLdsMax / kSpecMaxDma
 
 
 def stage_names(variant):

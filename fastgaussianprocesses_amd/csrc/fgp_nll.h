@@ -576,7 +576,8 @@ constexpr int kSpecRing = FGP_SPEC_RING;         // LDS ring depth of the spectr
 #endif
 constexpr int kSpecLdsMax = FGP_SPEC_LDS_KB * 1024;   // its dynamic LDS per workgroup, at most (80: 2 per CU)
 constexpr int kSpecScratch = 256;                  // doubles of the deferred step's totals / parameters (ring slot RING-1)
-constexpr int kSpecMaxDma = 10;                    // LDS-DMA wave-instructions per wave and chunk (tile <= 5120 doubles)
+constexpr int kSpecMaxDma = 6;                     // LDS-DMA wave-instructions per wave and chunk (tile <= 3072 doubles;
+                                                   // the per-wave source pointers live in registers)
 void spec_geometry(Nll& a);                        // nb and the spec_* fields of a spectral desc
 int64_t spec_chunks(bool net, int log2n);          // 64-frequency chunks of the spectra (fgp_spec_basis layout)
 // one fit iteration (loss + gradient partials); with fz (tile kernel only) also the reduction + Rprop

@@ -873,12 +873,16 @@ int launch_spec_iter(const Nll& a, hipStream_t st, const FitFuse* fz) {
       constexpr int D = decltype(dc)::value;
       if constexpr (D <= 5) {
         auto go = [&](auto kern) {
-          // the ring may exceed the 64 KB default of dynamic LDS: raise the kernel's limit once
-          static bool raised = false;
-          if (!raised) {
-            hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                kSpecLdsMax);
-            raised = true;
+          // the ring may exceed the 64 KB default of dynamic LDS: raise each kernel's limit once (one
+          // static for every kernel of this lambda's type: remember which ones)
+          static const void* raised[64];
+          static int nraised = 0;
+          const void* kp = reinterpret_cast<const void*>(kern);
+          bool done = false;
+          for (int i = 0; i < nraised; ++i) done = done || raised[i] == kp;
+          if (!done) {
+            hipFuncSetAttribute(kp, hipFuncAttributeMaxDynamicSharedMemorySize, kSpecLdsMax);
+            if (nraised < 64) raised[nraised++] = kp;
           }
           kern<<<grid, kWG, shm, st>>>(a, f);
         };
