@@ -95,6 +95,7 @@ _SIGNATURES = {
     "fgp_fwht": [_c_vp, _c_i64, _c_vp, _c_i64, _c_int, _c_int, _c_vp],
     "fgp_fftbr_real": [_c_vp, _c_i64, _c_vp, _c_vp, _c_i64, _c_int, _c_vp],
     "fgp_ifftbr_real": [_c_vp, _c_i64, _c_vp, _c_i64, _c_vp, _c_i64, _c_vp, _c_i64, _c_int, _c_vp],
+    "fgp_ifftbr_real_rf": [_c_vp, _c_i64, _c_vp, _c_i64, _c_vp, _c_i64, _c_vp, _c_i64, _c_int, _c_vp],
     "fgp_fftbr_c64": [_c_vp, _c_i64, _c_int, _c_vp, _c_i64, _c_int, _c_int, _c_vp],
     "fgp_ifftbr_c64": [_c_vp, _c_i64, _c_vp, _c_int, _c_vp, _c_i64, _c_int, _c_int, _c_vp],
     "fgp_fwht_f32": [_c_vp, _c_i64, _c_vp, _c_i64, _c_int, _c_int, _c_vp],
@@ -108,6 +109,7 @@ _SIGNATURES = {
     "fgp_nll_fwd": [_P_NLL, _c_vp],
     "fgp_nll_bwd": [_P_NLL, _c_vp],
     "fgp_nll_lam": [_P_NLL, _c_vp],
+    "fgp_spec_inv_eig": [_P_NLL, _c_vp, _c_vp],
     "fgp_nll_stage": [_P_NLL, _c_int, _c_vp],
     "fgp_post_var_qf": [_c_int, _c_vp, _c_i64, _c_vp, _c_int, _c_int, _c_int, _c_pi, _c_pd, _c_vp, _c_vp, _c_vp,
                         _c_vp, _c_vp, _c_vp],

@@ -17,7 +17,7 @@ import torch
 
 from . import _native as N
 from . import ops
-from .fit_engine import FusedMLL, LatticePartsGen, fused_lam, mll_constant, spec_basis, spectral_wanted
+from .fit_engine import FusedMLL, LatticePartsGen, fused_lam, mll_constant, spec_basis, spec_inv_eig, spectral_wanted
 
 
 class _LossReader(object):
@@ -357,6 +357,14 @@ class GPBatch(object):
             raw = self.raw()
             parts, gen = self._source()
             dl = self.dl
+            basis = self.basis()
+            if basis is not None and self.family == ops.LATTICE and 17 <= self.m <= 24:
+                # spectral path: A = 1/ev straight from the spectra (real), the product fused into the
+                # half-length inverse -- no lambda / ytilde * A arrays
+                wa = spec_inv_eig(self.family, raw[:, 0], raw[:, 1:1 + dl], raw[:, 1 + dl], self.P, self.n, basis)
+                self._st["coeffs"] = ops.ifftbr_real_rf(self.ytilde(), wa)
+                self._st["wa"] = wa
+                return self._st["coeffs"]
             lam = fused_lam(self.family, parts, raw[:, 0], raw[:, 1:1 + dl], raw[:, 1 + dl], self.P, gen=gen, n=self.n,
                             basis=self.basis())
             yt = self.ytilde()

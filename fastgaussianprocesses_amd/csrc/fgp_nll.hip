@@ -810,10 +810,11 @@ __global__ __launch_bounds__(kWG, 2) void k_fwd_cols_r2c(Nll a, const double2* _
 // (k, k + n/2; n/2 - k, n - k) once -- reading the four values, so X~ is the exact Hermitian part --
 // writes V of both partners into the LDS image and runs the adjoint column pass; the row kernel runs the
 // conjugate-twiddled adjoint row pass and writes the real rows.  f (optional): X = in * f, fused into the
-// loads (the tilde-domain solve of gram_matrix_solve, util.py:341-343).
-template <int P1>
+// loads (the tilde-domain solve of gram_matrix_solve, util.py:341-343); FR: f holds real factor rows
+// (float64: A = 1/ev of real eigenvalues, fgp_ifftbr_real_rf), else complex128.
+template <int P1, bool FR>
 __global__ __launch_bounds__(kWG, 2) void k_inv_cols_c2r(const double2* __restrict__ X, int64_t xs,
-                                                         const double2* __restrict__ f, int64_t fs,
+                                                         const void* __restrict__ f, int64_t fs,
                                                          double2* __restrict__ work, int log2n,
                                                          const double2* __restrict__ tw,
                                                          const double2* __restrict__ twmf) {
@@ -836,10 +837,15 @@ __global__ __launch_bounds__(kWG, 2) void k_inv_cols_c2r(const double2* __restri
   const bool col0 = blk == 0 && q == 0;                      // tile 0's self-mirrored columns
   const int64_t cp_gen = (int64_t)blk * HC + q;
   const double2* xg = X + g * xs;
-  const double2* fg = f ? f + g * fs : nullptr;
+  const double2* fg = (f && !FR) ? static_cast<const double2*>(f) + g * fs : nullptr;
+  const double* fr = (f && FR) ? static_cast<const double*>(f) + g * fs : nullptr;
   auto xv = [&](int64_t k) {
     const double2 v = xg[k];
-    return fg ? cmul(v, fg[k]) : v;
+    if constexpr (FR) {
+      return fr ? make_double2(v.x * fr[k], v.y * fr[k]) : v;
+    } else {
+      return fg ? cmul(v, fg[k]) : v;
+    }
   };
   // Hermitian part at (k, k + n/2) given the partner pair (n/2 - k, n - k): X~_k, X~_{k+n/2}
   auto herm = [&](int64_t k, int64_t ks, double2& h0, double2& h1) {
@@ -1553,6 +1559,15 @@ int fgp_nll_fwd(const fgp_nll_desc* desc, void* stream) {
   return nll_fwd(a, (hipStream_t)stream, desc->family == FGP_FAMILY_LATTICE);
 }
 
+int fgp_spec_inv_eig(const fgp_nll_desc* desc, double* wa, void* stream) {
+  Nll a;
+  int rc = to_nll(desc, a);
+  if (rc != kOk) return rc;
+  if (!a.spec || a.mt) return set_error(kErrInvalid, "fgp_spec_inv_eig: needs the spectral desc (basis)");
+  if (!wa) return set_error(kErrInvalid, "fgp_spec_inv_eig: null wa");
+  return launch_spec_inv_eig(a, wa, (hipStream_t)stream);
+}
+
 int fgp_nll_lam(const fgp_nll_desc* desc, void* stream) {
   Nll a;
   int rc = to_nll(desc, a);
@@ -1650,8 +1665,8 @@ int fgp_fftbr_real(const double* in, int64_t in_batch_stride, void* out, void* w
   return check_launch("k_fwd_cols_r2c");
 }
 
-int fgp_ifftbr_real(const void* in, int64_t in_batch_stride, const void* f, int64_t f_batch_stride, double* out,
-                    int64_t out_batch_stride, void* work, int64_t batch, int log2n, void* stream) {
+static int ifftbr_real_any(const void* in, int64_t in_batch_stride, const void* f, bool freal, int64_t f_batch_stride,
+                           double* out, int64_t out_batch_stride, void* work, int64_t batch, int log2n, void* stream) {
   if (log2n < 17 || log2n > 24 || batch < 0) return set_error(kErrInvalid, "fgp_ifftbr_real: needs 17 <= log2n <= 24");
   if (batch == 0) return kOk;
   if (!in || !out || !work) return set_error(kErrInvalid, "fgp_ifftbr_real: null pointer");
@@ -1667,10 +1682,15 @@ int fgp_ifftbr_real(const void* in, int64_t in_batch_stride, const void* f, int6
   const int mt = log2n - 1, p1 = mt - 12;
   const unsigned grid = (unsigned)(batch * tiles);
   const double2* X = static_cast<const double2*>(in);
-  const double2* F = static_cast<const double2*>(f);
   double2* wk = static_cast<double2*>(work);
   switch (p1) {
-#define FGP_C(PP) case PP: k_inv_cols_c2r<PP><<<grid, kWG, 0, st>>>(X, in_batch_stride, F, f_batch_stride, wk, log2n, tb->tw4096, tb->twm[log2n]); break;
+#define FGP_C(PP)                                                                                                \
+  case PP:                                                                                                       \
+    if (freal) k_inv_cols_c2r<PP, true><<<grid, kWG, 0, st>>>(X, in_batch_stride, f, f_batch_stride, wk, log2n,  \
+                                                              tb->tw4096, tb->twm[log2n]);                       \
+    else k_inv_cols_c2r<PP, false><<<grid, kWG, 0, st>>>(X, in_batch_stride, f, f_batch_stride, wk, log2n,       \
+                                                         tb->tw4096, tb->twm[log2n]);                            \
+    break;
     FGP_C(4) FGP_C(5) FGP_C(6) FGP_C(7) FGP_C(8) FGP_C(9) FGP_C(10) FGP_C(11)
 #undef FGP_C
     default: return set_error(kErrInvalid, "bad c2r m1");
@@ -1679,6 +1699,19 @@ int fgp_ifftbr_real(const void* in, int64_t in_batch_stride, const void* f, int6
   if (rc != kOk) return rc;
   k_inv_rows_c2r<<<grid, kWG, 0, st>>>(wk, log2n, out, out_batch_stride, tb->tw4096, tb->twm[mt]);
   return check_launch("k_inv_rows_c2r");
+}
+
+int fgp_ifftbr_real(const void* in, int64_t in_batch_stride, const void* f, int64_t f_batch_stride, double* out,
+                    int64_t out_batch_stride, void* work, int64_t batch, int log2n, void* stream) {
+  return ifftbr_real_any(in, in_batch_stride, f, false, f_batch_stride, out, out_batch_stride, work, batch, log2n,
+                         stream);
+}
+
+int fgp_ifftbr_real_rf(const void* in, int64_t in_batch_stride, const double* f, int64_t f_batch_stride, double* out,
+                       int64_t out_batch_stride, void* work, int64_t batch, int log2n, void* stream) {
+  if (!f) return set_error(kErrInvalid, "fgp_ifftbr_real_rf: null factor rows");
+  return ifftbr_real_any(in, in_batch_stride, f, true, f_batch_stride, out, out_batch_stride, work, batch, log2n,
+                         stream);
 }
 
 }  // extern "C"

@@ -790,6 +790,40 @@ __global__ __launch_bounds__(kWG) void k_mt_spec_iter(Nll a) {
   stamp_end(a);
 }
 
+// A = 1 / ev, ev = sqrt(n) lambda + noise (util.py:285,292-300) of every problem from the spectra
+// (fgp_spec_inv_eig): the real eigenvalues' inverse, wa [G][n] float64 -- the factor of the coefficient
+// solve (fgp_ifftbr_real_rf) and the post_var weights -- without materialising lambda.  Thread = frequency
+// k <= K - 1 (lattice: k and its mirror n - k from one evaluation), looping over the problems sharing the
+// spectra (one read of the 2^d values per frequency).
+template <int D, bool NET>
+__global__ __launch_bounds__(kWG) void k_spec_inv_eig(Nll a, double* __restrict__ wa) {
+  constexpr int NS = 1 << D;
+  const int64_t k = (int64_t)blockIdx.x * kWG + threadIdx.x;
+  const int64_t n = (int64_t)1 << a.log2n;
+  const double rootn = sqrt((double)n);
+  const bool shared = a.basis_stride == 0;
+  double phi[NS], dp[D];
+  if (k < a.spec_K && shared) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) phi[s] = a.basis[spec_at<NS>(k, s)];
+  }
+  for (int g = 0; g < a.G; ++g) {
+    Hyp h;
+    load_hyp_wave(a, g, h);
+    if (k >= a.spec_K) continue;
+    if (!shared) {
+      const double* phib = a.basis + (int64_t)g * a.basis_stride;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) phi[s] = phib[spec_at<NS>(k, s)];
+    }
+    const double lam = h.scale * mlin<D>(phi, h.ls, dp);
+    const double A = 1.0 / (rootn * lam + h.noise);
+    double* w = wa + (int64_t)g * n;
+    w[k] = A;
+    if (!NET && k > 0 && k < n / 2) w[n - k] = A;
+  }
+}
+
 template <typename Fn>
 static int with_spec_d(int d, Fn&& fn) {
   switch (d) {
@@ -947,6 +981,16 @@ int launch_spec_finish_step(const Nll& a, const FitFuse& fz, hipStream_t st) {
   return with_spec_d(a.d, [&](auto dc) {
     k_spec_finish_step<decltype(dc)::value><<<1, kWG, 0, st>>>(a, fz);
     return check_launch("k_spec_finish_step");
+  });
+}
+
+int launch_spec_inv_eig(const Nll& a, double* wa, hipStream_t st) {
+  const unsigned grid = (unsigned)((a.spec_K + kWG - 1) / kWG);
+  return with_spec_d(a.d, [&](auto dc) {
+    constexpr int D = decltype(dc)::value;
+    if (a.spec_net) k_spec_inv_eig<D, true><<<grid, kWG, 0, st>>>(a, wa);
+    else k_spec_inv_eig<D, false><<<grid, kWG, 0, st>>>(a, wa);
+    return check_launch("k_spec_inv_eig");
   });
 }
 

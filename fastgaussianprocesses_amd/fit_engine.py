@@ -369,6 +369,27 @@ def mll_constant(d_out, n):
     return d_out * n * math.log(2 * math.pi)
 
 
+def spec_inv_eig(family, raw_scale, raw_lengthscales, raw_noise, G, n, basis):
+    """A = 1/ev [G, n] float64 (ev = sqrt(n) lambda + noise, lambda = scale sum_S l^S Phi_S real) of G
+    problems from part-product spectra `basis` ([Q, 2^d, 64] shared or [G, Q, 2^d, 64]) via fgp_spec_inv_eig
+    -- fgp_inv_eig's wa without materialising lambda."""
+    require_device(basis, "spec_inv_eig")
+    d, dev = int(round(math.log2(basis.shape[-2]))), basis.device
+    m = log2_exact(n)
+    S, (Sl, Dl), Sn = raw_scale.numel(), raw_lengthscales.shape, raw_noise.numel()
+    raw = torch.cat([raw_scale.reshape(-1), raw_lengthscales.reshape(-1), raw_noise.reshape(-1)]).to(
+        device=dev, dtype=torch.float64).contiguous()
+    wa = torch.empty((G, n), dtype=torch.float64, device=dev)
+    basis = basis.contiguous()
+    desc = N.NllDesc(family=family, log2n=m, d=d, G=G, parts=0, parts_stride=0, ysq=wa.data_ptr(), ysq_stride=0,
+                     raw=raw.data_ptr(), scale_off=0, scale_pp=int(S == G and G > 1), ls_off=S,
+                     ls_pp=int(Sl == G and G > 1), ls_pd=int(Dl == d), noise_off=S + Sl * Dl,
+                     noise_pp=int(Sn == G and G > 1), logdet_weight=1.0, grad_lam=0, work=0, partials=wa.data_ptr(),
+                     basis=basis.data_ptr(), basis_stride=(basis[0].numel() if basis.dim() == 4 else 0))
+    N.call("fgp_spec_inv_eig", desc, N.ptr(wa), N.stream_ptr(dev))
+    return wa
+
+
 def fused_lam(family, parts, raw_scale, raw_lengthscales, raw_noise, G, gen=None, n=None, basis=None):
     """lambda = ft(k1) for G eigen-problems sharing `parts` ([d, n]), with parts of their own
     ([G, d, n]), with the generator `gen` (size n), or from part-product spectra `basis` ([Q, 2^d, 64]

@@ -126,6 +126,25 @@ def ifftbr_raw(x, stable=True, real_out=False):
     return out.reshape(shape)
 
 
+def ifftbr_real_rf(x, f):
+    """Re ifftbr(x * f) along the last dim for complex128 x [*, n] and REAL factor rows f (float64, one row or
+    one per row of x), 2^17 <= n <= 2^24, at half length (fgp_ifftbr_real_rf): the coefficient solve
+    ift(A * ytilde).real of gram_matrix_solve (util.py:341-343) with the spectral path's real A."""
+    require_device(x, "ifftbr_real_rf")
+    n = x.shape[-1]
+    m = log2_exact(n)
+    assert 17 <= m <= 24, "ifftbr_real_rf needs 2^17 <= n <= 2^24"
+    x = x.to(torch.complex128)
+    rows, bs = _as_rows(x)
+    f2 = resolved(f.to(device=x.device, dtype=torch.float64)).reshape(-1, n).contiguous()
+    assert f2.size(0) in (1, rows.size(0)), "one factor row, or one per row of x"
+    out = torch.empty(rows.shape, dtype=torch.float64, device=x.device)
+    work = torch.empty(rows.shape, dtype=torch.complex128, device=x.device)
+    N.call("fgp_ifftbr_real_rf", N.ptr(rows), bs, N.ptr(f2), 0 if f2.size(0) == 1 else n, N.ptr(out), n, N.ptr(work),
+           rows.size(0), m, _stream(x))
+    return out.reshape(x.shape)
+
+
 def fwht_raw(x, stable=True):
     """Orthonormal Sylvester FWHT along the last dim (fgp_fwht, or fgp_fwht_f32 for float32 input)."""
     require_device(x, "fwht")

@@ -80,6 +80,10 @@ int fgp_fftbr_real(const double* in, int64_t in_batch_stride, void* out, void* w
  * out.  out: [batch][n] float64 (16-byte aligned rows); work: device scratch of batch * n complex128. */
 int fgp_ifftbr_real(const void* in, int64_t in_batch_stride, const void* f, int64_t f_batch_stride, double* out,
                     int64_t out_batch_stride, void* work, int64_t batch, int log2n, void* stream);
+/* The same with REAL factor rows f (float64 [batch or 1][n], f_batch_stride 0: one shared row): out[b] =
+ * Re ifftbr(in[b] * f[b]) for the real A = 1/ev of the spectral path (ABI 12). */
+int fgp_ifftbr_real_rf(const void* in, int64_t in_batch_stride, const double* f, int64_t f_batch_stride, double* out,
+                       int64_t out_batch_stride, void* work, int64_t batch, int log2n, void* stream);
 
 /* Single-precision variants (complex64 / float32; SURVEY §8(b) fgp_fftbr_c64 / fgp_ifftbr_c64 /
  * fgp_fwht_f32): the same transforms, arguments and layouts with float / complex64 in place of
@@ -231,6 +235,11 @@ typedef struct fgp_nll_desc {
   const void* mt_ytilde;      /* [T][n] ytilde of every task (complex128 lattice / float64 net) */
   const double* mt_kt;        /* device [T][T] task kernel */
 } fgp_nll_desc;
+
+/* A = 1/ev, ev = sqrt(n) lambda + exp(raw_noise), of the G problems of a spectral desc (basis non-NULL;
+ * util.py:285,292-300 with lambda = scale sum_S l^S Phi_S, real): wa [G][n] float64 (lattice: the even
+ * spectrum mirrored) -- fgp_inv_eig's wa without materialising lambda (ABI 12).  ysq / partials unused. */
+int fgp_spec_inv_eig(const fgp_nll_desc* desc, double* wa, void* stream);
 
 /* Doubles the `partials` workspace of this desc needs (per-block partials + the fused fit's counters):
  * G (4 + d) (max(nb, n / 4096) + 1) + G, nb the kernels' block count (spectral path: up to 512). */

@@ -147,3 +147,40 @@ def test_spectral_batch_shares_one_basis_and_equals_individual_fits(monkeypatch)
         dp = gp.fit(iterations=8, stop_crit_wait_iterations=20, store_loss_hist=True, verbose=0)
         assert torch.equal(dp["loss_hist"], data[p]["loss_hist"])
         assert torch.equal(gp.raw_lengthscales.detach(), gps[p].raw_lengthscales.detach().reshape(gp.raw_lengthscales.shape))
+
+
+@pytest.mark.parametrize("m", [17, 20])
+def test_spectral_coefficients_from_spectra(m):
+    """GPBatch.coeffs on the spectral path (fgp_spec_inv_eig: A = 1/ev straight from the spectra, the product
+    fused into the half-length inverse with real factor rows, fgp_ifftbr_real_rf) against the lambda route
+    (fgp_nll_lam + fgp_inv_eig + fgp_ifftbr_real) and the oracle's K^-1 y (util.py:338-353)."""
+    from fastgaussianprocesses_amd import ops
+    d, P = 3, 3
+    gps = [F.FastGPLattice(F.Lattice(d, seed=40 + p, randomize="SHIFT"), device=DEV) for p in range(P)]
+    for p, gp in enumerate(gps):
+        x = gp.get_x_next(2 ** m)
+        gp.add_y_next(O.f_ackley(x.cpu()).to(DEV) * (1 + 0.1 * p))
+        with torch.no_grad():
+            gp.raw_lengthscales.add_(0.05 * p)
+    b = F.GPBatch(gps)
+    assert b.basis() is not None
+    c = b.coeffs()
+    wa = b._st["wa"]
+    raw = b.raw()
+    dl = b.dl
+    lam = fused_lam(0, None, raw[:, 0], raw[:, 1:1 + dl], raw[:, 1 + dl], P, n=2 ** m, basis=b.basis())
+    ev = math.sqrt(2 ** m) * lam.real + torch.exp(raw[:, 1 + dl])[:, None]
+    assert rel_err(wa, 1.0 / ev) < 1e-14
+    ref = ops.ifftbr_raw(b.ytilde() * (1.0 / ev), stable=True, real_out=True)
+    assert rel_err(c, ref) < 1e-12
+    # real factor rows: one shared row and per-row rows give Re ifftbr(x * f)
+    assert rel_err(ops.ifftbr_real_rf(b.ytilde(), wa[:1]), ops.ifftbr_raw(b.ytilde() * wa[:1], True, True)) < 1e-13
+    if m == 17:
+        for p, gp in enumerate(gps):
+            o = O.OracleFastGP("lattice", gp.get_x(0).cpu(), None, gp._y[0].cpu(), alpha=2)
+            with torch.no_grad():
+                o.raw_scale.copy_(gp.raw_scale.cpu())
+                o.raw_lengthscales.copy_(gp.raw_lengthscales.cpu())
+                o.raw_noise.copy_(gp.raw_noise.cpu())
+            # coeffs = K^-1 y at cond(K) ~ n / noise: the 1e-5 of DESIGN.md section 1 (measured 1.8e-6)
+            assert rel_err(c[p], o.coeffs().detach()) < 1e-5
