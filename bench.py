@@ -251,21 +251,25 @@ def secondary_configs(F, args, device, rank=0, world=1):
         sec = time_steps(lambda: step_single(sg, args, xm, xv), max(1, args.steps), 1, device)
         phases = None
         if world == 1:
-            ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
-            sg.reset()
-            ev[0].record()
-            sg.gp.fit(iterations=args.fit_iters, stop_crit_wait_iterations=args.fit_iters + 1, verbose=0)
-            ev[1].record()
-            with torch.no_grad():
-                sg.gp.coeffs                 # the graph-free coefficients post_mean uses
-            ev[2].record()
-            sg.gp.post_mean(xm)
-            ev[3].record()
-            sg.gp.post_var(xv)
-            ev[4].record()
-            torch.cuda.synchronize()
-            phases = {k: ev[i].elapsed_time(ev[i + 1]) for i, k in enumerate(("ytilde+fit", "coeffs", "post_mean",
-                                                                              "post_var"))}
+            # per-phase median of 3 event-timed steps (one sample can catch a host stall)
+            keys = ("ytilde+fit", "coeffs", "post_mean", "post_var")
+            samples = []
+            for _ in range(3):
+                ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
+                sg.reset()
+                ev[0].record()
+                sg.gp.fit(iterations=args.fit_iters, stop_crit_wait_iterations=args.fit_iters + 1, verbose=0)
+                ev[1].record()
+                with torch.no_grad():
+                    sg.gp.coeffs                 # the graph-free coefficients post_mean uses
+                ev[2].record()
+                sg.gp.post_mean(xm)
+                ev[3].record()
+                sg.gp.post_var(xv)
+                ev[4].record()
+                torch.cuda.synchronize()
+                samples.append([ev[i].elapsed_time(ev[i + 1]) for i in range(4)])
+            phases = {k: sorted(s[i] for s in samples)[1] for i, k in enumerate(keys)}
         total = getattr(sg, "total", 1)
         out.append({"metric": "GP fit+predict points/sec" if total == 1 else
                     "multi-output GP fit+predict output-points/sec",
@@ -425,7 +429,22 @@ def spec_tile_geometry(n, d, G, shared=True, family=0):
     rows = 2 ** d + G
     ok = (pg <= 4 and rows * ck * 8 * SPEC_RING <= SPEC_LDS_MAX and rows * ck <= 512 * SPEC_MAX_DMA and
           (rows * ck) % 128 == 0 and rows * ck >= 256 and nb % (4 // pgp) == 0 and main % (64 * nb) == 0)
-    return (nb // (4 // pgp), ppw, pg) if ok else None
+    if ok:
+        return (nb // (4 // pgp), ppw, pg)
+    # problem slices (G > 8): PS = 4 PPW problems per workgroup, one k block each (64 chunks per workgroup,
+    # more blocks while the grid has < 512 workgroups), snb x slices workgroups
+    sppw = 4 if d <= 3 else 2
+    ps = 4 * sppw
+    srows = 2 ** d + ps
+    nsl = (G + ps - 1) // ps
+    snb = max(1, main // (64 * 64))
+    while snb * nsl < 512 and snb * 2 <= max(1, main // 64):
+        snb *= 2
+    snb = min(snb, nb)
+    if (pg > 4 and srows * 64 * 8 * SPEC_RING <= SPEC_LDS_MAX and srows * 64 <= 512 * SPEC_MAX_DMA and
+            (srows * 64) % 128 == 0 and main % (64 * snb) == 0):
+        return (snb * nsl, sppw, 4)
+    return None
 
 
 def spec_geometry(n, d, G, shared=True, family=0):
@@ -435,7 +454,9 @@ def spec_geometry(n, d, G, shared=True, family=0):
     nb = min(SPEC_BLOCKS, max(1, main // 64))
     t = spec_tile_geometry(n, d, G, shared, family)
     if t is not None:
-        return nb, t[1], t[2]
+        ps = 4 * t[1]
+        sliced = (G + t[1] - 1) // t[1] > 4          # problem slices: the grid is k blocks x slices
+        return (t[0] // ((G + ps - 1) // ps) if sliced else nb), t[1], t[2]
     ppw = 2 if (G >= 2 and shared and d <= 5) else 1
     if ppw == 2 and G > 8 and d <= 3:
         ppw = 4
@@ -480,6 +501,8 @@ def fit_grid(n, P, variant, d=5):
     if variant == "spectral_fused":
         return {"k_spec_tile": (spec_tile_grid(n, d, P), 256)}
     if variant == "spectral":
+        if spec_tile_grid(n, d, P) is not None:       # staged tile launches (problem slices when P > 8)
+            return {"k_spec_tile": (spec_tile_grid(n, d, P), 256)}
         nb, _, pg = spec_geometry(n, d, P)
         return {"k_spec_iter": ((nb * pg + 3) // 4, 256)}
     if variant == "re":     # N1 = n / (2 N2) rows of N2: N1/2 row-pair workgroups of N2/8, n/16384 column tiles

@@ -40,6 +40,7 @@ struct Nll {
   int spec_kpl, spec_ppw, spec_pg;   // frequencies per lane and block, problems per wave, problem groups
   int spec_tile, spec_pgp, spec_ck;  // LDS-tiled kernel: problem-group slots, frequencies per chunk
   int64_t spec_kw;                   // ... and per workgroup
+  int spec_ps, spec_nsl;             // ... over problem slices: problems per slice, slices (1: none)
   int ysq_chunked;                   // ysq in the chunked layout [k / 64][G][64] (spectral path)
   // multitask spectral fit (ABI 12, fgp_spectral.hip k_mt_spec_iter): T tasks (0: off), pair spectra,
   // ytilde, task kernel; mt_F frequencies per chunk, mt_cpb chunks per block

@@ -1253,7 +1253,8 @@ static int to_nll(const fgp_nll_desc* d, Nll& a) {
   a.spec = d->basis != nullptr;
   a.spec_net = d->family == FGP_FAMILY_NET;
   a.spec_K = a.spec_KS = a.spec_main = a.spec_kw = 0;
-  a.spec_kpl = a.spec_ppw = a.spec_pg = a.spec_tile = a.spec_pgp = a.spec_ck = 0;
+  a.spec_kpl = a.spec_ppw = a.spec_pg = a.spec_tile = a.spec_pgp = a.spec_ck = a.spec_ps = 0;
+  a.spec_nsl = 1;
   if (a.spec) {
     a.re = a.r2c = 0;
     spec_geometry(a);

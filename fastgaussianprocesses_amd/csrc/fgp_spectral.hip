@@ -433,15 +433,16 @@ __device__ __forceinline__ void barrier_keep_vm() {
 }
 
 // One fit iteration when every problem shares ONE set of spectra and the problem groups fit in the four
-// waves of a workgroup (PG = ceil(G / PPW) <= 4; the C4 shifts, single GPs) and a chunk's tile is at most
-// 24 KB (a 3-deep ring: 72 KB of LDS, two workgroups per CU).  The k blocks are those of
+// waves of a workgroup (PG = ceil(G / PPW) <= 4; the C4 shifts, single GPs) -- or, for many problems, over
+// problem slices of 4 PPW problems (spec_geometry) -- and the ring of kSpecRing chunks fits kSpecLdsMax
+// (two workgroups per CU).  The k blocks are those of
 // k_spec_iter (nb blocks of B = 64 kpl frequencies, one partial per problem and block, lane l summing
 // k = block base + l + 64 i in ascending i): workgroup b owns NBW = 4 / PGP consecutive blocks (PGP = PG
 // rounded up to 1, 2 or 4), wave w the block w / PGP for problem group w mod PGP -- so every problem's
 // arithmetic, and its partials, are those of k_spec_iter whatever G is (a batch equals its GPs' own fits
-// bit for bit).  The spectra and Y stream through a 3-deep LDS ring in chunks of 64 frequencies per
+// bit for bit).  The spectra and Y stream through the LDS ring in chunks of 64 frequencies per
 // block: the chunk's (2^d + G) rows x NBW segments are read ONCE from HBM by all four waves (16-byte LDS-DMA
-// loads, global_load_lds_dwordx4, no register staging; two chunks in flight under each chunk's compute,
+// loads, global_load_lds_dwordx4, no register staging; RING - 1 chunks in flight under each chunk's compute,
 // counted vmcnt waits and raw barriers so they stay in flight: cdna_hip_programming.md section 5
 // "Pipelining across barriers") instead of once per problem group, and each wave reads its segment from
 // LDS (lane-consecutive 8-byte reads: conflict-free).  With fz.counters the LAST workgroup to finish (sc1 partials, an agent-scope arrival
@@ -451,23 +452,29 @@ template <int D, int PPW, bool NET>
 __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
   constexpr int NS = 1 << D;
   constexpr int RING = kSpecRing;                   // chunks in LDS; RING - 1 in flight under a compute
-  extern __shared__ double lds[];                   // [RING][NBW][NS + G][64] ring
+  extern __shared__ double lds[];                   // [RING][NBW][NS + PS][64] ring
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int PGP = a.spec_pgp, NBW = 4 / PGP, G = a.G;
-  const int rows = NS + G, tile = rows * NBW * 64, npieces = tile / 2, segp = 32 * rows;
+  // problem slices (many problems on one set of spectra, a.spec_nsl > 1): workgroup = (k block, slice),
+  // the slices of one block consecutive (they share its spectra chunks in L2); slice s holds problems
+  // [s PS, s PS + GS) in the tile's Y rows (rows past G re-read problem G - 1 and are not evaluated)
+  const int nsl = a.spec_nsl, PS = a.spec_ps ? a.spec_ps : G;
+  const int slice = nsl > 1 ? (int)blockIdx.x % nsl : 0, wgb = nsl > 1 ? (int)blockIdx.x / nsl : (int)blockIdx.x;
+  const int goff = slice * PS, GS = min(PS, G - goff);
+  const int rows = NS + PS, tile = rows * NBW * 64, npieces = tile / 2, segp = 32 * rows;
   const int ninst = npieces / 64;                   // 1-KiB LDS-DMA wave-instructions per chunk (whole)
   const int cnt_w = (ninst - w + 3) / 4;            // ... issued by this wave: j = w, w + 4, ...
   const int pg = w % PGP, bw = w / PGP;
   const int g0 = pg * PPW;
-  const bool active = g0 < G;
+  const bool active = g0 < GS;
   const int64_t B = 64 * (int64_t)a.spec_kpl;       // frequencies per block
-  const int blk = (int)blockIdx.x * NBW + bw;
+  const int blk = wgb * NBW + bw;
   stamp_begin(a);
   bool on[PPW];
 #pragma unroll
-  for (int p = 0; p < PPW; ++p) on[p] = g0 + p < G;
+  for (int p = 0; p < PPW; ++p) on[p] = g0 + p < GS;
   const double rootn = sqrt((double)((int64_t)1 << a.log2n)), wl = a.logdet_weight;
-  const int64_t wg_base = (int64_t)blockIdx.x * NBW * B;
+  const int64_t wg_base = (int64_t)wgb * NBW * B;
   // chunk c into buffer buf: piece i (16 bytes) = segment i / (32 rows) (the workgroup's block), row
   // (i mod 32 rows) / 32 (spectrum rows, then Y rows), column i mod 32, at LDS byte 16 i -- a wave's
   // spectra and Y of a chunk are then at compile-time offsets from one base.  Wave-instruction j moves
@@ -475,7 +482,7 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
   // and per-chunk step per lane, formed once (a chunk further is NS 64 doubles on in the chunked spectra,
   // 64 in a Y row).
   constexpr int kMaxDma = kSpecMaxDma;              // tile <= 512 kMaxDma doubles: 1-KiB instructions, kMaxDma per wave
-  static_assert(kSpecRing >= 2, "the deferred step's scratch lives in ring slot RING - 1");
+  static_assert(RING >= 2, "the deferred step's scratch lives in ring slot RING - 1");
   const double* src0[kMaxDma];
   int64_t step[kMaxDma];
 #pragma unroll
@@ -484,7 +491,8 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
     const int i = (jj < ninst ? jj : 0) * 64 + lane;
     const int sg = i / segp, rem = i - sg * segp, r = rem >> 5, col = rem & 31;
     const int64_t k = wg_base + sg * B;             // the segment's first frequency in chunk 0
-    src0[t] = (r < NS ? a.basis + spec_at<NS>(k, r) : a.ysq + ysq_at(a, r - NS, k)) + 2 * col;
+    const int gy = min(goff + r - NS, G - 1);
+    src0[t] = (r < NS ? a.basis + spec_at<NS>(k, r) : a.ysq + ysq_at(a, gy, k)) + 2 * col;
     step[t] = r < NS ? NS * 64 : (a.ysq_chunked ? (int64_t)G * 64 : 64);
   }
   auto issue = [&](int c, double* buf) {
@@ -521,7 +529,7 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
     for (int p = 0; p < PPW; ++p) load_hyp_wave(a, on[p] ? g0 + p : 0, h[p], nraw);
   } else {
 #pragma unroll
-    for (int p = 0; p < PPW; ++p) load_hyp_wave(a, on[p] ? g0 + p : 0, h[p]);
+    for (int p = 0; p < PPW; ++p) load_hyp_wave(a, on[p] ? goff + g0 + p : 0, h[p]);
   }
   for (int c = 0; c < nc; ++c) {
     // this wave's loads of chunk c have landed (chunks c + 1 .. c + RING - 2 may stay in flight)
@@ -543,13 +551,14 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
   // the block's partials (k_spec_iter's values; sc1 when handed to the last workgroup)
 #pragma unroll
   for (int p = 0; p < PPW; ++p)
-    if (on[p] && active) spec_block_partials<D, NET>(a, h[p], g0 + p, blk, rootn, wl, acc[p], fz.counters != nullptr);
+    if (on[p] && active)
+      spec_block_partials<D, NET>(a, h[p], goff + g0 + p, blk, rootn, wl, acc[p], fz.counters != nullptr);
   if (fz.counters) {
     // Level 1 of the fused reduction (MI355X_MICROARCH.md hand-off row 1: sc1 stores retired by every
     // storing wave, then ONE lane's agent-scope add; the waiter reads with sc1 loads after a barrier): the
     // last workgroup of each group of kSpecGroup blocks sums the group into the level-2 inputs of parity
     // fz.par.  Level 2 and the step follow in the next launch's prologue (or k_spec_finish_step).
-    const int grp = (int)blockIdx.x * NBW / kSpecGroup;
+    const int grp = wgb * NBW / kSpecGroup;
     const int wg_in_grp = (min(kSpecGroup, a.nb - grp * kSpecGroup) + NBW - 1) / NBW;
     unsigned* cnt_grp = fz.counters + grp;
     int* flag = reinterpret_cast<int*>(lds);        // the ring is free now
@@ -857,6 +866,8 @@ void spec_geometry(Nll& a) {
   a.spec_tile = 0;
   a.spec_pgp = a.spec_ck = 0;
   a.spec_kw = 0;
+  a.spec_ps = 0;
+  a.spec_nsl = 1;
   const char* te = getenv("FGP_SPEC_TILE");   // 0: the per-wave kernel only (A/B experiments)
   const bool tile_ok = !(te && te[0] == '0');
   // Tile kernel (one shared set of spectra, d <= 5): 2 problems per wave (1 for G = 1), problem groups
@@ -880,6 +891,34 @@ void spec_geometry(Nll& a) {
       a.spec_kw = (int64_t)(4 / pgp) * 64 * a.spec_kpl;
       return;
     }
+    // many problems (G > 8, e.g. per-output hyper-parameters): slices of PS = 4 PPW problems (PPW = 4 at
+    // d <= 3, else 2), one slot per wave, one k block per workgroup -- every slice streams its own Y rows
+    // and re-reads the shared spectra (from L2: the slices of a block run on consecutive workgroups)
+    const int sppw = a.d <= 3 ? 4 : 2, ps = 4 * sppw, srows = (1 << a.d) + ps;
+    // k blocks: 64 chunks per workgroup (with 4, the per-wave kernel's 512 blocks at n = 2^18, the
+    // workgroups spend their life in the prologue: 383 vs 153 us per C5 per-output iteration; a 4-deep ring
+    // does not pay, profiles/r03sl_exp_slices.jsonl), more blocks while the grid has fewer than 512
+    // workgroups; FGP_SPEC_SLICE_NB overrides (A/B experiments)
+    const int nsl = (a.G + ps - 1) / ps;
+    int64_t snb = std::max<int64_t>(1, a.spec_main / (64 * 64));
+    while (snb * nsl < 512 && snb * 2 <= lanes) snb *= 2;
+    snb = std::min<int64_t>(snb, a.nb);
+    const char* se = getenv("FGP_SPEC_SLICE_NB");
+    if (se) snb = std::max(1, std::min(a.nb, atoi(se)));
+    if (pg > 4 && srows * 64 * 8 * kSpecRing <= kSpecLdsMax && srows * 64 <= 512 * kSpecMaxDma &&
+        (srows * 64) % 128 == 0 && srows * 64 >= kSpecScratch && a.spec_main % (64 * snb) == 0) {
+      a.nb = (int)snb;
+      a.spec_kpl = (int)(a.spec_main / (64 * snb));
+      a.spec_tile = 1;
+      a.spec_ppw = sppw;
+      a.spec_pg = 4;
+      a.spec_pgp = 4;
+      a.spec_ck = 64;
+      a.spec_kw = 64 * a.spec_kpl;
+      a.spec_ps = ps;
+      a.spec_nsl = nsl;
+      return;
+    }
   }
   // per-wave kernel k_spec_iter: problems per wave sharing one read of the spectra, 2, and for many
   // problems (e.g. per-output hyper-parameters) 4 -- the spectra are then re-read from L2 G / 4 times
@@ -898,11 +937,13 @@ int64_t spec_chunks(bool net, int log2n) {
 int launch_spec_iter(const Nll& a, hipStream_t st, const FitFuse* fz) {
   if (a.spec_tile) {
     if (a.spec_ppw > 4) return set_error(kErrInvalid, "spectral tile kernel: %d problems per wave", a.spec_ppw);
+    if (fz && a.spec_ps) return set_error(kErrInvalid, "spectral tile kernel: no fused step over problem slices");
     FitFuse none{};
     none.counters = nullptr;
     const FitFuse& f = fz ? *fz : none;
-    const size_t shm = sizeof(double) * (size_t)kSpecRing * (size_t)(((1 << a.d) + a.G) * a.spec_ck);
-    const unsigned grid = (unsigned)(a.nb / (4 / a.spec_pgp));
+    const int trows = (1 << a.d) + (a.spec_ps ? a.spec_ps : a.G);
+    const size_t shm = sizeof(double) * (size_t)kSpecRing * (size_t)(trows * a.spec_ck);
+    const unsigned grid = (unsigned)(a.nb / (4 / a.spec_pgp) * a.spec_nsl);
     return with_spec_d(a.d, [&](auto dc) {
       constexpr int D = decltype(dc)::value;
       if constexpr (D <= 5) {
@@ -920,15 +961,14 @@ int launch_spec_iter(const Nll& a, hipStream_t st, const FitFuse* fz) {
           }
           kern<<<grid, kWG, shm, st>>>(a, f);
         };
-        if (a.spec_net) {
-          if (a.spec_ppw == 4) go(k_spec_tile<D, 4, true>);
-          else if (a.spec_ppw == 2) go(k_spec_tile<D, 2, true>);
-          else go(k_spec_tile<D, 1, true>);
-        } else {
-          if (a.spec_ppw == 4) go(k_spec_tile<D, 4, false>);
-          else if (a.spec_ppw == 2) go(k_spec_tile<D, 2, false>);
-          else go(k_spec_tile<D, 1, false>);
-        }
+        auto net = [&](auto nc) {
+          constexpr bool NET = decltype(nc)::value;
+          if (a.spec_ppw == 4) go(k_spec_tile<D, 4, NET>);
+          else if (a.spec_ppw == 2) go(k_spec_tile<D, 2, NET>);
+          else go(k_spec_tile<D, 1, NET>);
+        };
+        if (a.spec_net) net(std::true_type{});
+        else net(std::false_type{});
         return check_launch("k_spec_tile");
       } else {
         return set_error(kErrInvalid, "spectral tile kernel: d > 5");

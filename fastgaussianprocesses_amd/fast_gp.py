@@ -28,7 +28,7 @@ import torch
 from . import _native
 from . import ops
 from . import seqs as _seqs
-from .fit_engine import FusedMLL, LatticePartsGen, mll_constant, spec_basis, spectral_wanted
+from .fit_engine import FusedMLL, LatticePartsGen, mll_constant, spec_basis, spec_inv_eig, spectral_wanted
 
 
 def _log(x):
@@ -547,6 +547,20 @@ class AbstractFastGP(torch.nn.Module):
             y = self._y[0].to(torch.float64)
             yt = ops.fftbr_raw(y, stable=True) if self._FAMILY == ops.LATTICE else ops.fwht_raw(y, stable=True)
         pb = self._problem_batch() if (self._lam_fusable(n) and not self.adaptive_nugget) else None
+        basis = None
+        if (pb is not None and self._FAMILY == ops.LATTICE and 17 <= n.bit_length() - 1 <= 24
+                and pb[1] in (1, yt.numel() // n)):
+            basis = self._spec_basis(n, pb[1])
+        if basis is not None:
+            # spectral path: the real A = 1/ev straight from the part-product spectra (fgp_spec_inv_eig; one
+            # row shared by every output, or one per output's eigen-problem), the product fused into the
+            # half-length real inverse (fgp_ifftbr_real_rf) -- no lambda, no ytilde * A array
+            self._task_scalar()
+            wa = spec_inv_eig(self._FAMILY, self.raw_scale.detach().reshape(-1),
+                              self.raw_lengthscales.detach().reshape(-1, self.raw_lengthscales.shape[-1]),
+                              self.raw_noise.detach().reshape(-1), pb[1], n, basis)
+            self._cached(("inv_real", n), lambda: wa.reshape(tuple(pb[0]) + (n,)))
+            return ops.ifftbr_real_rf(yt, wa)
         if pb is not None and yt.numel() == pb[1] * n:
             # one output per eigen-problem: A = 1/ev and ytilde * A in ONE launch (fgp_inv_eig) instead of
             # the torch chain of get_inv_log_det; Re(A) kept for post_var's quadratic form

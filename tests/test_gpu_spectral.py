@@ -184,3 +184,32 @@ def test_spectral_coefficients_from_spectra(m):
                 o.raw_noise.copy_(gp.raw_noise.cpu())
             # coeffs = K^-1 y at cond(K) ~ n / noise: the 1e-5 of DESIGN.md section 1 (measured 1.8e-6)
             assert rel_err(c[p], o.coeffs().detach()) < 1e-5
+
+
+@pytest.mark.parametrize("m,d,G", [(14, 3, 40), (17, 3, 16), (14, 5, 19), (12, 2, 9)])
+def test_problem_slices_equal_per_wave_kernel(m, d, G, monkeypatch):
+    """Many eigen-problems on one set of spectra (per-output hyper-parameters, shape_scale = [G, 1],
+    docs/examples/batch_multitask/fgp_lattice.ipynb cell 6): the tile kernel over problem slices (G > 8:
+    slices of 16 problems at d <= 3, 8 above; ragged last slice) against the per-wave kernel k_spec_iter
+    (FGP_SPEC_TILE=0) -- the same per-block partials in the same order, so the fits agree to rounding of
+    the fixed reduction (1e-13); parameters after 6 iterations to 1e-12; the spectral coefficients
+    (fgp_spec_inv_eig + fgp_ifftbr_real_rf at m >= 17) against the lambda route to 1e-12."""
+    monkeypatch.setenv("FGP_FIT_PATH", "spectral")
+    g = torch.Generator().manual_seed(G)
+    ls0 = 0.3 * torch.randn((G, d), generator=g)
+    res = {}
+    for tile in ("1", "0"):
+        monkeypatch.setenv("FGP_SPEC_TILE", tile)
+        gp, _, _ = _gp("lattice", d, m, shape_batch=[G], shape_scale=[G, 1], shape_lengthscales=[G, d])
+        with torch.no_grad():
+            gp.raw_lengthscales.add_(ls0.to(DEV))
+        data = gp.fit(iterations=6, store_loss_hist=True, verbose=0, stop_crit_wait_iterations=20)
+        with torch.no_grad():
+            c = gp.coeffs.clone()
+            if m >= 17:      # the spectral coefficient route against ift(ft(y) / ev).real (util.py:338-353)
+                assert rel_err(c, gp._solve(gp._y[0], 2 ** m)) <= 1e-12
+        res[tile] = (data["loss_hist"].cpu(), gp.raw_lengthscales.detach().cpu().clone(), c.cpu())
+    (la, pa, ca), (lb, pb, cb) = res["1"], res["0"]
+    assert rel_err(la, lb) <= 1e-13
+    assert float((pa - pb).abs().max()) <= 1e-12
+    assert rel_err(ca, cb) <= 1e-12
