@@ -12,7 +12,7 @@ import torch
 
 _LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
 LIB_PATH = os.environ.get("FGP_LIB_PATH") or os.path.join(_LIB_DIR, "libfgp_hip.so")   # override: experiments
-ABI_VERSION = 12
+ABI_VERSION = 13
 MT_MAX_TASKS = 16
 MAX_D = 8
 PARTS_ARRAY = 0
@@ -110,6 +110,7 @@ _SIGNATURES = {
     "fgp_nll_bwd": [_P_NLL, _c_vp],
     "fgp_nll_lam": [_P_NLL, _c_vp],
     "fgp_spec_inv_eig": [_P_NLL, _c_vp, _c_vp],
+    "fgp_spec_post_var": [_P_NLL, _c_vp, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp],
     "fgp_nll_stage": [_P_NLL, _c_int, _c_vp],
     "fgp_post_var_qf": [_c_int, _c_vp, _c_i64, _c_vp, _c_int, _c_int, _c_int, _c_pi, _c_pd, _c_vp, _c_vp, _c_vp,
                         _c_vp, _c_vp, _c_vp],

@@ -591,7 +591,10 @@ RpState spec_scratch_state(const Nll& a, int par);
 // the deferred step of a fused spectral run's last iteration (after its last k_spec_tile launch)
 int launch_spec_finish_step(const Nll& a, const FitFuse& fz, hipStream_t st);
 int launch_spec_lam(const Nll& a, hipStream_t st);    // lambda of the current parameters into grad_lam
-int launch_spec_inv_eig(const Nll& a, double* wa, hipStream_t st);   // A = 1 / (sqrt(n) lambda + noise), [G][n]
+int launch_spec_inv_eig(const Nll& a, double* wa, hipStream_t st);
+constexpr int kSpvKpl = 16;   // fgp_spec_post_var: frequencies per lane of a wave's block (64 kSpvKpl per block)
+int launch_spec_post_var(const Nll& a, const double2* psi, int N, const double* part0, double* out, double* partial,
+                         int nblk, int kpl, hipStream_t st);   // A = 1 / (sqrt(n) lambda + noise), [G][n]
 // multitask spectral fit (ABI 12): at most kMtMaxT tasks, kMtF frequencies per chunk
 constexpr int kMtMaxT = 8;
 constexpr int kMtF = 32;

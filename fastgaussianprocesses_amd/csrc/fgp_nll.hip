@@ -1569,6 +1569,22 @@ int fgp_spec_inv_eig(const fgp_nll_desc* desc, double* wa, void* stream) {
   return launch_spec_inv_eig(a, wa, (hipStream_t)stream);
 }
 
+int fgp_spec_post_var(const fgp_nll_desc* desc, const void* psi, int64_t N, const double* part0, double* out,
+                      double* partial, void* stream) {
+  Nll a;
+  int rc = to_nll(desc, a);
+  if (rc != kOk) return rc;
+  if (!a.spec || a.mt || a.spec_net || a.basis_stride != 0 || a.d > 4)
+    return set_error(kErrInvalid, "fgp_spec_post_var: needs the lattice spectral desc with shared spectra, d <= 4");
+  if (N < 0 || N > 4096) return set_error(kErrInvalid, "fgp_spec_post_var: 0 <= N <= 4096");
+  if (N == 0) return kOk;
+  if (!psi || !part0 || !out || !partial) return set_error(kErrInvalid, "fgp_spec_post_var: null pointer");
+  const int64_t half = ((int64_t)1 << a.log2n) / 2;
+  const int nblk = (int)((half + 1 + 64 * kSpvKpl - 1) / (64 * kSpvKpl));
+  return launch_spec_post_var(a, static_cast<const double2*>(psi), (int)N, part0, out, partial, nblk, kSpvKpl,
+                              (hipStream_t)stream);
+}
+
 int fgp_nll_lam(const fgp_nll_desc* desc, void* stream) {
   Nll a;
   int rc = to_nll(desc, a);

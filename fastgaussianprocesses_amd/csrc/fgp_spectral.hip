@@ -833,6 +833,84 @@ __global__ __launch_bounds__(kWG) void k_spec_inv_eig(Nll a, double* __restrict_
   }
 }
 
+// ---------------------------------------------------------------- posterior variance over many problems
+// (fgp_spec_post_var, ABI 13).  G eigen-problems on ONE point set (per-output hyper-parameters, e.g. C5
+// per-output) and N test points: the reference forms, per problem g and test point t, the kernel row
+// r_gt[i] = K_g(x_t, x_i) and the quadratic form r^T K_g^-1 r = sum_k Re(A_gk) |ft(r_gt)_k|^2 (abstract_gp.py:
+// 407-413, util.py:338-353; k_qf_* evaluate it by one transform per (g, t)).  The row is multilinear in the
+// lengthscales, r_gt = scale_g sum_S l_g^S rho_S(t) with rho_S(t)[i] = prod_{j in S} part_j(x_t, x_i), so by
+// linearity of ft
+//     ft(r_gt)_k = scale_g sum_S l_g^S Psi_S(t, k),   Psi_S(t) = ft(rho_S(t))    (2^d N transforms, ONCE),
+// and A_gk = 1 / (sqrt(n) scale_g sum_S l_g^S Phi_S(k) + noise_g) from the fit's part-product spectra
+// (k_spec_inv_eig's arithmetic).  Real rows: |ft(r)_k| = |ft(r)_{n-k}| and A_k = A_{n-k}, so k <= n/2 with
+// weights 2 (1 at k = 0, n/2).  Wave = (block of 64 kpl frequencies, kSpvPS problems); the 4 waves of a
+// workgroup take consecutive problem slices of the same block (the Psi / Phi loads hit L1 / L2 three times
+// in four); per (t, g) a lane sum over its frequencies, the fixed wave reduction, one partial per block:
+// partial[(g N + t) nblk + blk] (k_qf_finish sums them in order and forms K(x,x) - sum).
+constexpr int kSpvPS = 16;
+template <int D>
+__global__ __launch_bounds__(kWG) void k_spec_post_var(Nll a, const double2* __restrict__ psi, int N, int kpl,
+                                                       int nblk, double* __restrict__ partial) {
+  constexpr int NS = 1 << D, HS = 2 + D;
+  __shared__ double hl[kWG / 64][kSpvPS][HS];          // scale, noise, l_j of the wave's problems
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int blk = (int)blockIdx.x;
+  const int g0 = ((int)blockIdx.y * (kWG / 64) + w) * kSpvPS;
+  if (g0 >= a.G) return;                              // wave-uniform; no barriers below
+  const int cnt = min(kSpvPS, a.G - g0);
+  for (int p = 0; p < cnt; ++p) {
+    Hyp h;
+    load_hyp_wave(a, g0 + p, h);
+    if (lane == 0) {
+      hl[w][p][0] = h.scale;
+      hl[w][p][1] = h.noise;
+#pragma unroll
+      for (int j = 0; j < D; ++j) hl[w][p][2 + j] = h.ls[j];
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the wave's own LDS stores, read back by every lane
+  const int64_t n = (int64_t)1 << a.log2n, half = n / 2;
+  const double rootn = sqrt((double)n);
+  double dp[D];
+  for (int t = 0; t < N; ++t) {
+    double acc[kSpvPS];
+#pragma unroll
+    for (int p = 0; p < kSpvPS; ++p) acc[p] = 0.0;
+    for (int i = 0; i < kpl; ++i) {
+      const int64_t k = ((int64_t)blk * kpl + i) * 64 + lane;
+      if (k > half) break;
+      double phi[NS], pr[NS], pi[NS];
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        phi[s] = a.basis[spec_at<NS>(k, s)];
+        const double2 v = psi[((int64_t)t * NS + s) * n + k];
+        pr[s] = v.x;
+        pi[s] = v.y;
+      }
+      const double wk = (k == 0 || k == half) ? 1.0 : 2.0;
+#pragma unroll
+      for (int p = 0; p < kSpvPS; ++p) {
+        if (p < cnt) {
+          double l[D];
+#pragma unroll
+          for (int j = 0; j < D; ++j) l[j] = hl[w][p][2 + j];
+          const double sc = hl[w][p][0];
+          const double A = 1.0 / (rootn * (sc * mlin<D>(phi, l, dp)) + hl[w][p][1]);
+          const double re = mlin<D>(pr, l, dp), im = mlin<D>(pi, l, dp);
+          acc[p] = __builtin_fma(wk * A * sc * sc, __builtin_fma(re, re, im * im), acc[p]);
+        }
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < kSpvPS; ++p) {
+      double v = acc[p];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      if (lane == 0 && p < cnt) partial[((int64_t)(g0 + p) * N + t) * nblk + blk] = v;
+    }
+  }
+}
+
 template <typename Fn>
 static int with_spec_d(int d, Fn&& fn) {
   switch (d) {
@@ -1021,6 +1099,44 @@ int launch_spec_finish_step(const Nll& a, const FitFuse& fz, hipStream_t st) {
   return with_spec_d(a.d, [&](auto dc) {
     k_spec_finish_step<decltype(dc)::value><<<1, kWG, 0, st>>>(a, fz);
     return check_launch("k_spec_finish_step");
+  });
+}
+
+// out[g, t] = K_g(x_t, x_t) - sum_b partial[(g N + t) nblk + b] (ascending b), negatives set to 0
+// (abstract_gp.py:407-413; K(x, x) = scale prod_j (1 + l_j part0_j), k_qf_finish's arithmetic)
+struct Part0 {
+  double v[FGP_MAX_D];
+};
+__global__ __launch_bounds__(kWG) void k_spec_post_var_finish(Nll a, const double* __restrict__ partial, int N, int nblk,
+                                                              Part0 p0, double* __restrict__ out) {
+  const int e = (int)blockIdx.x * kWG + threadIdx.x, g = e / max(N, 1);
+  if (e >= a.G * N) return;
+  Hyp h;
+  load_hyp(a, g, h);
+  double s = 0.0;
+  for (int b = 0; b < nblk; ++b) s += partial[(int64_t)e * nblk + b];
+  double pr = 1.0;
+  for (int j = 0; j < a.d; ++j) pr *= 1.0 + h.ls[j] * p0.v[j];
+  const double v = h.scale * pr - s;
+  out[e] = v < 0.0 ? 0.0 : v;
+}
+
+int launch_spec_post_var(const Nll& a, const double2* psi, int N, const double* part0, double* out, double* partial,
+                         int nblk, int kpl, hipStream_t st) {
+  const dim3 grid((unsigned)nblk, (unsigned)((a.G + kSpvPS * (kWG / 64) - 1) / (kSpvPS * (kWG / 64))));
+  return with_spec_d(a.d, [&](auto dc) {
+    constexpr int D = decltype(dc)::value;
+    if constexpr (D <= 4) {
+      k_spec_post_var<D><<<grid, kWG, 0, st>>>(a, psi, N, kpl, nblk, partial);
+      int rc = check_launch("k_spec_post_var");
+      if (rc != kOk) return rc;
+      Part0 p0{};
+      for (int j = 0; j < a.d && j < FGP_MAX_D; ++j) p0.v[j] = part0[j];
+      k_spec_post_var_finish<<<(unsigned)(((int64_t)a.G * N + kWG - 1) / kWG), kWG, 0, st>>>(a, partial, N, nblk, p0, out);
+      return check_launch("k_spec_post_var_finish");
+    } else {
+      return set_error(kErrInvalid, "fgp_spec_post_var: d <= 4");
+    }
   });
 }
 

@@ -28,7 +28,7 @@ import torch
 from . import _native
 from . import ops
 from . import seqs as _seqs
-from .fit_engine import FusedMLL, LatticePartsGen, mll_constant, spec_basis, spec_inv_eig, spectral_wanted
+from .fit_engine import FusedMLL, LatticePartsGen, mll_constant, spec_basis, spec_inv_eig, spec_post_var, spectral_wanted
 
 
 def _log(x):
@@ -942,6 +942,9 @@ class AbstractFastGP(torch.nn.Module):
         fgp_post_var_batched (shared points, z_stride 0), problems in chunks of <= work_bytes scratch --
         instead of G x N kernel rows solved by full-length transforms."""
         pb, G = self._problem_batch()
+        out = self._post_var_spectral(x, n, G)
+        if out is not None:
+            return out.reshape(tuple(self.shape_batch) + (x.size(0),))
         wa = self._cached(("inv_real", n), lambda: (lambda a: (a.real if a.is_complex() else a))(self._inv(n)))
         wa = wa.reshape(G, n).contiguous()
         hyp = self._hyp_rows(True).contiguous()                   # [G, 1 + d]
@@ -967,6 +970,36 @@ class AbstractFastGP(torch.nn.Module):
             _native.call("fgp_post_var_batched", desc, _native.ptr(x), 0, Nt, part0, _native.ptr(out[p0:p1]),
                          _native.ptr(work), _native.ptr(partial), _native.stream_ptr(self.device))
         return out.reshape(tuple(self.shape_batch) + (Nt,))
+
+    def _post_var_spectral(self, x, n, G):
+        """[G, N] posterior variances of G lattice eigen-problems on one point set from the row spectra of
+        the test points (fgp_spec_post_var): Psi_S(t) = ft(prod_{j in S} part_j(x_t, .)) -- 2^d N transforms
+        once, hyper-parameter free -- and ft(K_g(x_t, .)) = scale_g sum_S l_g^S Psi_S(t) by linearity, instead
+        of one transform per (problem, test point).  None when it does not apply (nets, d > 4, no shared
+        spectra, adaptive nugget, non-exp transforms, or fewer than 16 problems: the per-row transforms are
+        then as cheap)."""
+        if (self._FAMILY != ops.LATTICE or self.d > 4 or G < 16 or self.adaptive_nugget or not self._lam_fusable(n)
+                or os.environ.get("FGP_SPEC_POST_VAR", "1") == "0"):
+            return None
+        basis = self._spec_basis(n, G)
+        if basis is None or basis.dim() != 3:
+            return None
+        self._task_scalar()
+        d, Nt = self.d, x.size(0)
+        self._ensure_points(n)
+        xb = self._xb[:n]
+        rho = torch.empty((Nt, 2 ** d, n), dtype=torch.float64, device=self.device)
+        rho[:, 0] = 1.0
+        for t in range(Nt):
+            parts = ops.lattice_parts(xb, x[t], self._alphas)          # [d, n]: part_j(x_i, x_t)
+            for S in range(1, 2 ** d):
+                j = S.bit_length() - 1
+                torch.mul(rho[t, S ^ (1 << j)], parts[j], out=rho[t, S])
+        psi = ops.fftbr_raw(rho, stable=True)
+        return spec_post_var(self.raw_scale.detach().reshape(-1),
+                             self.raw_lengthscales.detach().reshape(-1, self.raw_lengthscales.shape[-1]),
+                             self.raw_noise.detach().reshape(-1), G, n, basis, psi.contiguous(),
+                             self._part_at_zero().tolist())
 
     def _kdiag(self, x):
         """K(x, x) (zero distance parts)."""

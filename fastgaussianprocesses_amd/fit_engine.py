@@ -390,6 +390,37 @@ def spec_inv_eig(family, raw_scale, raw_lengthscales, raw_noise, G, n, basis):
     return wa
 
 
+def _spec_desc(family, raw, S, Sl, Dl, Sn, G, n, d, basis, scratch):
+    m = log2_exact(n)
+    return N.NllDesc(family=family, log2n=m, d=d, G=G, parts=0, parts_stride=0, ysq=scratch.data_ptr(), ysq_stride=0,
+                     raw=raw.data_ptr(), scale_off=0, scale_pp=int(S == G and G > 1), ls_off=S,
+                     ls_pp=int(Sl == G and G > 1), ls_pd=int(Dl == d), noise_off=S + Sl * Dl,
+                     noise_pp=int(Sn == G and G > 1), logdet_weight=1.0, grad_lam=0, work=0,
+                     partials=scratch.data_ptr(), basis=basis.data_ptr(),
+                     basis_stride=(basis[0].numel() if basis.dim() == 4 else 0))
+
+
+def spec_post_var(raw_scale, raw_lengthscales, raw_noise, G, n, basis, psi, part0):
+    """Posterior variances [G, N] of G lattice problems sharing the part-product spectra `basis` ([Q, 2^d, 64])
+    at N test points from the row spectra psi [N, 2^d, n] (complex128, fftbr of the part-product rows of
+    each test point) via fgp_spec_post_var: ft(K_g(x_t, .)) = scale_g sum_S l_g^S psi[t, S] by linearity."""
+    require_device(basis, "spec_post_var")
+    d, dev = int(round(math.log2(basis.shape[-2]))), basis.device
+    Nt = psi.shape[0]
+    assert psi.shape == (Nt, 2 ** d, n) and psi.dtype == torch.complex128 and psi.is_contiguous()
+    S, (Sl, Dl), Sn = raw_scale.numel(), raw_lengthscales.shape, raw_noise.numel()
+    raw = torch.cat([raw_scale.reshape(-1), raw_lengthscales.reshape(-1), raw_noise.reshape(-1)]).to(
+        device=dev, dtype=torch.float64).contiguous()
+    nblk = (n // 2 + 1 + 1023) // 1024
+    partial = torch.empty((max(1, G * Nt * nblk),), dtype=torch.float64, device=dev)
+    out = torch.empty((G, Nt), dtype=torch.float64, device=dev)
+    basis = basis.contiguous()
+    desc = _spec_desc(0, raw, S, Sl, Dl, Sn, G, n, d, basis, partial)
+    N.call("fgp_spec_post_var", desc, N.ptr(psi), Nt, N.double_array([float(v) for v in part0]), N.ptr(out),
+           N.ptr(partial), N.stream_ptr(dev))
+    return out
+
+
 def fused_lam(family, parts, raw_scale, raw_lengthscales, raw_noise, G, gen=None, n=None, basis=None):
     """lambda = ft(k1) for G eigen-problems sharing `parts` ([d, n]), with parts of their own
     ([G, d, n]), with the generator `gen` (size n), or from part-product spectra `basis` ([Q, 2^d, 64]

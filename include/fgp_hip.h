@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define FGP_ABI_VERSION 12
+#define FGP_ABI_VERSION 13
 
 #define FGP_OK 0
 #define FGP_ERR_INVALID (-1)     /* bad argument (shape, stride, null pointer) */
@@ -240,6 +240,21 @@ typedef struct fgp_nll_desc {
  * util.py:285,292-300 with lambda = scale sum_S l^S Phi_S, real): wa [G][n] float64 (lattice: the even
  * spectrum mirrored) -- fgp_inv_eig's wa without materialising lambda (ABI 12).  ysq / partials unused. */
 int fgp_spec_inv_eig(const fgp_nll_desc* desc, double* wa, void* stream);
+
+/* Posterior variance of the G problems of a lattice spectral desc with SHARED spectra (per-output
+ * hyper-parameters on one point set; d <= 4) at N test points (ABI 13): abstract_gp.py:407-413's
+ * K(x,x) - r^T K^-1 r with r^T K^-1 r = sum_k Re(A_k) |ft(r)_k|^2 (util.py:338-353), where ft of the kernel
+ * row is formed from the hyper-parameter-free row spectra by linearity, ft(r_gt) = scale_g sum_S l_g^S
+ * Psi_S(t), and A from the fit's part-product spectra -- one pass over Psi for every problem instead of
+ * one transform per (problem, test point).
+ *   psi      device complex128 [N][2^d][n]: fftbr (stable) of rho_S(t)[i] = prod_{j in S} part_j(x_t, x_i),
+ *            the points in the GP's order (S = 0: the all-ones row)
+ *   part0    host [d]: the parts at zero distance (K(x, x) = scale prod_j (1 + l_j part0_j))
+ *   out      device float64 [G][N], clamped at 0
+ *   partial  device scratch of G N ceil((n/2 + 1) / 1024) doubles
+ * ysq / partials of the desc unused. */
+int fgp_spec_post_var(const fgp_nll_desc* desc, const void* psi, int64_t N, const double* part0, double* out,
+                      double* partial, void* stream);
 
 /* Doubles the `partials` workspace of this desc needs (per-block partials + the fused fit's counters):
  * G (4 + d) (max(nb, n / 4096) + 1) + G, nb the kernels' block count (spectral path: up to 512). */

@@ -213,3 +213,31 @@ def test_problem_slices_equal_per_wave_kernel(m, d, G, monkeypatch):
     assert rel_err(la, lb) <= 1e-13
     assert float((pa - pb).abs().max()) <= 1e-12
     assert rel_err(ca, cb) <= 1e-12
+
+
+@pytest.mark.parametrize("m,d,G", [(14, 3, 40), (17, 2, 16), (15, 4, 20)])
+def test_spectral_post_var_equals_per_row_transforms(m, d, G, monkeypatch):
+    """Posterior variance of G problems on one point set (per-output hyper-parameters) from the row spectra
+    of the test points (fgp_spec_post_var: ft(K_g(x_t, .)) = scale_g sum_S l_g^S Psi_S(t) by linearity, A
+    from the fit's spectra) against one transform per (problem, test point) (fgp_post_var_batched,
+    FGP_SPEC_POST_VAR=0): the quadratic forms agree to rounding; var = K(x,x) - qf is compared on the
+    scale of K(x,x) (1e-10), as it cancels near the data.  Also at a future n = 2^(m+1)."""
+    monkeypatch.setenv("FGP_FIT_PATH", "spectral")
+    g = torch.Generator().manual_seed(G + d)
+    gp, _, _ = _gp("lattice", d, m, shape_batch=[G], shape_scale=[G, 1], shape_lengthscales=[G, d])
+    with torch.no_grad():
+        gp.raw_lengthscales.add_((0.3 * torch.randn((G, d), generator=g)).to(DEV))
+        gp.raw_scale.add_((0.2 * torch.randn((G, 1), generator=g)).to(DEV))
+        gp.raw_noise.fill_(math.log(1e-4))
+    x = torch.rand((5, d), generator=g).to(DEV)
+    kxx = gp._kdiag(x).detach().reshape(G, 1)
+    for n in (None, 2 ** (m + 1)):
+        monkeypatch.setenv("FGP_SPEC_POST_VAR", "1")
+        gp._cache = {}
+        v_spec = gp.post_var(x, n=n).reshape(G, -1)
+        assert gp._post_var_spectral(x, n or 2 ** m, G) is not None
+        monkeypatch.setenv("FGP_SPEC_POST_VAR", "0")
+        gp._cache = {}
+        v_row = gp.post_var(x, n=n).reshape(G, -1)
+        assert float(((v_spec - v_row).abs() / kxx).max()) <= 1e-10
+        assert bool((v_spec >= 0).all())
