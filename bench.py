@@ -248,7 +248,8 @@ def secondary_configs(F, args, device, rank=0, world=1):
         sg = make()
         xm = torch.rand((args.n_mean, d), generator=g).to(device)
         xv = torch.rand((args.n_var, d), generator=g).to(device)
-        sec = time_steps(lambda: step_single(sg, args, xm, xv), max(1, args.steps), 1, device)
+        # at least 5 timed steps after 2 warm-ups: a one-off host stall in a ~1 ms step is not the config's rate
+        sec = time_steps(lambda: step_single(sg, args, xm, xv), max(5, args.steps), 2, device)
         phases = None
         if world == 1:
             # per-phase median of 3 event-timed steps (one sample can catch a host stall)
@@ -274,7 +275,7 @@ def secondary_configs(F, args, device, rank=0, world=1):
         out.append({"metric": "GP fit+predict points/sec" if total == 1 else
                     "multi-output GP fit+predict output-points/sec",
                     "value": sg.n * total / sec, "unit": "points/s" if total == 1 else "output-points/s",
-                    "ms_per_step": sec * 1e3, "steps": max(1, args.steps), "n_gpus": world,
+                    "ms_per_step": sec * 1e3, "steps": max(5, args.steps), "n_gpus": world,
                     "dtype": "f64" if sg.gp.data_dtype == torch.float64 else "f32 data / f64 eigenvalues",
                     "config": {"workload": "%s: fit %d Rprop iters + post_mean N=%d + post_var N=%d"
                                            % (name, args.fit_iters, args.n_mean, args.n_var),
@@ -622,9 +623,9 @@ def roofline_fit_kernels(F, shifts, iters):
 
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r03f_pmc_fit_kernels.json")
-PMC_SQ_SUMMARY = os.path.join(ROOT, "profiles", "r03f_pmc_sq_fit_kernels.json")
-ROCPROF_GRID_STATS = os.path.join(ROOT, "profiles", "r03f_bench_kernel_grid_stats.txt")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r03g_pmc_fit_kernels.json")
+PMC_SQ_SUMMARY = os.path.join(ROOT, "profiles", "r03g_pmc_sq_fit_kernels.json")
+ROCPROF_GRID_STATS = os.path.join(ROOT, "profiles", "r03g_bench_kernel_grid_stats.txt")
 # the read floor of the spectral iteration's footprint: tools/stream_microbench.hip over the same 168 MB,
 # re-read back to back, 24.0-24.3 us per pass (7.0 TB/s; profiles/r03v_stream_and_stamps.jsonl)
 STREAM_FLOOR_US = 24.0

@@ -842,12 +842,12 @@ __global__ __launch_bounds__(kWG) void k_spec_inv_eig(Nll a, double* __restrict_
 // linearity of ft
 //     ft(r_gt)_k = scale_g sum_S l_g^S Psi_S(t, k),   Psi_S(t) = ft(rho_S(t))    (2^d N transforms, ONCE),
 // and A_gk = 1 / (sqrt(n) scale_g sum_S l_g^S Phi_S(k) + noise_g) from the fit's part-product spectra
-// (k_spec_inv_eig's arithmetic).  Real rows: |ft(r)_k| = |ft(r)_{n-k}| and A_k = A_{n-k}, so k <= n/2 with
+// (k_spec_inv_eig's arithmetic; 1 / ev by rcp_nr, within an ulp).  Real rows: |ft(r)_k| = |ft(r)_{n-k}| and A_k = A_{n-k}, so k <= n/2 with
 // weights 2 (1 at k = 0, n/2).  Wave = (block of 64 kpl frequencies, kSpvPS problems); the 4 waves of a
 // workgroup take consecutive problem slices of the same block (the Psi / Phi loads hit L1 / L2 three times
 // in four); per (t, g) a lane sum over its frequencies, the fixed wave reduction, one partial per block:
 // partial[(g N + t) nblk + blk] (k_qf_finish sums them in order and forms K(x,x) - sum).
-constexpr int kSpvPS = 16;
+constexpr int kSpvPS = 8;
 template <int D>
 __global__ __launch_bounds__(kWG) void k_spec_post_var(Nll a, const double2* __restrict__ psi, int N, int kpl,
                                                        int nblk, double* __restrict__ partial) {
@@ -876,17 +876,30 @@ __global__ __launch_bounds__(kWG) void k_spec_post_var(Nll a, const double2* __r
     double acc[kSpvPS];
 #pragma unroll
     for (int p = 0; p < kSpvPS; ++p) acc[p] = 0.0;
+    // software-pipelined: the next frequency's spectra are in flight while this one is evaluated
+    double phn[NS], prn[NS], pin[NS];
+    auto fetch = [&](int64_t k) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        phn[s] = a.basis[spec_at<NS>(k, s)];
+        const double2 v = psi[((int64_t)t * NS + s) * n + k];
+        prn[s] = v.x;
+        pin[s] = v.y;
+      }
+    };
+    const int64_t k0 = (int64_t)blk * kpl * 64 + lane;
+    if (k0 <= half) fetch(k0);
     for (int i = 0; i < kpl; ++i) {
-      const int64_t k = ((int64_t)blk * kpl + i) * 64 + lane;
+      const int64_t k = k0 + 64 * i;
       if (k > half) break;
       double phi[NS], pr[NS], pi[NS];
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
-        phi[s] = a.basis[spec_at<NS>(k, s)];
-        const double2 v = psi[((int64_t)t * NS + s) * n + k];
-        pr[s] = v.x;
-        pi[s] = v.y;
+        phi[s] = phn[s];
+        pr[s] = prn[s];
+        pi[s] = pin[s];
       }
+      if (i + 1 < kpl && k + 64 <= half) fetch(k + 64);
       const double wk = (k == 0 || k == half) ? 1.0 : 2.0;
 #pragma unroll
       for (int p = 0; p < kSpvPS; ++p) {
@@ -895,9 +908,9 @@ __global__ __launch_bounds__(kWG) void k_spec_post_var(Nll a, const double2* __r
 #pragma unroll
           for (int j = 0; j < D; ++j) l[j] = hl[w][p][2 + j];
           const double sc = hl[w][p][0];
-          const double A = 1.0 / (rootn * (sc * mlin<D>(phi, l, dp)) + hl[w][p][1]);
+          const double A = rcp_nr(rootn * (sc * mlin<D>(phi, l, dp)) + hl[w][p][1]);
           const double re = mlin<D>(pr, l, dp), im = mlin<D>(pi, l, dp);
-          acc[p] = __builtin_fma(wk * A * sc * sc, __builtin_fma(re, re, im * im), acc[p]);
+          acc[p] = __builtin_fma(wk * A * (sc * sc), __builtin_fma(re, re, im * im), acc[p]);
         }
       }
     }
