@@ -811,8 +811,10 @@ __global__ __launch_bounds__(kWG, 2) void k_fwd_cols_r2c(Nll a, const double2* _
 // writes V of both partners into the LDS image and runs the adjoint column pass; the row kernel runs the
 // conjugate-twiddled adjoint row pass and writes the real rows.  f (optional): X = in * f, fused into the
 // loads (the tilde-domain solve of gram_matrix_solve, util.py:341-343); FR: f holds real factor rows
-// (float64: A = 1/ev of real eigenvalues, fgp_ifftbr_real_rf), else complex128.
-template <int P1, bool FR>
+// (float64: A = 1/ev of real eigenvalues, fgp_ifftbr_real_rf), else complex128.  HERM (with FR): X is
+// Hermitian (ytilde = ft of real data times a real even factor), so X~ = X, X~_{k+n/2} = conj X_{n/2-k} and
+// only k <= n/2 of `in` and `f` are read (half the input bytes).
+template <int P1, bool FR, bool HERM>
 __global__ __launch_bounds__(kWG, 2) void k_inv_cols_c2r(const double2* __restrict__ X, int64_t xs,
                                                          const void* __restrict__ f, int64_t fs,
                                                          double2* __restrict__ work, int log2n,
@@ -849,9 +851,15 @@ __global__ __launch_bounds__(kWG, 2) void k_inv_cols_c2r(const double2* __restri
   };
   // Hermitian part at (k, k + n/2) given the partner pair (n/2 - k, n - k): X~_k, X~_{k+n/2}
   auto herm = [&](int64_t k, int64_t ks, double2& h0, double2& h1) {
-    const double2 a0 = xv(k), a1 = xv(k + nt), b0 = xv(ks), b1 = xv(ks + nt);   // X_k, X_{k+nt}, X_{nt-k}, X_{n-k}
-    h0 = make_double2(0.5 * (a0.x + b1.x), 0.5 * (a0.y - b1.y));
-    h1 = make_double2(0.5 * (a1.x + b0.x), 0.5 * (a1.y - b0.y));
+    if constexpr (HERM) {
+      h0 = xv(k);
+      const double2 b0 = xv(ks);
+      h1 = make_double2(b0.x, -b0.y);
+    } else {
+      const double2 a0 = xv(k), a1 = xv(k + nt), b0 = xv(ks), b1 = xv(ks + nt);   // X_k, X_{k+nt}, X_{nt-k}, X_{n-k}
+      h0 = make_double2(0.5 * (a0.x + b1.x), 0.5 * (a0.y - b1.y));
+      h1 = make_double2(0.5 * (a1.x + b0.x), 0.5 * (a1.y - b0.y));
+    }
   };
   auto vpack = [](double2 h0, double2 h1, double2 W, double2& vp, double2& vs) {
     const double2 E = h0 + h1;
@@ -891,7 +899,7 @@ __global__ __launch_bounds__(kWG, 2) void k_inv_cols_c2r(const double2* __restri
     if (self) {   // column 0, row N1/2: frequencies n/4 and 3n/4, mirrors of each other
       constexpr int rh = N1 / 2;
       const int64_t kh = (int64_t)rh * N2;
-      const double2 a0 = xv(kh), a1 = xv(kh + nt);
+      const double2 a0 = xv(kh), a1 = HERM ? make_double2(a0.x, -a0.y) : xv(kh + nt);
       const double2 hh0 = make_double2(0.5 * (a0.x + a1.x), 0.5 * (a0.y - a1.y));
       const double2 hh1 = make_double2(hh0.x, -hh0.y);
       double2 vh, unused;
@@ -1703,10 +1711,10 @@ static int ifftbr_real_any(const void* in, int64_t in_batch_stride, const void* 
   switch (p1) {
 #define FGP_C(PP)                                                                                                \
   case PP:                                                                                                       \
-    if (freal) k_inv_cols_c2r<PP, true><<<grid, kWG, 0, st>>>(X, in_batch_stride, f, f_batch_stride, wk, log2n,  \
-                                                              tb->tw4096, tb->twm[log2n]);                       \
-    else k_inv_cols_c2r<PP, false><<<grid, kWG, 0, st>>>(X, in_batch_stride, f, f_batch_stride, wk, log2n,       \
-                                                         tb->tw4096, tb->twm[log2n]);                            \
+    if (freal) k_inv_cols_c2r<PP, true, true><<<grid, kWG, 0, st>>>(X, in_batch_stride, f, f_batch_stride, wk,  \
+                                                                    log2n, tb->tw4096, tb->twm[log2n]);          \
+    else k_inv_cols_c2r<PP, false, false><<<grid, kWG, 0, st>>>(X, in_batch_stride, f, f_batch_stride, wk,      \
+                                                                log2n, tb->tw4096, tb->twm[log2n]);              \
     break;
     FGP_C(4) FGP_C(5) FGP_C(6) FGP_C(7) FGP_C(8) FGP_C(9) FGP_C(10) FGP_C(11)
 #undef FGP_C

@@ -129,7 +129,8 @@ def ifftbr_raw(x, stable=True, real_out=False):
 def ifftbr_real_rf(x, f):
     """Re ifftbr(x * f) along the last dim for complex128 x [*, n] and REAL factor rows f (float64, one row or
     one per row of x), 2^17 <= n <= 2^24, at half length (fgp_ifftbr_real_rf): the coefficient solve
-    ift(A * ytilde).real of gram_matrix_solve (util.py:341-343) with the spectral path's real A."""
+    ift(A * ytilde).real of gram_matrix_solve (util.py:341-343) with the spectral path's real A.  x must be
+    Hermitian along the last dim (ft of real data, as ytilde) and f even (as A): only k <= n/2 are read."""
     require_device(x, "ifftbr_real_rf")
     n = x.shape[-1]
     m = log2_exact(n)

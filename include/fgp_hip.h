@@ -81,7 +81,9 @@ int fgp_fftbr_real(const double* in, int64_t in_batch_stride, void* out, void* w
 int fgp_ifftbr_real(const void* in, int64_t in_batch_stride, const void* f, int64_t f_batch_stride, double* out,
                     int64_t out_batch_stride, void* work, int64_t batch, int log2n, void* stream);
 /* The same with REAL factor rows f (float64 [batch or 1][n], f_batch_stride 0: one shared row): out[b] =
- * Re ifftbr(in[b] * f[b]) for the real A = 1/ev of the spectral path (ABI 12). */
+ * Re ifftbr(in[b] * f[b]) for the real A = 1/ev of the spectral path (ABI 12).  ABI 13: in[b] must be
+ * Hermitian (in_{n-k} = conj in_k: ft of real data, as ytilde) and f[b] even (f_{n-k} = f_k, as A): only
+ * k <= n/2 of both are read. */
 int fgp_ifftbr_real_rf(const void* in, int64_t in_batch_stride, const double* f, int64_t f_batch_stride, double* out,
                        int64_t out_batch_stride, void* work, int64_t batch, int log2n, void* stream);
 

@@ -241,3 +241,23 @@ def test_spectral_post_var_equals_per_row_transforms(m, d, G, monkeypatch):
         v_row = gp.post_var(x, n=n).reshape(G, -1)
         assert float(((v_spec - v_row).abs() / kxx).max()) <= 1e-10
         assert bool((v_spec >= 0).all())
+
+
+@pytest.mark.parametrize("m,rows", [(17, 3), (18, 2), (20, 1)])
+def test_real_factor_inverse_reads_half_of_hermitian_input(m, rows):
+    """fgp_ifftbr_real_rf (ABI 13) reads only k <= n/2 of its Hermitian input (ft of real data) and even
+    factor rows: equal to the full-length Re ifftbr(x * f) (1e-13 relative), for one shared factor row and one
+    row per input; the n - k half of the input is never read (poisoned with NaN here)."""
+    from fastgaussianprocesses_amd import ops
+    n = 2 ** m
+    g = torch.Generator().manual_seed(m)
+    y = torch.randn((rows, n), generator=g, dtype=torch.float64).to(DEV)
+    x = ops.fftbr_raw(y, stable=True)
+    h = torch.rand((rows, n), generator=g, dtype=torch.float64).to(DEV) + 0.5
+    f = h + h[:, (-torch.arange(n, device=DEV)) % n]                    # even: f_{n-k} = f_k
+    for fr in (f[:1], f):
+        ref = ops.ifftbr_raw(x * fr, stable=True, real_out=True)
+        xp = x.clone()
+        xp[:, n // 2 + 1:] = float("nan")
+        got = ops.ifftbr_real_rf(xp, fr)
+        assert rel_err(got, ref) <= 1e-13
