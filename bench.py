@@ -248,8 +248,11 @@ def secondary_configs(F, args, device, rank=0, world=1):
         sg = make()
         xm = torch.rand((args.n_mean, d), generator=g).to(device)
         xv = torch.rand((args.n_var, d), generator=g).to(device)
-        # at least 5 timed steps after 2 warm-ups: a one-off host stall in a ~1 ms step is not the config's rate
-        sec = time_steps(lambda: step_single(sg, args, xm, xv), max(5, args.steps), 2, device)
+        # the median of 3 windows of >= 5 timed steps (each bracketed as time_steps does) after 2 warm-ups: a
+        # one-off host stall (allocator growth, a page fault) in a ~1 ms step is not the config's rate
+        wins = sorted(time_steps(lambda: step_single(sg, args, xm, xv), max(5, args.steps), 2 if w == 0 else 0, device)
+                      for w in range(3))
+        sec = wins[1]
         phases = None
         if world == 1:
             # per-phase median of 3 event-timed steps (one sample can catch a host stall)
@@ -623,9 +626,9 @@ def roofline_fit_kernels(F, shifts, iters):
 
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r03g_pmc_fit_kernels.json")
-PMC_SQ_SUMMARY = os.path.join(ROOT, "profiles", "r03g_pmc_sq_fit_kernels.json")
-ROCPROF_GRID_STATS = os.path.join(ROOT, "profiles", "r03g_bench_kernel_grid_stats.txt")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r03h_pmc_fit_kernels.json")
+PMC_SQ_SUMMARY = os.path.join(ROOT, "profiles", "r03h_pmc_sq_fit_kernels.json")
+ROCPROF_GRID_STATS = os.path.join(ROOT, "profiles", "r03h_bench_kernel_grid_stats.txt")
 # the read floor of the spectral iteration's footprint: tools/stream_microbench.hip over the same 168 MB,
 # re-read back to back, 24.0-24.3 us per pass (7.0 TB/s; profiles/r03v_stream_and_stamps.jsonl)
 STREAM_FLOOR_US = 24.0
