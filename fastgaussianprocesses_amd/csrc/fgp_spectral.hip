@@ -184,7 +184,8 @@ template <int D, int PPW, bool NET>
 __global__ __launch_bounds__(kWG) void k_spec_iter(Nll a) {
   constexpr int NS = 1 << D;
   const int lane = threadIdx.x & 63;
-  const int task = (int)blockIdx.x * (kWG / 64) + (int)(threadIdx.x >> 6);
+  // the wave index through readfirstlane: wave-uniform to the compiler (scalar branches on the problem flags)
+  const int task = (int)blockIdx.x * (kWG / 64) + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int kb = task / a.spec_pg, pg = task - kb * a.spec_pg;
   stamp_begin(a);
   if (kb < a.nb) {
@@ -453,7 +454,9 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
   constexpr int NS = 1 << D;
   constexpr int RING = kSpecRing;                   // chunks in LDS; RING - 1 in flight under a compute
   extern __shared__ double lds[];                   // [RING][NBW][NS + PS][64] ring
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // w through readfirstlane: wave-uniform to the compiler, so the problem flags, the DMA counts and the vmcnt
+  // switch are scalar (a VGPR w compiled them into exec-mask branch trees inside the chunk loop)
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int PGP = a.spec_pgp, NBW = 4 / PGP, G = a.G;
   // problem slices (many problems on one set of spectra, a.spec_nsl > 1): workgroup = (k block, slice),
   // the slices of one block consecutive (they share its spectra chunks in L2); slice s holds problems
@@ -533,7 +536,7 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
   }
   for (int c = 0; c < nc; ++c) {
     // this wave's loads of chunk c have landed (chunks c + 1 .. c + RING - 2 may stay in flight)
-    wait_vmcnt(cnt_w * min(RING - 2, nc - 1 - c));
+    wait_vmcnt(RING == 2 ? 0 : cnt_w * min(RING - 2, nc - 1 - c));
     barrier_keep_vm();                              // ... every wave's; every wave done with chunk c - 1
     if (c + RING - 1 < nc) issue(c + RING - 1, lds + ((c + RING - 1) % RING) * tile);
     const double* buf = lds + (unsigned)(c % RING) * (unsigned)tile;
@@ -853,7 +856,7 @@ __global__ __launch_bounds__(kWG) void k_spec_post_var(Nll a, const double2* __r
                                                        int nblk, double* __restrict__ partial) {
   constexpr int NS = 1 << D, HS = 2 + D;
   __shared__ double hl[kWG / 64][kSpvPS][HS];          // scale, noise, l_j of the wave's problems
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int blk = (int)blockIdx.x;
   const int g0 = ((int)blockIdx.y * (kWG / 64) + w) * kSpvPS;
   if (g0 >= a.G) return;                              // wave-uniform; no barriers below
