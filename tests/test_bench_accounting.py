@@ -44,7 +44,7 @@ def test_stage_bytes_real_even(monkeypatch):
 
 
 def test_pmc_traffic_lookup_matches_kernel_and_grid():
-    """The committed profiles the bench line prices on (profiles/r03h_*): PMC traffic, VALU instructions
+    """The committed profiles the bench line prices on (profiles/r03i_*): PMC traffic, VALU instructions
     and the rocprofv3 average of the dominant kernel k_spec_tile at the bench grid; exact name match."""
     n, P, d = 2 ** 20, 8, 5
     wg = bench.spec_tile_grid(n, d, P)
