@@ -567,6 +567,9 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
     int* flag = reinterpret_cast<int*>(lds);        // the ring is free now
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    // (relaxed add on purpose: the partials are agent-scope atomic stores retired by the vmcnt(0) wait above,
+    // the asm's memory clobber keeps the compiler from moving them; an acq_rel add / release fence emits an
+    // L2 write-back per workgroup: 40.9 -> 46.4 us per C4 iteration, profiles/r03ar_exp_acq_rel_handoff.jsonl)
     if (threadIdx.x == 0) flag[0] = __hip_atomic_fetch_add(cnt_grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
                                     (unsigned)(wg_in_grp - 1);
     __syncthreads();
