@@ -72,6 +72,8 @@ def max_over_ranks(seconds, device):
     import torch.distributed as tdist
     if not (tdist.is_available() and tdist.is_initialized()) or tdist.get_world_size() == 1:
         return seconds
+    if tdist.get_backend() == "gloo":
+        device = "cpu"              # gloo reduces host tensors (the CPU / one-GPU multi-process tests)
     t = torch.tensor([seconds], dtype=torch.float64, device=device)
     tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
     return float(t)
@@ -211,12 +213,16 @@ def time_steps(fn, steps, warmup, device=None):
     return el / steps
 
 
+def total_outputs(sg):
+    return getattr(sg, "total", 1)
+
+
 def c5_shard(outputs, rank, world):
     from fastgaussianprocesses_amd.distributed import output_shard
     return output_shard(outputs, rank, world) if world > 1 else None
 
 
-def secondary_configs(F, args, device, rank=0, world=1):
+def secondary_configs(F, args, device, rank=0, world=1, collect=None):
     """The other BASELINE.json configs, each timed as its own step (fit K Rprop iterations without early
     stopping + post_mean N + post_var N):
       N = 1 only: C2 FastGPLattice n=2^16 d=3, C3 FastGPDigitalNetB2 n=2^16 d=3 (default alpha = 2), C5 with
@@ -224,8 +230,10 @@ def secondary_configs(F, args, device, rank=0, world=1):
       every N (all ranks take part, max-over-ranks time, value = all outputs x n / s): C5 multi-output
         FastGPLattice n=2^18 d=3 x B outputs, fp64, outputs sharded over the ranks (fit_sharded: one Y
         all-reduce), and C5 with per-output hyper-parameters (B independent eigen-problems; replicas, no
-        collective)."""
-    g = torch.Generator().manual_seed(17)
+        collective).
+    collect: a dict that receives, per case ("C2", "C5", "C5 per-output", ...), one more step's fitted raw
+    parameters, post_mean and post_var (host tensors) and the outputs this rank owns --
+    tests/test_gpu_multioutput.py compares the N = 2 lines' with the N = 1 run's."""
     B = args.c5_outputs
     sh = c5_shard(B, rank, world)
     cases = []
@@ -246,6 +254,7 @@ def secondary_configs(F, args, device, rank=0, world=1):
     out = []
     for name, make, d in cases:
         sg = make()
+        g = torch.Generator().manual_seed(17)      # per case: the same test points at every N
         xm = torch.rand((args.n_mean, d), generator=g).to(device)
         xv = torch.rand((args.n_var, d), generator=g).to(device)
         # the median of 3 windows of >= 5 timed steps (each bracketed as time_steps does) after 2 warm-ups: a
@@ -253,6 +262,13 @@ def secondary_configs(F, args, device, rank=0, world=1):
         wins = sorted(time_steps(lambda: step_single(sg, args, xm, xv), max(5, args.steps), 2 if w == 0 else 0, device)
                       for w in range(3))
         sec = wins[1]
+        if collect is not None:
+            pm, pv = step_single(sg, args, xm, xv)
+            collect[name.split(":")[0]] = dict(
+                raw_scale=sg.gp.raw_scale.detach().cpu().clone(),
+                raw_lengthscales=sg.gp.raw_lengthscales.detach().cpu().clone(),
+                post_mean=pm.detach().cpu().clone(), post_var=pv.detach().cpu().clone(),
+                outputs=c5_shard(total_outputs(sg), rank, world) if world > 1 else (0, total_outputs(sg)))
         phases = None
         if world == 1:
             # per-phase median of 3 event-timed steps (one sample can catch a host stall)

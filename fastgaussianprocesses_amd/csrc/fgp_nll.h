@@ -2,6 +2,7 @@
 // hyper-parameter / kernel-part helpers, eigenvalue terms and the intermediate layout.
 #pragma once
 #include <cmath>
+#include <cstdlib>
 #include <type_traits>
 
 #include "fgp_common.h"
@@ -9,6 +10,12 @@
 #include "../../include/fgp_hip.h"
 
 namespace fgp {
+
+// an A/B switch of the host code: the environment variable is set and starts with '0'
+inline bool getenv_off(const char* name) {
+  const char* e = std::getenv(name);
+  return e && e[0] == '0';
+}
 
 struct Nll {
   int log2n, d, G, nb, nq;
@@ -445,6 +452,18 @@ struct Fit {
   int hist_stride, hist_offset;   // loss_hist row stride in problems (0: G) and this desc's first problem
 };
 
+// torch.optim.Rprop single-tensor step of parameter p with gradient gp, state in f (raw, prev, step)
+__device__ __forceinline__ void rprop_update(const Fit& f, int p, double gp) {
+  const double prod = gp * f.prev[p];
+  const double sgn = prod > 0.0 ? f.eta_plus : (prod < 0.0 ? f.eta_minus : 1.0);
+  const double st = fmin(fmax(f.step[p] * sgn, f.step_min), f.step_max);
+  f.step[p] = st;
+  const double gg = (sgn == f.eta_minus) ? 0.0 : gp;
+  const double gs = gg > 0.0 ? 1.0 : (gg < 0.0 ? -1.0 : 0.0);
+  f.raw[p] = f.raw[p] + (-1.0) * (gs * st);
+  f.prev[p] = gg;
+}
+
 // Per-problem reduction + loss history + Rprop (torch.optim.Rprop single-tensor semantics) by one
 // workgroup of NT threads for problem g: k_fit_reduce_step, and the last row-pair workgroup of the
 // fused real-even backward kernel (SC1: the partials of that same launch are read with sc1 loads,
@@ -584,6 +603,11 @@ int64_t spec_chunks(bool net, int log2n);          // 64-frequency chunks of the
 // one fit iteration (loss + gradient partials); with fz (tile kernel only) also the reduction + Rprop
 int launch_spec_iter(const Nll& a, hipStream_t st, const FitFuse* fz = nullptr);
 int launch_spec_reduce_step(const Nll& a, const Fit& f, int iter, int do_update, hipStream_t st);
+// the step of one loss over many problems (not per_problem) from the spectral partials, ceil(G / 16) workgroups,
+// the shared part in the last arriver; its arrival counter (one word of the partials workspace) must be zero
+// before the first launch (each launch leaves it zero)
+int launch_spec_step_many(const Nll& a, const Fit& f, int iter, int do_update, hipStream_t st);
+unsigned* spec_step_many_counter(const Nll& a);
 // the fused spectral run's counters: doubles offset into partials and how many 32-bit counters
 int spec_counters_offset(const Nll& a, int64_t* off, int* count);
 // the fused spectral run's scratch copies of the Rprop state (parity 0, 1) in the partials workspace

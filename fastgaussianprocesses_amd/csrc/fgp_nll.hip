@@ -1026,16 +1026,6 @@ __global__ __launch_bounds__(kWG) void k_bwd_rows_r2c(Nll a, const double2* __re
 
 // ---------------------------------------------------------------- fit step (one workgroup)
 
-__device__ __forceinline__ void rprop_update(const Fit& f, int p, double gp) {
-  const double prod = gp * f.prev[p];
-  const double sgn = prod > 0.0 ? f.eta_plus : (prod < 0.0 ? f.eta_minus : 1.0);
-  const double st = fmin(fmax(f.step[p] * sgn, f.step_min), f.step_max);
-  f.step[p] = st;
-  const double gg = (sgn == f.eta_minus) ? 0.0 : gp;
-  const double gs = gg > 0.0 ? 1.0 : (gg < 0.0 ? -1.0 : 0.0);
-  f.raw[p] = f.raw[p] + (-1.0) * (gs * st);
-  f.prev[p] = gg;
-}
 
 __device__ __forceinline__ double* red_ptr(const Nll& a, int g, int q) {
   return a.partials + (int64_t)a.G * a.nq * a.nb + (int64_t)g * a.nq + q;
@@ -1467,8 +1457,14 @@ static int check_per_problem(const Nll& a, const Fit& f) {
   return kOk;
 }
 
-static int fit_step(const Nll& a, const Fit& f, int iter, int do_update, hipStream_t st) {
+static int fit_step(const Nll& a, const Fit& f, int iter, int do_update, hipStream_t st, bool counter_zero = false) {
   if (f.per_problem && a.spec) return launch_spec_reduce_step(a, f, iter, do_update, st);
+  if (a.spec && a.nb <= kSpecBlocks && !getenv_off("FGP_SPEC_STEP_MANY")) {
+    // one loss over many problems: the parallel step (k_spec_step_many); its counter is zeroed once per run
+    if (!counter_zero && hipMemsetAsync(spec_step_many_counter(a), 0, sizeof(unsigned), st) != hipSuccess)
+      return set_error(kErrHip, "fit step: counter reset failed");
+    return launch_spec_step_many(a, f, iter, do_update, st);
+  }
   if (f.per_problem) {
     k_fit_reduce_step<<<a.G, kWG, 0, st>>>(a, f, iter, do_update);
     return check_launch("k_fit_reduce_step");
@@ -1847,6 +1843,9 @@ int fgp_fit_run(const fgp_nll_desc* nll, const fgp_fit_desc* fit, int iter0, int
     }
     return kOk;
   }
+  const bool many = a.spec && !f.per_problem && a.nb <= kSpecBlocks && !getenv_off("FGP_SPEC_STEP_MANY");
+  if (many && iters > 0 && hipMemsetAsync(spec_step_many_counter(a), 0, sizeof(unsigned), st) != hipSuccess)
+    return set_error(kErrHip, "fgp_fit_run: counter reset failed");
   for (int it = 0; it < iters; ++it) {
     const int upd = !(final_no_update && it == iters - 1);
     if ((rc = nll_fwd(a, st, lat)) != kOk) return rc;
@@ -1857,7 +1856,7 @@ int fgp_fit_run(const fgp_nll_desc* nll, const fgp_fit_desc* fit, int iter0, int
       continue;
     }
     if ((rc = nll_bwd(a, st, lat)) != kOk) return rc;
-    if ((rc = fit_step(a, f, iter0 + it, upd, st)) != kOk) return rc;
+    if ((rc = fit_step(a, f, iter0 + it, upd, st, many)) != kOk) return rc;
   }
   return kOk;
 }

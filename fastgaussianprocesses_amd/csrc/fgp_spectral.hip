@@ -389,6 +389,125 @@ __global__ __launch_bounds__(kWG) void k_spec_reduce_step(Nll a, Fit f, int iter
   spec_finish<D>(a, f, tot, g0, cnt, iter, do_update, st, st, true, nullptr);
 }
 
+// The step of ONE loss over many problems (per-output hyper-parameters of one GP, e.g. C5 per-output: 512
+// eigen-problems, a summed MLL; not per_problem) -- k_fit_reduce + the one-workgroup k_fit_step of the
+// transform path, spread over ceil(G / 16) workgroups.  Workgroup b: both levels of the partials of problems
+// 16 b .. 16 b + 15 (k_spec_reduce_step's order) -> their totals red(g, q) (k_fit_reduce's output) and the
+// Rprop step of the parameters only they own (per-problem scale / lengthscales / noise: thread 16 i + slot,
+// k_fit_step's gradient of that parameter from red(g, .)); the workgroup whose arrival on `counter` comes
+// last (sc1 totals, an agent-scope add: MI355X_MICROARCH.md hand-off row 1) then runs k_fit_step's loss and
+// shared-parameter part -- the same per-thread (g = t, t + kWG, ...), wave and workgroup order, so the loss
+// and shared gradients equal k_fit_step's given the totals -- and resets the counter for the next launch.
+template <int D>
+__global__ __launch_bounds__(kWG) void k_spec_step_many(Nll a, Fit f, int iter, int do_update, unsigned* counter) {
+  constexpr int NQ = 4 + D, MAXG = kSpecBlocks / kSpecGroup, NV = 4 + FGP_MAX_D, NW = kWG / 64;
+  __shared__ double gs[16 * NQ * MAXG];
+  __shared__ double tot[16 * NQ];
+  __shared__ double red[NV * NW];
+  __shared__ int last;
+  const int tid = threadIdx.x;
+  const int g0 = (int)blockIdx.x * 16, cnt = min(16, a.G - g0), ng = spec_groups(a);
+  for (int t = tid; t < cnt * NQ * ng; t += kWG) {
+    const int pair = t / ng, grp = t % ng;
+    gs[pair * MAXG + grp] = spec_group_sum<false>(a, g0 + pair / NQ, pair % NQ, grp);
+  }
+  __syncthreads();
+  if (tid < cnt * NQ) {
+    double s = 0.0;
+    for (int grp = 0; grp < ng; ++grp) s += gs[tid * MAXG + grp];
+    tot[tid] = s;
+    __hip_atomic_store(a.partials + (int64_t)a.G * a.nq * a.nb + (int64_t)(g0 + tid / NQ) * a.nq + tid % NQ, s,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  // the parameters problem g0 + i owns: slot 0 scale, 1 .. dl lengthscales, dl + 1 noise
+  const int dl = a.ls_pd ? a.d : 1, i = tid >> 4, k = tid & 15;
+  if (i < cnt && k < 2 + dl) {
+    const int g = g0 + i;
+    const double* v = tot + i * NQ;
+    int p = -1, rg = 0;
+    double gp = 0.0;
+    if (k == 0 && a.scale_pp) {
+      p = a.scale_off + g;
+      rg = f.scale_rg;
+      gp = 0.0 + v[3];
+    } else if (k >= 1 && k <= dl && a.ls_pp) {
+      p = a.ls_off + g * dl + (k - 1);
+      rg = f.ls_rg;
+      gp = 0.0;
+      if (a.ls_pd) {
+        gp += v[4 + (k - 1)];
+      } else {
+        for (int j = 0; j < a.d; ++j) gp += v[4 + j];
+      }
+    } else if (k == dl + 1 && a.noise_pp) {
+      p = a.noise_off + g;
+      rg = f.noise_rg;
+      gp = 0.0 + exp(a.raw[p]) * v[2];
+    }
+    if (p >= 0) {
+      f.raw_hist[(int64_t)iter * f.n_params + p] = f.raw[p];
+      f.grad_out[p] = gp;
+      if (do_update && rg) rprop_update(f, p, gp);
+    }
+  }
+  // arrival: every wave's sc1 totals retired, then one add
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0)
+    last = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  // k_fit_step's loss and shared-parameter part over all G problems
+  auto rd = [&](int g, int q) {
+    return __hip_atomic_load(a.partials + (int64_t)a.G * a.nq * a.nb + (int64_t)g * a.nq + q, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+  };
+  double v[NV];
+#pragma unroll
+  for (int q = 0; q < NV; ++q) v[q] = 0.0;
+  const double en = a.noise_pp ? 0.0 : exp(a.raw[a.noise_off]);
+  for (int g = tid; g < a.G; g += kWG) {
+    v[0] += rd(g, 0);
+    v[1] += rd(g, 1);
+    if (!a.noise_pp) v[2] += en * rd(g, 2);
+    if (!a.scale_pp) v[3] += rd(g, 3);
+    if (!a.ls_pp)
+      for (int j = 0; j < a.d; ++j) v[4 + (a.ls_pd ? j : 0)] += rd(g, 4 + j);
+  }
+#pragma unroll
+  for (int q = 0; q < NV; ++q) {
+    double x = v[q];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+    if ((tid & 63) == 0) red[q * NW + (tid >> 6)] = x;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double t[NV];
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+      t[q] = 0.0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) t[q] += red[q * NW + w];
+    }
+    const double term2 = a.logdet_weight * t[1];
+    f.loss_hist[(int64_t)iter * 3 + 0] = 0.5 * (t[0] + term2 + f.mll_const);
+    f.loss_hist[(int64_t)iter * 3 + 1] = t[0];
+    f.loss_hist[(int64_t)iter * 3 + 2] = term2;
+    auto shared_param = [&](int p, int rg, double gp) {
+      f.raw_hist[(int64_t)iter * f.n_params + p] = f.raw[p];
+      f.grad_out[p] = gp;
+      if (do_update && rg) rprop_update(f, p, gp);
+    };
+    if (!a.noise_pp) shared_param(a.noise_off, f.noise_rg, 0.0 + t[2]);
+    if (!a.scale_pp) shared_param(a.scale_off, f.scale_rg, 0.0 + t[3]);
+    if (!a.ls_pp)
+      for (int j = 0; j < dl; ++j) shared_param(a.ls_off + j, f.ls_rg, 0.0 + t[4 + j]);
+    __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // The deferred step of a fused spectral run's LAST iteration (its own launch, one workgroup): the level-2 sum
 // of that iteration's group sums (parity fz.par ^ 1 as k_spec_tile's prologue reads them) and the step from
 // fz.sin to fz.sout (the fit's own state vectors)
@@ -1102,6 +1221,20 @@ int launch_spec_reduce_step(const Nll& a, const Fit& f, int iter, int do_update,
   return with_spec_d(a.d, [&](auto dc) {
     k_spec_reduce_step<decltype(dc)::value><<<(unsigned)((a.G + 15) / 16), kWG, 0, st>>>(a, f, iter, do_update);
     return check_launch("k_spec_reduce_step");
+  });
+}
+
+unsigned* spec_step_many_counter(const Nll& a) {
+  const int64_t nb_doc = std::max<int64_t>(1, ((int64_t)1 << a.log2n) >> 12);
+  return reinterpret_cast<unsigned*>(a.partials + (int64_t)a.G * a.nq * (std::max<int64_t>(a.nb, nb_doc) + 1));
+}
+
+int launch_spec_step_many(const Nll& a, const Fit& f, int iter, int do_update, hipStream_t st) {
+  if (a.nb > kSpecBlocks) return set_error(kErrInvalid, "k_spec_step_many: nb > %d", kSpecBlocks);
+  unsigned* counter = spec_step_many_counter(a);
+  return with_spec_d(a.d, [&](auto dc) {
+    k_spec_step_many<decltype(dc)::value><<<(unsigned)((a.G + 15) / 16), kWG, 0, st>>>(a, f, iter, do_update, counter);
+    return check_launch("k_spec_step_many");
   });
 }
 

@@ -103,7 +103,28 @@ def _wants_multitask(cls, args, kwargs):
     bound = inspect.signature(cls.__init__).bind_partial(None, *args, **kwargs).arguments
     nt = bound.get("num_tasks")
     return (nt is not None and nt != 1) or not _trivial_derivatives(bound.get("derivatives"),
-                                                                    bound.get("derivatives_coeffs"))
+                                                                    bound.get("derivatives_coeffs")) \
+        or _nonunit_task_kernel(bound)
+
+
+def _nonunit_task_kernel(bound):
+    """A single-task GP whose task kernel is not the constant 1: num_tasks = 1 keeps rank 0 (no factor), so
+    gram_matrix_tasks = noise_task_kernel (abstract_gp.py:116-139); a value != 1, a factor of positive rank
+    or a learned task kernel scales every eigenvalue (ev = (sqrt(n) lambda + noise) Kt, util.py:285-298) and
+    every kernel row (abstract_gp.py:375) -- the multitask class (T = 1) carries that."""
+    learned = bool(bound.get("requires_grad_noise_task_kernel")) or bool(bound.get("requires_grad_factor_task_kernel"))
+    if bound.get("derivatives") is not None or bound.get("derivatives_coeffs") is not None:
+        # derivative information: rank-1 factor, task noise 0 (abstract_gp.py:58-62) -> Kt = factor^2
+        f = bound.get("factor_task_kernel", 1.0)
+        f2 = (f.reshape(-1) ** 2).sum() if isinstance(f, torch.Tensor) else f * f
+        return learned or not bool(f2 == 1)
+    v = bound.get("noise_task_kernel", 1.0)
+    unit = bool((v == 1).all()) if isinstance(v, torch.Tensor) else (v == 1)
+    r, sf = bound.get("rank_factor_task_kernel"), bound.get("shape_factor_task_kernel")
+    f = bound.get("factor_task_kernel")
+    factor = (r not in (None, 0)) or (sf is not None and tuple(sf)[-1] != 0) or \
+        (isinstance(f, torch.Tensor) and f.shape[-1] != 0)
+    return (not unit) or factor or learned
 
 
 class AbstractFastGP(torch.nn.Module):
@@ -1180,13 +1201,95 @@ class AbstractFastGP(torch.nn.Module):
         return pcmean, pcvar, q, pcmean - pcerror, pcmean + pcerror
 
     def kernel(self, x, z, beta0=None, beta1=None, c0=None, c1=None):
-        """K(x, z) with broadcasting (abstract_gp.py:693-706), beta = kappa = 0 only."""
+        """K(x, z) with broadcasting of x [..., d] and z [..., d] (abstract_gp.py:693-706 ->
+        abstract_fast_gp.py:192-196).  beta = 0 with unit coefficients: the differentiable torch form of the
+        family kernel; derivative multi-indices beta0 [p0, d] / beta1 [p1, d] with coefficients c0 / c1: the
+        parts with derivative orders (fgp_mt_parts: lattice Bernoulli order 2 alpha - beta - kappa, net
+        (-2)^(beta+kappa) (ind + omega)) combined by _kernel_from_parts (abstract_fast_gp.py:181-191)."""
         assert isinstance(x, torch.Tensor) and x.size(-1) == self.d
         assert isinstance(z, torch.Tensor) and z.size(-1) == self.d
-        for b in (beta0, beta1):
-            if b is not None and (b != 0).any():
-                raise NotImplementedError("derivative kernels (beta != 0) are not built yet")
-        return self._kernel_torch(x, z)
+        dev = self.device
+        plain = all(b is None or not bool((b != 0).any()) for b in (beta0, beta1)) and \
+            all(c is None or (c.numel() == 1 and float(c.reshape(-1)[0]) == 1.0) for c in (c0, c1)) and \
+            all(b is None or b.numel() == self.d for b in (beta0, beta1))
+        if plain and not self._MULTITASK:
+            return self._kernel_torch(x, z)
+        if beta0 is None:
+            beta0 = torch.zeros((1, self.d), dtype=torch.int64, device=dev)
+        if beta0.shape == (len(beta0),):
+            beta0 = beta0[None, :]
+        assert isinstance(beta0, torch.Tensor) and beta0.ndim == 2 and beta0.size(1) == self.d
+        if beta1 is None:
+            beta1 = torch.zeros((1, self.d), dtype=torch.int64, device=dev)
+        if beta1.shape == (len(beta1),):
+            beta1 = beta1[None, :]
+        assert isinstance(beta1, torch.Tensor) and beta1.ndim == 2 and beta1.size(1) == self.d
+        if c0 is None:
+            c0 = torch.ones(len(beta0), device=dev)
+        assert isinstance(c0, torch.Tensor) and c0.shape == (beta0.size(0),)
+        if c1 is None:
+            c1 = torch.ones(len(beta1), device=dev)
+        assert isinstance(c1, torch.Tensor) and c1.shape == (beta1.size(0),)
+        shape = torch.broadcast_shapes(x.shape[:-1], z.shape[:-1])
+        xe = x.expand(shape + (self.d,)).reshape(-1, self.d)
+        ze = z.expand(shape + (self.d,)).reshape(-1, self.d)
+        p = self._parts_pairs(xe, ze, beta0.cpu(), beta1.cpu(), zip_pairs=True)
+        k = self._kernel_from_parts(p, beta0.to(dev), beta1.to(dev), c0.to(dev, torch.float64), c1.to(dev, torch.float64))
+        return k.reshape(k.shape[:-1] + tuple(shape))
+
+    # ------------------------------------------------------------------ kernel parts with derivative orders
+    def _pair_spec(self, beta0, beta1):
+        """(order, coef, add) [p0 p1, d] for fgp_mt_parts (fast_gp_lattice.py:267-273,
+        fast_gp_digital_net_b2.py:289-301); coefficients evaluated with the reference's own ops."""
+        alpha = torch.tensor(self._alphas, dtype=torch.int64)
+        order, coef, add = [], [], []
+        for b0 in beta0:
+            for b1 in beta1:
+                bpk = b0 + b1
+                if self._FAMILY == ops.LATTICE:
+                    o = 2 * alpha - bpk
+                    assert (2 <= o).all(), "order must all be at least 2, but got order = %s" % str(o)
+                    c = (-1) ** (alpha + b1 + 1) * torch.exp(2 * alpha * np.log(2 * np.pi) - torch.lgamma(o + 1))
+                    a = torch.zeros(self.d)
+                else:
+                    o = alpha - bpk
+                    assert (1 <= o).all() and (o <= 4).all(), \
+                        "order must all be between 2 and 4, but got order = %s. Try increasing alpha" % str(o)
+                    c = ((-2) ** bpk).to(torch.float64)
+                    a = (bpk > 0).to(torch.float64)
+                order.append([int(v) for v in o.tolist()])
+                coef.append([float(v) for v in c.tolist()])
+                add.append([float(v) for v in a.tolist()])
+        return order, coef, add
+
+    def _kargs(self, x):
+        """points as the parts kernel takes them: float64 lattice points, int64 t-bit net points."""
+        if self._FAMILY == ops.LATTICE:
+            x = x.to(device=self.device, dtype=torch.float64)
+            assert bool(((0 <= x) & (x <= 1)).all()), "x should have all elements in [0,1]"
+            return x
+        if torch.is_floating_point(x):
+            x = x.to(self.device)
+            assert bool(((0 <= x) & (x <= 1)).all()), "x should have all elements in [0,1]"
+            return torch.floor((x % 1) * 2 ** self.t).to(torch.int64)
+        return x.to(device=self.device, dtype=torch.int64)
+
+    def _parts_pairs(self, x, z, beta0, beta1, zip_pairs=False):
+        """_kernel_parts (abstract_fast_gp.py:173-180) for all (x_i, z_k) pairs -> [N, M, p0, p1, d]
+        (or the (x_i, z_i) pairs -> [N, p0, p1, d])."""
+        order, coef, add = self._pair_spec(beta0, beta1)
+        p = ops.mt_parts(self._FAMILY, self._kargs(x), self._kargs(z), order, coef, add, self._tbits(), zip_pairs)
+        return p.reshape(p.shape[:-2] + (len(beta0), len(beta1), self.d))
+
+    def _kernel_from_parts(self, parts, beta0, beta1, c0, c1):
+        """abstract_fast_gp.py:181-191."""
+        ndim = parts.ndim
+        scale = self.scale.reshape(self.scale.shape + torch.Size([1] * (ndim - 2)))
+        ls = self.lengthscales
+        ls = ls.reshape(ls.shape[:-1] + torch.Size([1] * (ndim - 1) + [ls.size(-1)]))
+        ind = ((beta0[:, None, :] + beta1[None, :, :]) == 0).to(torch.int64)
+        terms = scale * (ind + ls * parts).prod(-1)
+        return ((terms * c1).sum(-1) * c0).sum(-1)
 
 
 class FastGPLattice(AbstractFastGP):

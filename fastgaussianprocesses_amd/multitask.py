@@ -392,59 +392,7 @@ class MultiTaskFastGP(AbstractFastGP):
                         mt=dict(basis=self._mt_spectra(n), ytilde=yt, kt=self.gram_matrix_tasks.detach()))
 
     # ------------------------------------------------------------------ kernel parts and kernels
-    def _pair_spec(self, beta0, beta1):
-        """(order, coef, add) [p0 p1, d] for fgp_mt_parts (fast_gp_lattice.py:267-273,
-        fast_gp_digital_net_b2.py:289-301); coefficients evaluated with the reference's own ops."""
-        alpha = torch.tensor(self._alphas, dtype=torch.int64)
-        order, coef, add = [], [], []
-        for b0 in beta0:
-            for b1 in beta1:
-                bpk = b0 + b1
-                if self._FAMILY == ops.LATTICE:
-                    o = 2 * alpha - bpk
-                    assert (2 <= o).all(), "order must all be at least 2, but got order = %s" % str(o)
-                    c = (-1) ** (alpha + b1 + 1) * torch.exp(2 * alpha * np.log(2 * np.pi) - torch.lgamma(o + 1))
-                    a = torch.zeros(self.d)
-                else:
-                    o = alpha - bpk
-                    assert (1 <= o).all() and (o <= 4).all(), \
-                        "order must all be between 2 and 4, but got order = %s. Try increasing alpha" % str(o)
-                    c = ((-2) ** bpk).to(torch.float64)
-                    a = (bpk > 0).to(torch.float64)
-                order.append([int(v) for v in o.tolist()])
-                coef.append([float(v) for v in c.tolist()])
-                add.append([float(v) for v in a.tolist()])
-        return order, coef, add
-
-    def _kargs(self, x):
-        """points as the parts kernel takes them: float64 lattice points, int64 t-bit net points."""
-        if self._FAMILY == ops.LATTICE:
-            x = x.to(device=self.device, dtype=torch.float64)
-            assert bool(((0 <= x) & (x <= 1)).all()), "x should have all elements in [0,1]"
-            return x
-        if torch.is_floating_point(x):
-            x = x.to(self.device)
-            assert bool(((0 <= x) & (x <= 1)).all()), "x should have all elements in [0,1]"
-            return torch.floor((x % 1) * 2 ** self.t).to(torch.int64)
-        return x.to(device=self.device, dtype=torch.int64)
-
-    def _parts_pairs(self, x, z, beta0, beta1, zip_pairs=False):
-        """_kernel_parts (abstract_fast_gp.py:173-180) for all (x_i, z_k) pairs -> [N, M, p0, p1, d]
-        (or the (x_i, z_i) pairs -> [N, p0, p1, d])."""
-        order, coef, add = self._pair_spec(beta0, beta1)
-        p = ops.mt_parts(self._FAMILY, self._kargs(x), self._kargs(z), order, coef, add, self._tbits(), zip_pairs)
-        return p.reshape(p.shape[:-2] + (len(beta0), len(beta1), self.d))
-
-    def _kernel_from_parts(self, parts, beta0, beta1, c0, c1):
-        """abstract_fast_gp.py:181-191."""
-        ndim = parts.ndim
-        scale = self.scale.reshape(self.scale.shape + torch.Size([1] * (ndim - 2)))
-        ls = self.lengthscales
-        ls = ls.reshape(ls.shape[:-1] + torch.Size([1] * (ndim - 1) + [ls.size(-1)]))
-        ind = ((beta0[:, None, :] + beta1[None, :, :]) == 0).to(torch.int64)
-        terms = scale * (ind + ls * parts).prod(-1)
-        return ((terms * c1).sum(-1) * c0).sum(-1)
-
+    # (_pair_spec, _kargs, _parts_pairs, _kernel_from_parts: AbstractFastGP, fast_gp.py)
     def _kmat_block(self, x, z, ta, tb, zip_pairs=False, chunk_elems=1 << 24):
         """K_{ta,tb}(x_i, z_k) -> [*param batch, N, M] ([*, N] with zip_pairs), chunked over x."""
         b0, b1 = self._derivs_h[ta], self._derivs_h[tb]
@@ -518,30 +466,6 @@ class MultiTaskFastGP(AbstractFastGP):
             self._yt_state[task] = (n, yt)
             return yt
         return self._cached(("ytilde", (task, n)), f, grad_sensitive=False)
-
-    def kernel(self, x, z, beta0=None, beta1=None, c0=None, c1=None):
-        """abstract_gp.py:693-706 with broadcasting of x [..., d] and z [..., d]."""
-        assert isinstance(x, torch.Tensor) and x.size(-1) == self.d
-        assert isinstance(z, torch.Tensor) and z.size(-1) == self.d
-        dev = self.device
-        if beta0 is None:
-            beta0 = torch.zeros((1, self.d), dtype=torch.int64, device=dev)
-        if beta0.shape == (len(beta0),):
-            beta0 = beta0[None, :]
-        if beta1 is None:
-            beta1 = torch.zeros((1, self.d), dtype=torch.int64, device=dev)
-        if beta1.shape == (len(beta1),):
-            beta1 = beta1[None, :]
-        if c0 is None:
-            c0 = torch.ones(len(beta0), device=dev)
-        if c1 is None:
-            c1 = torch.ones(len(beta1), device=dev)
-        shape = torch.broadcast_shapes(x.shape[:-1], z.shape[:-1])
-        xe = x.expand(shape + (self.d,)).reshape(-1, self.d)
-        ze = z.expand(shape + (self.d,)).reshape(-1, self.d)
-        p = self._parts_pairs(xe, ze, beta0.cpu(), beta1.cpu(), zip_pairs=True)
-        k = self._kernel_from_parts(p, beta0.to(dev), beta1.to(dev), c0.to(dev, torch.float64), c1.to(dev, torch.float64))
-        return k.reshape(k.shape[:-1] + tuple(shape))
 
     # ------------------------------------------------------------------ the block inverse
     def _nvec(self, n):

@@ -4,6 +4,8 @@ reference's own FFT-backend sensitivity there (VERDICT r02 "Next round" item 1).
 
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_c5.py
 
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_c5.py --per-output
+
 Writes tests/golden/c5_m18_d3_b512.npz (inputs: the point set's generating vector + shift and the data
 seed; outputs: the reference's fit(iterations=3) loss / parameter trajectory, post_mean at 16 test points,
 post_var at 2), tests/golden/c5_m18_d3_b512_f32data.npz (the same on the observations rounded to float32:
@@ -11,6 +13,11 @@ the mixed-precision path's data) and profiles/r03_c5_backend_spread.json: the sa
 fftbr_torch / ifftbr_torch replaced by numpy's pocketfft (a differentiable wrapper, adjoints by the
 inverse transform) -- the spread a correct implementation of the reference can show at this size and
 nugget.  tests/test_gpu_multioutput.py allows 5x it.
+
+--per-output: the benched per-output regime instead (docs/examples/batch_multitask/fgp_lattice.ipynb
+cell 6: shape_scale = [512, 1], shape_lengthscales = [512, 3] -- 512 independent eigen-problems on one point
+set, one summed loss; nugget 1e-8): tests/golden/c5_m18_d3_b512_po.npz and
+profiles/r04_c5_po_backend_spread.json.
 """
 import json
 import os
@@ -98,11 +105,85 @@ def run(fg, qmcpy, backend, f32_data=False):
                 kxx=float(gp.kernel(xt[:NV], xt[:NV]).detach().abs().max()))
 
 
+def rel(a, b):
+    return float(np.max(np.abs(np.asarray(a) - np.asarray(b))) / np.max(np.abs(np.asarray(b))))
+
+
+PO_CHUNK = 64
+
+
+def run_per_output(fg, qmcpy, backend):
+    """The per-output regime through the REAL reference, in chunks of PO_CHUNK outputs: the reference's
+    per-output problems are independent (Rprop steps every parameter element on its own gradient, the loss
+    is the sum of the per-output MLLs with logdet weight d_out / numel(logdet) = 1 and constant d_out n
+    log 2 pi), so the 512-output run is the concatenation of the chunks' parameters / posteriors and the sum
+    of their loss histories -- at 1/8 of the reference's memory (one 512-output autograd graph does not fit
+    this container's 64 GB).  Each chunk gets its rows of the full [512, n] observations."""
+    if backend == "numpy":
+        qmcpy.fftbr_torch, qmcpy.ifftbr_torch = _NpFFTBR.apply, _NpIFFTBR.apply
+    n = 2 ** M
+    shift = np.random.default_rng(7).uniform(size=D)
+    outs = []
+    yfull = None
+    for a in range(0, B, PO_CHUNK):
+        Bc = min(PO_CHUNK, B - a)
+        seq = qmcpy.Lattice(D, randomize="SHIFT", generating_vector=LATTICE_Z[:D], shift=shift)
+        gp = fg.FastGPLattice(seq, alpha=2, shape_batch=[Bc], shape_scale=[Bc, 1], shape_lengthscales=[Bc, D])
+        x = gp.get_x_next(n)
+        if yfull is None:
+            yfull = c5_data(x, B)
+        gp.add_y_next(yfull[a:a + Bc].clone())
+        data = gp.fit(iterations=ITS, store_hists=True, verbose=0, stop_crit_wait_iterations=ITS + 5)
+        xt = torch.rand((NM, D), generator=torch.Generator().manual_seed(17))
+        pm = gp.post_mean(xt)
+        pv = gp.post_var(xt[:NV])
+        outs.append(dict(loss_hist=data["loss_hist"].detach().numpy(), raw_scale=gp.raw_scale.detach().numpy(),
+                         raw_lengthscales=gp.raw_lengthscales.detach().numpy(), pmean=pm.detach().numpy(),
+                         pvar=pv.detach().numpy(), kxx_all=gp.kernel(xt[:NV], xt[:NV]).detach().numpy(),
+                         x_test=xt.numpy()))
+        del gp, data
+        print("chunk", a, "done", flush=True)
+    cat = lambda k: np.concatenate([o[k] for o in outs], 0)
+    return dict(z=np.array(LATTICE_Z[:D], dtype=np.int64), shift=shift, x_test=outs[0]["x_test"],
+                loss_hist=np.sum([o["loss_hist"] for o in outs], 0), raw_scale=cat("raw_scale"),
+                raw_lengthscales=cat("raw_lengthscales"), pmean=cat("pmean"), pvar=cat("pvar"),
+                kxx_all=cat("kxx_all"), chunk=np.array(PO_CHUNK))
+
+
+def main_per_output(fg, qmcpy):
+    keep = (qmcpy.fftbr_torch, qmcpy.ifftbr_torch)
+    path = os.path.join(HERE, "c5_m18_d3_b512_po.npz")
+    if "--reuse" in sys.argv and os.path.isfile(path):      # the torch-backend fixture of an earlier run
+        ref = dict(np.load(path))
+    else:
+        ref = run_per_output(fg, qmcpy, "torch")
+        np.savez_compressed(path, m=np.array(M), d=np.array(D), B=np.array(B), its=np.array(ITS),
+                            **{k: np.asarray(v) for k, v in ref.items()})
+    alt = run_per_output(fg, qmcpy, "numpy")
+    qmcpy.fftbr_torch, qmcpy.ifftbr_torch = keep
+    kdiag = np.abs(ref["kxx_all"])        # [B, NV]: each output's own K(x_t, x_t) (per-output scales)
+    spread = {"config": "C5 per-output: lattice n=2^%d d=%d x %d outputs, shape_scale=[%d,1], "
+                        "shape_lengthscales=[%d,%d], nugget 1e-8, fit(iterations=%d), post_mean N=%d, post_var N=%d"
+                        % (M, D, B, B, B, D, ITS, NM, NV),
+              "what": "the REAL reference (tests/golden/make_golden_c5.py --per-output, chunks of %d outputs) with "
+                      "qmcpy.fftbr_torch/ifftbr_torch (torch.fft) vs numpy pocketfft" % PO_CHUNK,
+              "loss_hist_rel": rel(alt["loss_hist"], ref["loss_hist"]),
+              "raw_lengthscales_abs": float(np.max(np.abs(alt["raw_lengthscales"] - ref["raw_lengthscales"]))),
+              "raw_scale_abs": float(np.max(np.abs(alt["raw_scale"] - ref["raw_scale"]))),
+              "pmean_rel": rel(alt["pmean"], ref["pmean"]),
+              "pvar_abs_over_kxx": float(np.max(np.abs(alt["pvar"] - ref["pvar"]) / kdiag))}
+    with open(os.path.join(ROOT, "profiles", "r04_c5_po_backend_spread.json"), "w") as f:
+        json.dump(spread, f, indent=1)
+    print(json.dumps(spread, indent=1))
+
+
 def main():
     torch.set_default_dtype(torch.float64)
     torch.set_num_threads(os.cpu_count() or 1)
     fg = import_reference()
     import qmcpy
+    if "--per-output" in sys.argv:
+        return main_per_output(fg, qmcpy)
     keep = (qmcpy.fftbr_torch, qmcpy.ifftbr_torch)
     ref = run(fg, qmcpy, "torch")
     np.savez_compressed(os.path.join(HERE, "c5_m18_d3_b512.npz"), m=np.array(M), d=np.array(D), B=np.array(B),
@@ -112,9 +193,6 @@ def main():
                         B=np.array(B), its=np.array(ITS), **{k: np.asarray(v) for k, v in r32.items()})
     alt = run(fg, qmcpy, "numpy")
     qmcpy.fftbr_torch, qmcpy.ifftbr_torch = keep
-
-    def rel(a, b):
-        return float(np.max(np.abs(np.asarray(a) - np.asarray(b))) / np.max(np.abs(np.asarray(b))))
     spread = {"config": "C5 lattice n=2^%d d=%d x %d outputs, nugget 1e-8, fit(iterations=%d), post_mean N=%d, "
                         "post_var N=%d" % (M, D, B, ITS, NM, NV),
               "what": "the REAL reference (tests/golden/make_golden_c5.py) with qmcpy.fftbr_torch/ifftbr_torch "

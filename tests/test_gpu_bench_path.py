@@ -1,8 +1,10 @@
 """Parity of the exact path bench.py times (BASELINE config C4, one GPU's share): a GPBatch of P = 8
-randomly shifted lattice GPs (seeds 1000..1007, d = 5) through bench.step_batched -- the half-length
-(R2C) fit kernels with G = 8 problems and per-problem shift regeneration (FGP_R2C=1, FGP_PARTS_GEN=1,
-the defaults), the batched coefficient solve, fgp_post_mean_batched and fgp_post_var_batched with
-regenerated training points.
+randomly shifted lattice GPs (seeds 1000..1007, d = 5) through bench.step_batched -- by default the
+spectral fit path (fit_engine.spectral_wanted: one set of part-product spectra shared by the 8 problems,
+one fused k_spec_tile launch per Rprop iteration), the coefficient solve from the spectra
+(fgp_spec_inv_eig + fgp_ifftbr_real_rf), fgp_post_mean_batched and fgp_post_var_batched with regenerated
+training points; and, forced with FGP_FIT_PATH=transform, the real-even transform fit kernels the
+spectral path replaced (still selected for d > 6 or n >= 2^22).
 
 Per GP, against
   * the CPU oracle (oracle/fgp_oracle.py, the reference's op sequence: abstract_gp.py:152-416) at the
@@ -27,9 +29,10 @@ torch.set_default_dtype(torch.float64)
 ITERS = 5
 
 
-@pytest.mark.parametrize("m,mode", [(17, "2"), (20, "2"), (20, "1")])
-def test_bench_step_matches_oracle_and_individual_fits(monkeypatch, m, mode):
-    monkeypatch.setenv("FGP_R2C", mode)
+@pytest.mark.parametrize("m,path", [(17, "spectral"), (20, "spectral"), (20, "transform")])
+def test_bench_step_matches_oracle_and_individual_fits(monkeypatch, m, path):
+    if path == "transform":
+        monkeypatch.setenv("FGP_FIT_PATH", "transform")
     monkeypatch.setenv("FGP_PARTS_GEN", "1")
     d, n, P = 5, 2 ** m, 8
     seeds = bench.shard_seeds(0, 1, P)

@@ -78,6 +78,41 @@ def test_benched_c5_regime_matches_reference(mixed):
     assert float((pv - torch.from_numpy(g["pvar"])).abs().max()) <= C5_TOL["pvar_kxx"] * float(g["kxx"])
 
 
+# The per-output regime bench.py also times (C5 per-output: shape_scale = [512, 1], shape_lengthscales = [512, 3],
+# nugget 1e-8): 5x the REAL reference's torch.fft vs numpy-pocketfft spread there (tests/golden/
+# make_golden_c5.py --per-output -> profiles/r04_c5_po_backend_spread.json: loss history 7.1e-7 relative,
+# post_mean 1.7e-7 relative, post_var 2.8e-16 of each output's K(x, x), fitted parameters identical); the
+# variance keeps the 1e-8 K(x, x) of the golden tests.
+C5_PO_TOL = dict(loss=3.6e-6, pmean=8.3e-7, pvar_kxx=1e-8, params=1e-10)
+
+
+def test_benched_c5_per_output_regime_matches_reference():
+    """C5 per-output as bench.py times it: 512 eigen-problems on one point set (the sliced k_spec_tile<3, 4>,
+    the parallel many-problem step k_spec_step_many, fgp_spec_post_var at G = 512), fit(iterations=3),
+    post_mean at 16 and post_var at 2 test points -- against the REAL reference (tests/golden/
+    c5_m18_d3_b512_po.npz; the reference ran in chunks of 64 outputs, its per-output problems being
+    independent)."""
+    import numpy as np
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "c5_m18_d3_b512_po.npz"))
+    m, d, B, its = int(g["m"]), int(g["d"]), int(g["B"]), int(g["its"])
+    seq = F.Lattice(d, randomize="SHIFT", generating_vector=g["z"], shift=g["shift"])
+    gp = F.FastGPLattice(seq, alpha=2, shape_batch=[B], shape_scale=[B, 1], shape_lengthscales=[B, d], device=DEV)
+    x = gp.get_x_next(2 ** m).cpu()
+    gp.add_y_next(_c5_data(x, B).to(DEV))
+    data = gp.fit(iterations=its, store_loss_hist=True, verbose=0, stop_crit_wait_iterations=its + 5)
+    assert rel_err(data["loss_hist"], torch.from_numpy(g["loss_hist"])) <= C5_PO_TOL["loss"]
+    for k in ("raw_lengthscales", "raw_scale"):
+        assert float((getattr(gp, k).detach().cpu() - torch.from_numpy(g[k])).abs().max()) <= C5_PO_TOL["params"], k
+    xt = torch.from_numpy(g["x_test"])
+    pm = gp.post_mean(xt.to(DEV)).cpu()
+    assert pm.shape == tuple(g["pmean"].shape)
+    assert rel_err(pm, g["pmean"]) <= C5_PO_TOL["pmean"]
+    pv = gp.post_var(xt[:g["pvar"].shape[-1]].to(DEV)).cpu()
+    assert pv.shape == tuple(g["pvar"].shape)
+    kxx = torch.from_numpy(np.abs(g["kxx_all"]))
+    assert float(((pv - torch.from_numpy(g["pvar"])).abs() / kxx).max()) <= C5_PO_TOL["pvar_kxx"]
+
+
 @pytest.mark.parametrize("per_output", [False, True])
 def test_multi_output_fit_and_predict_match_oracle(per_output):
     m, d, B, its = 18, 3, 16, 3
@@ -224,3 +259,57 @@ def test_fp32_data_coefficients_same_with_and_without_graph():
     gp._cache = {}
     c1 = gp.coeffs.detach()
     assert rel_err(c1, c0) <= 1e-6
+
+
+def _bench_secondary_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import argparse
+    import torch.distributed as dist
+    torch.set_default_dtype(torch.float64)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        args = argparse.Namespace(fit_iters=50, n_mean=64, n_var=4, c5_outputs=512, steps=1)
+        got = {}
+        lines = bench.secondary_configs(F, args, "cuda:0", rank, world, collect=got)
+        q.put((rank, lines, got))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_secondary_c5_lines_two_ranks_equal_one_rank():
+    """bench.py's N > 1 C5 path, executed: bench.secondary_configs itself at world size 2 (gloo, both ranks on
+    cuda:0) -- C5 with the outputs sharded over the ranks (distributed.fit_sharded: one Y all-reduce) and C5
+    per-output (replicas of 256 outputs) -- against the same function at world size 1: every rank's fitted
+    parameters equal the N = 1 fit's to 1e-10 (Y summed in another order; the per-output problems are
+    independent), and its post_mean / post_var are the N = 1 run's rows of the outputs it owns."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_secondary_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=600) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    import argparse
+    import bench
+    args = argparse.Namespace(fit_iters=50, n_mean=64, n_var=4, c5_outputs=512, steps=1)
+    ref = {}
+    bench.secondary_configs(F, args, DEV, 0, 1, collect=ref)
+    for rank, lines, got in res:
+        assert [ln["n_gpus"] for ln in lines] == [2, 2]
+        assert all(ln["value"] > 0 for ln in lines)
+        for case in ("C5", "C5 per-output"):
+            r, o = ref[case], got[case]
+            a, b = o["outputs"]
+            assert (a, b) == bench.c5_shard(512, rank, world)
+            for k in ("raw_scale", "raw_lengthscales"):
+                rv = r[k][a:b] if (case == "C5 per-output" and r[k].shape[0] == 512) else r[k]
+                assert float((o[k] - rv).abs().max()) <= 1e-10, (case, k)
+            assert rel_err(o["post_mean"], r["post_mean"][a:b]) <= 1e-9, case
+            kxx = float(r["post_var"].abs().max()) + 1e-300
+            assert float((o["post_var"] - r["post_var"][a:b]).abs().max()) <= 1e-9 * max(kxx, 1.0), case
