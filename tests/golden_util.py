@@ -10,9 +10,10 @@ GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 def golden_names(family=None, multitask=False):
     """Single-task fixtures (make_golden.py) by default; multitask=True: the multitask /
     derivative-informed ones (make_golden_multitask.py, names mt_* / deriv_*)."""
-    # (c5_*: the benched C5 regime of make_golden_c5.py, read by tests/test_gpu_multioutput.py only)
+    # (c5_*: the benched C5 regime of make_golden_c5.py, read by tests/test_gpu_multioutput.py only;
+    # single_extras: make_golden_single_extras.py, read by tests/test_gpu_single_extras.py only)
     names = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz"))
-                   if not os.path.basename(p).startswith("c5_"))
+                   if not os.path.basename(p).startswith(("c5_", "single_extras")))
     mt = [n for n in names if n.startswith("mt_") or n.startswith("deriv_")]
     names = mt if multitask else [n for n in names if n not in mt]
     if family is not None:
