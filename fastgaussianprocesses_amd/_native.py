@@ -12,7 +12,7 @@ import torch
 
 _LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
 LIB_PATH = os.environ.get("FGP_LIB_PATH") or os.path.join(_LIB_DIR, "libfgp_hip.so")   # override: experiments
-ABI_VERSION = 13
+ABI_VERSION = 14
 MT_MAX_TASKS = 16
 MAX_D = 8
 PARTS_ARRAY = 0
@@ -81,7 +81,25 @@ class MtLayout(ctypes.Structure):
     _fields_ = [("T", _c_int), ("n", _c_i64 * 16)]
 
 
+class MtFitDesc(ctypes.Structure):
+    """Mirror of fgp_mt_fit_desc (include/fgp_hip.h, ABI 14)."""
+    _fields_ = [
+        ("family", _c_int), ("d", _c_int), ("B", _c_int),
+        ("layout", MtLayout), ("task", _c_int * 16),
+        ("T_all", _c_int), ("rank", _c_int), ("dl", _c_int),
+        ("spectra", _c_vp), ("spec_off", _c_i64 * 136), ("y", _c_vp), ("raw", _c_vp),
+        ("vtask_exp", _c_int),
+        ("rg_scale", _c_int), ("rg_ls", _c_int), ("rg_noise", _c_int), ("rg_factor", _c_int), ("rg_vtask", _c_int),
+        ("rprop_prev", _c_vp), ("rprop_step", _c_vp), ("grad_out", _c_vp), ("loss_hist", _c_vp), ("raw_hist", _c_vp),
+        ("grad_norm", _c_dbl), ("grad_logdet", _c_dbl),
+        ("logdet_weight", _c_dbl), ("mll_const", _c_dbl), ("eta_minus", _c_dbl), ("eta_plus", _c_dbl),
+        ("step_min", _c_dbl), ("step_max", _c_dbl),
+        ("work", _c_vp),
+    ]
+
+
 _P_NLL = ctypes.POINTER(NllDesc)
+_P_MTFIT = ctypes.POINTER(MtFitDesc)
 _P_MT = ctypes.POINTER(MtLayout)
 _P_FIT = ctypes.POINTER(FitDesc)
 _P_PRED = ctypes.POINTER(PredDesc)
@@ -130,6 +148,9 @@ _SIGNATURES = {
     "fgp_mt_solve": [_P_MT, _c_vp, _c_i64, _c_vp, _c_i64, _c_i64, _c_vp, _c_vp],
     "fgp_mt_selinv": [_P_MT, _c_vp, _c_i64, _c_vp, _c_vp],
     "fgp_mt_mll_grad": [_P_MT, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_i64, _c_vp, _c_vp],
+    "fgp_mt_fit_nparams": [_P_MTFIT, _c_pi],
+    "fgp_mt_fit_work": [_P_MTFIT, _c_pl],
+    "fgp_mt_fit_run": [_P_MTFIT, _c_int, _c_int, _c_int, _c_vp],
     "fgp_nll_partials_len": [_P_NLL, _c_pl],
     "fgp_spec_basis": [_c_int, _c_vp, _c_i64, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_i64, _c_vp],
     "fgp_spec_basis_work": [_c_int, _c_int, _c_int, _c_pl],

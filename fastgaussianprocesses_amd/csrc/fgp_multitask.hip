@@ -15,6 +15,9 @@
 // arrays in the packed layout of the lams [problem][sum_{k<=l} n_k] with the frequency class fastest,
 // one thread per (problem, class) so that a wavefront's accesses are contiguous.
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <type_traits>
 #include <math.h>
 #include <stdint.h>
 
@@ -108,15 +111,11 @@ __device__ __forceinline__ double2 cmul_cj(double2 a, double2 b) {   // conj(a) 
 // layout of the lams themselves: D on the diagonal entries, u on the coupling entries.  Work per
 // frequency class is R T^2 / 2 instead of the R^3 / 3 of a dense factorisation (and the reference's
 // bordering, util.py:301-323, which grows a dense [R, R] inverse).  logdet_j = sum log |D|.
-__global__ __launch_bounds__(kWG) void k_mt_ldl(const double2* __restrict__ lp, int64_t G, MtLay lay,
-                                                double2* __restrict__ fac, double* __restrict__ logdet,
-                                                int* __restrict__ info) {
-  const int64_t e = (int64_t)blockIdx.x * kWG + threadIdx.x;
-  if (e >= G * lay.nmin) return;
-  const int64_t g = e / lay.nmin, j = e - g * lay.nmin;
+// the factor of class j of problem g (src / F: that problem's packed arrays offset by j); returns the
+// class's logdet, *bad set on a non-positive pivot
+__device__ __forceinline__ double mt_ldl_class(const double2* __restrict__ src, double2* __restrict__ F, const MtLay& lay,
+                                               bool* bad_out) {
   const int64_t nm = lay.nmin;
-  const double2* src = lp + g * lay.L + j;
-  double2* F = fac + g * lay.L + j;
   for (int64_t i = 0; i < lay.L / nm; ++i) F[i * nm] = src[i * nm];
   double ld = 0.0;
   bool bad = false;
@@ -146,23 +145,28 @@ __global__ __launch_bounds__(kWG) void k_mt_ldl(const double2* __restrict__ lp, 
       }
     }
   }
-  logdet[e] = ld;            // a non-positive pivot still counts as log|pivot| (the reference's log|S|); info flags it
+  *bad_out = bad;
+  return ld;                 // a non-positive pivot still counts as log|pivot| (the reference's log|S|); info flags it
+}
+
+__global__ __launch_bounds__(kWG) void k_mt_ldl(const double2* __restrict__ lp, int64_t G, MtLay lay,
+                                                double2* __restrict__ fac, double* __restrict__ logdet,
+                                                int* __restrict__ info) {
+  const int64_t e = (int64_t)blockIdx.x * kWG + threadIdx.x;
+  if (e >= G * lay.nmin) return;
+  const int64_t g = e / lay.nmin, j = e - g * lay.nmin;
+  bool bad = false;
+  logdet[e] = mt_ldl_class(lp + g * lay.L + j, fac + g * lay.L + j, lay, &bad);
   if (bad) info[0] = 1;
 }
 
 // out[b] = Lambda_{g(b)}^-1 v[b] (g(b) = b mod G), per frequency class: forward substitution with L,
 // scaling by D^-1, back substitution with L^H -- O(R T) per vector and class.  v, out: [B][R nmin]
 // (rows of the sorted tasks concatenated, the reference's [..., R, n_min] view, util.py:356-360).
-__global__ __launch_bounds__(kWG) void k_mt_solve(const double2* __restrict__ fac, int64_t G, MtLay lay,
-                                                  const double2* __restrict__ v, int64_t vs, int64_t B,
-                                                  double2* __restrict__ out) {
-  const int64_t e = (int64_t)blockIdx.x * kWG + threadIdx.x;
-  if (e >= B * lay.nmin) return;
+// one vector of class j: F the factor, vb the right-hand side, o the solution (all offset by j)
+__device__ __forceinline__ void mt_solve_class(const double2* __restrict__ F, const MtLay& lay, const double2* __restrict__ vb,
+                                               double2* __restrict__ o) {
   const int64_t nm = lay.nmin;
-  const int64_t b = e / nm, j = e - b * nm, g = b % G;
-  const double2* F = fac + g * lay.L + j;
-  const double2* vb = v + b * vs + j;
-  double2* o = out + b * (int64_t)lay.R * nm + j;
   for (int r = 0; r < lay.R; ++r) o[(int64_t)r * nm] = vb[(int64_t)r * nm];
   for (int k = 0; k < lay.T; ++k) {                    // w = L^-1 v
     const int qk = (int)(lay.n[k] / nm);
@@ -197,6 +201,16 @@ __global__ __launch_bounds__(kWG) void k_mt_solve(const double2* __restrict__ fa
   }
 }
 
+__global__ __launch_bounds__(kWG) void k_mt_solve(const double2* __restrict__ fac, int64_t G, MtLay lay,
+                                                  const double2* __restrict__ v, int64_t vs, int64_t B,
+                                                  double2* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * kWG + threadIdx.x;
+  if (e >= B * lay.nmin) return;
+  const int64_t nm = lay.nmin;
+  const int64_t b = e / nm, j = e - b * nm, g = b % G;
+  mt_solve_class(fac + g * lay.L + j, lay, v + b * vs + j, out + b * (int64_t)lay.R * nm + j);
+}
+
 // Entries of A = Lambda^-1 on the coupling pattern (Takahashi's recurrence Z = D^-1 L^-1 + (I - L^H) Z,
 // evaluated on the pattern only, which is closed under it): rows (k, q) from the last task back,
 //   Z[(k,q),(m, q mod q_m)] = - sum_{l > k} u_kl[q] Z[(l, q mod q_l), (m, q mod q_m)]     (m > k)
@@ -209,14 +223,8 @@ __device__ __forceinline__ double2 zpat(const double2* Z, const MtLay& lay, int 
                 : conj2(Z[lay.off[m * FGP_MT_MAX_TASKS + l] + (int64_t)pm * nm]);
 }
 
-__global__ __launch_bounds__(kWG) void k_mt_selinv(const double2* __restrict__ fac, int64_t G, MtLay lay,
-                                                   double2* __restrict__ zinv) {
-  const int64_t e = (int64_t)blockIdx.x * kWG + threadIdx.x;
-  if (e >= G * lay.nmin) return;
+__device__ __forceinline__ void mt_selinv_class(const double2* __restrict__ F, const MtLay& lay, double2* __restrict__ Z) {
   const int64_t nm = lay.nmin;
-  const int64_t g = e / nm, j = e - g * nm;
-  const double2* F = fac + g * lay.L + j;
-  double2* Z = zinv + g * lay.L + j;
   for (int k = lay.T - 1; k >= 0; --k) {
     const int qk = (int)(lay.n[k] / nm);
     for (int q = 0; q < qk; ++q) {
@@ -240,22 +248,26 @@ __global__ __launch_bounds__(kWG) void k_mt_selinv(const double2* __restrict__ f
   }
 }
 
+__global__ __launch_bounds__(kWG) void k_mt_selinv(const double2* __restrict__ fac, int64_t G, MtLay lay,
+                                                   double2* __restrict__ zinv) {
+  const int64_t e = (int64_t)blockIdx.x * kWG + threadIdx.x;
+  if (e >= G * lay.nmin) return;
+  const int64_t g = e / lay.nmin, j = e - g * lay.nmin;
+  mt_selinv_class(fac + g * lay.L + j, lay, zinv + g * lay.L + j);
+}
+
 // Gradient of the MLL data + logdet terms w.r.t. the packed lams (torch's convention for complex
 // inputs: dL/dRe + i dL/dIm), with z_b = A y_b, gn[b] = dL/dnorm_b, gl[g] = dL/dlogdet_g and Z the
 // selected inverse:
 //   coupling entry (r < c):  -2 sum_b gn[b] z_br conj(z_bc) + 2 gl[g] Z_rc
 //   diagonal entry:          -sum_b gn[b] |z_br|^2 + gl[g] Z_rr      (real; the imaginary part of a
 //                            Hermitian diagonal does not enter)
-__global__ __launch_bounds__(kWG) void k_mt_mll_grad(const double2* __restrict__ zinv, const double2* __restrict__ z,
-                                                     const double* __restrict__ gn, const double* __restrict__ gl,
-                                                     int64_t B, int64_t G, MtLay lay, double2* __restrict__ glp) {
-  const int64_t e = (int64_t)blockIdx.x * kWG + threadIdx.x;
-  if (e >= G * lay.nmin) return;
-  const int64_t g = e / lay.nmin, j = e - g * lay.nmin;
+// class j of problem g: Z, out offset by g L + j; z the solutions [B][R nmin] (not offset); gn(b) per vector
+template <typename GN>
+__device__ __forceinline__ void mt_grad_class(const double2* __restrict__ Z, const double2* __restrict__ z, GN gn, double glg,
+                                              int64_t B, int64_t G, int64_t g, int64_t j, const MtLay& lay,
+                                              double2* __restrict__ out) {
   const int64_t nm = lay.nmin, zs = (int64_t)lay.R * nm;
-  const double glg = gl[g];
-  const double2* Z = zinv + g * lay.L + j;
-  double2* out = glp + g * lay.L + j;
   for (int k = 0; k < lay.T; ++k) {
     const int qk = (int)(lay.n[k] / nm);
     for (int l = k; l < lay.T; ++l) {
@@ -266,8 +278,9 @@ __global__ __launch_bounds__(kWG) void k_mt_mll_grad(const double2* __restrict__
         double2 w = make_double2(0.0, 0.0);
         for (int64_t b = g; b < B; b += G) {
           const double2 p = cmulc(z[b * zs + (int64_t)r * nm + j], z[b * zs + (int64_t)c * nm + j]);
-          w.x = __builtin_fma(gn[b], p.x, w.x);
-          w.y = __builtin_fma(gn[b], p.y, w.y);
+          const double gb = gn(b);
+          w.x = __builtin_fma(gb, p.x, w.x);
+          w.y = __builtin_fma(gb, p.y, w.y);
         }
         const double2 a = Z[off + (int64_t)q * nm];
         double2 gv;
@@ -276,6 +289,269 @@ __global__ __launch_bounds__(kWG) void k_mt_mll_grad(const double2* __restrict__
         out[off + (int64_t)q * nm] = gv;
       }
     }
+  }
+}
+
+__global__ __launch_bounds__(kWG) void k_mt_mll_grad(const double2* __restrict__ zinv, const double2* __restrict__ z,
+                                                     const double* __restrict__ gn, const double* __restrict__ gl,
+                                                     int64_t B, int64_t G, MtLay lay, double2* __restrict__ glp) {
+  const int64_t e = (int64_t)blockIdx.x * kWG + threadIdx.x;
+  if (e >= G * lay.nmin) return;
+  const int64_t g = e / lay.nmin, j = e - g * lay.nmin;
+  mt_grad_class(zinv + g * lay.L + j, z, [&](int64_t b) { return gn[b]; }, gl[g], B, G, g, j, lay, glp + g * lay.L + j);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Device-resident fit of a general multitask GP (ABI 14, fgp_mt_fit_run).  One iteration = four launches:
+//   k_mtg_lams          packed lams from the pair spectra and the current parameters (thread per entry)
+//   k_mtg_factor_grad   per frequency class: structured LDL^H, solves of the B data vectors, selected inverse,
+//                       dL/dlams (thread per class: mt_ldl_class / mt_solve_class / mt_selinv_class /
+//                       mt_grad_class, the generic path's kernels' bodies)
+//   k_mtg_contract      dL/dlams contracted with dlams/dtheta (thread per entry): block partials of the norm,
+//                       logdet, dL/dnoise, dL/draw_scale, dL/draw_l_m; the per-entry dL/dK_task terms
+//   k_mtg_step          one workgroup: fixed-order reductions, loss history, dL/d(task factor / noise) by
+//                       the chain rule through K_task = F F^T + diag(v), torch.optim.Rprop on every element
+struct MtFit {
+  MtLay lay;
+  int family, d, B, T_all, rank, dl, vtask_exp, P;
+  int task[FGP_MT_MAX_TASKS];
+  int rg_scale, rg_ls, rg_noise, rg_factor, rg_vtask;
+  const double2* spec;
+  int64_t spec_off[FGP_MT_MAX_TASKS * (FGP_MT_MAX_TASKS + 1) / 2];
+  const double2* y;
+  double* raw;
+  double *prev, *step, *grad, *loss_hist, *raw_hist;
+  double gn, gl, logdet_weight, mll_const, eta_minus, eta_plus, step_min, step_max;
+  int n_params, f_off, v_off;
+  // workspace
+  double2 *lams, *fac, *zinv, *glp, *z;
+  double *logdet, *dkt, *part;
+  int* info;
+  int nblk;
+};
+
+constexpr int kMtgQ = 4 + FGP_MAX_D;   // norm, logdet, dnoise (/ noise), draw_scale, draw_l[FGP_MAX_D]
+
+__device__ __forceinline__ double mtg_scale(const MtFit& m) { return exp(m.raw[0]); }
+__device__ __forceinline__ double mtg_ls(const MtFit& m, int j) { return exp(m.raw[1 + (m.dl > 1 ? j : 0)]); }
+__device__ __forceinline__ double mtg_noise(const MtFit& m) { return exp(m.raw[1 + m.dl]); }
+// K_task[a, b] = sum_r F[a, r] F[b, r] + [a == b] v_a  (util.py:157-162; F identity, v exp / identity)
+__device__ __forceinline__ double mtg_kt(const MtFit& m, int a, int b) {
+  double s = 0.0;
+  for (int r = 0; r < m.rank; ++r) s += m.raw[m.f_off + a * m.rank + r] * m.raw[m.f_off + b * m.rank + r];
+  if (a == b) s += m.vtask_exp ? exp(m.raw[m.v_off + a]) : m.raw[m.v_off + a];
+  return s;
+}
+
+// entry e of the packed lams -> sorted pair (k, l), its index p and the position i in lams[k, l]
+__device__ __forceinline__ void mtg_entry(const MtFit& m, int64_t e, int& k, int& l, int& p, int64_t& i) {
+  const MtLay& lay = m.lay;
+  k = 0;
+  l = 0;
+  p = 0;
+  for (int kk = 0; kk < lay.T; ++kk)
+    for (int ll = kk; ll < lay.T; ++ll) {
+      const int64_t o = lay.off[kk * FGP_MT_MAX_TASKS + ll];
+      if (e >= o && e < o + lay.n[kk]) {
+        k = kk;
+        l = ll;
+      }
+    }
+  p = k * lay.T - k * (k - 1) / 2 + (l - k);
+  i = e - lay.off[k * FGP_MT_MAX_TASKS + l];
+}
+
+// P = sum_S l^S Phi_S[i] of pair p (ascending S) and, with DER, dp[j] = sum_{S containing j} l^S Phi_S[i]
+template <int D, bool DER>
+__device__ __forceinline__ double2 mtg_poly(const MtFit& m, int p, int64_t nk, int64_t i, const double* lpow,
+                                            double2* dp) {
+  constexpr int NS = 1 << D;
+  const double2* ph = m.spec + m.spec_off[p] + i;
+  double2 P = make_double2(0.0, 0.0);
+#pragma unroll
+  for (int j = 0; j < (DER ? D : 0); ++j) dp[j] = make_double2(0.0, 0.0);
+#pragma unroll
+  for (int S = 0; S < NS; ++S) {
+    const double2 f = ph[(int64_t)S * nk];
+    const double w = lpow[S];
+    P.x = __builtin_fma(w, f.x, P.x);
+    P.y = __builtin_fma(w, f.y, P.y);
+    if constexpr (DER) {
+#pragma unroll
+      for (int j = 0; j < D; ++j)
+        if ((S >> j) & 1) {
+          dp[j].x = __builtin_fma(w, f.x, dp[j].x);
+          dp[j].y = __builtin_fma(w, f.y, dp[j].y);
+        }
+    }
+  }
+  return P;
+}
+
+template <int D>
+__device__ __forceinline__ void mtg_lpow(const MtFit& m, double* lpow) {
+#pragma unroll
+  for (int S = 0; S < (1 << D); ++S) {
+    double w = 1.0;
+#pragma unroll
+    for (int j = 0; j < D; ++j)
+      if ((S >> j) & 1) w *= mtg_ls(m, j);
+    lpow[S] = w;
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(kWG) void k_mtg_lams(MtFit m) {
+  const int64_t e = (int64_t)blockIdx.x * kWG + threadIdx.x;
+  if (e >= m.lay.L) return;
+  double lpow[1 << D];
+  mtg_lpow<D>(m, lpow);
+  int k, l, p;
+  int64_t i;
+  mtg_entry(m, e, k, l, p, i);
+  const double2 P = mtg_poly<D, false>(m, p, m.lay.n[k], i, lpow, nullptr);
+  const double sc = mtg_scale(m), rn = sqrt((double)m.lay.n[l]);
+  // lams = K_task (sqrt(n_l) lam + noise [k == l]),  lam = scale P  (util.py:284-298)
+  double2 v = make_double2(rn * (sc * P.x), rn * (sc * P.y));
+  if (k == l) v.x += mtg_noise(m);
+  const double kt = mtg_kt(m, m.task[k], m.task[l]);
+  m.lams[e] = make_double2(v.x * kt, v.y * kt);
+}
+
+__global__ __launch_bounds__(kWG) void k_mtg_factor_grad(MtFit m) {
+  const int64_t j = (int64_t)blockIdx.x * kWG + threadIdx.x;
+  const MtLay& lay = m.lay;
+  if (j >= lay.nmin) return;
+  bool bad = false;
+  m.logdet[j] = mt_ldl_class(m.lams + j, m.fac + j, lay, &bad);
+  if (bad) m.info[0] = 1;
+  const int64_t rn = (int64_t)lay.R * lay.nmin;
+  for (int b = 0; b < m.B; ++b) mt_solve_class(m.fac + j, lay, m.y + b * rn + j, m.z + b * rn + j);
+  mt_selinv_class(m.fac + j, lay, m.zinv + j);
+  const double gn = m.gn;
+  mt_grad_class(m.zinv + j, m.z, [&](int64_t) { return gn; }, m.gl, m.B, 1, 0, j, lay, m.glp + j);
+}
+
+template <int D>
+__global__ __launch_bounds__(kWG) void k_mtg_contract(MtFit m) {
+  __shared__ double red[kWG / 64];
+  const int64_t t0 = (int64_t)blockIdx.x * kWG + threadIdx.x, nt = (int64_t)gridDim.x * kWG;
+  const MtLay& lay = m.lay;
+  double lpow[1 << D];
+  mtg_lpow<D>(m, lpow);
+  const double sc = mtg_scale(m);
+  double acc[4 + D];
+#pragma unroll
+  for (int q = 0; q < 4 + D; ++q) acc[q] = 0.0;
+  for (int64_t e = t0; e < lay.L; e += nt) {
+    int k, l, p;
+    int64_t i;
+    mtg_entry(m, e, k, l, p, i);
+    double2 dp[D];
+    const double2 P = mtg_poly<D, true>(m, p, lay.n[k], i, lpow, dp);
+    const double rn = sqrt((double)lay.n[l]);
+    const double kt = mtg_kt(m, m.task[k], m.task[l]);
+    const double2 c = m.glp[e];            // dL/dRe + i dL/dIm of lams[e]: dL/dtheta = Re(conj(c) dlams/dtheta)
+    const double f = kt * rn * sc;
+    acc[3] = __builtin_fma(f, __builtin_fma(c.x, P.x, c.y * P.y), acc[3]);             // draw_scale
+#pragma unroll
+    for (int j = 0; j < D; ++j) acc[4 + j] = __builtin_fma(f, __builtin_fma(c.x, dp[j].x, c.y * dp[j].y), acc[4 + j]);
+    double bx = rn * (sc * P.x), by = rn * (sc * P.y);
+    if (k == l) {
+      bx += mtg_noise(m);
+      acc[2] = __builtin_fma(kt, c.x, acc[2]);                                         // dnoise / noise
+    }
+    m.dkt[e] = __builtin_fma(c.x, bx, c.y * by);                                       // dL/dK_task of entry e
+  }
+  const int64_t rnm = (int64_t)lay.R * lay.nmin;
+  for (int64_t e = t0; e < (int64_t)m.B * rnm; e += nt) {
+    const double2 yv = m.y[e], zv = m.z[e];
+    acc[0] = __builtin_fma(yv.x, zv.x, __builtin_fma(yv.y, zv.y, acc[0]));             // Re(conj(y) z)
+  }
+  for (int64_t j = t0; j < lay.nmin; j += nt) acc[1] += m.logdet[j];
+#pragma unroll
+  for (int q = 0; q < 4 + D; ++q) {
+    const double s = block_sum(acc[q], red);
+    if (threadIdx.x == 0) m.part[(int64_t)blockIdx.x * kMtgQ + q] = s;
+  }
+}
+
+// fixed-order workgroup sum of v(t) over t < cnt (thread-strided, wave shuffles, waves in order)
+template <typename F>
+__device__ __forceinline__ double mtg_sum(int64_t cnt, F v, double* red) {
+  double s = 0.0;
+  for (int64_t t = threadIdx.x; t < cnt; t += kWG) s += v(t);
+  return block_sum(s, red);
+}
+
+template <int D>
+__global__ __launch_bounds__(kWG) void k_mtg_step(MtFit m, int iter, int do_update) {
+  __shared__ double red[kWG / 64];
+  __shared__ double tot[kMtgQ];
+  __shared__ double gkt[FGP_MT_MAX_TASKS * (FGP_MT_MAX_TASKS + 1) / 2];
+  __shared__ double grad[FGP_MT_MAX_TASKS * FGP_MT_MAX_TASKS + FGP_MT_MAX_TASKS + 3 + FGP_MAX_D];
+  const int tid = threadIdx.x;
+  const MtLay& lay = m.lay;
+  for (int q = 0; q < 4 + D; ++q) {
+    const double s = mtg_sum(m.nblk, [&](int64_t b) { return m.part[b * kMtgQ + q]; }, red);
+    if (tid == 0) tot[q] = s;
+  }
+  for (int k = 0, p = 0; k < lay.T; ++k)
+    for (int l = k; l < lay.T; ++l, ++p) {
+      const int64_t o = lay.off[k * FGP_MT_MAX_TASKS + l];
+      const double s = mtg_sum(lay.n[k], [&](int64_t i) { return m.dkt[o + i]; }, red);
+      if (tid == 0) gkt[p] = s;
+    }
+  __syncthreads();
+  if (tid == 0) {
+    const double term2 = m.logdet_weight * tot[1];
+    double* lh = m.loss_hist + (int64_t)iter * 3;
+    lh[0] = 0.5 * (tot[0] + term2 + m.mll_const);
+    lh[1] = tot[0];
+    lh[2] = term2;
+    // gradients in the raw vector's order
+    grad[0] = tot[3];
+    if (m.dl > 1) {
+      for (int j = 0; j < m.d; ++j) grad[1 + j] = tot[4 + j];
+    } else {
+      double g = 0.0;
+      for (int j = 0; j < m.d; ++j) g += tot[4 + j];
+      grad[1] = g;
+    }
+    grad[1 + m.dl] = mtg_noise(m) * tot[2];
+    for (int q = m.f_off; q < m.n_params; ++q) grad[q] = 0.0;
+    // K_task[a, b] = sum_r F[a, r] F[b, r] + [a == b] v_a:  dF[c, r] += g_ab (F[b, r] [a == c] + F[a, r] [b == c])
+    for (int k = 0, p = 0; k < lay.T; ++k)
+      for (int l = k; l < lay.T; ++l, ++p) {
+        const int a = m.task[k], b = m.task[l];
+        const double g = gkt[p];
+        for (int r = 0; r < m.rank; ++r) {
+          grad[m.f_off + a * m.rank + r] += g * m.raw[m.f_off + b * m.rank + r];
+          grad[m.f_off + b * m.rank + r] += g * m.raw[m.f_off + a * m.rank + r];
+        }
+        if (a == b) grad[m.v_off + a] += m.vtask_exp ? g * exp(m.raw[m.v_off + a]) : g;
+      }
+  }
+  __syncthreads();
+  for (int q = tid; q < m.n_params; q += kWG) {
+    const double gp = grad[q];
+    m.raw_hist[(int64_t)iter * m.n_params + q] = m.raw[q];
+    m.grad[q] = gp;
+    int rg;
+    if (q == 0) rg = m.rg_scale;
+    else if (q <= m.dl) rg = m.rg_ls;
+    else if (q == 1 + m.dl) rg = m.rg_noise;
+    else if (q < m.v_off) rg = m.rg_factor;
+    else rg = m.rg_vtask;
+    if (!(do_update && rg)) continue;
+    const double prod = gp * m.prev[q];
+    const double sgn = prod > 0.0 ? m.eta_plus : (prod < 0.0 ? m.eta_minus : 1.0);
+    const double st = fmin(fmax(m.step[q] * sgn, m.step_min), m.step_max);
+    m.step[q] = st;
+    const double gg = (sgn == m.eta_minus) ? 0.0 : gp;
+    const double gs = gg > 0.0 ? 1.0 : (gg < 0.0 ? -1.0 : 0.0);
+    m.raw[q] = m.raw[q] + (-1.0) * (gs * st);
+    m.prev[q] = gg;
   }
 }
 
@@ -304,6 +580,99 @@ static int make_layout(const fgp_mt_layout* in, MtLay* lay) {
   lay->nmin = nmin;
   lay->L = L;
   return kOk;
+}
+
+static size_t mtg_align(size_t b) { return (b + 255) & ~(size_t)255; }
+
+static int to_mtfit(const fgp_mt_fit_desc* d, MtFit* m, int64_t* work_bytes) {
+  if (!d) return set_error(kErrInvalid, "fgp_mt_fit: null desc");
+  *m = MtFit{};
+  int rc = make_layout(&d->layout, &m->lay);
+  if (rc != kOk) return rc;
+  if (d->family != 0 && d->family != 1) return set_error(kErrInvalid, "fgp_mt_fit: family %d", d->family);
+  if (d->d < 1 || d->d > 6) return set_error(kErrUnsupported, "fgp_mt_fit: d = %d outside [1, 6]", d->d);
+  if (d->B < 1) return set_error(kErrInvalid, "fgp_mt_fit: B = %d", d->B);
+  if (d->T_all < m->lay.T || d->T_all > FGP_MT_MAX_TASKS || d->rank < 0 || d->rank > FGP_MT_MAX_TASKS)
+    return set_error(kErrInvalid, "fgp_mt_fit: T_all = %d, rank = %d", d->T_all, d->rank);
+  if (d->dl != 1 && d->dl != d->d) return set_error(kErrInvalid, "fgp_mt_fit: dl = %d", d->dl);
+  m->family = d->family;
+  m->d = d->d;
+  m->B = d->B;
+  m->T_all = d->T_all;
+  m->rank = d->rank;
+  m->dl = d->dl;
+  m->vtask_exp = d->vtask_exp;
+  m->P = m->lay.T * (m->lay.T + 1) / 2;
+  for (int k = 0; k < m->lay.T; ++k) {
+    if (d->task[k] < 0 || d->task[k] >= d->T_all) return set_error(kErrInvalid, "fgp_mt_fit: task[%d] = %d", k, d->task[k]);
+    m->task[k] = d->task[k];
+  }
+  for (int p = 0; p < m->P; ++p) m->spec_off[p] = d->spec_off[p];
+  m->rg_scale = d->rg_scale;
+  m->rg_ls = d->rg_ls;
+  m->rg_noise = d->rg_noise;
+  m->rg_factor = d->rg_factor;
+  m->rg_vtask = d->rg_vtask;
+  m->spec = static_cast<const double2*>(d->spectra);
+  m->y = static_cast<const double2*>(d->y);
+  m->raw = d->raw;
+  m->prev = d->rprop_prev;
+  m->step = d->rprop_step;
+  m->grad = d->grad_out;
+  m->loss_hist = d->loss_hist;
+  m->raw_hist = d->raw_hist;
+  m->gn = d->grad_norm;
+  m->gl = d->grad_logdet;
+  m->logdet_weight = d->logdet_weight;
+  m->mll_const = d->mll_const;
+  m->eta_minus = d->eta_minus;
+  m->eta_plus = d->eta_plus;
+  m->step_min = d->step_min;
+  m->step_max = d->step_max;
+  m->f_off = 2 + m->dl;
+  m->v_off = m->f_off + m->T_all * m->rank;
+  m->n_params = m->v_off + m->T_all;
+  const int64_t L = m->lay.L, rn = (int64_t)m->lay.R * m->lay.nmin;
+  const int64_t cover = std::max<int64_t>(std::max<int64_t>(L, (int64_t)m->B * rn), m->lay.nmin);
+  m->nblk = (int)std::min<int64_t>(1024, (cover + kWG - 1) / kWG);
+  // workspace: lams, fac, zinv, glp [L] double2; z [B][R nmin] double2; logdet [nmin]; dkt [L]; part
+  // [nblk][kMtgQ]; info
+  size_t off = 0;
+  const size_t o_lams = off; off += mtg_align(16 * (size_t)L);
+  const size_t o_fac = off; off += mtg_align(16 * (size_t)L);
+  const size_t o_zinv = off; off += mtg_align(16 * (size_t)L);
+  const size_t o_glp = off; off += mtg_align(16 * (size_t)L);
+  const size_t o_z = off; off += mtg_align(16 * (size_t)m->B * rn);
+  const size_t o_ld = off; off += mtg_align(8 * (size_t)m->lay.nmin);
+  const size_t o_dkt = off; off += mtg_align(8 * (size_t)L);
+  const size_t o_part = off; off += mtg_align(8 * (size_t)m->nblk * kMtgQ);
+  const size_t o_info = off; off += 256;
+  if (work_bytes) *work_bytes = (int64_t)off;
+  char* w = static_cast<char*>(d->work);
+  if (w) {
+    m->lams = reinterpret_cast<double2*>(w + o_lams);
+    m->fac = reinterpret_cast<double2*>(w + o_fac);
+    m->zinv = reinterpret_cast<double2*>(w + o_zinv);
+    m->glp = reinterpret_cast<double2*>(w + o_glp);
+    m->z = reinterpret_cast<double2*>(w + o_z);
+    m->logdet = reinterpret_cast<double*>(w + o_ld);
+    m->dkt = reinterpret_cast<double*>(w + o_dkt);
+    m->part = reinterpret_cast<double*>(w + o_part);
+    m->info = reinterpret_cast<int*>(w + o_info);
+  }
+  return kOk;
+}
+
+template <typename Fn>
+static int mtg_with_d(int d, Fn&& fn) {
+  switch (d) {
+    case 1: return fn(std::integral_constant<int, 1>{});
+    case 2: return fn(std::integral_constant<int, 2>{});
+    case 3: return fn(std::integral_constant<int, 3>{});
+    case 4: return fn(std::integral_constant<int, 4>{});
+    case 5: return fn(std::integral_constant<int, 5>{});
+    default: return fn(std::integral_constant<int, 6>{});
+  }
 }
 
 }  // namespace fgp
@@ -381,6 +750,47 @@ int fgp_mt_mll_grad(const fgp_mt_layout* layout, const void* zinv, const void* z
       static_cast<const double2*>(zinv), static_cast<const double2*>(z), grad_norm, grad_logdet, B, G, lay,
       static_cast<double2*>(grad_lams));
   return check_launch("k_mt_mll_grad");
+}
+
+
+int fgp_mt_fit_nparams(const fgp_mt_fit_desc* desc, int* n_params) {
+  MtFit m;
+  int rc = to_mtfit(desc, &m, nullptr);
+  if (rc != kOk) return rc;
+  if (!n_params) return set_error(kErrInvalid, "fgp_mt_fit_nparams: null n_params");
+  *n_params = m.n_params;
+  return kOk;
+}
+
+int fgp_mt_fit_work(const fgp_mt_fit_desc* desc, int64_t* bytes) {
+  MtFit m;
+  if (!bytes) return set_error(kErrInvalid, "fgp_mt_fit_work: null bytes");
+  return to_mtfit(desc, &m, bytes);
+}
+
+int fgp_mt_fit_run(const fgp_mt_fit_desc* desc, int iter0, int iters, int final_no_update, void* stream) {
+  MtFit m;
+  int rc = to_mtfit(desc, &m, nullptr);
+  if (rc != kOk) return rc;
+  if (!desc->work || !desc->spectra || !desc->y || !desc->raw || !desc->rprop_prev || !desc->rprop_step ||
+      !desc->grad_out || !desc->loss_hist || !desc->raw_hist)
+    return set_error(kErrInvalid, "fgp_mt_fit_run: null pointer");
+  if (iter0 < 0 || iters < 0) return set_error(kErrInvalid, "fgp_mt_fit_run: iter0 / iters");
+  hipStream_t st = (hipStream_t)stream;
+  const unsigned ge = (unsigned)((m.lay.L + kWG - 1) / kWG), gc = (unsigned)((m.lay.nmin + kWG - 1) / kWG);
+  return mtg_with_d(m.d, [&](auto dc) {
+    constexpr int D = decltype(dc)::value;
+    for (int it = 0; it < iters; ++it) {
+      const int upd = !(final_no_update && it == iters - 1);
+      k_mtg_lams<D><<<ge, kWG, 0, st>>>(m);
+      k_mtg_factor_grad<<<gc, kWG, 0, st>>>(m);
+      k_mtg_contract<D><<<(unsigned)m.nblk, kWG, 0, st>>>(m);
+      k_mtg_step<D><<<1, kWG, 0, st>>>(m, iter0 + it, upd);
+      const int r = check_launch("fgp_mt_fit_run");
+      if (r != kOk) return r;
+    }
+    return (int)kOk;
+  });
 }
 
 }  // extern "C"

@@ -756,8 +756,12 @@ class AbstractFastGP(torch.nn.Module):
         # (a device index tensor: index_select, not raw_hist[t] -- a 0-d index tensor is read back to the host)
         best_row = raw_hist.index_select(0, best_i.reshape(1))[0] if torch.is_tensor(best_i) else raw_hist[best_i]
         b_s, b_l, b_n = eng.split_raw(best_row)
+        restore = [("raw_scale", b_s), ("raw_lengthscales", b_l), ("raw_noise", b_n)]
+        if hasattr(eng, "split_task"):                  # the general multitask engine also learns the task kernel
+            b_f, b_v = eng.split_task(best_row)
+            restore += [("raw_factor_task_kernel", b_f), ("raw_noise_task_kernel", b_v)]
         with torch.no_grad():
-            for name, val in (("raw_scale", b_s), ("raw_lengthscales", b_l), ("raw_noise", b_n)):
+            for name, val in restore:
                 old = getattr(self, name)
                 setattr(self, name, torch.nn.Parameter(val.reshape(old.shape).clone(), requires_grad=old.requires_grad))
         self._cache = {k: v for k, v in self._cache.items() if not k[2]}    # keep data-only entries (ytilde, spectra)
@@ -772,8 +776,11 @@ class AbstractFastGP(torch.nn.Module):
         if hists["noise"]:
             data["noise_hist"] = self.tf_noise(nz_raw.reshape((-1,) + self.raw_noise.shape)).cpu()
         if hists["task_kernel"]:
-            data["task_kernel_hist"] = self.gram_matrix_tasks.detach().cpu()[None].expand(
-                (i + 1,) + self.gram_matrix_tasks.shape).clone()
+            if hasattr(eng, "task_kernel_rows"):
+                data["task_kernel_hist"] = eng.task_kernel_rows(raw_hist).detach().cpu()
+            else:
+                data["task_kernel_hist"] = self.gram_matrix_tasks.detach().cpu()[None].expand(
+                    (i + 1,) + self.gram_matrix_tasks.shape).clone()
         return data
 
     def _loss_generic(self, loss_metric, masks, cv_weights, d_out):

@@ -19,6 +19,7 @@ The GCV / CV losses and predictions requested WITH an autograd graph use a dense
 statement of the same blocks (torch.linalg on the device) -- they need gradients of functionals of
 the whole inverse that the structured kernels do not provide.  There is no CPU fallback.
 """
+import ctypes
 import math
 import os
 
@@ -26,8 +27,9 @@ import numpy as np
 import torch
 
 from . import ops
-from .fast_gp import _IDENTITY_TFS, AbstractFastGP, _Hyper, _as_size, _exp
-from .fit_engine import FusedMLL, mll_constant
+from . import _native as N
+from .fast_gp import _IDENTITY_TFS, AbstractFastGP, _Hyper, _as_size, _exp, _identity
+from .fit_engine import RPROP_ETAS, RPROP_STEPS, FusedMLL, mll_constant
 
 
 def _to_n_tensor(n):
@@ -337,7 +339,7 @@ class MultiTaskFastGP(AbstractFastGP):
         include/fgp_hip.h mt_tasks) covers: every task with the same n >= 16, at most 8 tasks, d <= 6, no
         parameter batch, the task kernel fixed (derivative-informed GPs fix it at 1, abstract_gp.py:146-150),
         exp parameter transforms, no adaptive nugget.  FGP_MT_FUSED=0 takes the generic autograd loop."""
-        if os.environ.get("FGP_MT_FUSED", "1")[:1] == "0":
+        if os.environ.get("FGP_MT_FUSED", "1")[:1] == "0" or os.environ.get("FGP_MT_GENERAL", "0")[:1] == "1":
             return False
         ns = self._ns
         n = ns[0]
@@ -348,8 +350,35 @@ class MultiTaskFastGP(AbstractFastGP):
             return False
         if any(self._tfs[k][1] is not _exp for k in ("scale", "lengthscales", "noise")):
             return False
+        T = self.num_tasks
+        if (T * (T + 1) // 2) * (1 << self.d) * n * 16 > MT_SPECTRA_CAP:
+            return False
         return tuple(self.raw_scale.shape) == (1,) and tuple(self.raw_noise.shape) == (1,) and \
             tuple(self.raw_lengthscales.shape) in ((1,), (self.d,))
+
+    def _mt_general_ok(self):
+        """The device-resident fit of the GENERAL case (fgp_mt_fit_run, ABI 14: MtGeneralEngine) -- the reference's
+        default multitask setting (abstract_gp.py:116-139: the task kernel F F^T + diag(v) learned), any n per
+        task (util.py:273-323), a data batch sharing the hyper-parameters: at most 16 active tasks, d <= 6, no
+        parameter batch, exp transforms for scale / lengthscales / noise, the identity for the task factor and
+        exp or the identity for the task noise, no adaptive nugget, pair spectra within MT_SPECTRA_CAP bytes."""
+        if os.environ.get("FGP_MT_FUSED", "1")[:1] == "0":
+            return False
+        lo_ns = [v for v in self._ns if v > 0]
+        if not lo_ns or self.d > 6 or len(lo_ns) > N.MT_MAX_TASKS or self.adaptive_nugget:
+            return False
+        if any(self._tfs[k][1] is not _exp for k in ("scale", "lengthscales", "noise")):
+            return False
+        if self.tf_factor_task_kernel is not _identity or self.tf_noise_task_kernel not in (_exp, _identity):
+            return False
+        T = self.num_tasks
+        if tuple(self.raw_scale.shape) != (1,) or tuple(self.raw_noise.shape) != (1,) or \
+                tuple(self.raw_lengthscales.shape) not in ((1,), (self.d,)) or \
+                self.raw_factor_task_kernel.dim() != 2 or tuple(self.raw_noise_task_kernel.shape) != (T,):
+            return False
+        srt = sorted(lo_ns, reverse=True)
+        spec = sum(srt[k] for k in range(len(srt)) for _ in range(k, len(srt))) * (1 << self.d) * 16
+        return spec <= MT_SPECTRA_CAP
 
     def _mt_spectra(self, n):
         """Pair spectra Phi^{kl}_S = ft(B^{kl}_S) [T (T+1)/2, 2^d, n] (pairs k <= l row-major): with the
@@ -378,8 +407,44 @@ class MultiTaskFastGP(AbstractFastGP):
             return self.ft(B).contiguous()
         return self._cached(("mt_spec", n), f, grad_sensitive=False)
 
+    def _pair_spectra(self, lo):
+        """Spectra of the sorted pairs of the general engine (fgp_mt_fit_desc.spectra): for sorted pair
+        (k, l), tasks a = active[k], b = active[l], the reference's lam_kl is get_lam(a, b, n_k) for a <= b and
+        get_lam(b, a, n_k).conj() otherwise (util.py:280-284), so Phi^{kl}_S = ft(B_S) (conjugated for a > b),
+        B_S the part products of get_k1parts(min, max, n_k) as in _mt_spectra.  Returns (flat complex128
+        tensor, offsets of every pair in complex elements)."""
+        def f():
+            d, dev = self.d, self.device
+            NS = 1 << d
+            ins = torch.tensor([[bool((S >> j) & 1) for j in range(d)] for S in range(NS)])
+            insd = ins.to(dev)
+            rows, offs, off = [], [], 0
+            for (k, l) in lo.pairs:
+                a, b = lo.active[k], lo.active[l]
+                t0, t1 = (a, b) if a <= b else (b, a)
+                nk = lo.nsrt[k]
+                parts = self.get_k1parts(t0, t1, nk)                              # [nk, p0, p1, d]
+                b0, b1 = self._derivs_h[t0], self._derivs_h[t1]
+                need = (b0[:, None, :] + b1[None, :, :]) > 0
+                valid = (~need[None] | ins[:, None, None, :]).all(-1)
+                cc = self.derivatives_coeffs[t0][:, None] * self.derivatives_coeffs[t1][None, :]
+                prod = torch.where(insd[:, None, None, None, :], parts[None], 1.0).prod(-1)
+                w = cc[None] * valid.to(device=dev, dtype=torch.float64)
+                B = (prod * w[:, None]).sum((-1, -2))                            # [NS, nk]
+                spec = self.ft(B).to(torch.complex128)
+                if a > b:
+                    spec = spec.conj()
+                rows.append(spec.resolve_conj().reshape(-1))
+                offs.append(off)
+                off += NS * nk
+            return torch.cat(rows).contiguous(), offs
+        return self._cached(("mt_pair_spec", tuple(lo.nsrt), tuple(lo.active)), f, grad_sensitive=False)
+
     def _fused_engine(self, iterations, lr, ysq=None, d_out=None):
-        """FusedMLL in multitask spectral mode (G = 1)."""
+        """FusedMLL in multitask spectral mode (G = 1); the general engine (MtGeneralEngine) outside its
+        domain (_mt_fused_ok: equal n, fixed task kernel)."""
+        if not self._mt_fused_ok():
+            return MtGeneralEngine(self, lr, min(iterations + 1, 64))
         n, T = self._ns[0], self.num_tasks
         yt = torch.stack([self.get_ytilde(k).reshape(n) for k in range(T)])
         ls = self.raw_lengthscales.detach()
@@ -658,12 +723,14 @@ class MultiTaskFastGP(AbstractFastGP):
         assert isinstance(stop_crit_wait_iterations, int) and stop_crit_wait_iterations > 0
         assert masks is None or isinstance(masks, torch.Tensor)
         loss_metric = loss_metric.upper()
-        if loss_metric == "MLL" and default_optimizer and masks is None and self._mt_fused_ok():
+        if loss_metric == "MLL" and default_optimizer and masks is None and (self._mt_fused_ok() or
+                                                                            self._mt_general_ok()):
+            learned_tk = self.raw_factor_task_kernel.requires_grad or self.raw_noise_task_kernel.requires_grad
             hists = dict(loss=store_hists or store_loss_hist,
                          scale=store_hists or (store_scale_hist and self.raw_scale.requires_grad),
                          lengthscales=store_hists or (store_lengthscales_hist and self.raw_lengthscales.requires_grad),
                          noise=store_hists or (store_noise_hist and self.raw_noise.requires_grad),
-                         task_kernel=store_hists)       # the task kernel is fixed on this path
+                         task_kernel=store_hists or (store_task_kernel_hist and learned_tk))
             return self._fit_fused(iterations, 1e-1 if lr is None else lr,
                                    (np.log(1 + stop_crit_improvement_threshold), stop_crit_wait_iterations), hists,
                                    verbose, verbose_indent)
@@ -953,3 +1020,109 @@ def _bind_family_classes():
 
 
 _bind_family_classes()
+
+
+MT_SPECTRA_CAP = 4 << 30      # bytes of pair spectra the device-resident multitask fits may hold
+
+
+class MtGeneralEngine(object):
+    """Device-resident MLL fit of a general multitask / derivative-informed GP (include/fgp_hip.h ABI 14,
+    fgp_mt_fit_run): the FusedMLL interface _fit_fused drives (run / loss_hist / raw_hist / split_raw), plus
+    the task-kernel parameters (split_task / task_kernel_rows).
+
+    raw = [raw_scale, raw_lengthscales (1 or d), raw_noise, raw_factor_task_kernel (T x r), raw_noise_task_kernel
+    (T)]; one loss over the data batch (norm summed over B vectors, logdet weighted d_out / numel(logdet) = B,
+    abstract_gp.py:252-260), gradients in closed form through the structured factor."""
+
+    def __init__(self, gp, lr, max_iters):
+        self.gp = gp
+        self.device = dev = gp.device
+        lo = _Layout(gp._ns)
+        self.lo = lo
+        spec, offs = gp._pair_spectra(lo)
+        self.spec = spec
+        T, d = gp.num_tasks, gp.d
+        Y = lo.pack([gp.get_ytilde(l).to(torch.complex128) for l in range(T)])
+        B = int(np.prod(tuple(Y.shape[:-1]))) if Y.dim() > 1 else 1
+        self.y = Y.reshape(B, -1).resolve_conj().contiguous()
+        self.B = B
+        dl = gp.raw_lengthscales.numel()
+        r = int(gp.raw_factor_task_kernel.shape[-1])
+        self.sizes = (1, dl, 1, T * r, T)
+        self.raw = torch.cat([gp.raw_scale.detach().reshape(-1), gp.raw_lengthscales.detach().reshape(-1),
+                              gp.raw_noise.detach().reshape(-1), gp.raw_factor_task_kernel.detach().reshape(-1),
+                              gp.raw_noise_task_kernel.detach().reshape(-1)]).to(dev, torch.float64).contiguous()
+        self.n_params = int(self.raw.numel())
+        self.prev = torch.zeros(self.n_params, dtype=torch.float64, device=dev)
+        self.step = torch.full((self.n_params,), float(lr), dtype=torch.float64, device=dev)
+        self.grad = torch.zeros(self.n_params, dtype=torch.float64, device=dev)
+        d_out = int(torch.tensor(tuple(gp.shape_batch)).prod()) if len(gp.shape_batch) else 1
+        desc = N.MtFitDesc()
+        desc.family, desc.d, desc.B = int(gp._FAMILY), int(d), B
+        desc.layout = lo.lay
+        for k, a in enumerate(lo.active):
+            desc.task[k] = int(a)
+        desc.T_all, desc.rank, desc.dl = int(T), r, int(dl)
+        desc.spectra = self.spec.data_ptr()
+        for p, o in enumerate(offs):
+            desc.spec_off[p] = int(o)
+        desc.y = self.y.data_ptr()
+        desc.raw = self.raw.data_ptr()
+        desc.vtask_exp = int(gp.tf_noise_task_kernel is _exp)
+        desc.rg_scale, desc.rg_ls, desc.rg_noise = (int(gp.raw_scale.requires_grad), int(gp.raw_lengthscales.requires_grad),
+                                                    int(gp.raw_noise.requires_grad))
+        desc.rg_factor, desc.rg_vtask = int(gp.raw_factor_task_kernel.requires_grad), int(gp.raw_noise_task_kernel.requires_grad)
+        desc.rprop_prev, desc.rprop_step, desc.grad_out = self.prev.data_ptr(), self.step.data_ptr(), self.grad.data_ptr()
+        desc.grad_norm = 0.5
+        desc.grad_logdet = 0.5 * d_out
+        desc.logdet_weight = float(d_out)
+        desc.mll_const = float(mll_constant(d_out, sum(gp._ns)))
+        desc.eta_minus, desc.eta_plus = RPROP_ETAS
+        desc.step_min, desc.step_max = RPROP_STEPS
+        wb = ctypes.c_int64(0)
+        N.call("fgp_mt_fit_work", desc, ctypes.byref(wb))
+        self.work = torch.empty((max(1, wb.value),), dtype=torch.uint8, device=dev)
+        desc.work = self.work.data_ptr()
+        npar = ctypes.c_int(0)
+        N.call("fgp_mt_fit_nparams", desc, ctypes.byref(npar))
+        assert npar.value == self.n_params
+        self.desc = desc
+        self.max_iters = 0
+        self.loss_hist = None
+        self.raw_hist = None
+        self.ensure_history(max_iters)
+
+    def ensure_history(self, iters):
+        if iters <= self.max_iters:
+            return
+        new_max = max(iters, 2 * self.max_iters, 16)
+        lh = torch.zeros((new_max, 1, 3), dtype=torch.float64, device=self.device)
+        rh = torch.zeros((new_max, self.n_params), dtype=torch.float64, device=self.device)
+        if self.loss_hist is not None:
+            lh[:self.max_iters] = self.loss_hist
+            rh[:self.max_iters] = self.raw_hist
+        self.loss_hist, self.raw_hist, self.max_iters = lh, rh, new_max
+        self.desc.loss_hist, self.desc.raw_hist = lh.data_ptr(), rh.data_ptr()
+
+    def run(self, iter0, iters, final_no_update=False):
+        self.ensure_history(iter0 + iters)
+        N.call("fgp_mt_fit_run", self.desc, int(iter0), int(iters), int(bool(final_no_update)),
+               N.stream_ptr(self.device))
+
+    def _cut(self, raw_vec, i):
+        o = sum(self.sizes[:i])
+        return raw_vec[..., o:o + self.sizes[i]]
+
+    def split_raw(self, raw_vec):
+        return self._cut(raw_vec, 0), self._cut(raw_vec, 1), self._cut(raw_vec, 2)
+
+    def split_task(self, raw_vec):
+        return self._cut(raw_vec, 3), self._cut(raw_vec, 4)
+
+    def task_kernel_rows(self, raw_rows):
+        """K_task = F F^T + diag(v) of every history row (util.py:157-162)."""
+        gp = self.gp
+        f, v = self.split_task(raw_rows)
+        F = gp.tf_factor_task_kernel(f.reshape((-1,) + tuple(gp.raw_factor_task_kernel.shape)))
+        vv = gp.tf_noise_task_kernel(v.reshape(-1, gp.num_tasks))
+        return torch.einsum("...il,...kl->...ik", F, F) + torch.diag_embed(vv)

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define FGP_ABI_VERSION 13
+#define FGP_ABI_VERSION 14
 
 #define FGP_OK 0
 #define FGP_ERR_INVALID (-1)     /* bad argument (shape, stride, null pointer) */
@@ -485,6 +485,49 @@ int fgp_mt_selinv(const fgp_mt_layout* layout, const void* factor, int64_t G, vo
  * problem b mod G); grad_lams [G][L] in torch's complex-gradient convention (dL/dRe + i dL/dIm). */
 int fgp_mt_mll_grad(const fgp_mt_layout* layout, const void* zinv, const void* z, const double* grad_norm,
                     const double* grad_logdet, int64_t B, int64_t G, void* grad_lams, void* stream);
+
+/* ABI 14 -- device-resident MLL fit of a GENERAL multitask / derivative-informed GP: any n per task (the
+ * structured blocks above), the task kernel K_task = F F^T + diag(v) learned or fixed, a data batch of B
+ * vectors sharing the hyper-parameters.  Replaces AbstractGP.fit's MLL loop (abstract_gp.py:152-306) with
+ * _FastInverseLogDetCache's lams / block inverse (util.py:275-370), its autograd gradient (:294, including
+ * raw_factor_task_kernel / raw_noise_task_kernel, abstract_gp.py:116-139) and torch.optim.Rprop
+ * (abstract_fast_gp.py:53-57).  Per iteration, with no host work:
+ *   lams[k, l] = K_task[a_k, a_l] (sqrt(n_l) lam_kl + noise [k == l]),  lam_kl = scale sum_S l^S Phi^{kl}_S
+ *   (the pair spectra: Phi^{kl}_S = fftbr / fwht of the part products of get_lam(a_k, a_l, n_k), conjugated
+ *   when a_k > a_l -- util.py:280-284), the structured factor / solve / selected inverse / gradient of each
+ *   frequency class, the contraction of dL/dlams with the spectra into the parameter gradients, and one
+ *   reduction + Rprop step.
+ * raw = [raw_scale, raw_lengthscales (dl), raw_noise, raw_factor_task_kernel (T_all x rank, row-major),
+ *        raw_noise_task_kernel (T_all)]: scale / lengthscales / noise exp-transformed, the factor identity,
+ *        the task noise exp (vtask_exp = 1) or identity (0).
+ * loss_hist [iters][3] (loss, term1 = sum_b norm_b, term2 = logdet_weight logdet), raw_hist [iters][n_params]
+ * (the parameters at which the row's loss was evaluated), grad_out [n_params] of the last iteration. */
+typedef struct fgp_mt_fit_desc {
+  int family, d, B;                   /* B data vectors (the reference's shape_batch, parameters unbatched) */
+  fgp_mt_layout layout;               /* active tasks sorted by n descending */
+  int task[FGP_MT_MAX_TASKS];         /* task index of active (sorted) task k */
+  int T_all, rank, dl;                /* num_tasks, columns of the task factor, lengthscale count (1 or d) */
+  const void* spectra;                /* complex128 pair spectra: sorted pair p = (k, l), k <= l row-major over
+                                         (k, l), at spec_off[p]: [2^d][n_k] */
+  int64_t spec_off[FGP_MT_MAX_TASKS * (FGP_MT_MAX_TASKS + 1) / 2];
+  const void* y;                      /* complex128 [B][R nmin]: ytilde of the sorted tasks, rows concatenated */
+  double* raw;
+  int vtask_exp;
+  int rg_scale, rg_ls, rg_noise, rg_factor, rg_vtask;   /* requires_grad of each parameter tensor */
+  double* rprop_prev;                 /* [n_params] Rprop state (torch.optim.Rprop: prev, step_size) */
+  double* rprop_step;
+  double* grad_out;
+  double* loss_hist;
+  double* raw_hist;
+  double grad_norm, grad_logdet;      /* dL/dnorm_b (1/2), dL/dlogdet (1/2 d_out / numel(logdet)) */
+  double logdet_weight, mll_const, eta_minus, eta_plus, step_min, step_max;
+  void* work;                         /* fgp_mt_fit_work bytes */
+} fgp_mt_fit_desc;
+
+int fgp_mt_fit_nparams(const fgp_mt_fit_desc* desc, int* n_params);
+int fgp_mt_fit_work(const fgp_mt_fit_desc* desc, int64_t* bytes);
+/* iterations iter0 .. iter0 + iters - 1 (history rows); with final_no_update the last one evaluates only */
+int fgp_mt_fit_run(const fgp_mt_fit_desc* desc, int iter0, int iters, int final_no_update, void* stream);
 
 #ifdef __cplusplus
 }

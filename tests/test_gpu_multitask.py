@@ -152,19 +152,24 @@ def test_multitask_predictions(name):
     assert torch.allclose(pc[r0, r0][:, r1, r1], gp.post_var(xd)) and (gp.post_var(xd) >= 0).all()
 
 
-@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("path", ["fused", "general", "generic"])
 @pytest.mark.parametrize("name", MT_NAMES)
-def test_multitask_fit_trajectory(name, fused, monkeypatch):
-    """fit(store_hists) against the reference's trajectory: through the device-resident multitask fit
-    (k_mt_spec_iter + the spectral step) where it applies (equal n, fixed task kernel), and through the
-    generic autograd loop (FGP_MT_FUSED=0)."""
+def test_multitask_fit_trajectory(name, path, monkeypatch):
+    """fit(store_hists) against the reference's trajectory: through the device-resident multitask fits --
+    "fused" (k_mt_spec_iter + the spectral step: equal n, fixed task kernel) and "general" (fgp_mt_fit_run,
+    ABI 14: any n per task, the learned task kernel of the reference's default multitask setting; forced on
+    the equal-n fixtures too with FGP_MT_GENERAL=1) -- and through the generic autograd loop
+    (FGP_MT_FUSED=0)."""
     g = load_golden(name)
     if name in REF_INVERSE_ERROR:
         pytest.skip("the reference's own inverse is inaccurate for this fixture (REF_INVERSE_ERROR)")
-    monkeypatch.setenv("FGP_MT_FUSED", "1" if fused else "0")
+    monkeypatch.setenv("FGP_MT_FUSED", "0" if path == "generic" else "1")
+    monkeypatch.setenv("FGP_MT_GENERAL", "1" if path == "general" else "0")
     gp = product_mt(g)
-    if fused and not gp._mt_fused_ok():
-        pytest.skip("outside the device-resident multitask fit's domain (unequal n / learned task kernel)")
+    if path == "fused" and not gp._mt_fused_ok():
+        pytest.skip("outside the k_mt_spec_iter fit's domain (unequal n / learned task kernel): the general path")
+    if path == "general":
+        assert gp._mt_general_ok() and not gp._mt_fused_ok()
     its = int(g["fit_iterations"])
     data = gp.fit(iterations=its, store_hists=True, verbose=0, stop_crit_wait_iterations=its + 5)
     assert data["iterations"] == its
@@ -198,6 +203,37 @@ def test_multitask_fused_loss_and_gradient(name):
         assert abs(loss - float(g["loss"])) <= 2e-7 * abs(float(g["loss"]))
     else:       # the oracle's (dense, accurate) values at the blocks' conditioning
         assert abs(loss - lo.item()) <= 1e-6 * abs(lo.item())
+
+
+@pytest.mark.parametrize("name", MT_NAMES)
+def test_multitask_general_engine_loss_and_gradient(name, monkeypatch):
+    """One iteration of the general device-resident multitask fit (fgp_mt_fit_run, evaluation only) at the
+    fixture's initial parameters: loss and the gradient of EVERY raw parameter -- including the task factor
+    and task noise the reference learns by default (abstract_gp.py:116-139) -- against the dense oracle's
+    autograd and, where its inverse is accurate, the reference's own values."""
+    monkeypatch.setenv("FGP_MT_GENERAL", "1")
+    g = load_golden(name)
+    gp = product_mt(g)
+    assert gp._mt_general_ok()
+    eng = gp._fused_engine(1, 0.1)
+    eng.run(0, 1, final_no_update=True)
+    loss = float(eng.loss_hist[0, 0, 0])
+    grad = eng.grad.cpu()
+    o = make_oracle(g)
+    lo = o.mll_loss()
+    names = ["raw_scale", "raw_lengthscales", "raw_noise", "raw_factor_task_kernel", "raw_noise_task_kernel"]
+    parts = dict(zip(names, list(eng.split_raw(grad)) + list(eng.split_task(grad))))
+    gnames = [str(s) for s in g["grad_names"]]
+    go = torch.autograd.grad(lo, [getattr(o, nm) for nm in gnames])
+    tol = REF_INVERSE_ERROR.get(name)
+    assert abs(loss - lo.item()) <= (1e-9 if tol is None else 1e-6) * abs(lo.item())
+    for nm, b in zip(gnames, go):
+        a = parts[nm].reshape(b.shape)
+        assert rel_err(a, b) < (1e-7 if tol is None else 1e-5), nm
+    if tol is None:
+        assert abs(loss - float(g["loss"])) <= 2e-7 * abs(float(g["loss"]))
+        for nm in gnames:
+            assert rel_err(parts[nm].reshape(g["grad_" + nm].shape), g["grad_" + nm]) < 2e-7, nm
 
 
 def _paper_gp(family, d, T, n, seed=7):

@@ -51,7 +51,8 @@ def test_struct_layouts_match_header(tmp_path):
         pytest.skip("gcc not available")
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "fgp_hip.h"', "int main(void) {"]
     expect = []
-    for cname, cls in (("fgp_nll_desc", N.NllDesc), ("fgp_fit_desc", N.FitDesc), ("fgp_pred_desc", N.PredDesc)):
+    for cname, cls in (("fgp_nll_desc", N.NllDesc), ("fgp_fit_desc", N.FitDesc), ("fgp_pred_desc", N.PredDesc),
+                       ("fgp_mt_layout", N.MtLayout), ("fgp_mt_fit_desc", N.MtFitDesc)):
         lines.append('printf("%%zu\\n", sizeof(%s));' % cname)
         expect.append(ctypes.sizeof(cls))
         for fname, _ in cls._fields_:

@@ -136,6 +136,7 @@ struct Args {
   int nblk, cpb;         // blocks, chunks per block
   unsigned* counters;    // [0] head, [1] done (DYN)
   unsigned long long* stamps;   // [grid][2] start / end (optional)
+  int* xcc;                     // [grid] XCC id of the workgroup (with stamps)
 };
 
 // 20 wave-instructions of 1 KiB per chunk: j < 16 spectra (chunk q at basis + q NS 64), j >= 16 Y; wave w
@@ -262,7 +263,10 @@ __global__ __launch_bounds__(256, WPC) void k_lab(Args a) {
       }
     }
   }
-  if (a.stamps && threadIdx.x == 0) a.stamps[blockIdx.x * 2 + 1] = wall_clock64();
+  if (a.stamps && threadIdx.x == 0) {
+    a.stamps[blockIdx.x * 2 + 1] = wall_clock64();
+    a.xcc[blockIdx.x] = __builtin_amdgcn_s_getreg((3 << 11) | 20);   // HW_REG_XCC_ID[3:0]
+  }
 }
 
 template <typename F>
@@ -302,6 +306,9 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&dp, (size_t)G * NQ * 8192 * 8));
   CK(hipMalloc(&dc, 64));
   CK(hipMalloc(&ds, 8192 * 2 * 8));
+  int* dx;
+  CK(hipMalloc(&dx, 8192 * 4));
+  a.xcc = dx;
   CK(hipMemset(dc, 0, 64));
   CK(hipMemcpy(db, hb.data(), nb * 8, hipMemcpyHostToDevice));
   CK(hipMemcpy(dy, hy.data(), ny * 8, hipMemcpyHostToDevice));
@@ -339,19 +346,32 @@ int main(int argc, char** argv) {
     kern<<<grid, 256, shm>>>(a);
     CK(hipDeviceSynchronize());
     std::vector<unsigned long long> st((size_t)grid * 2);
+    std::vector<int> xc(grid);
     CK(hipMemcpy(st.data(), ds, st.size() * 8, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(xc.data(), dx, grid * 4, hipMemcpyDeviceToHost));
     unsigned long long t0 = ~0ull, t1 = 0;
-    std::vector<double> dur(grid);
+    std::vector<double> dur(grid), endt(grid);
+    std::vector<std::vector<double>> per(8);
+    for (int b = 0; b < grid; ++b) t0 = std::min(t0, st[2 * b]);
     for (int b = 0; b < grid; ++b) {
-      t0 = std::min(t0, st[2 * b]);
       t1 = std::max(t1, st[2 * b + 1]);
       dur[b] = (st[2 * b + 1] - st[2 * b]) / 100.0;
+      endt[b] = (st[2 * b + 1] - t0) / 100.0;
+      per[xc[b] & 7].push_back(endt[b]);
     }
     std::sort(dur.begin(), dur.end());
+    std::sort(endt.begin(), endt.end());
+    char xs[256];
+    int o = 0;
+    for (int x = 0; x < 8; ++x) {
+      std::sort(per[x].begin(), per[x].end());
+      o += snprintf(xs + o, sizeof xs - o, "%s%.1f", x ? "," : "", per[x].empty() ? 0.0 : per[x].back());
+    }
     printf("{\"variant\": \"%s\", \"ring\": %d, \"grid\": %d, \"cpb\": %d, \"us\": %.2f, \"GBps\": %.0f, "
-           "\"span_us\": %.2f, \"dur_p10\": %.2f, \"dur_p50\": %.2f, \"dur_p90\": %.2f, \"check_rel\": %.3g}\n",
+           "\"span_us\": %.2f, \"dur_p10\": %.2f, \"dur_p50\": %.2f, \"dur_p90\": %.2f, \"end_p50\": %.2f, "
+           "\"end_p90\": %.2f, \"xcc_last_end\": [%s], \"check_rel\": %.3g}\n",
            name, ring, grid, cpb, us, (nb + ny) * 8.0 / us / 1e3, (t1 - t0) / 100.0, dur[grid / 10], dur[grid / 2],
-           dur[grid * 9 / 10], err);
+           dur[grid * 9 / 10], endt[grid / 2], endt[grid * 9 / 10], xs, err);
     fflush(stdout);
   };
   // the current structure: fixed block per workgroup, 512 x 16 chunks, pointer arrays, 2-slot ring
