@@ -56,6 +56,8 @@ def parse():
     p.add_argument("--no-secondary", dest="secondary", action="store_false",
                    help="skip the secondary BASELINE configs (C2, C3, C5) reported under 'secondary'")
     p.add_argument("--c5-outputs", type=int, default=512)
+    p.add_argument("--no-multitask", dest="multitask", action="store_false",
+                   help="skip the docs/examples/multitask per-step timings reported under 'multitask'")
     p.add_argument("--no-paper", dest="paper", action="store_false",
                    help="skip the probnum25 paper's n=2^10 per-step timings reported under 'paper'")
     return p.parse_args()
@@ -393,6 +395,49 @@ def paper_configs(F, device, log2n=10, iterations=5000, warm=True):
                             "paper_s_per_step": PAPER_S_PER_STEP[name][col],
                             "class": type(gp).__name__})
                 del gp
+    return out
+
+
+def multitask_configs(F, device, iterations=40):
+    """The reference's default multitask setting (docs/examples/multitask/fgp_lattice.ipynb cells 3-4: d = 1,
+    three tasks -- low / high fidelity Ackley and a cosine sum -- at n = [2^6, 2^3, 2^8], the task kernel
+    F F^T + diag(v) LEARNED, abstract_gp.py:116-139) and the same at 16x the points, each fitted `iterations`
+    Rprop steps (early stopping off) through the device-resident general multitask fit (fgp_mt_fit_run) and
+    through the generic autograd loop (FGP_MT_FUSED=0): time per optimisation step = fit wall time /
+    iterations."""
+    fs = [lambda x: f_ackley(x, c=0), lambda x: f_ackley(x), lambda x: torch.cos(2 * np.pi * x).sum(1)]
+    out = []
+    for scale in (1, 16):
+        ns = [64 * scale, 8 * scale, 256 * scale]
+        row = {"workload": "docs/examples/multitask: FastGPLattice d=1, 3 tasks, n=%s, learned task kernel" % ns,
+               "iterations": iterations}
+        for path in ("device", "generic"):
+            old = os.environ.get("FGP_MT_FUSED")
+            os.environ["FGP_MT_FUSED"] = "1" if path == "device" else "0"
+            try:
+                times = []
+                for rep in range(2 if path == "device" else 1):       # the first device pass loads the kernels
+                    gp = F.FastGPLattice(1, seed_for_seq=7, num_tasks=3, device=device)
+                    xs = gp.get_x_next(n=ns)
+                    gp.add_y_next([fs[i](xs[i]) for i in range(3)])
+                    torch.cuda.synchronize()
+                    t0 = time.perf_counter()
+                    data = gp.fit(iterations=iterations, verbose=0, stop_crit_wait_iterations=iterations + 1,
+                                  store_loss_hist=True)
+                    torch.cuda.synchronize()
+                    times.append((time.perf_counter() - t0) / max(1, int(data["iterations"])))
+                row[path + "_s_per_step"] = min(times)
+                row[path + "_final_loss"] = float(-data["loss_hist"][-1])
+                if path == "device":
+                    row["device_path"] = "general (fgp_mt_fit_run)" if gp._mt_general_ok() and not gp._mt_fused_ok() \
+                        else ("k_mt_spec_iter" if gp._mt_fused_ok() else "generic")
+            finally:
+                if old is None:
+                    os.environ.pop("FGP_MT_FUSED", None)
+                else:
+                    os.environ["FGP_MT_FUSED"] = old
+        row["speedup"] = row["generic_s_per_step"] / row["device_s_per_step"]
+        out.append(row)
     return out
 
 
@@ -853,6 +898,9 @@ def main():
                            "step, s; the paper's hardware is unstated) with the protocol of probnum25_paper.ipynb "
                            "cell 15 (fit wall time / iterations, reference fit defaults)",
                  "configs": paper_configs(F, device)}
+    multitask = None
+    if args.multitask and world == 1:
+        multitask = multitask_configs(F, device)
     if rank == 0:
         out = {"metric": "GP fit+predict points/sec at n=2^20 fp64; achieved HBM GB/s vs roofline",
                "value": value, "unit": "points/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -863,7 +911,7 @@ def main():
                                       (args.log2n, d, args.shifts, args.fit_iters, args.n_mean, args.n_var),
                           "global_shifts": args.shifts * world, "parallelism": "replicas%d" % world},
                "roofline": roof, "cpu_baseline": cpu, "phases_ms": phases, "secondary": secondary,
-               "paper": paper}
+               "paper": paper, "multitask": multitask}
         print(json.dumps(out))
     if dist:
         tdist.destroy_process_group()
