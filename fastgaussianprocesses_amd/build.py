@@ -17,6 +17,8 @@ OBJ_DIR = os.path.join(LIB_DIR, "obj")
 SOURCES = ["fgp_runtime.hip", "fgp_transforms.hip", "fgp_nll.hip", "fgp_nll_re.hip", "fgp_predict.hip", "fgp_multitask.hip", "fgp_points.hip",
            "fgp_spectral.hip"]
 HEADERS = ["fgp_common.h", "fgp_runtime.h", "fgp_nll.h"]
+# gfx950 (MI355X) only: the kernels' inter-workgroup hand-offs rely on gfx9 store counting (csrc/fgp_spectral.hip
+# refuses to compile for other families)
 ARCH = os.environ.get("FGP_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 

@@ -23,6 +23,14 @@
 
 #include "fgp_nll.h"
 
+// The last-arriver hand-offs of this file (k_spec_tile, k_spec_step_many) publish sc1 partial stores with a
+// relaxed agent-scope add after `s_waitcnt vmcnt(0)`: on gfx9 (CDNA) vmcnt also counts the stores, so the
+// add cannot overtake them (MI355X_MICROARCH.md hand-off row 1).  gfx10+ counts stores separately (vscnt):
+// building for such a target needs a release fence before the add.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__GFX9__)
+#error "fgp_spectral.hip: the relaxed sc1 hand-offs assume gfx9 (CDNA) store counting -- build for gfx950"
+#endif
+
 namespace fgp {
 
 // P(l) = sum_{S < 2^D} l^S phi[S] (bit j of S = dimension j) and dp[j] = dP/dl_j, by recursion on the

@@ -45,6 +45,8 @@ def _identity(x):
 
 _DEFAULT_TFS = (_log, _exp)
 _IDENTITY_TFS = (_identity, _identity)     # module-level functions: a GP pickles (torch.save) whole
+SPEC_POST_VAR_MAX_N = 4096            # test points per fgp_spec_post_var call (include/fgp_hip.h)
+SPEC_POST_VAR_WORK = 1 << 30          # bytes of row products + row spectra per slice of test points
 
 
 def _as_size(s):
@@ -1016,18 +1018,29 @@ class AbstractFastGP(torch.nn.Module):
         d, Nt = self.d, x.size(0)
         self._ensure_points(n)
         xb = self._xb[:n]
-        rho = torch.empty((Nt, 2 ** d, n), dtype=torch.float64, device=self.device)
-        rho[:, 0] = 1.0
-        for t in range(Nt):
-            parts = ops.lattice_parts(xb, x[t], self._alphas)          # [d, n]: part_j(x_i, x_t)
+        # test points in slices: fgp_spec_post_var takes at most SPEC_POST_VAR_MAX_N points per call, and the
+        # row products rho [Nt, 2^d, n] float64 + their spectra psi complex128 (24 2^d n bytes per point) stay
+        # within SPEC_POST_VAR_WORK bytes
+        per = max(1, min(SPEC_POST_VAR_MAX_N, SPEC_POST_VAR_WORK // (24 * (2 ** d) * n)))
+        raws = (self.raw_scale.detach().reshape(-1), self.raw_lengthscales.detach().reshape(-1, self.raw_lengthscales.shape[-1]),
+                self.raw_noise.detach().reshape(-1))
+        part0 = self._part_at_zero().tolist()
+        outs = []
+        for t0 in range(0, Nt, per):
+            xs = x[t0:t0 + per]
+            Nc = xs.size(0)
+            parts = torch.stack([ops.lattice_parts(xb, xs[t], self._alphas) for t in range(Nc)])   # [Nc, d, n]
+            rho = torch.empty((Nc, 2 ** d, n), dtype=torch.float64, device=self.device)
+            rho[:, 0] = 1.0
             for S in range(1, 2 ** d):
                 j = S.bit_length() - 1
-                torch.mul(rho[t, S ^ (1 << j)], parts[j], out=rho[t, S])
-        psi = ops.fftbr_raw(rho, stable=True)
-        return spec_post_var(self.raw_scale.detach().reshape(-1),
-                             self.raw_lengthscales.detach().reshape(-1, self.raw_lengthscales.shape[-1]),
-                             self.raw_noise.detach().reshape(-1), G, n, basis, psi.contiguous(),
-                             self._part_at_zero().tolist())
+                torch.mul(rho[:, S ^ (1 << j)], parts[:, j], out=rho[:, S])
+            del parts
+            psi = ops.fftbr_raw(rho, stable=True)
+            del rho
+            outs.append(spec_post_var(*raws, G, n, basis, psi.contiguous(), part0))
+            del psi
+        return torch.cat(outs, 1)
 
     def _kdiag(self, x):
         """K(x, x) (zero distance parts)."""

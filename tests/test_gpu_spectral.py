@@ -243,6 +243,26 @@ def test_spectral_post_var_equals_per_row_transforms(m, d, G, monkeypatch):
         assert bool((v_spec >= 0).all())
 
 
+def test_spectral_post_var_slices_test_points(monkeypatch):
+    """fgp_spec_post_var takes at most 4096 test points per call and the row products / spectra are sized per
+    slice: slices of 2 points (forced through fast_gp.SPEC_POST_VAR_MAX_N) give the unsliced
+    result bit for bit, and the per-row transforms (FGP_SPEC_POST_VAR=0) to 1e-10 K(x,x)."""
+    from fastgaussianprocesses_amd import fast_gp
+    monkeypatch.setenv("FGP_FIT_PATH", "spectral")
+    G, d, m = 16, 2, 17
+    gp, _, _ = _gp("lattice", d, m, shape_batch=[G], shape_scale=[G, 1], shape_lengthscales=[G, d])
+    x = torch.rand((7, d), generator=torch.Generator().manual_seed(3)).to(DEV)
+    whole = gp._post_var_spectral(x, 2 ** m, G)
+    monkeypatch.setattr(fast_gp, "SPEC_POST_VAR_MAX_N", 2)
+    sliced = gp._post_var_spectral(x, 2 ** m, G)
+    assert torch.equal(whole, sliced)
+    monkeypatch.setenv("FGP_SPEC_POST_VAR", "0")
+    gp._cache = {}
+    v_row = gp.post_var(x).reshape(G, -1)
+    kxx = gp._kdiag(x).detach().reshape(G, 1)
+    assert float(((sliced - v_row).abs() / kxx).max()) <= 1e-10
+
+
 @pytest.mark.parametrize("m,rows", [(17, 3), (18, 2), (20, 1)])
 def test_real_factor_inverse_reads_half_of_hermitian_input(m, rows):
     """fgp_ifftbr_real_rf (ABI 13) reads only k <= n/2 of its Hermitian input (ft of real data) and even
