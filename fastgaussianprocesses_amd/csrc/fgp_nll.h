@@ -614,6 +614,10 @@ int spec_counters_offset(const Nll& a, int64_t* off, int* count);
 RpState spec_scratch_state(const Nll& a, int par);
 // the deferred step of a fused spectral run's last iteration (after its last k_spec_tile launch)
 int launch_spec_finish_step(const Nll& a, const FitFuse& fz, hipStream_t st);
+// the whole fit of one small spectral problem in one launch (fgp_fit_persist): geometry / applicability, launch
+int spec_persist_geometry(const Nll& a, int* W, int* bpw, size_t* shm);
+int launch_spec_persist(const Nll& a, const Fit& f, int iters, double logtol, int wait_max, unsigned* counter, int* out,
+                        hipStream_t st);
 int launch_spec_lam(const Nll& a, hipStream_t st);    // lambda of the current parameters into grad_lam
 int launch_spec_inv_eig(const Nll& a, double* wa, hipStream_t st);
 constexpr int kSpvKpl = 16;   // fgp_spec_post_var: frequencies per lane of a wave's block (64 kSpvKpl per block)

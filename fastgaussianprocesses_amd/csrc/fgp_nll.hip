@@ -1635,6 +1635,7 @@ int fgp_nll_partials_len(const fgp_nll_desc* desc, int64_t* len) {
     int cnt;
     spec_counters_offset(a, &off, &cnt);
     *len = std::max<int64_t>(*len, off + cnt + 1);
+    *len = std::max<int64_t>(*len, 2 * (int64_t)a.G * a.nq * a.nb);   // fgp_fit_persist's two partial parities
   }
   return kOk;
 }
@@ -1787,6 +1788,37 @@ int fgp_fit_step(const fgp_nll_desc* nll, const fgp_fit_desc* fit, int iter, int
   if (rc == kOk) rc = check_per_problem(a, f);
   if (rc != kOk) return rc;
   return fit_step(a, f, iter, do_update, (hipStream_t)stream);
+}
+
+int fgp_fit_persist_ok(const fgp_nll_desc* nll, int* ok) {
+  if (!ok) return set_error(kErrInvalid, "fgp_fit_persist_ok: null ok");
+  *ok = 0;
+  fgp_nll_desc probe = *nll;
+  static const double dummy = 0.0;
+  if (!probe.partials) probe.partials = const_cast<double*>(&dummy);
+  if (!probe.ysq) probe.ysq = &dummy;
+  if (!probe.raw) probe.raw = &dummy;
+  Nll a;
+  int rc = to_nll(&probe, a);
+  if (rc != kOk) return rc;
+  int W, bpw;
+  size_t shm;
+  *ok = spec_persist_geometry(a, &W, &bpw, &shm) == kOk ? W : 0;
+  return kOk;
+}
+
+int fgp_fit_persist(const fgp_nll_desc* nll, const fgp_fit_desc* fit, int iters, double logtol, int wait_max, void* ctrl,
+                    void* stream) {
+  Nll a;
+  Fit f;
+  int rc = to_nll(nll, a);
+  if (rc == kOk) rc = to_fit(fit, f);
+  if (rc != kOk) return rc;
+  if (!ctrl) return set_error(kErrInvalid, "fgp_fit_persist: null ctrl");
+  if (iters < 0 || wait_max < 1) return set_error(kErrInvalid, "fgp_fit_persist: iters / wait_max");
+  unsigned* counter = static_cast<unsigned*>(ctrl);
+  return launch_spec_persist(a, f, iters, logtol, wait_max, counter, reinterpret_cast<int*>(counter + 1),
+                             (hipStream_t)stream);
 }
 
 int fgp_fit_run(const fgp_nll_desc* nll, const fgp_fit_desc* fit, int iter0, int iters, int final_no_update,

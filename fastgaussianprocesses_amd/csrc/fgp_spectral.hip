@@ -132,7 +132,7 @@ __device__ __forceinline__ void spec_values(const SpecAcc<D>& acc, double* v) {
 // corrections reload their spectra and Y from global memory, so every kernel computes the same values.
 template <int D, bool NET>
 __device__ __forceinline__ void spec_block_partials(const Nll& a, const Hyp& h, int g, int blk, double rootn, double wl,
-                                                    const SpecAcc<D>& acc, bool sc1) {
+                                                    const SpecAcc<D>& acc, bool sc1, double* pbase) {
   constexpr int NS = 1 << D, NV = 4 + D;
   const int lane = threadIdx.x & 63;
   double v[NV];
@@ -174,7 +174,7 @@ __device__ __forceinline__ void spec_block_partials(const Nll& a, const Hyp& h, 
     for (int j = 0; j < D; ++j) v[4 + j] *= gsc * h.ls[j];
 #pragma unroll
     for (int q = 0; q < NV; ++q) {
-      double* dst = part_ptr(a, g, q, blk);
+      double* dst = pbase + ((int64_t)g * a.nq + q) * a.nb + blk;     // part_ptr's layout from this base
       if (sc1) __hip_atomic_store(dst, v[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       else *dst = v[q];
     }
@@ -234,7 +234,7 @@ __global__ __launch_bounds__(kWG) void k_spec_iter(Nll a) {
     }
 #pragma unroll
     for (int p = 0; p < PPW; ++p)
-      if (on[p]) spec_block_partials<D, NET>(a, h[p], g0 + p, kb, rootn, wl, acc[p], false);
+      if (on[p]) spec_block_partials<D, NET>(a, h[p], g0 + p, kb, rootn, wl, acc[p], false, a.partials);
   }
   stamp_end(a);
 }
@@ -313,7 +313,8 @@ __device__ __forceinline__ void spec_level2(const Nll& a, int par, double* tot) 
 template <int D>
 __device__ __forceinline__ void spec_finish(const Nll& a, const Fit& f, const double* tot, int g0, int cnt, int iter,
                                             int do_update, const RpState& in, const RpState& out, bool write,
-                                            double* newraw) {
+                                            double* newraw, int state_write = -1) {
+  const bool wstate = state_write < 0 ? write : state_write != 0;   // the new state to `out` (default: with write)
   const int i = threadIdx.x >> 4, k = threadIdx.x & 15;
   if (i >= cnt) return;
   const int g = g0 + i;
@@ -364,7 +365,7 @@ __device__ __forceinline__ void spec_finish(const Nll& a, const Fit& f, const do
     const double gs = nprev > 0.0 ? 1.0 : (nprev < 0.0 ? -1.0 : 0.0);
     nraw = raw_p + (-1.0) * (gs * nstep);
   }
-  if (write) {
+  if (wstate) {
     out.raw[p] = nraw;
     out.step[p] = nstep;
     out.prev[p] = nprev;
@@ -527,6 +528,155 @@ __global__ __launch_bounds__(kWG) void k_spec_finish_step(Nll a, FitFuse fz) {
   spec_finish<D>(a, fz.f, tot, 0, a.G, fz.iter - 1, fz.do_update, fz.sin, fz.sout, true, nullptr);
 }
 
+// ---------------------------------------------------------------- the whole fit of ONE small problem in one launch
+// (fgp_fit_persist, ABI 14).  A single GP whose spectra and Y fit the LDS of kPersistMaxW workgroups (C2 / C3 at
+// n = 2^16, the probnum25 paper's n = 2^10): workgroup b loads the blocks [b bpw, (b + 1) bpw) of k_spec_iter's
+// geometry into LDS once, then every Rprop iteration is
+//   block partials (spec_terms / spec_block_partials: k_spec_iter's arithmetic) -> sc1 stores -> grid barrier
+//   (one agent-scope counter, MI355X_MICROARCH.md hand-off row 1; a bounded poll) -> every workgroup sums the
+//   partials in the two-level order of k_spec_reduce_step and applies the same Rprop step to its own LDS copy of
+//   the state -> AbstractGP.fit's early-stopping rule (abstract_gp.py:276-284) evaluated on the same loss values
+// so the trajectory is the multi-launch fit's bit for bit, without a launch per iteration.  Workgroup 0 writes
+// the histories and the final state; out[0] = the last iteration, out[1] = 1 if a barrier poll gave up.
+constexpr int kPersistMaxW = 64;
+constexpr int kPersistLdsMax = 96 * 1024;
+constexpr long long kPersistPollMax = 1ll << 22;
+
+template <int D, bool NET>
+__global__ __launch_bounds__(kWG) void k_spec_persist(Nll a, Fit f, int iters, double logtol, int wait_max, int bpw,
+                                                      unsigned* counter, int* out) {
+  constexpr int NS = 1 << D, NQ = 4 + D, MAXG = kSpecBlocks / kSpecGroup;
+  extern __shared__ double lds[];                  // [bpw][kpl][NS + 1][64] spectra + Y of this workgroup's blocks
+  __shared__ double st_raw[kSpecScratch], st_prev[kSpecScratch], st_step[kSpecScratch];
+  __shared__ double gsum[NQ * MAXG];
+  __shared__ double tot[NQ];
+  __shared__ double es[3];                         // early stopping: best, save, waited
+  __shared__ int brk_s, fail_s;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int W = gridDim.x, kpl = a.spec_kpl, np = spec_nparams(a), ng = spec_groups(a);
+  const int64_t main = a.spec_main, B = 64 * (int64_t)kpl;
+  const int blk0 = (int)blockIdx.x * bpw;
+  // the blocks' spectra and Y into LDS (chunked layouts: chunk q of the spectra at q NS 64, Y at q 64 for G = 1)
+  const int per_blk = kpl * (NS + 1) * 64;
+  for (int e = tid; e < bpw * per_blk; e += kWG) {
+    const int t = e / per_blk, r = e - t * per_blk, c = r / ((NS + 1) * 64), rr = r - c * (NS + 1) * 64;
+    const int row = rr >> 6, col = rr & 63;
+    const int64_t q = ((int64_t)(blk0 + t) * kpl + c);           // chunk
+    double v = 0.0;
+    if (blk0 + t < a.nb && q * 64 + col < a.spec_KS)
+      v = row < NS ? a.basis[(q * NS + row) * 64 + col] : a.ysq[q * 64 + col];
+    lds[e] = v;
+  }
+  for (int p = tid; p < np; p += kWG) {
+    st_raw[p] = f.raw[p];
+    st_prev[p] = f.prev[p];
+    st_step[p] = f.step[p];
+  }
+  if (tid == 0) {
+    es[0] = INFINITY;
+    es[1] = INFINITY;
+    es[2] = 0.0;
+    brk_s = 0;
+    fail_s = 0;
+  }
+  __syncthreads();
+  const double rootn = sqrt((double)((int64_t)1 << a.log2n)), wl = a.logdet_weight;
+  const RpState st{st_raw, st_prev, st_step};
+  const int64_t psize = (int64_t)a.nq * a.nb;      // one parity's partials (G = 1)
+  for (int it = 0; it <= iters; ++it) {
+    double* pbase = a.partials + (it & 1) * psize;
+    Hyp h;
+    load_hyp_wave(a, 0, h, st_raw);
+    for (int t = w; t < bpw; t += kWG / 64) {
+      const int blk = blk0 + t;
+      if (blk >= a.nb) break;
+      SpecAcc<D> acc;
+      const double* lb = lds + (int64_t)t * per_blk;
+      for (int i = 0; i < kpl; ++i) {
+        const int64_t k = (int64_t)blk * B + lane + 64 * i;
+        if (k >= main) break;
+        const double* cb = lb + i * (NS + 1) * 64 + lane;
+        double phi[NS];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) phi[s] = cb[64 * s];
+        spec_terms<D>(phi, h, rootn, wl, cb[64 * NS], acc);
+      }
+      spec_block_partials<D, NET>(a, h, 0, blk, rootn, wl, acc, true, pbase);
+    }
+    // grid barrier it + 1: every wave's sc1 partials retired, one add per workgroup, one bounded poller
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned target = (unsigned)(it + 1) * (unsigned)W;
+      long long polls = 0;
+      while (__hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++polls > kPersistPollMax) {
+          fail_s = 1;
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    if (fail_s) {
+      if (tid == 0) out[1] = 1;
+      return;
+    }
+    // level 1 (groups of kSpecGroup blocks, ascending) and level 2 (groups ascending): k_spec_reduce_step's order
+    for (int e = tid; e < NQ * ng; e += kWG) {
+      const int q = e / ng, grp = e - q * ng;
+      const int b0 = grp * kSpecGroup, nbg = min(kSpecGroup, a.nb - b0);
+      const double* pp = pbase + (int64_t)q * a.nb + b0;
+      double tv[kSpecGroup];
+#pragma unroll
+      for (int b = 0; b < kSpecGroup; ++b) tv[b] = ld_part<true>(pp + (b < nbg ? b : 0));
+      double sgrp = 0.0;
+#pragma unroll
+      for (int b = 0; b < kSpecGroup; ++b) sgrp += b < nbg ? tv[b] : 0.0;
+      gsum[q * MAXG + grp] = sgrp;
+    }
+    __syncthreads();
+    if (tid < NQ) {
+      double sq = 0.0;
+      for (int grp = 0; grp < ng; ++grp) sq += gsum[tid * MAXG + grp];
+      tot[tid] = sq;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      // AbstractGP.fit's bookkeeping on the loss of this iteration (the value spec_finish records)
+      const double lv = 0.5 * (tot[0] + a.logdet_weight * tot[1] + f.mll_const);
+      double best = es[0], save = es[1], waited = es[2];
+      if (lv < best) best = lv;
+      if ((save - lv) > logtol) {
+        waited = 0.0;
+        save = best;
+      } else {
+        waited += 1.0;
+      }
+      es[0] = best;
+      es[1] = save;
+      es[2] = waited;
+      brk_s = (it == iters || waited == (double)wait_max) ? 1 : 0;
+    }
+    __syncthreads();
+    const int brk = brk_s;
+    spec_finish<D>(a, f, tot, 0, 1, it, brk ? 0 : 1, st, st, blockIdx.x == 0, nullptr, 1);
+    __syncthreads();
+    if (brk) {
+      if (blockIdx.x == 0) {
+        for (int p = tid; p < np; p += kWG) {
+          f.raw[p] = st_raw[p];
+          f.prev[p] = st_prev[p];
+          f.step[p] = st_step[p];
+        }
+        if (tid == 0) out[0] = it;
+      }
+      return;
+    }
+  }
+}
+
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void glb_void;
 
@@ -682,7 +832,7 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
 #pragma unroll
   for (int p = 0; p < PPW; ++p)
     if (on[p] && active)
-      spec_block_partials<D, NET>(a, h[p], goff + g0 + p, blk, rootn, wl, acc[p], fz.counters != nullptr);
+      spec_block_partials<D, NET>(a, h[p], goff + g0 + p, blk, rootn, wl, acc[p], fz.counters != nullptr, a.partials);
   if (fz.counters) {
     // Level 1 of the fused reduction (MI355X_MICROARCH.md hand-off row 1: sc1 stores retired by every
     // storing wave, then ONE lane's agent-scope add; the waiter reads with sc1 loads after a barrier): the
@@ -1229,6 +1379,44 @@ int launch_spec_reduce_step(const Nll& a, const Fit& f, int iter, int do_update,
   return with_spec_d(a.d, [&](auto dc) {
     k_spec_reduce_step<decltype(dc)::value><<<(unsigned)((a.G + 15) / 16), kWG, 0, st>>>(a, f, iter, do_update);
     return check_launch("k_spec_reduce_step");
+  });
+}
+
+int spec_persist_geometry(const Nll& a, int* W, int* bpw, size_t* shm) {
+  if (!a.spec || a.G != 1 || a.basis_stride != 0 || a.d > kSpecMaxD || !a.ysq_chunked)
+    return set_error(kErrUnsupported, "fgp_fit_persist: one problem on the spectral path only");
+  if (spec_nparams(a) > kSpecScratch) return set_error(kErrUnsupported, "fgp_fit_persist: parameters");
+  const size_t per_blk = (size_t)a.spec_kpl * (((size_t)1 << a.d) + 1) * 64 * sizeof(double);
+  for (int w = 1; w <= kPersistMaxW && w <= a.nb; w *= 2) {
+    const int b = (a.nb + w - 1) / w;
+    if ((size_t)b * per_blk <= (size_t)kPersistLdsMax) {
+      *W = w;
+      *bpw = b;
+      *shm = (size_t)b * per_blk;
+      return kOk;
+    }
+  }
+  return set_error(kErrUnsupported, "fgp_fit_persist: the spectra do not fit %d workgroups' LDS", kPersistMaxW);
+}
+
+int launch_spec_persist(const Nll& a, const Fit& f, int iters, double logtol, int wait_max, unsigned* counter, int* out,
+                        hipStream_t st) {
+  int W, bpw;
+  size_t shm;
+  int rc = spec_persist_geometry(a, &W, &bpw, &shm);
+  if (rc != kOk) return rc;
+  if (hipMemsetAsync(counter, 0, sizeof(unsigned), st) != hipSuccess || hipMemsetAsync(out, 0, 2 * sizeof(int), st) != hipSuccess)
+    return set_error(kErrHip, "fgp_fit_persist: counter reset failed");
+  return with_spec_d(a.d, [&](auto dc) {
+    constexpr int D = decltype(dc)::value;
+    auto go = [&](auto kern) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                kPersistLdsMax);
+      kern<<<(unsigned)W, kWG, shm, st>>>(a, f, iters, logtol, wait_max, bpw, counter, out);
+    };
+    if (a.spec_net) go(k_spec_persist<D, true>);
+    else go(k_spec_persist<D, false>);
+    return check_launch("k_spec_persist");
   });
 }
 

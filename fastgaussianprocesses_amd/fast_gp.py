@@ -715,7 +715,26 @@ class AbstractFastGP(torch.nn.Module):
         total = iterations + 1
         done = False
         losses = []
-        if wait_max > iterations:
+        if getattr(eng, "persist_ok", lambda: False)():
+            # the whole fit in one launch (fgp_fit_persist: the early-stopping rule on the device).  Without a
+            # possible early stop nothing is read back (every iteration runs; the best iterate is found on the
+            # device, as below); otherwise the last iteration and the host rule on the loss history.
+            no_stop = wait_max > iterations
+            i = eng.run_persist(iterations, logtol, wait_max, sync=not no_stop)
+            done = True
+            if no_stop:
+                l0 = eng.loss_hist[:total, 0, 0]
+                best_i = torch.where(torch.isnan(l0), torch.full_like(l0, math.inf), l0).argmin()
+            if not no_stop or verbose or hists["loss"]:
+                rows = eng.loss_hist[:i + 1, 0].cpu().tolist()
+                for r, row in enumerate(rows):
+                    lv = float(row[0])
+                    losses.append((lv, float(row[1]), float(row[2])))
+                    if lv < best and not no_stop:
+                        best, best_i = lv, r
+                    if verbose and (r % verbose == 0 or r == i):
+                        self._log_row(r, lv, row[1], row[2], indent)
+        elif wait_max > iterations:
             # no early stop is possible: every iteration runs, the best iterate is the first minimum of
             # the loss history (the host rule `lv < best`; NaN never best), found on the device -- one
             # enqueue, no host sync unless losses are logged or returned

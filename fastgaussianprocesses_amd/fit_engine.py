@@ -280,6 +280,40 @@ class FusedMLL(object):
             done.record(st)
             cur.wait_event(done)
 
+    def persist_ok(self):
+        """fgp_fit_persist applies (one problem on the spectral path whose spectra fit the LDS of at most 64
+        workgroups: the whole fit in one launch); FGP_FIT_PERSIST=0 keeps the launch per iteration."""
+        if os.environ.get("FGP_FIT_PERSIST", "1")[:1] == "0" or self.G != 1 or self.basis is None:
+            return False
+        ok = ctypes.c_int(0)
+        N.call("fgp_fit_persist_ok", self._nll, ctypes.byref(ok))
+        return ok.value > 0
+
+    def run_persist(self, iterations, logtol, wait_max, sync=True):
+        """AbstractGP.fit's iterations 0 .. iterations with its early-stopping rule, in one launch
+        (fgp_fit_persist); returns the last iteration evaluated (its row applied no update).  sync=False (no
+        early stop possible): nothing is read back and `iterations` is returned; the barrier flag is checked at
+        the next synchronising call (check_persist)."""
+        self.check_persist()
+        self.ensure_history(iterations + 1)
+        ctrl = torch.zeros((4,), dtype=torch.int32, device=self.device)
+        N.call("fgp_fit_persist", self._nll, self._fit, int(iterations), float(logtol), int(wait_max),
+               ctrl.data_ptr(), self.stream())
+        self._ctrl = ctrl
+        if not sync:
+            return int(iterations)
+        return self.check_persist()
+
+    def check_persist(self):
+        ctrl = getattr(self, "_ctrl", None)
+        if ctrl is None:
+            return None
+        self._ctrl = None
+        c = ctrl.cpu().tolist()
+        if c[2]:
+            raise RuntimeError("fgp_fit_persist: an in-kernel barrier gave up (workgroups not co-resident?)")
+        return int(c[1])
+
     def groups(self):
         """Problem groups of run(): FGP_FIT_STREAMS (default 1) for independent problems, else 1.
         Measured on MI355X (8 GPs, n = 2^20, profiles/r02e_exp_fit_streams.jsonl): 1 group 93.6 us per

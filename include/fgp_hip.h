@@ -486,6 +486,18 @@ int fgp_mt_selinv(const fgp_mt_layout* layout, const void* factor, int64_t G, vo
 int fgp_mt_mll_grad(const fgp_mt_layout* layout, const void* zinv, const void* z, const double* grad_norm,
                     const double* grad_logdet, int64_t B, int64_t G, void* grad_lams, void* stream);
 
+/* ABI 14 -- the WHOLE fit of one small problem on the spectral path in ONE launch (G = 1, the part-product
+ * spectra and Y within the LDS of 64 workgroups: e.g. n = 2^16, d = 3, or the probnum25 paper's n = 2^10):
+ * iterations 0 .. iters of AbstractGP.fit (abstract_gp.py:241-296) -- loss history, gradient, Rprop and the
+ * early-stopping rule (:276-284, logtol = log(1 + stop_crit_improvement_threshold), wait_max =
+ * stop_crit_wait_iterations) -- with the multi-launch fgp_fit_run's arithmetic (bit-identical histories).
+ * The last evaluated iteration applies no update.  ctrl: device scratch of >= 16 bytes; afterwards
+ * ((int*)ctrl)[1] = the last iteration, ((int*)ctrl)[2] = 1 if an in-kernel barrier gave up (an error).
+ * fgp_fit_persist_ok: *ok = the workgroup count it would use, 0 when the desc is outside its domain. */
+int fgp_fit_persist_ok(const fgp_nll_desc* nll, int* ok);
+int fgp_fit_persist(const fgp_nll_desc* nll, const fgp_fit_desc* fit, int iters, double logtol, int wait_max, void* ctrl,
+                    void* stream);
+
 /* ABI 14 -- device-resident MLL fit of a GENERAL multitask / derivative-informed GP: any n per task (the
  * structured blocks above), the task kernel K_task = F F^T + diag(v) learned or fixed, a data batch of B
  * vectors sharing the hyper-parameters.  Replaces AbstractGP.fit's MLL loop (abstract_gp.py:152-306) with

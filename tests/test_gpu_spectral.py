@@ -281,3 +281,25 @@ def test_real_factor_inverse_reads_half_of_hermitian_input(m, rows):
         xp[:, n // 2 + 1:] = float("nan")
         got = ops.ifftbr_real_rf(xp, fr)
         assert rel_err(got, ref) <= 1e-13
+
+
+@pytest.mark.parametrize("family,m,d,wait", [("lattice", 16, 3, 60), ("net", 16, 3, 60), ("lattice", 10, 6, 10),
+                                             ("net", 10, 2, 10), ("lattice", 12, 1, 4)])
+def test_single_launch_fit_equals_launch_per_iteration(family, m, d, wait, monkeypatch):
+    """fgp_fit_persist (the whole fit of one small spectral problem in one launch: LDS-resident spectra, an
+    in-kernel grid barrier per iteration, the early-stopping rule on the device) against the launch per
+    iteration (FGP_FIT_PERSIST=0): the same iterations, loss history and fitted parameters bit for bit --
+    with early stopping impossible (wait 60 > 50 iterations: C2 / C3's bench step) and possible."""
+    monkeypatch.setenv("FGP_FIT_PATH", "spectral")
+    out = {}
+    for persist in ("1", "0"):
+        monkeypatch.setenv("FGP_FIT_PERSIST", persist)
+        gp, _, _ = _gp(family, d, m)
+        assert gp._fused_engine(1, 0.1).persist_ok() == (persist == "1")
+        data = gp.fit(iterations=50, store_hists=True, verbose=0, stop_crit_wait_iterations=wait)
+        out[persist] = (data, gp.raw_scale.detach().cpu().clone(), gp.raw_lengthscales.detach().cpu().clone())
+    (a, sa, la), (b, sb, lb) = out["1"], out["0"]
+    assert a["iterations"] == b["iterations"]
+    assert torch.equal(a["loss_hist"], b["loss_hist"])
+    assert torch.equal(a["lengthscales_hist"], b["lengthscales_hist"])
+    assert torch.equal(sa, sb) and torch.equal(la, lb)
