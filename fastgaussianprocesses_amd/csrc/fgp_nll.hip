@@ -538,8 +538,19 @@ __global__ __launch_bounds__(kWG) void k_fwd_rows_r2c_prod(const double* __restr
   __shared__ double2 red[kWG / 64];
   const int mt = log2n - 1, m1 = mt - P2;
   const int64_t n = (int64_t)1 << log2n, nt = n >> 1;
-  const int c = (int)(blockIdx.x % (unsigned)cnt);
-  const int row0 = (int)(blockIdx.x / (unsigned)cnt);
+  // XCD-aware order (speed only): workgroups b and b + 8 share an XCD, so with (rows of the grid) % 8 == 0 the
+  // cnt subsets of a row go to ONE XCD, consecutively -- its parts cross the fabric into that XCD's L2 once
+  // instead of once per XCD
+  const unsigned rows = gridDim.x / (unsigned)cnt;
+  int c, row0;
+  if (rows % 8u == 0u) {
+    const unsigned xcd = blockIdx.x & 7u, local = blockIdx.x >> 3;
+    c = (int)(local % (unsigned)cnt);
+    row0 = (int)((local / (unsigned)cnt) * 8u + xcd);
+  } else {
+    c = (int)(blockIdx.x % (unsigned)cnt);
+    row0 = (int)(blockIdx.x / (unsigned)cnt);
+  }
   const int S = s0 + c;
   const int tid = threadIdx.x;
   const double* x = parts + (int64_t)row0 * N2 + 16 * tid;
