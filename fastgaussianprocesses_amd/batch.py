@@ -312,28 +312,51 @@ class GPBatch(object):
         return self._st["basis"]
 
     def _put_ytilde(self):
-        yt = self._st.get("yt")
-        if yt is not None:
-            for p, gp in enumerate(self.gps):
+        yt, yth = self._st.get("yt"), self._st.get("yth")
+        for p, gp in enumerate(self.gps):
+            if yt is not None:
                 gp._cache[("ytilde", self.n, False, False)] = yt[p]
+            if yth is not None:
+                gp._cache[("ytilde_half", self.n, False, False)] = yth[p]
+
+    def _y_rows(self):
+        return self._y if self._y is not None else torch.stack([gp._y[0] for gp in self.gps])
+
+    def ytilde_half(self):
+        """[P, n/2 + 1] Hermitian halves of ytilde (lattice, real fp64 observations, 2^17 <= n <= 2^24;
+        ops.fftbr_real_half): all that Y and the spectral coefficient solve read.  None when it does not apply."""
+        if "yth" not in self._st:
+            if "yt" in self._st:
+                return self._st["yt"][:, :self.n // 2 + 1] if self.family == ops.LATTICE else None
+            y = self._y_rows()
+            if self.family != ops.LATTICE or not ops.half_spectrum_ok(y):
+                return None
+            self._st["yth"] = ops.fftbr_real_half(y)
+            self._put_ytilde()
+        return self._st["yth"]
 
     def ytilde(self):
         """[P, n] ytilde = ft(y) of every GP (AbstractFastGP.get_ytilde / _YtildeCache, util.py:164-183),
-        one batched transform; also installed in each GP's cache."""
+        one batched transform (or the mirror of the Hermitian halves when only those were formed); also
+        installed in each GP's cache."""
         if "yt" not in self._st:
-            y = self._y if self._y is not None else torch.stack([gp._y[0] for gp in self.gps])
-            if self.family == ops.LATTICE:
-                yt = ops.fftbr_raw(y, stable=True)
+            if "yth" in self._st:
+                yt = ops.hermitian_full(self._st["yth"], self.n)
+            elif self.family == ops.LATTICE:
+                yt = ops.fftbr_raw(self._y_rows(), stable=True)
             else:
-                yt = ops.fwht_raw(y, stable=True)
+                yt = ops.fwht_raw(self._y_rows(), stable=True)
             self._st["yt"] = yt
             self._put_ytilde()
         return self._st["yt"]
 
     def ysq(self):
         if "ysq" not in self._st:
-            yt = self.ytilde()
-            self._st["ysq"] = ops.sum_sq(yt, G=self.P)          # |ytilde|^2 per GP (fgp_sum_sq)
+            yth = self.ytilde_half()
+            if yth is not None:                                 # |ytilde|^2 per GP from the halves (fgp_sum_sq_half)
+                self._st["ysq"] = ops.sum_sq_half(yth, self.n, G=self.P)
+            else:
+                self._st["ysq"] = ops.sum_sq(self.ytilde(), G=self.P)   # (fgp_sum_sq)
         return self._st["ysq"]
 
     # ---------------------------------------------------------------------------- fit
@@ -362,7 +385,8 @@ class GPBatch(object):
                 # spectral path: A = 1/ev straight from the spectra (real), the product fused into the
                 # half-length inverse -- no lambda / ytilde * A arrays
                 wa = spec_inv_eig(self.family, raw[:, 0], raw[:, 1:1 + dl], raw[:, 1 + dl], self.P, self.n, basis)
-                self._st["coeffs"] = ops.ifftbr_real_rf(self.ytilde(), wa)
+                yth = self.ytilde_half()
+                self._st["coeffs"] = ops.ifftbr_real_rf(yth if yth is not None else self.ytilde(), wa, n=self.n)
                 self._st["wa"] = wa
                 return self._st["coeffs"]
             lam = fused_lam(self.family, parts, raw[:, 0], raw[:, 1:1 + dl], raw[:, 1 + dl], self.P, gen=gen, n=self.n,

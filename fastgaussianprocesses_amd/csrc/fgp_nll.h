@@ -55,6 +55,7 @@ struct Nll {
   const void* mt_basis;
   const void* mt_ytilde;
   const double* mt_kt;
+  int64_t out_stride;                // fgp_fftbr_real_half: row stride of the half spectra (grad_lam)
 };
 
 // Device-clock kernel timing (fgp_nll_desc.stamps; off when NULL -- a uniform branch on a kernel

@@ -703,6 +703,7 @@ __global__ __launch_bounds__(kWG, 2) void k_fwd_cols_r2c(Nll a, const double2* _
   EigAcc acc2, acc1;          // regular pairs (weight 2), self-mirrored frequencies (weight 1)
   double2* gl = OUT == 1 ? static_cast<double2*>(a.grad_lam) + (int64_t)g * n : nullptr;
   double* gb = OUT == 2 ? static_cast<double*>(a.grad_lam) + (int64_t)g * 64 : nullptr;   // basis + (s0 + g) 64
+  double2* gh = OUT == 3 ? static_cast<double2*>(a.grad_lam) + (int64_t)g * a.out_stride : nullptr;   // k <= n/2
   const int ns = 1 << a.d;
   const double2 wcp = twmf[col0 ? 0 : cp_gen];
 #pragma unroll 2
@@ -746,6 +747,11 @@ __global__ __launch_bounds__(kWG, 2) void k_fwd_cols_r2c(Nll a, const double2* _
       gb[spec_pos(kp, ns)] = A0.x * inv_rootn;
       if (kp == 0) gb[spec_pos(nt, ns)] = A1.x * inv_rootn;                 // the Nyquist frequency n/2
       if (!self) gb[spec_pos((col0 ? cp : N2 - cp) + (int64_t)rs * N2, ns)] = A1.x * inv_rootn;
+    } else if constexpr (OUT == 3) {   // OUT == 1's values at k <= n/2 only (the Hermitian half of ft(real))
+      const int64_t kp = cp + (int64_t)rp * N2;
+      gh[kp] = A0 * inv_rootn;
+      if (kp == 0) gh[nt] = A1 * inv_rootn;
+      if (!self) gh[(col0 ? cp : N2 - cp) + (int64_t)rs * N2] = make_double2(A1.x, -A1.y) * inv_rootn;
     } else {
       const double2 E = g0 + g1;
       const double2 O = cmulc(g0 - g1, W);
@@ -768,6 +774,8 @@ __global__ __launch_bounds__(kWG, 2) void k_fwd_cols_r2c(Nll a, const double2* _
         gl[(int64_t)rh * N2 + nt] = A1 * inv_rootn;
       } else if constexpr (OUT == 2) {
         gb[spec_pos((int64_t)rh * N2, ns)] = A0.x * inv_rootn;              // n/4 (3n/4 is past n/2)
+      } else if constexpr (OUT == 3) {
+        gh[(int64_t)rh * N2] = A0 * inv_rootn;
       } else {
         const double2 E = g0 + g1;
         const double2 O = cmulc(g0 - g1, Wh);
@@ -1665,8 +1673,23 @@ int fgp_nll_bwd(const fgp_nll_desc* desc, void* stream) {
   return nll_bwd(a, (hipStream_t)stream, desc->family == FGP_FAMILY_LATTICE);
 }
 
+static int fftbr_real_any(const double* in, int64_t in_batch_stride, void* out, int64_t out_stride, bool half,
+                          void* work, int64_t batch, int log2n, void* stream);
+
 int fgp_fftbr_real(const double* in, int64_t in_batch_stride, void* out, void* work, int64_t batch, int log2n,
                    void* stream) {
+  return fftbr_real_any(in, in_batch_stride, out, (int64_t)1 << log2n, false, work, batch, log2n, stream);
+}
+
+int fgp_fftbr_real_half(const double* in, int64_t in_batch_stride, void* out, int64_t out_batch_stride, void* work,
+                        int64_t batch, int log2n, void* stream) {
+  if (log2n >= 1 && batch > 1 && out_batch_stride < ((int64_t)1 << (log2n - 1)) + 1)
+    return set_error(kErrInvalid, "fgp_fftbr_real_half: out row stride below n/2 + 1");
+  return fftbr_real_any(in, in_batch_stride, out, out_batch_stride, true, work, batch, log2n, stream);
+}
+
+static int fftbr_real_any(const double* in, int64_t in_batch_stride, void* out, int64_t out_stride, bool half,
+                          void* work, int64_t batch, int log2n, void* stream) {
   if (log2n < 17 || log2n > 24 || batch < 0) return set_error(kErrInvalid, "fgp_fftbr_real: needs 17 <= log2n <= 24");
   if (batch == 0) return kOk;
   if (!in || !out || !work) return set_error(kErrInvalid, "fgp_fftbr_real: null pointer");
@@ -1688,9 +1711,14 @@ int fgp_fftbr_real(const double* in, int64_t in_batch_stride, void* out, void* w
   a.G = (int)batch;
   a.work = work;
   a.grad_lam = out;
+  a.out_stride = out_stride;
   a.stamps = nullptr;
   switch (p1) {
-#define FGP_C(PP) case PP: k_fwd_cols_r2c<PP, 1><<<grid, kWG, 0, st>>>(a, tb->tw4096, tb->twm[log2n]); break;
+#define FGP_C(PP)                                                                                   \
+  case PP:                                                                                          \
+    if (half) k_fwd_cols_r2c<PP, 3><<<grid, kWG, 0, st>>>(a, tb->tw4096, tb->twm[log2n]);           \
+    else k_fwd_cols_r2c<PP, 1><<<grid, kWG, 0, st>>>(a, tb->tw4096, tb->twm[log2n]);                \
+    break;
     FGP_C(4) FGP_C(5) FGP_C(6) FGP_C(7) FGP_C(8) FGP_C(9) FGP_C(10) FGP_C(11)
 #undef FGP_C
     default: return set_error(kErrInvalid, "bad r2c m1");
@@ -1704,7 +1732,8 @@ static int ifftbr_real_any(const void* in, int64_t in_batch_stride, const void* 
   if (batch == 0) return kOk;
   if (!in || !out || !work) return set_error(kErrInvalid, "fgp_ifftbr_real: null pointer");
   const int64_t n = (int64_t)1 << log2n;
-  if (batch > 1 && (in_batch_stride < n || out_batch_stride < n))
+  // the Hermitian-input variant (fgp_ifftbr_real_rf) reads only k <= n/2: rows of n/2 + 1 (a half spectrum) do
+  if (batch > 1 && (in_batch_stride < (freal ? n / 2 + 1 : n) || out_batch_stride < n))
     return set_error(kErrInvalid, "fgp_ifftbr_real: batch stride below n");
   if (((uintptr_t)out & 15) || (out_batch_stride & 1)) return set_error(kErrInvalid, "fgp_ifftbr_real: out must be 16-byte aligned rows");
   const int64_t tiles = (int64_t)1 << (log2n - 1 - kTileLog);

@@ -360,6 +360,26 @@ __global__ __launch_bounds__(kWG) void k_sum_sq(const T* __restrict__ x, int64_t
   out[e] = acc;
 }
 
+// Y from the Hermitian halves of ft(real rows): x [R G][H] complex128 rows holding k = 0 .. n/2 (H = n/2 + 1,
+// row stride xs >= H); out[g][k] and out[g][n - k] = sum_r |x[r G + g][k]|^2 (ascending r: k_sum_sq's values on the
+// full spectra bit for bit, |X_{n-k}| = |conj X_k|).
+__global__ __launch_bounds__(kWG) void k_sum_sq_half(const double2* __restrict__ x, int64_t xs, int64_t R, int64_t G,
+                                                      int64_t n, double* __restrict__ out) {
+  const int64_t H = n / 2 + 1;
+  const int64_t e = (int64_t)blockIdx.x * kWG + threadIdx.x;
+  if (e >= G * H) return;
+  const int64_t g = e / H, k = e % H;
+  const double2* p = x + g * xs + k;
+  double acc = 0.0;
+#pragma unroll 8
+  for (int64_t r = 0; r < R; ++r) {
+    const double2 v = p[r * G * xs];
+    acc += v.x * v.x + v.y * v.y;
+  }
+  out[g * n + k] = acc;
+  if (k > 0 && k < n / 2) out[g * n + n - k] = acc;
+}
+
 // Entry-point bodies for the fp64 (T = double2 / double) and fp32 (T = float2 / float) variants.
 template <typename T>
 static int fftbr_impl(const void* in, int64_t in_bs, int in_real, void* out, int64_t batch, int log2n, int stable,
@@ -484,6 +504,16 @@ int fgp_ifftbr_c64(const void* in, int64_t in_batch_stride, void* out, int out_r
 int fgp_fwht_f32(const float* in, int64_t in_batch_stride, float* out, int64_t batch, int log2n, int stable,
                  void* stream) {
   return fwht_impl<float>(in, in_batch_stride, out, batch, log2n, stable, (hipStream_t)stream);
+}
+
+int fgp_sum_sq_half(const void* x, int64_t x_row_stride, int64_t R, int64_t G, int64_t n, double* out, void* stream) {
+  if (R < 1 || G < 1 || n < 2 || (n & (n - 1)) || x_row_stride < n / 2 + 1)
+    return set_error(kErrInvalid, "fgp_sum_sq_half: bad sizes");
+  if (!x || !out) return set_error(kErrInvalid, "fgp_sum_sq_half: null pointer");
+  const int64_t cnt = G * (n / 2 + 1);
+  k_sum_sq_half<<<(unsigned)((cnt + kWG - 1) / kWG), kWG, 0, (hipStream_t)stream>>>(static_cast<const double2*>(x),
+                                                                                   x_row_stride, R, G, n, out);
+  return check_launch("k_sum_sq_half");
 }
 
 int fgp_sum_sq(const void* x, int64_t x_row_stride, int kind, int64_t R, int64_t G, int64_t n, double* out,

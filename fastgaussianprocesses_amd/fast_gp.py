@@ -517,7 +517,11 @@ class AbstractFastGP(torch.nn.Module):
         def f():
             y = self._y[0]
             st = getattr(self, "_yt_state", None)
-            if st is not None and 1 < st[0] < n and y.dtype == torch.float64 and n % st[0] == 0:
+            half = self._cache.get(("ytilde_half", n, False, False))
+            if half is not None:
+                # the fused consumers took only the Hermitian half (_ytilde_half): the full spectrum is its mirror
+                yt = ops.hermitian_full(half, n)
+            elif st is not None and 1 < st[0] < n and y.dtype == torch.float64 and n % st[0] == 0:
                 ns, yt = st
                 while ns < n:
                     yt = ops.double_update(self._FAMILY, yt, self.ft(y[..., ns:2 * ns]))
@@ -527,6 +531,22 @@ class AbstractFastGP(torch.nn.Module):
             self._yt_state = (n, yt)
             return yt
         return self._cached(("ytilde", n), f, grad_sensitive=False)
+
+    def _ytilde_half(self):
+        """The Hermitian half (k <= n/2) of ytilde = ft(y) of real float64 lattice observations, 2^17 <= n <= 2^24
+        (ops.fftbr_real_half): all that Y = sum |ytilde|^2 and the spectral coefficient solve read, at half the
+        bytes written; a view of the full ytilde when that is cached already.  None when it does not apply."""
+        n = self._nh
+        y = self._y[0]
+        if self._FAMILY != ops.LATTICE or n < 2 or not ops.half_spectrum_ok(y):
+            return None
+        full = self._cache.get(("ytilde", n, False, False))
+        if full is not None:
+            return full[..., :n // 2 + 1]
+        st = getattr(self, "_yt_state", None)
+        if st is not None and 1 < st[0] < n and n % st[0] == 0:
+            return None                           # the doubling update of the cached ytilde (get_ytilde) is cheaper
+        return self._cached(("ytilde_half", n), lambda: ops.fftbr_real_half(y), grad_sensitive=False)
 
     def _ev(self, n):
         """sqrt(n) lam + noise (util.py:285,292-298, single task; adaptive nugget: util.py:286-290)."""
@@ -565,15 +585,20 @@ class AbstractFastGP(torch.nn.Module):
         # coefficients still come from an fp64 transform of the (fp32) observations -- cond(K) ~ n /
         # noise makes fp32 coefficients useless for the posterior mean (measured O(1) relative error,
         # tools/diag_mixed.py), so only the MLL's Y uses the complex64 ytilde.
-        yt = self.get_ytilde(0)
-        if self.data_dtype != torch.float64:
-            y = self._y[0].to(torch.float64)
-            yt = ops.fftbr_raw(y, stable=True) if self._FAMILY == ops.LATTICE else ops.fwht_raw(y, stable=True)
+        rows_y = self._y[0].numel() // n
         pb = self._problem_batch() if (self._lam_fusable(n) and not self.adaptive_nugget) else None
         basis = None
         if (pb is not None and self._FAMILY == ops.LATTICE and 17 <= n.bit_length() - 1 <= 24
-                and pb[1] in (1, yt.numel() // n)):
+                and pb[1] in (1, rows_y)):
             basis = self._spec_basis(n, pb[1])
+        half = self._ytilde_half() if (basis is not None and self.data_dtype == torch.float64) else None
+        if half is not None:
+            yt = half                     # the Hermitian half is all fgp_ifftbr_real_rf reads
+        elif self.data_dtype != torch.float64:
+            y = self._y[0].to(torch.float64)
+            yt = ops.fftbr_raw(y, stable=True) if self._FAMILY == ops.LATTICE else ops.fwht_raw(y, stable=True)
+        else:
+            yt = self.get_ytilde(0)
         if basis is not None:
             # spectral path: the real A = 1/ev straight from the part-product spectra (fgp_spec_inv_eig; one
             # row shared by every output, or one per output's eigen-problem), the product fused into the
@@ -583,7 +608,7 @@ class AbstractFastGP(torch.nn.Module):
                               self.raw_lengthscales.detach().reshape(-1, self.raw_lengthscales.shape[-1]),
                               self.raw_noise.detach().reshape(-1), pb[1], n, basis)
             self._cached(("inv_real", n), lambda: wa.reshape(tuple(pb[0]) + (n,)))
-            return ops.ifftbr_real_rf(yt, wa)
+            return ops.ifftbr_real_rf(yt, wa, n=n)
         if pb is not None and yt.numel() == pb[1] * n:
             # one output per eigen-problem: A = 1/ev and ytilde * A in ONE launch (fgp_inv_eig) instead of
             # the torch chain of get_inv_log_det; Re(A) kept for post_var's quadratic form
@@ -669,7 +694,11 @@ class AbstractFastGP(torch.nn.Module):
         return big, G
 
     def _ysq(self, pb_shape, G):
-        """Y[g] = sum over the outputs of problem g of |ytilde|^2 (fgp_sum_sq, one pass over ytilde)."""
+        """Y[g] = sum over the outputs of problem g of |ytilde|^2 (fgp_sum_sq, one pass over ytilde; over its
+        Hermitian half -- fgp_sum_sq_half, the same values -- when only that exists)."""
+        half = self._ytilde_half()
+        if half is not None:
+            return ops.sum_sq_half(half.reshape(-1, half.shape[-1]), self._nh, G)
         yt = self.get_ytilde(0)
         return ops.sum_sq(yt.reshape(-1, yt.shape[-1]), G)
 

@@ -89,6 +89,52 @@ def fftbr_raw(x, stable=True):
     return out.reshape(shape)
 
 
+def half_spectrum_ok(x):
+    """fgp_fftbr_real_half applies to x: real float64 rows, 2^17 <= n <= 2^24 (FGP_YT_HALF=0 / FGP_R2C=0 off)."""
+    n = x.shape[-1]
+    return (x.dtype == torch.float64 and n >= 2 and (n & (n - 1)) == 0 and 17 <= n.bit_length() - 1 <= 24
+            and rows_ok_env() and os.environ.get("FGP_YT_HALF", "1")[:1] != "0")
+
+
+def fftbr_real_half(x):
+    """The Hermitian half (k = 0 .. n/2) of the stable fftbr of real float64 rows x [*, n] -> complex128
+    [*, n/2 + 1] (fgp_fftbr_real_half: fgp_fftbr_real's values there, half the bytes written)."""
+    require_device(x, "fftbr_real_half")
+    shape = x.shape
+    n = shape[-1]
+    m = log2_exact(n)
+    assert x.dtype == torch.float64 and 17 <= m <= 24, "fftbr_real_half: float64 rows, 2^17 <= n <= 2^24"
+    rows, bs = _as_rows(x)
+    if rows.data_ptr() % 16 or bs % 2:
+        rows, bs = rows.contiguous(), n
+    H = n // 2 + 1
+    out = torch.empty((rows.size(0), H), dtype=torch.complex128, device=x.device)
+    work = torch.empty((rows.size(0), n), dtype=torch.complex128, device=x.device)
+    N.call("fgp_fftbr_real_half", N.ptr(rows), bs, N.ptr(out), H, N.ptr(work), rows.size(0), m, _stream(x))
+    return out.reshape(shape[:-1] + (H,))
+
+
+def hermitian_full(xh, n):
+    """[*, n/2 + 1] Hermitian half -> the full [*, n] spectrum (X_{n-k} = conj X_k)."""
+    H = n // 2 + 1
+    assert xh.shape[-1] == H
+    full = torch.empty(xh.shape[:-1] + (n,), dtype=xh.dtype, device=xh.device)
+    full[..., :H] = xh
+    full[..., H:] = xh[..., 1:n // 2].flip(-1).conj()
+    return full
+
+
+def sum_sq_half(xh, n, G=1):
+    """Y[g, k] = sum_r |X[r G + g, k]|^2 [G, n] from Hermitian halves xh [R G, n/2 + 1] complex128
+    (fgp_sum_sq_half: sum_sq of the full spectra, bit for bit)."""
+    require_device(xh, "sum_sq_half")
+    rows, bs = _as_rows(xh)
+    assert rows.dtype == torch.complex128 and rows.size(0) % G == 0
+    out = torch.empty((G, n), dtype=torch.float64, device=xh.device)
+    N.call("fgp_sum_sq_half", N.ptr(rows), bs, rows.size(0) // G, G, n, N.ptr(out), _stream(xh))
+    return out
+
+
 def _real_half_length(x, m):
     """fgp_fftbr_real applies: float64 real input, 17 <= m <= 24 (FGP_R2C=0 keeps the full-length path)."""
     return (x.dtype == torch.float64 and 17 <= m <= 24 and rows_ok_env())
@@ -126,24 +172,26 @@ def ifftbr_raw(x, stable=True, real_out=False):
     return out.reshape(shape)
 
 
-def ifftbr_real_rf(x, f):
+def ifftbr_real_rf(x, f, n=None):
     """Re ifftbr(x * f) along the last dim for complex128 x [*, n] and REAL factor rows f (float64, one row or
     one per row of x), 2^17 <= n <= 2^24, at half length (fgp_ifftbr_real_rf): the coefficient solve
     ift(A * ytilde).real of gram_matrix_solve (util.py:341-343) with the spectral path's real A.  x must be
-    Hermitian along the last dim (ft of real data, as ytilde) and f even (as A): only k <= n/2 are read."""
+    Hermitian along the last dim (ft of real data, as ytilde) and f even (as A): only k <= n/2 are read -- so
+    x may also be just that half, [*, n/2 + 1] (fftbr_real_half), with n given."""
     require_device(x, "ifftbr_real_rf")
-    n = x.shape[-1]
+    half = n is not None and x.shape[-1] == n // 2 + 1
+    n = x.shape[-1] if n is None else int(n)
     m = log2_exact(n)
     assert 17 <= m <= 24, "ifftbr_real_rf needs 2^17 <= n <= 2^24"
     x = x.to(torch.complex128)
     rows, bs = _as_rows(x)
     f2 = resolved(f.to(device=x.device, dtype=torch.float64)).reshape(-1, n).contiguous()
     assert f2.size(0) in (1, rows.size(0)), "one factor row, or one per row of x"
-    out = torch.empty(rows.shape, dtype=torch.float64, device=x.device)
-    work = torch.empty(rows.shape, dtype=torch.complex128, device=x.device)
+    out = torch.empty((rows.size(0), n), dtype=torch.float64, device=x.device)
+    work = torch.empty((rows.size(0), n), dtype=torch.complex128, device=x.device)
     N.call("fgp_ifftbr_real_rf", N.ptr(rows), bs, N.ptr(f2), 0 if f2.size(0) == 1 else n, N.ptr(out), n, N.ptr(work),
            rows.size(0), m, _stream(x))
-    return out.reshape(x.shape)
+    return out.reshape(x.shape[:-1] + (n,)) if half else out.reshape(x.shape)
 
 
 def fwht_raw(x, stable=True):

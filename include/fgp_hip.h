@@ -486,6 +486,15 @@ int fgp_mt_selinv(const fgp_mt_layout* layout, const void* factor, int64_t G, vo
 int fgp_mt_mll_grad(const fgp_mt_layout* layout, const void* zinv, const void* z, const double* grad_norm,
                     const double* grad_logdet, int64_t B, int64_t G, void* grad_lams, void* stream);
 
+/* ABI 14 -- the Hermitian half of ft(real): fgp_fftbr_real's values at k = 0 .. n/2 only, rows of
+ * out_batch_stride >= n/2 + 1 complex128 (ytilde of real observations: the coefficient solve
+ * fgp_ifftbr_real_rf and Y read no more, and the other half is the conjugate mirror -- half the bytes
+ * written).  fgp_sum_sq_half: Y [G][n] from such halves (x [R G] rows, Y mirrored to k > n/2), fgp_sum_sq's
+ * values bit for bit. */
+int fgp_fftbr_real_half(const double* in, int64_t in_batch_stride, void* out, int64_t out_batch_stride, void* work,
+                        int64_t batch, int log2n, void* stream);
+int fgp_sum_sq_half(const void* x, int64_t x_row_stride, int64_t R, int64_t G, int64_t n, double* out, void* stream);
+
 /* ABI 14 -- the WHOLE fit of one small problem on the spectral path in ONE launch (G = 1, the part-product
  * spectra and Y within the LDS of 64 workgroups: e.g. n = 2^16, d = 3, or the probnum25 paper's n = 2^10):
  * iterations 0 .. iters of AbstractGP.fit (abstract_gp.py:241-296) -- loss history, gradient, Rprop and the

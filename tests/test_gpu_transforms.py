@@ -305,3 +305,25 @@ def test_ifftbr_real_half_length_matches_full_length(monkeypatch, m, batch, shar
     _close(half_mul, full_mul, m)
     if m <= 20:
         _close(half, O.ft_stable(x.cpu(), O.ifftbr).real, m)
+
+
+@pytest.mark.parametrize("m,rows", [(17, 3), (18, 5), (20, 2)])
+def test_hermitian_half_spectra_equal_full_length_ones(m, rows):
+    """fgp_fftbr_real_half (ABI 14) writes fgp_fftbr_real's values at k <= n/2 only: bit for bit, and the
+    mirror (ops.hermitian_full) rebuilds the full output bit for bit; fgp_sum_sq_half from the halves equals
+    fgp_sum_sq of the full spectra bit for bit (G = 1 and per-row groups); fgp_ifftbr_real_rf on the halves
+    (rows of n/2 + 1) equals it on the full rows bit for bit."""
+    from fastgaussianprocesses_amd import ops
+    n = 2 ** m
+    g = torch.Generator().manual_seed(m)
+    y = (torch.randn((rows, n), generator=g) + 3.0).to(DEV)
+    full = ops.fftbr_raw(y, stable=True)
+    half = ops.fftbr_real_half(y)
+    assert half.shape == (rows, n // 2 + 1)
+    assert torch.equal(half, full[:, :n // 2 + 1])
+    assert torch.equal(ops.hermitian_full(half, n), full)
+    for G in (1, rows):
+        assert torch.equal(ops.sum_sq_half(half, n, G=G), ops.sum_sq(full, G=G))
+    f = (torch.rand((1, n), generator=g) + 0.5).to(DEV)
+    f = 0.5 * (f + torch.roll(f.flip(-1), 1, -1))            # an even factor row, as A = 1/ev
+    assert torch.equal(ops.ifftbr_real_rf(half, f, n=n), ops.ifftbr_real_rf(full, f))
