@@ -580,7 +580,10 @@ struct FitFuse {
   // parameters from sin; workgroup 0 writes histories and sout); this launch's level-1 sums go to parity par
   int pending, par;
   RpState sin, sout;
+  // fgp_handoff_check (a test hook): [kSpecBlocks / kSpecGroup][G nq] XOR words, then checks, mismatches
+  unsigned long long* check;
 };
+constexpr int kHandoffWords = 16 * 8 * 16;         // XOR words of the check buffer (groups x G x nq, at most)
 int launch_re_bwd_fused(const Nll& a, const FitFuse& fz, const Tables* tb, hipStream_t st);
 
 // spectral fit path (fgp_spectral.hip): d <= kSpecMaxD, at most kSpecBlocks k blocks per problem

@@ -1816,6 +1816,9 @@ int spec_basis_r2c(const double* parts, int d, int log2n, int s0, int cnt, doubl
   return check_launch("k_fwd_cols_r2c");
 }
 
+// fgp_handoff_check's device buffer while armed (kHandoffWords XOR words, checks, mismatches)
+static unsigned long long* g_handoff_check = nullptr;
+
 }  // namespace fgp
 
 extern "C" {
@@ -1861,6 +1864,27 @@ int fgp_fit_persist(const fgp_nll_desc* nll, const fgp_fit_desc* fit, int iters,
                              (hipStream_t)stream);
 }
 
+int fgp_handoff_check(int enable, unsigned long long* out) {
+  const size_t bytes = sizeof(unsigned long long) * (kHandoffWords + 2);
+  if (enable) {
+    if (!g_handoff_check && hipMalloc(reinterpret_cast<void**>(&g_handoff_check), bytes) != hipSuccess) {
+      g_handoff_check = nullptr;
+      return set_error(kErrHip, "fgp_handoff_check: allocation failed");
+    }
+    if (hipMemset(g_handoff_check, 0, bytes) != hipSuccess) return set_error(kErrHip, "fgp_handoff_check: reset failed");
+    return kOk;
+  }
+  if (!out) return set_error(kErrInvalid, "fgp_handoff_check: out is null");
+  out[0] = out[1] = 0;
+  if (!g_handoff_check) return kOk;
+  if (hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpy(out, g_handoff_check + kHandoffWords, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
+    return set_error(kErrHip, "fgp_handoff_check: read-back failed");
+  (void)hipFree(g_handoff_check);
+  g_handoff_check = nullptr;
+  return kOk;
+}
+
 int fgp_fit_run(const fgp_nll_desc* nll, const fgp_fit_desc* fit, int iter0, int iters, int final_no_update,
                 void* stream) {
   Nll a;
@@ -1894,6 +1918,7 @@ int fgp_fit_run(const fgp_nll_desc* nll, const fgp_fit_desc* fit, int iter0, int
     }
     if (hipMemsetAsync(fz.counters, 0, sizeof(unsigned) * (size_t)ncnt, st) != hipSuccess)
       return set_error(kErrHip, "fgp_fit_run: counter reset failed");
+    if (fuse_spec) fz.check = g_handoff_check;
   }
   if (fuse_spec) {
     // one k_spec_tile launch per iteration; the step of iteration i runs in launch i + 1's prologue (its

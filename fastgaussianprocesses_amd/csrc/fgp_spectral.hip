@@ -710,6 +710,35 @@ __device__ __forceinline__ void barrier_keep_vm() {
   asm volatile("" ::: "memory");
 }
 
+// fgp_handoff_check (a test hook, fz.check): lane 0 of each storing wave reads back the partials it stored
+// (its own retired stores) and XORs their bits into the group's words [grp][g][q] with agent-scope atomics,
+// before the workgroup's arrival -- ordered like the partials by the same vmcnt(0) wait ...
+__device__ __noinline__ void handoff_check_store(const Nll& a, const FitFuse& fz, int grp, int g0, int ppw, int GS,
+                                                 int blk, bool active) {
+  if (!active || (threadIdx.x & 63) != 0) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  for (int p = 0; p < ppw && g0 + p < GS; ++p)
+    for (int q = 0; q < a.nq; ++q) {
+      const double v = __hip_atomic_load(part_ptr(a, g0 + p, q, blk), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_xor(fz.check + ((int64_t)grp * a.G + g0 + p) * a.nq + q, (unsigned long long)__double_as_longlong(v),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// ... and the group's last arriver (thread (g, q)) recomputes the XOR from the partials it reads (sc1 loads, as
+// spec_group_sum), counts a mismatch, and re-arms the word
+__device__ __noinline__ void handoff_check_verify(const Nll& a, const FitFuse& fz, int grp, int g, int q) {
+  const int b0 = grp * kSpecGroup, nbg = min(kSpecGroup, a.nb - b0);
+  unsigned long long x = 0;
+  for (int b = 0; b < nbg; ++b)
+    x ^= (unsigned long long)__double_as_longlong(
+        __hip_atomic_load(part_ptr(a, g, q, b0 + b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  unsigned long long* wd = fz.check + ((int64_t)grp * a.G + g) * a.nq + q;
+  if (__hip_atomic_load(wd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != x)
+    __hip_atomic_fetch_add(fz.check + kHandoffWords + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(wd, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // One fit iteration when every problem shares ONE set of spectra and the problem groups fit in the four
 // waves of a workgroup (PG = ceil(G / PPW) <= 4; the C4 shifts, single GPs) -- or, for many problems, over
 // problem slices of 4 PPW problems (spec_geometry) -- and the ring of kSpecRing chunks fits kSpecLdsMax
@@ -833,6 +862,7 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
   for (int p = 0; p < PPW; ++p)
     if (on[p] && active)
       spec_block_partials<D, NET>(a, h[p], goff + g0 + p, blk, rootn, wl, acc[p], fz.counters != nullptr, a.partials);
+  if (fz.check && fz.counters) handoff_check_store(a, fz, blk / kSpecGroup, g0, PPW, GS, blk, active);
   if (fz.counters) {
     // Level 1 of the fused reduction (MI355X_MICROARCH.md hand-off row 1: sc1 stores retired by every
     // storing wave, then ONE lane's agent-scope add; the waiter reads with sc1 loads after a barrier): the
@@ -856,7 +886,10 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
         const int g = t / a.nq, q = t % a.nq;
         __hip_atomic_store(part2_ptr(a, fz.par, g, q, grp), spec_group_sum<true>(a, g, q, grp), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
+        if (fz.check) handoff_check_verify(a, fz, grp, g, q);
       }
+      if (fz.check && threadIdx.x == 0)
+        __hip_atomic_fetch_add(fz.check + kHandoffWords, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (threadIdx.x == 0) __hip_atomic_store(cnt_grp, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }

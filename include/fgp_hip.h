@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define FGP_ABI_VERSION 14
+#define FGP_ABI_VERSION 15
 
 #define FGP_OK 0
 #define FGP_ERR_INVALID (-1)     /* bad argument (shape, stride, null pointer) */
@@ -549,6 +549,14 @@ int fgp_mt_fit_nparams(const fgp_mt_fit_desc* desc, int* n_params);
 int fgp_mt_fit_work(const fgp_mt_fit_desc* desc, int64_t* bytes);
 /* iterations iter0 .. iter0 + iters - 1 (history rows); with final_no_update the last one evaluates only */
 int fgp_mt_fit_run(const fgp_mt_fit_desc* desc, int iter0, int iters, int final_no_update, void* stream);
+
+/* ABI 15 -- consistency check of the fused spectral fit's last-arriver hand-off (a test hook, no reference
+ * counterpart).  enable != 0 arms it for the following fgp_fit_run calls: every wave of the one-launch
+ * iteration kernel XORs the bits of the partials it stored into a per-group word (agent-scope atomics, before
+ * its arrival), and each group's last arriver recomputes that XOR from the partials it reads and counts a
+ * mismatch.  enable == 0 synchronises the device, disarms it and returns out[0] = group hand-offs checked,
+ * out[1] = mismatches (0 when every arriver saw every stored partial). */
+int fgp_handoff_check(int enable, unsigned long long* out);
 
 #ifdef __cplusplus
 }

@@ -81,3 +81,29 @@ def test_bench_step_matches_oracle_and_individual_fits(monkeypatch, m, path):
         opv = o.post_var(xv)
         kxx = float(o.kernel(xv, xv).detach().abs().max())
         assert float((pv[p] - opv).abs().max()) <= 1e-8 * kxx
+
+
+def test_fused_iteration_handoff_is_consistent(monkeypatch):
+    """The relaxed last-arriver hand-off of k_spec_tile (sc1 partial stores, vmcnt(0), a relaxed agent-scope
+    add: MI355X_MICROARCH.md hand-off row 1) checked in the suite, once: fgp_handoff_check arms a per-group
+    XOR of the partials' bits accumulated by the storing waves before their arrival, and every group's last
+    arriver recomputes it from what it reads -- C4's 16 groups x 40 iterations, no mismatch allowed."""
+    import ctypes
+    from fastgaussianprocesses_amd import _native as N
+    monkeypatch.setenv("FGP_PARTS_GEN", "1")
+    d, n, P, iters = 5, 2 ** 20, 8, 40
+    dev = torch.device(DEV, 0)
+    sh = bench.Shifts(F, d, n, bench.shard_seeds(0, 1, P), dev)
+    g = torch.Generator().manual_seed(17)
+    xm, xv = torch.rand((8, d), generator=g).to(dev), torch.rand((2, d), generator=g).to(dev)
+    out = (ctypes.c_ulonglong * 2)()
+    N.call("fgp_handoff_check", 1, out)
+    try:
+        data, _, _ = bench.step_batched(sh, argparse.Namespace(fit_iters=iters), xm, xv, store_loss_hist=True)
+    finally:
+        N.call("fgp_handoff_check", 0, out)
+    assert all(dd["iterations"] == iters for dd in data)
+    groups = 512 // 32                      # nb = 512 k blocks at n = 2^20, kSpecGroup = 32
+    # one k_spec_tile launch per evaluated iteration (iterations 0 .. iters: the last evaluates only)
+    assert out[0] % groups == 0 and iters * groups <= out[0] <= (iters + 1) * groups, (out[0], out[1])
+    assert out[1] == 0, "last arrivers read %d partial groups that differ from what was stored" % out[1]
