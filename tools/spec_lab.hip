@@ -143,36 +143,38 @@ struct Args {
 // issues j = w, w + 4, ...  (5 each).  DYN: the workgroup's blocks come from an atomic counter, dequeued two
 // ahead into an LDS ring seq[4] (thread 0 issues the add behind a chunk's DMA; its value is stored to LDS at
 // the next iteration, before that iteration's barrier); requires cpb >= RING - 1.
-template <int RING, bool DYN, bool SADDR, int MODE, int WPC>
-__global__ __launch_bounds__(256, WPC) void k_lab(Args a) {
+template <int RING, bool DYN, bool SADDR, int MODE, int WPC, int PPW = 2>
+__global__ __launch_bounds__(64 * G / PPW, WPC) void k_lab(Args a) {
+  constexpr int W = G / PPW, TPW = (20 + W - 1) / W;   // waves; DMA wave-instructions per wave (at most)
   extern __shared__ double lds[];
   __shared__ int seq[4];
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   if (a.stamps && threadIdx.x == 0) a.stamps[blockIdx.x * 2] = wall_clock64();
-  HypS h[2];
+  HypS h[PPW];
 #pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    const double* hp = a.hyp + (2 * w + p) * (2 + D);
+  for (int p = 0; p < PPW; ++p) {
+    const double* hp = a.hyp + (PPW * w + p) * (2 + D);
     h[p].scale = hp[0];
     h[p].noise = hp[1];
 #pragma unroll
     for (int j = 0; j < D; ++j) h[p].ls[j] = hp[2 + j];
   }
   const double rootn = 1024.0, wl = 1.0;
-  const double* src0[5];
-  long step[5];
+  const double* src0[TPW];
+  long step[TPW];
   if (!SADDR) {
 #pragma unroll
-    for (int t = 0; t < 5; ++t) {
-      const int j = w + 4 * t;
+    for (int t = 0; t < TPW; ++t) {
+      const int j = w + W * t;
       src0[t] = j < 16 ? a.basis + j * 128 + lane * 2 : a.ysq + (j - 16) * 128 + lane * 2;
       step[t] = j < 16 ? NS * 64 : G * 64;
     }
   }
   auto issue = [&](long q, double* buf) {
 #pragma unroll
-    for (int t = 0; t < 5; ++t) {
-      const int j = w + 4 * t;
+    for (int t = 0; t < TPW; ++t) {
+      const int j = w + W * t;
+      if (j >= 20) break;
       const double* src;
       if (SADDR) {
         const double* base = j < 16 ? a.basis + q * (NS * 64) + j * 128 : a.ysq + q * (G * 64) + (j - 16) * 128;
@@ -186,11 +188,12 @@ __global__ __launch_bounds__(256, WPC) void k_lab(Args a) {
   const int cpb = a.cpb, nblk = a.nblk;
   int kd = 0;   // blocks dequeued (DYN)
   if (DYN) {
-    if (threadIdx.x == 0) {
-      seq[0] = (int)atomicAdd(a.counters, 1u);
-      seq[1] = (int)atomicAdd(a.counters, 1u);
-    }
-    kd = 2;
+    // RING blocks ahead: the issue position runs up to RING - 1 chunks (<= one block at cpb >= RING - 1) past
+    // the compute position, and the block after it must be known by then
+    static_assert(RING <= 3, "seq[4] holds the compute block and at most 3 ahead");
+    if (threadIdx.x == 0)
+      for (int i = 0; i < RING; ++i) seq[i] = (int)atomicAdd(a.counters, 1u);
+    kd = RING;
     __syncthreads();
   }
   auto block_of = [&](int k) -> int { return DYN ? seq[k & 3] : (k == 0 ? (int)blockIdx.x : nblk); };
@@ -199,7 +202,7 @@ __global__ __launch_bounds__(256, WPC) void k_lab(Args a) {
   int ib = block_of(0);
   int issued = 0;
   auto issue_next = [&](int slot) {
-    if (ib >= nblk) return;
+    if ((unsigned)ib >= (unsigned)nblk) return;
     if (MODE != 2) issue((long)ib * cpb + ii, lds + slot * TILE);
     ++issued;
     if (++ii == cpb) {
@@ -210,14 +213,14 @@ __global__ __launch_bounds__(256, WPC) void k_lab(Args a) {
   };
 #pragma unroll
   for (int c = 0; c < RING - 1; ++c) issue_next(c);
-  Acc acc[2];
+  Acc acc[PPW];
   int c = 0, kp = 0, pi = 0;
   int pb = block_of(0);
   unsigned pend = 0;      // thread 0: a dequeue in flight (its value goes to seq[pend_slot] next iteration)
   int pend_slot = -1;
-  while (pb < nblk) {
+  while ((unsigned)pb < (unsigned)nblk) {
     const int behind = issued - c - 1;
-    wait_ring<RING>(MODE == 2 ? 0 : 5 * std::min(behind, RING - 2));
+    wait_ring<RING>(MODE == 2 ? 0 : TPW * std::min(behind, RING - 2));
     if (DYN && pend_slot >= 0) {
       if (threadIdx.x == 0) seq[pend_slot] = (int)pend;
       pend_slot = -1;
@@ -230,15 +233,15 @@ __global__ __launch_bounds__(256, WPC) void k_lab(Args a) {
 #pragma unroll
       for (int s = 0; s < NS; ++s) phi[s] = buf[64 * s + lane];
 #pragma unroll
-      for (int p = 0; p < 2; ++p) terms(phi, h[p], rootn, wl, buf[64 * (NS + 2 * w + p) + lane], acc[p]);
+      for (int p = 0; p < PPW; ++p) terms(phi, h[p], rootn, wl, buf[64 * (NS + PPW * w + p) + lane], acc[p]);
     } else {
-      acc[0].norm += buf[lane] + buf[64 * (NS + 2 * w) + lane];
+      acc[0].norm += buf[lane] + buf[64 * (NS + PPW * w) + lane];
     }
     ++c;
     if (++pi == cpb) {
 #pragma unroll
-      for (int p = 0; p < 2; ++p) {
-        wave_partials(acc[p], a.partials + (long)(2 * w + p) * NQ * nblk + pb, nblk);
+      for (int p = 0; p < PPW; ++p) {
+        wave_partials(acc[p], a.partials + (long)(PPW * w + p) * NQ * nblk + pb, nblk);
         acc[p] = Acc();
       }
       pi = 0;
@@ -266,6 +269,81 @@ __global__ __launch_bounds__(256, WPC) void k_lab(Args a) {
   if (a.stamps && threadIdx.x == 0) {
     a.stamps[blockIdx.x * 2 + 1] = wall_clock64();
     a.xcc[blockIdx.x] = __builtin_amdgcn_s_getreg((3 << 11) | 20);   // HW_REG_XCC_ID[3:0]
+  }
+}
+
+
+template <int N>
+__device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+// Second family (fixed block per workgroup, 2-slot ring, 2 problems per wave, wave-uniform DMA bases):
+//   CK     64-frequency sub-chunks per ring slot (fewer barriers per byte; CK = 2: 80 KB of LDS per workgroup)
+//   AUX    cache-policy bits of the LDS-DMA loads (2 = nt)
+//   PROUS  a synthetic prologue of PROUS us before the loop (the fused kernel's deferred step: level-2 sums +
+//          Rprop), with PRE = 1 or 2 chunks issued in front of it
+template <int CK, int AUX, int PROUS, int PRE, int MODE>
+__global__ __launch_bounds__(256, 2) void k_lab2(Args a) {
+  constexpr int W = 4, NI = 20 * CK, TPW = NI / W, T2 = TILE * CK, SPX = CK * NS * 64;
+  static_assert(NI % W == 0, "whole DMA rounds");
+  extern __shared__ double lds[];
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  if (a.stamps && threadIdx.x == 0) a.stamps[blockIdx.x * 2] = wall_clock64();
+  HypS h[2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const double* hp = a.hyp + (2 * w + p) * (2 + D);
+    h[p].scale = hp[0];
+    h[p].noise = hp[1];
+#pragma unroll
+    for (int j = 0; j < D; ++j) h[p].ls[j] = hp[2 + j];
+  }
+  const double rootn = 1024.0, wl = 1.0;
+  const int nc = a.cpb;
+  const long q0 = (long)blockIdx.x * nc;
+  auto issue = [&](int c, double* buf) {
+    const long q = q0 + c;
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+      const int j = w + W * t;
+      const double* base = j < 16 * CK ? a.basis + q * (CK * NS * 64) + j * 128 : a.ysq + q * (CK * G * 64) + (j - 16 * CK) * 128;
+      __builtin_amdgcn_global_load_lds((glb_void*)(base + lane * 2), (lds_void*)(buf + 128 * j), 16, 0, AUX);
+    }
+  };
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (MODE != 2) {
+    issue(0, lds);
+    if (PRE == 2 && nc > 1) issue(1, lds + T2);
+  }
+  if (PROUS > 0) {
+    const unsigned long long t0 = wall_clock64();
+    while (wall_clock64() - t0 < (unsigned long long)(PROUS * 100)) __builtin_amdgcn_s_sleep(2);
+  }
+  Acc acc[2];
+  for (int c = 0; c < nc; ++c) {
+    if (PRE == 2 && c == 0 && nc > 1 && MODE != 2) wait_vm<TPW>();
+    else wait_vm<0>();
+    barrier_keep_vm();
+    if (MODE != 2 && c + 1 < nc && c + 1 >= PRE) issue(c + 1, lds + ((c + 1) & 1) * T2);
+    const double* buf = lds + (c & 1) * T2;
+    if (MODE != 1) {
+#pragma unroll
+      for (int sc = 0; sc < CK; ++sc) {
+        double phi[NS];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) phi[s] = buf[(sc * NS + s) * 64 + lane];
+#pragma unroll
+        for (int p = 0; p < 2; ++p) terms(phi, h[p], rootn, wl, buf[SPX + (sc * G + 2 * w + p) * 64 + lane], acc[p]);
+      }
+    } else {
+      acc[0].norm += buf[lane] + buf[SPX + 2 * w * 64 + lane];
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int p = 0; p < 2; ++p) wave_partials(acc[p], a.partials + (long)(2 * w + p) * NQ * a.nblk + blockIdx.x, a.nblk);
+  if (a.stamps && threadIdx.x == 0) {
+    a.stamps[blockIdx.x * 2 + 1] = wall_clock64();
+    a.xcc[blockIdx.x] = __builtin_amdgcn_s_getreg((3 << 11) | 20);
   }
 }
 
@@ -319,14 +397,14 @@ int main(int argc, char** argv) {
   a.partials = dp;
   a.counters = dc;
   std::vector<double> ref;
-  auto run = [&](const char* name, auto kern, int ring, int grid, int cpb, bool check) {
+  auto run = [&](const char* name, auto kern, int ring, int grid, int cpb, bool check, int threads = 256, int ck = 1) {
     a.cpb = cpb;
-    a.nblk = (int)(Q / cpb);
+    a.nblk = (int)(Q / ((long)cpb * ck));
     a.stamps = nullptr;
-    const size_t shm = (size_t)ring * TILE * 8;
+    const size_t shm = (size_t)ring * TILE * 8 * ck;
     CK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
     CK(hipMemset(dp, 0, (size_t)G * NQ * 8192 * 8));
-    const double us = time_us([&] { kern<<<grid, 256, shm>>>(a); }, 50);
+    const double us = time_us([&] { kern<<<grid, threads, shm>>>(a); }, 50);
     CK(hipGetLastError());
     CK(hipDeviceSynchronize());
     // checksum of the partials against the first full variant (same blocks => same values)
@@ -343,7 +421,7 @@ int main(int argc, char** argv) {
     }
     // stamps pass
     a.stamps = ds;
-    kern<<<grid, 256, shm>>>(a);
+    kern<<<grid, threads, shm>>>(a);
     CK(hipDeviceSynchronize());
     std::vector<unsigned long long> st((size_t)grid * 2);
     std::vector<int> xc(grid);
@@ -374,6 +452,7 @@ int main(int argc, char** argv) {
            dur[grid * 9 / 10], endt[grid / 2], endt[grid * 9 / 10], xs, err);
     fflush(stdout);
   };
+  const bool all = argc > 1;   // the slower families measured in r04a / r04b (profiles/r04_lab.jsonl)
   // the current structure: fixed block per workgroup, 512 x 16 chunks, pointer arrays, 2-slot ring
   run("fixed ptr r2", k_lab<2, false, false, 0, 2>, 2, 512, 16, true);
   run("fixed ptr r2 stream", k_lab<2, false, false, 1, 2>, 2, 512, 16, false);
@@ -381,9 +460,10 @@ int main(int argc, char** argv) {
   run("fixed saddr r2", k_lab<2, false, true, 0, 2>, 2, 512, 16, true);
   run("fixed saddr r3", k_lab<3, false, true, 0, 2>, 3, 512, 16, true);
   run("fixed saddr r2 1024x8", k_lab<2, false, true, 0, 2>, 2, 1024, 8, true);
-  run("fixed saddr r2 1024x8 wpc3", k_lab<2, false, true, 0, 3>, 2, 1024, 8, true);
-  run("fixed saddr r2 2048x4 wpc3", k_lab<2, false, true, 0, 3>, 2, 2048, 4, true);
+  if (all) run("fixed saddr r2 1024x8 wpc3", k_lab<2, false, true, 0, 3>, 2, 1024, 8, true);
+  if (all) run("fixed saddr r2 2048x4 wpc3", k_lab<2, false, true, 0, 3>, 2, 2048, 4, true);
   for (int cpb : {2, 4, 8}) {
+    if (!all) break;
     for (int res : {2, 3}) {
       char nm[64];
       snprintf(nm, sizeof nm, "dyn saddr r2 res%d", res);
@@ -393,10 +473,28 @@ int main(int argc, char** argv) {
       if (res == 2) run(nm, k_lab<3, true, true, 0, 2>, 3, 256 * res, cpb, true);
     }
   }
-  run("fixed saddr r2 1024x8 wpc4", k_lab<2, false, true, 0, 4>, 2, 1024, 8, true);
-  run("dyn saddr r2 res4 cpb4", k_lab<2, true, true, 0, 4>, 2, 1024, 4, true);
-  run("dyn saddr r2 res4 cpb8", k_lab<2, true, true, 0, 4>, 2, 1024, 8, true);
-  run("dyn saddr r2 res3 stream", k_lab<2, true, true, 1, 3>, 2, 768, 4, false);
-  run("dyn saddr r2 res3 compute", k_lab<2, true, true, 2, 3>, 2, 768, 4, false);
+  if (all) run("fixed saddr r2 1024x8 wpc4", k_lab<2, false, true, 0, 4>, 2, 1024, 8, true);
+  if (all) run("dyn saddr r2 res4 cpb4", k_lab<2, true, true, 0, 4>, 2, 1024, 4, true);
+  if (all) run("dyn saddr r2 res4 cpb8", k_lab<2, true, true, 0, 4>, 2, 1024, 8, true);
+  if (all) run("dyn saddr r2 res3 stream", k_lab<2, true, true, 1, 3>, 2, 768, 4, false);
+  if (all) run("dyn saddr r2 res3 compute", k_lab<2, true, true, 2, 3>, 2, 768, 4, false);
+  // one problem per wave, 8 waves per workgroup (one acc set, fewer VGPRs, 4 waves per SIMD)
+  run("fixed saddr r2 ppw1 wpc4", k_lab<2, false, true, 0, 4, 1>, 2, 512, 16, true, 512);
+  run("fixed saddr r2 ppw1 wpc4 stream", k_lab<2, false, true, 1, 4, 1>, 2, 512, 16, false, 512);
+  run("fixed saddr r2 ppw1 wpc4 compute", k_lab<2, false, true, 2, 4, 1>, 2, 512, 16, false, 512);
+  run("fixed saddr r2 ppw1 1024x8 wpc4", k_lab<2, false, true, 0, 4, 1>, 2, 1024, 8, true, 512);
+  if (all) run("dyn saddr r2 ppw1 res2 cpb4", k_lab<2, true, true, 0, 4, 1>, 2, 512, 4, true, 512);
+  if (all) run("dyn saddr r2 ppw1 res2 cpb8", k_lab<2, true, true, 0, 4, 1>, 2, 512, 8, true, 512);
+  // second family: sub-chunks per slot, nt, prologue overlap
+  run("lab2 ck1", k_lab2<1, 0, 0, 1, 0>, 2, 512, 16, true, 256, 1);
+  run("lab2 ck2", k_lab2<2, 0, 0, 1, 0>, 2, 512, 8, true, 256, 2);
+  run("lab2 ck2 compute", k_lab2<2, 0, 0, 1, 2>, 2, 512, 8, false, 256, 2);
+  run("lab2 ck2 stream", k_lab2<2, 0, 0, 1, 1>, 2, 512, 8, false, 256, 2);
+  run("lab2 ck1 nt", k_lab2<1, 2, 0, 1, 0>, 2, 512, 16, true, 256, 1);
+  run("lab2 ck1 nt stream", k_lab2<1, 2, 0, 1, 1>, 2, 512, 16, false, 256, 1);
+  run("lab2 ck2 nt", k_lab2<2, 2, 0, 1, 0>, 2, 512, 8, true, 256, 2);
+  run("lab2 ck1 pro2 pre1", k_lab2<1, 0, 2, 1, 0>, 2, 512, 16, true, 256, 1);
+  run("lab2 ck1 pro2 pre2", k_lab2<1, 0, 2, 2, 0>, 2, 512, 16, true, 256, 1);
+  run("lab2 ck2 pro2 pre2", k_lab2<2, 0, 2, 2, 0>, 2, 512, 8, true, 256, 2);
   return 0;
 }
