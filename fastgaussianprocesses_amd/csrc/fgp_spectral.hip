@@ -310,10 +310,17 @@ __device__ __forceinline__ void spec_level2(const Nll& a, int par, double* tot) 
 // single-tensor, loss = 1/2 (norm + w logdet + const), histories).  The state is read from `in`; with
 // `write` the histories, the gradient and the new state (to `out`, which may be `in`) are stored; the new
 // raw parameters also go to newraw[p] when given (the deferred step of k_spec_tile, in every workgroup).
+// parameter slot k (0 scale, 1 .. dl lengthscales, dl + 1 noise) of problem g: its index in the raw vector
+__device__ __forceinline__ int spec_slot_param(const Nll& a, int g, int k, int dl) {
+  if (k == 0) return a.scale_off + (a.scale_pp ? g : 0);
+  if (k <= dl) return a.ls_off + (a.ls_pp ? g : 0) * dl + (k - 1);
+  return a.noise_off + (a.noise_pp ? g : 0);
+}
+
 template <int D>
 __device__ __forceinline__ void spec_finish(const Nll& a, const Fit& f, const double* tot, int g0, int cnt, int iter,
                                             int do_update, const RpState& in, const RpState& out, bool write,
-                                            double* newraw, int state_write = -1) {
+                                            double* newraw, int state_write = -1, const double* pf = nullptr) {
   const bool wstate = state_write < 0 ? write : state_write != 0;   // the new state to `out` (default: with write)
   const int i = threadIdx.x >> 4, k = threadIdx.x & 15;
   if (i >= cnt) return;
@@ -328,14 +335,13 @@ __device__ __forceinline__ void spec_finish(const Nll& a, const Fit& f, const do
     lh[2] = term2;
   }
   if (k >= 2 + dl) return;
-  int p, rg;
+  const int p = spec_slot_param(a, g, k, dl);
+  int rg;
   double gp;
   if (k == 0) {
-    p = a.scale_off + (a.scale_pp ? g : 0);
     rg = f.scale_rg;
     gp = v[3];
   } else if (k <= dl) {
-    p = a.ls_off + (a.ls_pp ? g : 0) * dl + (k - 1);
     rg = f.ls_rg;
     gp = 0.0;
     if (a.ls_pd) {
@@ -346,11 +352,11 @@ __device__ __forceinline__ void spec_finish(const Nll& a, const Fit& f, const do
       for (int j = 0; j < D; ++j) gp += v[4 + j];
     }
   } else {
-    p = a.noise_off + (a.noise_pp ? g : 0);
     rg = f.noise_rg;
     gp = 0.0;
   }
-  const double raw_p = in.raw[p], prev_p = in.prev[p], step_p = in.step[p];
+  // (pf: this thread's state, prefetched by the caller beside its other loads)
+  const double raw_p = pf ? pf[0] : in.raw[p], prev_p = pf ? pf[1] : in.prev[p], step_p = pf ? pf[2] : in.step[p];
   if (k == dl + 1) gp = exp(raw_p) * v[2];
   if (write) {
     f.raw_hist[(int64_t)iter * f.n_params + p] = raw_p;
@@ -713,7 +719,7 @@ __device__ __forceinline__ void barrier_keep_vm() {
 // fgp_handoff_check (a test hook, fz.check): lane 0 of each storing wave reads back the partials it stored
 // (its own retired stores) and XORs their bits into the group's words [grp][g][q] with agent-scope atomics,
 // before the workgroup's arrival -- ordered like the partials by the same vmcnt(0) wait ...
-__device__ __noinline__ void handoff_check_store(const Nll& a, const FitFuse& fz, int grp, int g0, int ppw, int GS,
+__device__ __forceinline__ void handoff_check_store(const Nll& a, const FitFuse& fz, int grp, int g0, int ppw, int GS,
                                                  int blk, bool active) {
   if (!active || (threadIdx.x & 63) != 0) return;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -727,7 +733,7 @@ __device__ __noinline__ void handoff_check_store(const Nll& a, const FitFuse& fz
 
 // ... and the group's last arriver (thread (g, q)) recomputes the XOR from the partials it reads (sc1 loads, as
 // spec_group_sum), counts a mismatch, and re-arms the word
-__device__ __noinline__ void handoff_check_verify(const Nll& a, const FitFuse& fz, int grp, int g, int q) {
+__device__ __forceinline__ void handoff_check_verify(const Nll& a, const FitFuse& fz, int grp, int g, int q) {
   const int b0 = grp * kSpecGroup, nbg = min(kSpecGroup, a.nb - b0);
   unsigned long long x = 0;
   for (int b = 0; b < nbg; ++b)
@@ -791,7 +797,7 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
   // and per-chunk step per lane, formed once (a chunk further is NS 64 doubles on in the chunked spectra,
   // 64 in a Y row).
   constexpr int kMaxDma = kSpecMaxDma;              // tile <= 512 kMaxDma doubles: 1-KiB instructions, kMaxDma per wave
-  static_assert(RING >= 2, "the deferred step's scratch lives in ring slot RING - 1");
+  static_assert(RING >= 2, "a chunk in flight under each chunk's compute");
   const double* src0[kMaxDma];
   int64_t step[kMaxDma];
 #pragma unroll
@@ -818,21 +824,33 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
   const unsigned wofs = (unsigned)(bw * rows * 64 + lane);   // this lane's spectra in a buffer: wofs + 64 s
   const unsigned yofs = wofs + (unsigned)(NS + g0) * 64u;     // ... its problems' Y: yofs + 64 p
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // only the chunk loads below are counted
+  // every ring slot filled before the loop (the prologue below runs under them): chunks 0 .. pre - 1
+  const int pre = min(RING, nc);
 #pragma unroll
-  for (int c = 0; c < RING - 1; ++c)
-    if (c < nc) issue(c, lds + c * tile);
+  for (int c = 0; c < RING; ++c)
+    if (c < pre) issue(c, lds + c * tile);
+  int issued = pre;
   // The parameters of this iteration.  With fz.pending the previous iteration's step was deferred into
   // this launch: every workgroup sums its group sums (level 2, fixed order) and applies the Rprop step
   // (identical arithmetic, identical results), workgroup 0 alone storing histories and the new state,
-  // while the first chunks are in flight; the parameters then come from LDS (scratch after the ring).
+  // while the first chunks are in flight; the parameters then come from LDS (scr).  The Rprop state is
+  // loaded beside the level-2 sums (one round trip, not two).
+  __shared__ double scr[kSpecScratch];              // [G nq] level-2 totals, then [np] new raw parameters
   Hyp h[PPW];
   if (fz.counters && fz.pending) {
-    double* tot = lds + (RING - 1) * tile;          // [G nq] level-2 totals, then [np] new raw parameters, in the
-                                                    // ring slot no chunk is loaded into before the loop
+    double* tot = scr;
     double* nraw = tot + G * a.nq;
+    const int si = threadIdx.x >> 4, sk = threadIdx.x & 15, dl = a.ls_pd ? a.d : 1;
+    double pf[3] = {0.0, 0.0, 0.0};
+    if (si < G && sk < 2 + dl) {
+      const int p = spec_slot_param(a, si, sk, dl);
+      pf[0] = fz.sin.raw[p];
+      pf[1] = fz.sin.prev[p];
+      pf[2] = fz.sin.step[p];
+    }
     spec_level2<D>(a, fz.par ^ 1, tot);
     __syncthreads();
-    spec_finish<D>(a, fz.f, tot, 0, G, fz.iter - 1, 1, fz.sin, fz.sout, blockIdx.x == 0, nraw);
+    spec_finish<D>(a, fz.f, tot, 0, G, fz.iter - 1, 1, fz.sin, fz.sout, blockIdx.x == 0, nraw, -1, pf);
     __syncthreads();
 #pragma unroll
     for (int p = 0; p < PPW; ++p) load_hyp_wave(a, on[p] ? g0 + p : 0, h[p], nraw);
@@ -841,10 +859,13 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
     for (int p = 0; p < PPW; ++p) load_hyp_wave(a, on[p] ? goff + g0 + p : 0, h[p]);
   }
   for (int c = 0; c < nc; ++c) {
-    // this wave's loads of chunk c have landed (chunks c + 1 .. c + RING - 2 may stay in flight)
-    wait_vmcnt(RING == 2 ? 0 : cnt_w * min(RING - 2, nc - 1 - c));
+    // this wave's loads of chunk c have landed (chunks c + 1 .. issued - 1 may stay in flight)
+    wait_vmcnt(cnt_w * (issued - 1 - c));
     barrier_keep_vm();                              // ... every wave's; every wave done with chunk c - 1
-    if (c + RING - 1 < nc) issue(c + RING - 1, lds + ((c + RING - 1) % RING) * tile);
+    if (issued < nc && issued <= c + RING - 1) {    // into the slot of chunk c - 1
+      issue(issued, lds + (issued % RING) * tile);
+      ++issued;
+    }
     const double* buf = lds + (unsigned)(c % RING) * (unsigned)tile;
     if (active) {
       const double* wb = buf + wofs;
