@@ -708,6 +708,15 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
   }
 }
 
+// k_spec_tile's prologue (A/B builds, tools/build_exp.sh): chunks issued before the deferred step (at most the
+// ring), and the Rprop state loaded beside the level-2 sums (1) or after them (0)
+#ifndef FGP_SPEC_PRE
+#define FGP_SPEC_PRE 2
+#endif
+#ifndef FGP_SPEC_PF
+#define FGP_SPEC_PF 1
+#endif
+
 // workgroup barrier that lets LDS-DMA loads stay in flight across it (__syncthreads() would drain them
 // with vmcnt(0)): the waves' LDS accesses retired (lgkmcnt), the raw barrier, a compiler memory fence
 __device__ __forceinline__ void barrier_keep_vm() {
@@ -825,7 +834,7 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
   const unsigned yofs = wofs + (unsigned)(NS + g0) * 64u;     // ... its problems' Y: yofs + 64 p
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // only the chunk loads below are counted
   // every ring slot filled before the loop (the prologue below runs under them): chunks 0 .. pre - 1
-  const int pre = min(RING, nc);
+  const int pre = min(min(FGP_SPEC_PRE, RING), nc);
 #pragma unroll
   for (int c = 0; c < RING; ++c)
     if (c < pre) issue(c, lds + c * tile);
@@ -842,7 +851,7 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
     double* nraw = tot + G * a.nq;
     const int si = threadIdx.x >> 4, sk = threadIdx.x & 15, dl = a.ls_pd ? a.d : 1;
     double pf[3] = {0.0, 0.0, 0.0};
-    if (si < G && sk < 2 + dl) {
+    if (FGP_SPEC_PF && si < G && sk < 2 + dl) {
       const int p = spec_slot_param(a, si, sk, dl);
       pf[0] = fz.sin.raw[p];
       pf[1] = fz.sin.prev[p];
@@ -850,7 +859,7 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
     }
     spec_level2<D>(a, fz.par ^ 1, tot);
     __syncthreads();
-    spec_finish<D>(a, fz.f, tot, 0, G, fz.iter - 1, 1, fz.sin, fz.sout, blockIdx.x == 0, nraw, -1, pf);
+    spec_finish<D>(a, fz.f, tot, 0, G, fz.iter - 1, 1, fz.sin, fz.sout, blockIdx.x == 0, nraw, -1, FGP_SPEC_PF ? pf : nullptr);
     __syncthreads();
 #pragma unroll
     for (int p = 0; p < PPW; ++p) load_hyp_wave(a, on[p] ? g0 + p : 0, h[p], nraw);
@@ -1384,7 +1393,7 @@ int launch_spec_iter(const Nll& a, hipStream_t st, const FitFuse* fz) {
           bool done = false;
           for (int i = 0; i < nraised; ++i) done = done || raised[i] == kp;
           if (!done) {
-            hipFuncSetAttribute(kp, hipFuncAttributeMaxDynamicSharedMemorySize, kSpecLdsMax);
+            (void)hipFuncSetAttribute(kp, hipFuncAttributeMaxDynamicSharedMemorySize, kSpecLdsMax);
             if (nraised < 64) raised[nraised++] = kp;
           }
           kern<<<grid, kWG, shm, st>>>(a, f);
