@@ -71,6 +71,15 @@ __device__ __forceinline__ void stamp_end(const Nll& a) {
     a.stamps[(int64_t)blockIdx.x * kStampStride + 1 + (threadIdx.x >> 6)] = (unsigned long long)wall_clock64();
 }
 
+// threadIdx.x behind an opaque asm: values derived from it cannot be hoisted out of the loop around the call
+// site (in the persistent k_spec_tile, the reduction / step addresses of every iteration would otherwise be
+// computed once before the iteration loop and held in VGPRs through its chunk loop)
+__device__ __forceinline__ int tid_fresh() {
+  int t = (int)threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
+
 struct Hyp {
   double scale, noise;
   double ls[FGP_MAX_D];
@@ -582,7 +591,13 @@ struct FitFuse {
   RpState sin, sout;
   // fgp_handoff_check (a test hook): [kSpecBlocks / kSpecGroup][G nq] XOR words, then checks, mismatches
   unsigned long long* check;
+  // persistent k_spec_tile (piters > 0): iterations iter .. iter + piters - 1 AND the last one's step in ONE
+  // launch; counters[ng] counts the published group sums, counters[ng + 1] is set when a bounded wait gave up
+  int piters;
 };
+constexpr int kSpecStateMax = 64;                  // Rprop parameters of a persistent k_spec_tile (LDS copies)
+// parameters of a spectral fit (the raw vector's length: the noise block is last)
+__host__ __device__ __forceinline__ int spec_nparams(const Nll& a) { return a.noise_off + (a.noise_pp ? a.G : 1); }
 constexpr int kHandoffWords = 16 * 8 * 16;         // XOR words of the check buffer (groups x G x nq, at most)
 int launch_re_bwd_fused(const Nll& a, const FitFuse& fz, const Tables* tb, hipStream_t st);
 

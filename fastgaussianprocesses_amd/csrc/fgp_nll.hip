@@ -1920,6 +1920,19 @@ int fgp_fit_run(const fgp_nll_desc* nll, const fgp_fit_desc* fit, int iter0, int
       return set_error(kErrHip, "fgp_fit_run: counter reset failed");
     if (fuse_spec) fz.check = g_handoff_check;
   }
+  if (fuse_spec && !getenv_off("FGP_SPEC_PERSIST") && spec_nparams(a) <= kSpecStateMax) {
+    // every iteration and the last step in ONE persistent k_spec_tile launch (falls through to the launch
+    // per iteration when the grid cannot be co-resident)
+    fz.iter = iter0;
+    fz.par = iter0 & 1;
+    fz.pending = 0;
+    fz.piters = iters;
+    fz.sin = fz.sout = RpState{f.raw, f.prev, f.step};
+    fz.do_update = !final_no_update;
+    rc = launch_spec_iter(a, st, &fz);
+    if (rc != kErrUnsupported) return rc;
+    fz.piters = 0;
+  }
   if (fuse_spec) {
     // one k_spec_tile launch per iteration; the step of iteration i runs in launch i + 1's prologue (its
     // state read from the fit's vectors for the first step, else from the scratch copy of parity i,

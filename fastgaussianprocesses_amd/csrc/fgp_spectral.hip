@@ -134,7 +134,7 @@ template <int D, bool NET>
 __device__ __forceinline__ void spec_block_partials(const Nll& a, const Hyp& h, int g, int blk, double rootn, double wl,
                                                     const SpecAcc<D>& acc, bool sc1, double* pbase) {
   constexpr int NS = 1 << D, NV = 4 + D;
-  const int lane = threadIdx.x & 63;
+  const int lane = tid_fresh() & 63;
   double v[NV];
   spec_values<D>(acc, v);
   const double wlin = NET ? 1.0 : 2.0;
@@ -252,7 +252,6 @@ __device__ __forceinline__ int spec_groups(const Nll& a) { return (a.nb + kSpecG
 // The fused run's workspace after the level-1 partials [G][nq][nb]: level-2 inputs (the group sums) of two
 // iterations [2][G][nq][ng] (parity of the iteration: a launch writes its own while it reads the previous
 // one's), two Rprop state copies [2][3][np], then the group counters (ng)
-__host__ __device__ __forceinline__ int spec_nparams(const Nll& a) { return a.noise_off + (a.noise_pp ? a.G : 1); }
 __host__ __device__ __forceinline__ int64_t spec_part2_off(const Nll& a, int par) {
   return (int64_t)a.G * a.nq * a.nb + (int64_t)par * a.G * a.nq * ((a.nb + kSpecGroup - 1) / kSpecGroup);
 }
@@ -286,16 +285,17 @@ __device__ __forceinline__ double spec_group_sum(const Nll& a, int g, int q, int
 
 // level 2 of the fused run: tot[g nq + q] = the ascending sum over the groups of the level-1 sums of parity
 // par (k_spec_reduce_step's order); every group's sum in flight at once (a serial chain of loads costs ~1 us
-// each).  Threads t < G nq; plain loads (the sums were stored by an earlier launch).
-template <int D>
+// each).  Threads t < G nq; plain loads when the sums were stored by an earlier launch, sc1 loads (SC1) when
+// by this one (the persistent k_spec_tile: hand-off row 1).
+template <int D, bool SC1 = false>
 __device__ __forceinline__ void spec_level2(const Nll& a, int par, double* tot) {
   constexpr int MAXG = kSpecBlocks / kSpecGroup;
-  const int t = threadIdx.x, ng = spec_groups(a);
+  const int t = tid_fresh(), ng = spec_groups(a);
   if (t < a.G * a.nq) {
     const int g = t / a.nq, q = t % a.nq;
     double v[MAXG];
 #pragma unroll
-    for (int gr = 0; gr < MAXG; ++gr) v[gr] = *part2_ptr(a, par, g, q, gr < ng ? gr : 0);
+    for (int gr = 0; gr < MAXG; ++gr) v[gr] = ld_part<SC1>(part2_ptr(a, par, g, q, gr < ng ? gr : 0));
     double s = 0.0;
 #pragma unroll
     for (int gr = 0; gr < MAXG; ++gr)
@@ -322,7 +322,7 @@ __device__ __forceinline__ void spec_finish(const Nll& a, const Fit& f, const do
                                             int do_update, const RpState& in, const RpState& out, bool write,
                                             double* newraw, int state_write = -1, const double* pf = nullptr) {
   const bool wstate = state_write < 0 ? write : state_write != 0;   // the new state to `out` (default: with write)
-  const int i = threadIdx.x >> 4, k = threadIdx.x & 15;
+  const int tf = tid_fresh(), i = tf >> 4, k = tf & 15;
   if (i >= cnt) return;
   const int g = g0 + i;
   const double* v = tot + i * a.nq;
@@ -545,6 +545,7 @@ __global__ __launch_bounds__(kWG) void k_spec_finish_step(Nll a, FitFuse fz) {
 // so the trajectory is the multi-launch fit's bit for bit, without a launch per iteration.  Workgroup 0 writes
 // the histories and the final state; out[0] = the last iteration, out[1] = 1 if a barrier poll gave up.
 constexpr int kPersistMaxW = 64;
+constexpr long long kSpecPollMax = 1ll << 22;     // bounded waits of the persistent k_spec_tile
 constexpr int kPersistLdsMax = 96 * 1024;
 constexpr long long kPersistPollMax = 1ll << 22;
 
@@ -589,8 +590,14 @@ __global__ __launch_bounds__(kWG) void k_spec_persist(Nll a, Fit f, int iters, d
   const double rootn = sqrt((double)((int64_t)1 << a.log2n)), wl = a.logdet_weight;
   const RpState st{st_raw, st_prev, st_step};
   const int64_t psize = (int64_t)a.nq * a.nb;      // one parity's partials (G = 1)
+  // (a.stamps: workgroup 0's device clock per iteration -- start, partials stored, barrier passed, reduced,
+  // stepped -- at stamps[5 it + phase]; tools/exp_persist_stamps.py)
+  auto stamp = [&](int it, int ph) {
+    if (a.stamps && blockIdx.x == 0 && tid == 0) a.stamps[5 * it + ph] = wall_clock64();
+  };
   for (int it = 0; it <= iters; ++it) {
     double* pbase = a.partials + (it & 1) * psize;
+    stamp(it, 0);
     Hyp h;
     load_hyp_wave(a, 0, h, st_raw);
     for (int t = w; t < bpw; t += kWG / 64) {
@@ -612,6 +619,7 @@ __global__ __launch_bounds__(kWG) void k_spec_persist(Nll a, Fit f, int iters, d
     // grid barrier it + 1: every wave's sc1 partials retired, one add per workgroup, one bounded poller
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    stamp(it, 1);
     if (tid == 0) {
       __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const unsigned target = (unsigned)(it + 1) * (unsigned)W;
@@ -629,6 +637,7 @@ __global__ __launch_bounds__(kWG) void k_spec_persist(Nll a, Fit f, int iters, d
       if (tid == 0) out[1] = 1;
       return;
     }
+    stamp(it, 2);
     // level 1 (groups of kSpecGroup blocks, ascending) and level 2 (groups ascending): k_spec_reduce_step's order
     for (int e = tid; e < NQ * ng; e += kWG) {
       const int q = e / ng, grp = e - q * ng;
@@ -649,6 +658,7 @@ __global__ __launch_bounds__(kWG) void k_spec_persist(Nll a, Fit f, int iters, d
       tot[tid] = sq;
     }
     __syncthreads();
+    stamp(it, 3);
     if (tid == 0) {
       // AbstractGP.fit's bookkeeping on the loss of this iteration (the value spec_finish records)
       const double lv = 0.5 * (tot[0] + a.logdet_weight * tot[1] + f.mll_const);
@@ -669,6 +679,7 @@ __global__ __launch_bounds__(kWG) void k_spec_persist(Nll a, Fit f, int iters, d
     const int brk = brk_s;
     spec_finish<D>(a, f, tot, 0, 1, it, brk ? 0 : 1, st, st, blockIdx.x == 0, nullptr, 1);
     __syncthreads();
+    stamp(it, 4);
     if (brk) {
       if (blockIdx.x == 0) {
         for (int p = tid; p < np; p += kWG) {
@@ -770,7 +781,7 @@ __device__ __forceinline__ void handoff_check_verify(const Nll& a, const FitFuse
 // LDS (lane-consecutive 8-byte reads: conflict-free).  With fz.counters the LAST workgroup to finish (sc1 partials, an agent-scope arrival
 // counter: MI355X_MICROARCH.md hand-off row 1, as the real-even backward kernel) runs every problem's
 // reduction + Rprop, wave w taking problems w, w + 4, ...
-template <int D, int PPW, bool NET>
+template <int D, int PPW, bool NET, bool PERSIST = false>
 __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
   constexpr int NS = 1 << D;
   constexpr int RING = kSpecRing;                   // chunks in LDS; RING - 1 in flight under a compute
@@ -828,11 +839,52 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
       }
     }
   };
-  SpecAcc<D> acc[PPW];
   const int nc = a.spec_kpl;
   const unsigned wofs = (unsigned)(bw * rows * 64 + lane);   // this lane's spectra in a buffer: wofs + 64 s
   const unsigned yofs = wofs + (unsigned)(NS + g0) * 64u;     // ... its problems' Y: yofs + 64 p
+  __shared__ double scr[kSpecScratch];              // [G nq] level-2 totals, then [np] new raw parameters
+  // Persistent mode (fz.piters > 0, fgp_fit_run): the launch runs iterations fz.iter .. fz.iter + piters - 1,
+  // every workgroup holding the Rprop state in LDS (st_*, updated identically by all, as k_spec_persist); the
+  // launch boundary between iterations becomes a wait on the count of published group sums (the group
+  // finishers' agent-scope adds after their sc1 stores: hand-off row 1; a bounded poll by one lane).
+  __shared__ double st_raw[kSpecStateMax], st_prev[kSpecStateMax], st_step[kSpecStateMax];
+  __shared__ int wfail;
+  constexpr bool persist = PERSIST;                 // (fz.piters > 0: the launcher picks this instance)
+  const int nit = persist ? fz.piters : 1, ng = spec_groups(a);
+  const RpState lst{st_raw, st_prev, st_step};
+  unsigned* done_ctr = fz.counters ? fz.counters + ng : nullptr;
+  if constexpr (PERSIST) {
+    const int np = spec_nparams(a);
+    for (int p = threadIdx.x; p < np; p += kWG) {
+      st_raw[p] = fz.sin.raw[p];
+      st_prev[p] = fz.sin.prev[p];
+      st_step[p] = fz.sin.step[p];
+    }
+  }
+  // thread 0: wait until `target` group sums are published; false (and the fail word set) if the bounded
+  // poll gave up.  Uniform over the workgroup (LDS word + barrier).
+  auto wait_published = [&](unsigned target) -> bool {
+    if (threadIdx.x == 0) {
+      int f = 0;
+      long long polls = 0;
+      while (__hip_atomic_load(done_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++polls > kSpecPollMax) {
+          f = 1;
+          __hip_atomic_store(done_ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+      wfail = f;
+    }
+    __syncthreads();
+    return wfail == 0;
+  };
+  for (int li = 0; li < nit; ++li) {
+  const int iter = fz.iter + li, par = persist ? (iter & 1) : fz.par;
+  SpecAcc<D> acc[PPW];
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // only the chunk loads below are counted
+  if (persist) __syncthreads();                     // the previous iteration's ring / flag reads done; st_* loaded
   // every ring slot filled before the loop (the prologue below runs under them): chunks 0 .. pre - 1
   const int pre = min(min(FGP_SPEC_PRE, RING), nc);
 #pragma unroll
@@ -844,12 +896,26 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
   // (identical arithmetic, identical results), workgroup 0 alone storing histories and the new state,
   // while the first chunks are in flight; the parameters then come from LDS (scr).  The Rprop state is
   // loaded beside the level-2 sums (one round trip, not two).
-  __shared__ double scr[kSpecScratch];              // [G nq] level-2 totals, then [np] new raw parameters
   Hyp h[PPW];
-  if (fz.counters && fz.pending) {
+  if (fz.counters && persist && li > 0) {
+    // the previous iteration's group sums (all ng published), its step on the LDS state
+    if (!wait_published((unsigned)(li * ng))) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      return;
+    }
+    spec_level2<D, true>(a, par ^ 1, scr);
+    __syncthreads();
+    spec_finish<D>(a, fz.f, scr, 0, G, iter - 1, 1, lst, lst, blockIdx.x == 0, nullptr, 1);
+    __syncthreads();
+#pragma unroll
+    for (int p = 0; p < PPW; ++p) load_hyp_wave(a, on[p] ? g0 + p : 0, h[p], st_raw);
+  } else if (persist) {
+#pragma unroll
+    for (int p = 0; p < PPW; ++p) load_hyp_wave(a, on[p] ? g0 + p : 0, h[p], st_raw);
+  } else if (fz.counters && fz.pending) {
     double* tot = scr;
     double* nraw = tot + G * a.nq;
-    const int si = threadIdx.x >> 4, sk = threadIdx.x & 15, dl = a.ls_pd ? a.d : 1;
+    const int tf = tid_fresh(), si = tf >> 4, sk = tf & 15, dl = a.ls_pd ? a.d : 1;
     double pf[3] = {0.0, 0.0, 0.0};
     if (FGP_SPEC_PF && si < G && sk < 2 + dl) {
       const int p = spec_slot_param(a, si, sk, dl);
@@ -911,17 +977,31 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
                                     (unsigned)(wg_in_grp - 1);
     __syncthreads();
     if (flag[0]) {
-      const int t = threadIdx.x;
+      const int t = tid_fresh();
       if (t < G * a.nq) {
         const int g = t / a.nq, q = t % a.nq;
-        __hip_atomic_store(part2_ptr(a, fz.par, g, q, grp), spec_group_sum<true>(a, g, q, grp), __ATOMIC_RELAXED,
+        __hip_atomic_store(part2_ptr(a, par, g, q, grp), spec_group_sum<true>(a, g, q, grp), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
         if (fz.check) handoff_check_verify(a, fz, grp, g, q);
       }
       if (fz.check && threadIdx.x == 0)
         __hip_atomic_fetch_add(fz.check + kHandoffWords, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (threadIdx.x == 0) __hip_atomic_store(cnt_grp, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (persist) {
+        // publish: every storing wave's group sums (and the counter reset) retired, then one add
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_fetch_add(done_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
+  }
+  }   // iterations
+  // persistent: the last iteration's step (k_spec_finish_step's work) by workgroup 0, into the fit's vectors
+  if (persist && fz.counters && blockIdx.x == 0) {
+    if (!wait_published((unsigned)(nit * ng))) return;
+    spec_level2<D, true>(a, (fz.iter + nit - 1) & 1, scr);
+    __syncthreads();
+    spec_finish<D>(a, fz.f, scr, 0, G, fz.iter + nit - 1, fz.do_update, lst, fz.sout, true, nullptr, 1);
   }
   stamp_end(a);
 }
@@ -1378,6 +1458,7 @@ int launch_spec_iter(const Nll& a, hipStream_t st, const FitFuse* fz) {
     FitFuse none{};
     none.counters = nullptr;
     const FitFuse& f = fz ? *fz : none;
+    bool persist_ok = false;
     const int trows = (1 << a.d) + (a.spec_ps ? a.spec_ps : a.G);
     const size_t shm = sizeof(double) * (size_t)kSpecRing * (size_t)(trows * a.spec_ck);
     const unsigned grid = (unsigned)(a.nb / (4 / a.spec_pgp) * a.spec_nsl);
@@ -1396,16 +1477,31 @@ int launch_spec_iter(const Nll& a, hipStream_t st, const FitFuse* fz) {
             (void)hipFuncSetAttribute(kp, hipFuncAttributeMaxDynamicSharedMemorySize, kSpecLdsMax);
             if (nraised < 64) raised[nraised++] = kp;
           }
+          if (f.piters > 0) {
+            // persistent: every workgroup must be resident at once (they wait on each other)
+            int per_cu = 0, dev = 0, cus = 0;
+            if (hipGetDevice(&dev) != hipSuccess ||
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kp, kWG, shm) != hipSuccess ||
+                (int64_t)per_cu * cus < (int64_t)grid)
+              return;                                // (rc stays kErrUnsupported: the caller launches per iteration)
+            persist_ok = true;
+          }
           kern<<<grid, kWG, shm, st>>>(a, f);
         };
         auto net = [&](auto nc) {
           constexpr bool NET = decltype(nc)::value;
-          if (a.spec_ppw == 4) go(k_spec_tile<D, 4, NET>);
+          if (f.piters > 0) {
+            if (a.spec_ppw == 2) go(k_spec_tile<D, 2, NET, true>);
+            else if (a.spec_ppw == 1) go(k_spec_tile<D, 1, NET, true>);
+          } else if (a.spec_ppw == 4) go(k_spec_tile<D, 4, NET>);
           else if (a.spec_ppw == 2) go(k_spec_tile<D, 2, NET>);
           else go(k_spec_tile<D, 1, NET>);
         };
         if (a.spec_net) net(std::true_type{});
         else net(std::false_type{});
+        if (f.piters > 0 && !persist_ok)
+          return set_error(kErrUnsupported, "persistent k_spec_tile: the grid is not co-resident");
         return check_launch("k_spec_tile");
       } else {
         return set_error(kErrInvalid, "spectral tile kernel: d > 5");
@@ -1500,7 +1596,7 @@ int launch_spec_step_many(const Nll& a, const Fit& f, int iter, int do_update, h
 int spec_counters_offset(const Nll& a, int64_t* off, int* count) {
   const int ng = (a.nb + kSpecGroup - 1) / kSpecGroup;
   *off = spec_part2_off(a, 2) + 2 * 3 * (int64_t)spec_nparams(a);
-  *count = ng;
+  *count = ng + 2;                                  // group counters, published-sums count, persistent fail word
   return kOk;
 }
 

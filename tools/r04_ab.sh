@@ -14,3 +14,11 @@ for rep in 1 2; do
   done
 done
 cat $OUT/ab.jsonl
+if [ -n "$PROF_SMALL" ]; then timeout -k 10 200 python -u tools/prof_fit_small.py > $OUT/prof_small.txt 2>&1; head -80 $OUT/prof_small.txt; fi
+if [ -n "$PERSIST" ]; then timeout -k 10 200 python -u tools/exp_persist_stamps.py > $OUT/persist.jsonl 2> $OUT/persist.err; cat $OUT/persist.jsonl; fi
+if [ -n "$STEPTRACE" ]; then
+  timeout -k 10 200 python -u tools/step_trace.py $STEPTRACE > $OUT/step_host_$STEPTRACE.txt 2>&1
+  timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/st -o t -- python3 tools/step_trace.py $STEPTRACE > /dev/null 2> $OUT/st.err
+  python tools/step_trace.py --trace $OUT/st/t_kernel_trace.csv > $OUT/step_trace_$STEPTRACE.txt 2>&1
+  head -60 $OUT/step_host_$STEPTRACE.txt; head -80 $OUT/step_trace_$STEPTRACE.txt
+fi

@@ -1,0 +1,24 @@
+#!/bin/bash
+# Persistent k_spec_tile: parity subset, then A/B (FGP_SPEC_PERSIST=1 / 0) of the C4 fit iteration and the C4
+# bench line.  Each GPU step has its own limit; a crash or time limit ends the script.
+export TMPDIR=/tmp
+OUT=gpurun_out/${TAG:-r04p}
+mkdir -p $OUT
+rc=0
+timeout -k 10 400 python -u -m pytest tests/test_gpu_bench_path.py tests/test_gpu_spectral.py -m gpu -q --maxfail=5 --timeout 150 --timeout-method thread > $OUT/pytest.log 2>&1 || rc=$?
+tail -15 $OUT/pytest.log
+if [ $rc -gt 1 ]; then echo "pytest rc=$rc"; exit $rc; fi
+set -e
+for rep in 1 2; do
+  for P in 1 0; do
+    echo "{\"persist\": $P, \"rep\": $rep}" >> $OUT/ab.jsonl
+    FGP_SPEC_PERSIST=$P timeout -k 10 120 python -u tools/exp_spec_stamps.py --iters 30 >> $OUT/ab.jsonl 2>> $OUT/ab.err
+  done
+done
+cat $OUT/ab.jsonl
+for P in 1 0; do
+  FGP_SPEC_PERSIST=$P timeout -k 10 300 python -u bench.py --no-secondary --no-multitask --no-paper --no-cpu-baseline > $OUT/bench_p$P.json 2> $OUT/bench_p$P.err
+  python -c "import json;d=json.load(open('$OUT/bench_p$P.json'));print($P, d['value'], d['ms_per_step'], d.get('phases_ms'))"
+done
+if [ $rc -eq 1 ]; then echo "pytest: failures"; exit 1; fi
+echo done
