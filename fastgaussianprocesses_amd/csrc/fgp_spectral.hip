@@ -781,6 +781,21 @@ __device__ __forceinline__ void handoff_check_verify(const Nll& a, const FitFuse
 // LDS (lane-consecutive 8-byte reads: conflict-free).  With fz.counters the LAST workgroup to finish (sc1 partials, an agent-scope arrival
 // counter: MI355X_MICROARCH.md hand-off row 1, as the real-even backward kernel) runs every problem's
 // reduction + Rprop, wave w taking problems w, w + 4, ...
+// The persistent k_spec_tile re-reads its kernel arguments in each phase (iteration prologue, epilogue) from the
+// kernarg segment behind an opaque asm: otherwise their scalar values are held from one iteration to the next,
+// through the chunk loop, and spill (SGPRs into VGPR lanes, v_readlane in the loop).
+struct TileArgs {
+  Nll a;
+  FitFuse fz;
+};
+template <bool FRESH>
+__device__ __forceinline__ const TileArgs* tile_args() {
+  typedef const __attribute__((address_space(4))) TileArgs* KargPtr;
+  KargPtr p = (KargPtr)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return (const TileArgs*)p;
+}
+
 template <int D, int PPW, bool NET, bool PERSIST = false>
 __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
   constexpr int NS = 1 << D;
@@ -903,12 +918,13 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       return;
     }
-    spec_level2<D, true>(a, par ^ 1, scr);
+    const TileArgs* ka = tile_args<PERSIST>();
+    spec_level2<D, true>(ka->a, par ^ 1, scr);
     __syncthreads();
-    spec_finish<D>(a, fz.f, scr, 0, G, iter - 1, 1, lst, lst, blockIdx.x == 0, nullptr, 1);
+    spec_finish<D>(ka->a, ka->fz.f, scr, 0, G, iter - 1, 1, lst, lst, blockIdx.x == 0, nullptr, 1);
     __syncthreads();
 #pragma unroll
-    for (int p = 0; p < PPW; ++p) load_hyp_wave(a, on[p] ? g0 + p : 0, h[p], st_raw);
+    for (int p = 0; p < PPW; ++p) load_hyp_wave(ka->a, on[p] ? g0 + p : 0, h[p], st_raw);
   } else if (persist) {
 #pragma unroll
     for (int p = 0; p < PPW; ++p) load_hyp_wave(a, on[p] ? g0 + p : 0, h[p], st_raw);
@@ -953,6 +969,13 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
         if (on[p]) spec_terms<D>(phi, h[p], rootn, wl, yb[64u * p], acc[p]);
     }
   }
+  {
+  const TileArgs* ka = PERSIST ? tile_args<PERSIST>() : nullptr;
+  const Nll& a_ = PERSIST ? ka->a : a;
+  const FitFuse& fz_ = PERSIST ? ka->fz : fz;
+  {
+  const Nll& a = a_;
+  const FitFuse& fz = fz_;
   // the block's partials (k_spec_iter's values; sc1 when handed to the last workgroup)
 #pragma unroll
   for (int p = 0; p < PPW; ++p)
@@ -994,6 +1017,8 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
         if (threadIdx.x == 0) __hip_atomic_fetch_add(done_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
+  }
+  }
   }
   }   // iterations
   // persistent: the last iteration's step (k_spec_finish_step's work) by workgroup 0, into the fit's vectors
