@@ -159,6 +159,7 @@ _SIGNATURES = {
     "fgp_nll_partials_len": [_P_NLL, _c_pl],
     "fgp_spec_basis": [_c_int, _c_vp, _c_i64, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_i64, _c_vp],
     "fgp_spec_basis_work": [_c_int, _c_int, _c_int, _c_pl],
+    "fgp_spec_basis_gen": [_c_pl, _c_int, _c_int, _c_int, _c_pd, _c_vp, _c_vp, _c_i64, _c_vp],
     "fgp_inv_eig": [_c_int, _c_vp, _c_vp, _c_i64, _c_vp, _c_i64, _c_i64, _c_int, _c_vp, _c_vp, _c_vp],
 }
 

@@ -17,7 +17,7 @@ import torch
 
 from . import _native as N
 from . import ops
-from .fit_engine import FusedMLL, LatticePartsGen, fused_lam, mll_constant, spec_basis, spec_inv_eig, spectral_wanted
+from .fit_engine import FusedMLL, LatticePartsGen, fused_lam, mll_constant, spec_basis, spec_basis_gen, spec_inv_eig, spectral_wanted
 
 
 class _LossReader(object):
@@ -176,6 +176,9 @@ def _basis_for(gps, n, parts, gen):
     if not spectral_wanted(g0._FAMILY, n, g0.d, P, 1 if shared else P):
         return None
     if gen is not None:
+        b = spec_basis_gen(gen, n, g0.device)                  # the parts regenerated in the transform
+        if b is not None:
+            return b
         p = ops.lattice_parts_gen(gen.z, gen.shift[0], gen.alphas, n)
     else:
         p = parts[0] if P == 1 else parts

@@ -648,7 +648,10 @@ constexpr int kMtF = 32;
 int launch_mt_spec_iter(const Nll& a, hipStream_t st);   // loss / gradient partials of one iteration
 // lattice spectra of the subsets s0 .. s0 + cnt - 1 (log2n >= 17) by the fused R2C pair: products formed in
 // the row kernel, real parts k <= n/2 written by the column kernel (work: 16 n cnt bytes)
-int spec_basis_r2c(const double* parts, int d, int log2n, int s0, int cnt, double* basis, void* work, hipStream_t st);
+struct GenSpec;
+// (gen: the lattice parts regenerated in the row kernel instead of read from `parts`)
+int spec_basis_r2c(const double* parts, int d, int log2n, int s0, int cnt, double* basis, void* work, hipStream_t st,
+                   const GenSpec* gen = nullptr);
 // their row length log2 (11) for a transform of 2^log2n, or -1 when no split fits
 int re_row_log2(int log2n);
 

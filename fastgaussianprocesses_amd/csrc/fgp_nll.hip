@@ -1180,6 +1180,69 @@ __global__ __launch_bounds__(kWG) void k_lattice_parts_gen(GenSpec g, const doub
   for (int j = 0; j < d; ++j) parts[(int64_t)j * n + i] = g.coef[j] * lattice_gen_part<ORD>(g.z[j], br, mask, inv_n);
 }
 
+// k_fwd_rows_r2c_prod with the lattice parts regenerated in the row (fgp_spec_basis_gen): part_j(i) =
+// coef_j B_ORD((brev_m(i) z_j mod n) / n), k_lattice_parts_gen's values bit for bit, multiplied in ascending j
+// from 1.0 as the parts-array kernel does -- so the spectra equal fgp_spec_basis(fgp_lattice_parts_gen(...))
+// bit for bit, without the d n parts array written and re-read by every subset (the parts kernel's loads
+// per subset dimension were the row kernel's bound: 152 us of C4's 32 subsets, profiles/r04c_*).
+template <int D, int ORD>
+__global__ __launch_bounds__(kWG) void k_fwd_rows_r2c_gen(GenSpec g, int log2n, int s0, int cnt,
+                                                          double2* __restrict__ work, const double2* __restrict__ tw,
+                                                          const double2* __restrict__ twm) {
+  constexpr int P2 = 12, N2 = 1 << P2;
+  __shared__ double ldsd[kTile + kTile / 16];
+  __shared__ double2 red[kWG / 64];
+  const int mt = log2n - 1, m1 = mt - P2;
+  const int64_t n = (int64_t)1 << log2n;
+  // XCD-aware order as k_fwd_rows_r2c_prod (speed only)
+  const unsigned rows = gridDim.x / (unsigned)cnt;
+  int c, row0;
+  if (rows % 8u == 0u) {
+    const unsigned xcd = blockIdx.x & 7u, local = blockIdx.x >> 3;
+    c = (int)(local % (unsigned)cnt);
+    row0 = (int)((local / (unsigned)cnt) * 8u + xcd);
+  } else {
+    c = (int)(blockIdx.x % (unsigned)cnt);
+    row0 = (int)(blockIdx.x / (unsigned)cnt);
+  }
+  const int S = s0 + c;
+  const int tid = threadIdx.x;
+  const unsigned mask = (unsigned)(n - 1);
+  const double inv_n = ldexp(1.0, -log2n);
+  // element i0 + t of x[:n/2] (real parts) and its partner i0 + t + n/2 (imaginary parts): brev_m(i + n/2) =
+  // brev_m(i) + 1 (i < n/2: bit 0 of brev_m(i) is clear)
+  const unsigned br0 = brev_bits((unsigned)((int64_t)row0 * N2 + 16 * tid), log2n);
+  double2 v[16];
+#pragma unroll
+  for (int t = 0; t < 16; ++t) v[t] = make_double2(1.0, 1.0);
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+    if ((S >> j) & 1) {                      // uniform over the workgroup
+      const unsigned zj = g.z[j];
+      const double cj = g.coef[j];
+      static_for<0, 16>([&](auto tc) {
+        constexpr int t = decltype(tc)::value;
+        const unsigned br = brev_run<t>(br0, log2n);
+        v[t].x *= cj * lattice_gen_part<ORD>(zj, br, mask, inv_n);
+        v[t].y *= cj * lattice_gen_part<ORD>(zj, br | 1u, mask, inv_n);
+      });
+    }
+  }
+  double2 sum = make_double2(0.0, 0.0);
+#pragma unroll
+  for (int t = 0; t < 16; ++t) sum += v[t];
+  const double2 mean = block_sum_t(sum, red) * (1.0 / N2);
+#pragma unroll
+  for (int t = 0; t < 16; ++t) v[t] -= mean;
+  fwd_reg_passes<P2, 0, true>(v, ldsd, tid, tw);
+  if (tid == 0) v[0] += mean * (double)N2;
+  const RowTwiddle rt((unsigned)row0, tid, P2, m1, tw, twm);
+  double2* out = work + (int64_t)c * n;
+#pragma unroll
+  for (int k = 0; k < 16; ++k)
+    out[work_pos_pair(row0, tid + k * kWG, m1, N2)] = tw_mul<double2>(v[k], rt.at(k, P2, m1, tw, twm), false);
+}
+
 // ------------------------------------------------------------------------------------------------
 // host-side launch logic
 static int to_nll(const fgp_nll_desc* d, Nll& a) {
@@ -1576,6 +1639,33 @@ int fgp_lattice_parts_gen(const int64_t* z, const double* shift, int log2n, int 
   return check_launch("k_lattice_parts_gen");
 }
 
+int fgp_spec_basis_gen(const int64_t* z, int log2n, int d, int order, const double* coef, double* basis, void* work,
+                       int64_t work_bytes, void* stream) {
+  if (d < 1 || d > kSpecMaxD || log2n < 17 || log2n > 24)
+    return set_error(kErrUnsupported, "fgp_spec_basis_gen: needs 1 <= d <= %d, 17 <= log2n <= 24", kSpecMaxD);
+  if (!z || !coef || !basis || !work) return set_error(kErrInvalid, "fgp_spec_basis_gen: null pointer");
+  if (order != 2 && order != 4 && order != 6 && order != 8)
+    return set_error(kErrUnsupported, "Bernoulli order %d unsupported", order);
+  GenSpec g{};
+  const uint64_t zmask = ((uint64_t)1 << log2n) - 1;
+  for (int j = 0; j < d; ++j) {
+    if (z[j] <= 0 || z[j] >= ((int64_t)1 << (53 - log2n)))
+      return set_error(kErrUnsupported, "fgp_spec_basis_gen: z[%d] outside (0, 2^(53-log2n))", j);
+    g.z[j] = (unsigned)((uint64_t)z[j] & zmask);
+    g.coef[j] = coef[j];
+  }
+  g.order = order;
+  const int64_t n = (int64_t)1 << log2n, per = 16 * n, NS = 1 << d;
+  const int chunk = (int)std::min<int64_t>(NS, work_bytes / per);
+  if (chunk < 1) return set_error(kErrInvalid, "fgp_spec_basis_gen: work below one subset (%lld bytes)", (long long)per);
+  for (int s0 = 0; s0 < NS; s0 += chunk) {
+    const int rc = spec_basis_r2c(nullptr, d, log2n, s0, (int)std::min<int64_t>(chunk, NS - s0), basis, work,
+                                  (hipStream_t)stream, &g);
+    if (rc != kOk) return rc;
+  }
+  return kOk;
+}
+
 int fgp_nll_fwd(const fgp_nll_desc* desc, void* stream) {
   Nll a;
   int rc = to_nll(desc, a);
@@ -1780,7 +1870,8 @@ int fgp_ifftbr_real_rf(const void* in, int64_t in_batch_stride, const double* f,
 
 namespace fgp {
 
-int spec_basis_r2c(const double* parts, int d, int log2n, int s0, int cnt, double* basis, void* work, hipStream_t st) {
+int spec_basis_r2c(const double* parts, int d, int log2n, int s0, int cnt, double* basis, void* work, hipStream_t st,
+                   const GenSpec* gen) {
   if (log2n < 17 || log2n > 24 || d < 1 || d > kSpecMaxD || cnt < 1 || s0 < 0 || s0 + cnt > (1 << d))
     return set_error(kErrInvalid, "spec_basis_r2c: bad shape");
   const int64_t n = (int64_t)1 << log2n, nt = n >> 1;
@@ -1793,12 +1884,30 @@ int spec_basis_r2c(const double* parts, int d, int log2n, int s0, int cnt, doubl
     return set_error(kErrHip, "spec_basis_r2c: memset failed");
   const unsigned grid = (unsigned)(tiles * cnt);
   double2* wk = static_cast<double2*>(work);
-  switch (d) {
-#define FGP_R(DD) case DD: k_fwd_rows_r2c_prod<DD><<<grid, kWG, 0, st>>>(parts, log2n, s0, cnt, wk, tb->tw4096, tb->twm[mt]); break;
-    FGP_R(1) FGP_R(2) FGP_R(3) FGP_R(4) FGP_R(5) FGP_R(6)
+  if (gen) {
+    auto go = [&](auto oc) {
+      constexpr int O = decltype(oc)::value;
+      switch (d) {
+#define FGP_R(DD) case DD: k_fwd_rows_r2c_gen<DD, O><<<grid, kWG, 0, st>>>(*gen, log2n, s0, cnt, wk, tb->tw4096, tb->twm[mt]); break;
+        FGP_R(1) FGP_R(2) FGP_R(3) FGP_R(4) FGP_R(5) FGP_R(6)
 #undef FGP_R
+      }
+    };
+    switch (gen->order) {
+      case 2: go(std::integral_constant<int, 2>{}); break;
+      case 4: go(std::integral_constant<int, 4>{}); break;
+      case 6: go(std::integral_constant<int, 6>{}); break;
+      case 8: go(std::integral_constant<int, 8>{}); break;
+      default: return set_error(kErrUnsupported, "Bernoulli order %d unsupported", gen->order);
+    }
+  } else {
+    switch (d) {
+#define FGP_R(DD) case DD: k_fwd_rows_r2c_prod<DD><<<grid, kWG, 0, st>>>(parts, log2n, s0, cnt, wk, tb->tw4096, tb->twm[mt]); break;
+      FGP_R(1) FGP_R(2) FGP_R(3) FGP_R(4) FGP_R(5) FGP_R(6)
+#undef FGP_R
+    }
   }
-  int rc = check_launch("k_fwd_rows_r2c_prod");
+  int rc = check_launch(gen ? "k_fwd_rows_r2c_gen" : "k_fwd_rows_r2c_prod");
   if (rc != kOk) return rc;
   Nll a{};
   a.log2n = log2n;

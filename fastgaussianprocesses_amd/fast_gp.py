@@ -28,7 +28,7 @@ import torch
 from . import _native
 from . import ops
 from . import seqs as _seqs
-from .fit_engine import FusedMLL, LatticePartsGen, mll_constant, spec_basis, spec_inv_eig, spec_post_var, spectral_wanted
+from .fit_engine import FusedMLL, LatticePartsGen, mll_constant, spec_basis, spec_basis_gen, spec_inv_eig, spec_post_var, spectral_wanted
 
 
 def _log(x):
@@ -504,6 +504,10 @@ class AbstractFastGP(torch.nn.Module):
 
         def f():
             gen = self._parts_gen(n)
+            if gen is not None:
+                b = spec_basis_gen(gen, n, self.device)      # the parts regenerated in the transform
+                if b is not None:
+                    return b
             parts = ops.lattice_parts_gen(gen.z, gen.shift[0], gen.alphas, n) if gen is not None else self._k1parts(n)
             return spec_basis(self._FAMILY, parts, n)
         return self._cached(("basis", n), f, grad_sensitive=False)

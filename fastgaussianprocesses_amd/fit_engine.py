@@ -16,7 +16,7 @@ import os
 import torch
 
 from . import _native as N
-from .ops import lattice_coefficient, log2_exact, require_device
+from .ops import LATTICE, lattice_coefficient, log2_exact, require_device
 
 # torch.optim.Rprop defaults (etas=(0.5, 1.2), step_sizes=(1e-6, 50))
 RPROP_ETAS = (0.5, 1.2)
@@ -113,6 +113,28 @@ def spec_basis(family, parts, n):
     out = torch.empty(((P,) if parts.dim() == 3 else ()) + (Q, 2 ** d, 64), dtype=torch.float64, device=parts.device)
     N.call("fgp_spec_basis", int(family), N.ptr(parts), d * n, P, m, int(d), N.ptr(out), N.ptr(work), wbytes,
            N.stream_ptr(parts.device))
+    return out
+
+
+def spec_basis_gen(gen, n, device):
+    """spec_basis of lattice parts regenerated from the generating vector inside the transform (fgp_spec_basis_gen,
+    ABI 15): the basis of spec_basis(ops.lattice_parts_gen(gen...)) bit for bit, without the d x n parts array;
+    None outside its domain (17 <= log2 n <= 24, d <= 6, one smoothness) or with FGP_SPEC_BASIS_GEN=0."""
+    m = log2_exact(n)
+    d = len(gen.z)
+    if os.environ.get("FGP_SPEC_BASIS_GEN", "1")[:1] == "0" or not (17 <= m <= 24) or d > 6 \
+            or len(set(int(a) for a in gen.alphas)) != 1:
+        return None
+    Q = spec_chunks(LATTICE, n)
+    total = ctypes.c_int64(0)
+    N.call("fgp_spec_basis_work", LATTICE, m, int(d), ctypes.byref(total))
+    one = total.value >> d
+    wbytes = max(one, min(total.value, SPEC_WORK_CAP))
+    work = torch.empty((wbytes,), dtype=torch.uint8, device=device)
+    out = torch.empty((Q, 2 ** d, 64), dtype=torch.float64, device=device)
+    N.call("fgp_spec_basis_gen", N.int64_array(gen.z), m, int(d), 2 * int(gen.alphas[0]),
+           N.double_array([lattice_coefficient(a) for a in gen.alphas]), N.ptr(out), N.ptr(work), wbytes,
+           N.stream_ptr(device))
     return out
 
 

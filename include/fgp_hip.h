@@ -282,6 +282,12 @@ int fgp_spec_basis(int family, const double* parts, int64_t parts_stride, int64_
                    void* work, int64_t work_bytes, void* stream);
 /* Bytes of `work` for all 2^d subsets at once (divide by 2^d for the one-subset minimum). */
 int fgp_spec_basis_work(int family, int log2n, int d, int64_t* bytes);
+/* ABI 15 -- fgp_spec_basis of a LATTICE from its generating vector: the parts of fgp_lattice_parts_gen
+ * (coef_j B_order((brev_m(i) z_j mod n) / n), z: [d] int64, coef: [d] host) regenerated inside the transform's
+ * row pass instead of read from a d n parts array -- the same basis bit for bit.  17 <= log2n <= 24 (the
+ * half-length transform path); work as fgp_spec_basis (family lattice). */
+int fgp_spec_basis_gen(const int64_t* z, int log2n, int d, int order, const double* coef, double* basis, void* work,
+                       int64_t work_bytes, void* stream);
 
 #define FGP_PARTS_ARRAY 0
 #define FGP_PARTS_LATTICE 1

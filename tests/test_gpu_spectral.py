@@ -303,3 +303,23 @@ def test_single_launch_fit_equals_launch_per_iteration(family, m, d, wait, monke
     assert torch.equal(a["loss_hist"], b["loss_hist"])
     assert torch.equal(a["lengthscales_hist"], b["lengthscales_hist"])
     assert torch.equal(sa, sb) and torch.equal(la, lb)
+
+
+@pytest.mark.parametrize("m,d,alpha", [(17, 1, 2), (17, 5, 2), (18, 3, 1), (18, 6, 2), (17, 2, 4)])
+def test_basis_from_generating_vector_equals_parts_array_basis(m, d, alpha):
+    """fgp_spec_basis_gen (ABI 15: the lattice parts regenerated in the transform's row pass) against
+    fgp_spec_basis of the fgp_lattice_parts_gen array: the same spectra bit for bit (so the batch / single
+    GP fits that switched to it keep their trajectories), and the lengthscale-free subsets against the
+    oracle's transform of the product of parts."""
+    from fastgaussianprocesses_amd import ops
+    from fastgaussianprocesses_amd.fit_engine import LatticePartsGen, spec_basis_gen
+    n = 2 ** m
+    rng = np.random.default_rng(m + d)
+    z = [int(v) for v in (2 * rng.integers(1, 2 ** (m - 1), size=d) + 1)]
+    shift = torch.rand((1, d), dtype=torch.float64, generator=torch.Generator().manual_seed(d)).to(DEV)
+    gen = LatticePartsGen(z, [alpha] * d, shift)
+    got = spec_basis_gen(gen, n, torch.device(DEV))
+    assert got is not None
+    ref = spec_basis(0, ops.lattice_parts_gen(gen.z, gen.shift[0], gen.alphas, n), n)
+    assert got.shape == ref.shape
+    assert torch.equal(got, ref)

@@ -20,5 +20,8 @@ for P in 1 0; do
   FGP_SPEC_PERSIST=$P timeout -k 10 300 python -u bench.py --no-secondary --no-multitask --no-paper --no-cpu-baseline > $OUT/bench_p$P.json 2> $OUT/bench_p$P.err
   python -c "import json;d=json.load(open('$OUT/bench_p$P.json'));print($P, d['value'], d['ms_per_step'], d.get('phases_ms'))"
 done
+FGP_SPEC_BASIS_GEN=0 timeout -k 10 300 python -u bench.py --no-secondary --no-multitask --no-paper --no-cpu-baseline > $OUT/bench_nogen.json 2> $OUT/bench_nogen.err
+python -c "import json;d=json.load(open('$OUT/bench_nogen.json'));print('basis_gen=0', d['value'], d['ms_per_step'], d.get('phases_ms'))"
+if [ -n "$PERSIST_STAMPS" ]; then timeout -k 10 200 python -u tools/exp_persist_stamps.py > $OUT/persist.jsonl 2> $OUT/persist.err; cat $OUT/persist.jsonl; fi
 if [ $rc -eq 1 ]; then echo "pytest: failures"; exit 1; fi
 echo done
