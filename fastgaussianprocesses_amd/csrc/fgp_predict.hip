@@ -24,6 +24,9 @@ namespace fgp {
 constexpr int kPmB = 4;          // outputs per launch
 constexpr int kSlab = 256;       // train points per LDS slab
 constexpr int kChunk = 1024;     // train points per workgroup (4 slabs)
+#ifndef FGP_PM_UNROLL
+#define FGP_PM_UNROLL 2          // training points per k_post_mean loop trip (A/B builds: tools/build_exp.sh)
+#endif
 
 struct PredSpec {
   int order[FGP_MAX_D];
@@ -164,7 +167,7 @@ __global__ __launch_bounds__(kWG) void k_post_mean(const double* __restrict__ xt
         for (int b = 0; b < NB; ++b) cs[b][tid] = b < B ? coeffs[(int64_t)b * coeff_stride + s0 + tid] : 0.0;
       }
       __syncthreads();
-#pragma unroll 2
+#pragma unroll FGP_PM_UNROLL
       for (int i = 0; i < cnt; ++i) {
         double p[NB];
 #pragma unroll

@@ -23,5 +23,11 @@ done
 FGP_SPEC_BASIS_GEN=0 timeout -k 10 300 python -u bench.py --no-secondary --no-multitask --no-paper --no-cpu-baseline > $OUT/bench_nogen.json 2> $OUT/bench_nogen.err
 python -c "import json;d=json.load(open('$OUT/bench_nogen.json'));print('basis_gen=0', d['value'], d['ms_per_step'], d.get('phases_ms'))"
 if [ -n "$PERSIST_STAMPS" ]; then timeout -k 10 200 python -u tools/exp_persist_stamps.py > $OUT/persist.jsonl 2> $OUT/persist.err; cat $OUT/persist.jsonl; fi
+if [ -n "$LIBAB" ]; then
+  for v in $LIBAB; do
+    FGP_LIB_PATH=fastgaussianprocesses_amd/_lib/exp/libfgp_$v.so timeout -k 10 300 python -u bench.py --no-secondary --no-multitask --no-paper --no-cpu-baseline > $OUT/bench_$v.json 2> $OUT/bench_$v.err
+    python -c "import json;d=json.load(open('$OUT/bench_$v.json'));print('$v', d['value'], d['ms_per_step'], d.get('phases_ms'))"
+  done
+fi
 if [ $rc -eq 1 ]; then echo "pytest: failures"; exit 1; fi
 echo done
