@@ -56,6 +56,8 @@ def parse():
     p.add_argument("--no-secondary", dest="secondary", action="store_false",
                    help="skip the secondary BASELINE configs (C2, C3, C5) reported under 'secondary'")
     p.add_argument("--c5-outputs", type=int, default=512)
+    p.add_argument("--no-graph", dest="graph", action="store_false",
+                   help="time the eager enqueue of every step instead of replaying a hipGraph of it")
     p.add_argument("--no-multitask", dest="multitask", action="store_false",
                    help="skip the docs/examples/multitask per-step timings reported under 'multitask'")
     p.add_argument("--no-paper", dest="paper", action="store_false",
@@ -792,6 +794,38 @@ def cpu_baseline(args, n, d):
             "seconds_per_gp": t_gp}
 
 
+def capture_step(sh, args, xm, xv):
+    """The whole batched step (data re-ingest + parameter reset, ytilde, spectra, 50 fit iterations, coefficients,
+    post_mean, post_var) captured once into a hipGraph (torch.cuda.graph) and replayed per timed step: the same
+    device work, without the host's per-launch Python.  Checked on the spot: a replay's post_mean / post_var equal
+    an eager step's bit for bit, else the eager loop is timed (graph_info says why)."""
+    info = {"used": False}
+    try:
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            step_batched(sh, args, xm, xv)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            out = step_batched(sh, args, xm, xv)
+        g.replay()
+        torch.cuda.synchronize()
+        pm_g, pv_g = out[1].clone(), out[2].clone()
+        _, pm_e, pv_e = step_batched(sh, args, xm, xv)
+        torch.cuda.synchronize()
+        if not (torch.equal(pm_g, pm_e) and torch.equal(pv_g, pv_e)):
+            info["error"] = "replay differs from the eager step"
+            return None, info
+        info.update({"used": True, "check": "replay == eager step (post_mean, post_var bit for bit)"})
+        return g, info
+    except Exception as e:          # capture not possible here: time the eager enqueue
+        info["error"] = repr(e)[:300]
+        torch.cuda.synchronize()
+        return None, info
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -818,17 +852,31 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    graph, graph_info = None, {"used": False}
+    if args.graph and args.batched:
+        graph, graph_info = capture_step(shifts, args, xm, xv)
     if dist:
         tdist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        if graph is not None:
+            graph.replay()
+        else:
+            step()
     torch.cuda.synchronize()
     if dist:
         tdist.barrier()
     el = max_over_ranks(time.perf_counter() - t0, device)
     sec_step = el / args.steps
     value = args.shifts * n * world / sec_step
+    if graph is not None:
+        # the same steps enqueued eagerly (host-side Python per launch), for comparison
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        graph_info["eager_ms_per_step"] = (time.perf_counter() - t0) / args.steps * 1e3
 
     phases = phase_breakdown(shifts, args.fit_iters, xm, xv)
     n_, variant, us, us_ev, t_iter, khz = roofline_fit_kernels(F, shifts, args.fit_iters)
@@ -911,7 +959,7 @@ def main():
                                       (args.log2n, d, args.shifts, args.fit_iters, args.n_mean, args.n_var),
                           "global_shifts": args.shifts * world, "parallelism": "replicas%d" % world},
                "roofline": roof, "cpu_baseline": cpu, "phases_ms": phases, "secondary": secondary,
-               "paper": paper, "multitask": multitask}
+               "paper": paper, "multitask": multitask, "graph": graph_info}
         print(json.dumps(out))
     if dist:
         tdist.destroy_process_group()

@@ -1503,13 +1503,29 @@ int launch_spec_iter(const Nll& a, hipStream_t st, const FitFuse* fz) {
             if (nraised < 64) raised[nraised++] = kp;
           }
           if (f.piters > 0) {
-            // persistent: every workgroup must be resident at once (they wait on each other)
-            int per_cu = 0, dev = 0, cus = 0;
-            if (hipGetDevice(&dev) != hipSuccess ||
-                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kp, kWG, shm) != hipSuccess ||
-                (int64_t)per_cu * cus < (int64_t)grid)
-              return;                                // (rc stays kErrUnsupported: the caller launches per iteration)
+            // persistent: every workgroup must be resident at once (they wait on each other).  The residency
+            // (workgroups per CU x CUs) is queried once per kernel and LDS size and remembered, so a launch
+            // inside a hipGraph capture makes no query.
+            static const void* rk[64];
+            static size_t rshm[64];
+            static int64_t rres[64];
+            static int nr = 0;
+            int64_t resident = -1;
+            for (int i = 0; i < nr; ++i)
+              if (rk[i] == kp && rshm[i] == shm) resident = rres[i];
+            if (resident < 0) {
+              int per_cu = 0, dev = 0, cus = 0;
+              resident = (hipGetDevice(&dev) == hipSuccess &&
+                          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+                          hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kp, kWG, shm) == hipSuccess)
+                             ? (int64_t)per_cu * cus : 0;
+              if (nr < 64) {
+                rk[nr] = kp;
+                rshm[nr] = shm;
+                rres[nr++] = resident;
+              }
+            }
+            if (resident < (int64_t)grid) return;    // (rc stays kErrUnsupported: the caller launches per iteration)
             persist_ok = true;
           }
           kern<<<grid, kWG, shm, st>>>(a, f);
