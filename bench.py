@@ -263,9 +263,18 @@ def secondary_configs(F, args, device, rank=0, world=1, collect=None):
         xv = torch.rand((args.n_var, d), generator=g).to(device)
         # the median of 3 windows of >= 5 timed steps (each bracketed as time_steps does) after 2 warm-ups: a
         # one-off host stall (allocator growth, a page fault) in a ~1 ms step is not the config's rate
-        wins = sorted(time_steps(lambda: step_single(sg, args, xm, xv), max(5, args.steps), 2 if w == 0 else 0, device)
-                      for w in range(3))
+        one = lambda: step_single(sg, args, xm, xv)
+        graph, ginfo = None, {"used": False}
+        if world == 1 and getattr(args, "graph", False):
+            for _ in range(2):
+                one()
+            graph, ginfo = capture_fn(one)
+        run = graph.replay if graph is not None else one
+        wins = sorted(time_steps(run, max(5, args.steps), 2 if w == 0 else 0, device) for w in range(3))
         sec = wins[1]
+        if graph is not None:
+            ginfo["eager_ms_per_step"] = sorted(time_steps(one, max(5, args.steps), 0, device)
+                                                for _ in range(3))[1] * 1e3
         if collect is not None:
             pm, pv = step_single(sg, args, xm, xv)
             collect[name.split(":")[0]] = dict(
@@ -303,8 +312,8 @@ def secondary_configs(F, args, device, rank=0, world=1, collect=None):
                     "config": {"workload": "%s: fit %d Rprop iters + post_mean N=%d + post_var N=%d"
                                            % (name, args.fit_iters, args.n_mean, args.n_var),
                                "n": sg.n, "outputs": total},
-                    "phases_ms": phases})
-        del sg
+                    "phases_ms": phases, "graph": ginfo})
+        del graph, sg
         torch.cuda.empty_cache()
     return out
 
@@ -792,6 +801,36 @@ def cpu_baseline(args, n, d):
                        "to %d fit iterations + post_mean N=%d + post_var N=%d per GP" %
                        (int(math.log2(n)), d, k, nm, args.fit_iters, args.n_mean, args.n_var)),
             "seconds_per_gp": t_gp}
+
+
+def capture_fn(fn):
+    """fn() (returning a tuple of device tensors) captured once into a hipGraph; (graph, info).  The replay's
+    outputs must equal an eager call's bit for bit, else (None, info) and the caller times the eager calls."""
+    info = {"used": False}
+    try:
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            fn()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            out = fn()
+        g.replay()
+        torch.cuda.synchronize()
+        got = [t.clone() for t in out]
+        ref = fn()
+        torch.cuda.synchronize()
+        if not all(torch.equal(a, b) for a, b in zip(got, ref)):
+            info["error"] = "replay differs from the eager call"
+            return None, info
+        info.update({"used": True, "check": "replay == eager call (post_mean, post_var bit for bit)"})
+        return g, info
+    except Exception as e:          # capture not possible here: time the eager enqueue
+        info["error"] = repr(e)[:300]
+        torch.cuda.synchronize()
+        return None, info
 
 
 def capture_step(sh, args, xm, xv):

@@ -634,7 +634,10 @@ __global__ __launch_bounds__(kWG) void k_spec_persist(Nll a, Fit f, int iters, d
     }
     __syncthreads();
     if (fail_s) {
+      // a barrier gave up (every workgroup's next wait then fails too, so no final state is written): the
+      // fit's parameters become NaN -- visible downstream even when the caller never reads `out`
       if (tid == 0) out[1] = 1;
+      for (int p = tid; p < np; p += kWG) f.raw[p] = NAN;
       return;
     }
     stamp(it, 2);
@@ -915,6 +918,8 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
   if (fz.counters && persist && li > 0) {
     // the previous iteration's group sums (all ng published), its step on the LDS state
     if (!wait_published((unsigned)(li * ng))) {
+      // (as k_spec_persist: no workgroup writes the final state after a failed wait; the parameters become NaN)
+      for (int p = threadIdx.x; p < spec_nparams(a); p += kWG) fz.sout.raw[p] = NAN;
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       return;
     }
@@ -1023,7 +1028,10 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
   }   // iterations
   // persistent: the last iteration's step (k_spec_finish_step's work) by workgroup 0, into the fit's vectors
   if (persist && fz.counters && blockIdx.x == 0) {
-    if (!wait_published((unsigned)(nit * ng))) return;
+    if (!wait_published((unsigned)(nit * ng))) {
+      for (int p = threadIdx.x; p < spec_nparams(a); p += kWG) fz.sout.raw[p] = NAN;
+      return;
+    }
     spec_level2<D, true>(a, (fz.iter + nit - 1) & 1, scr);
     __syncthreads();
     spec_finish<D>(a, fz.f, scr, 0, G, fz.iter + nit - 1, fz.do_update, lst, fz.sout, true, nullptr, 1);
