@@ -2029,7 +2029,8 @@ int fgp_fit_run(const fgp_nll_desc* nll, const fgp_fit_desc* fit, int iter0, int
       return set_error(kErrHip, "fgp_fit_run: counter reset failed");
     if (fuse_spec) fz.check = g_handoff_check;
   }
-  if (fuse_spec && !getenv_off("FGP_SPEC_PERSIST") && spec_nparams(a) <= kSpecStateMax) {
+  const char* pe = getenv("FGP_SPEC_PERSIST");   // (opt-in until measured on the device: FGP_SPEC_PERSIST=1)
+  if (fuse_spec && pe && pe[0] == '1' && spec_nparams(a) <= kSpecStateMax) {
     // every iteration and the last step in ONE persistent k_spec_tile launch (falls through to the launch
     // per iteration when the grid cannot be co-resident)
     fz.iter = iter0;

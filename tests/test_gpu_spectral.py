@@ -318,8 +318,35 @@ def test_basis_from_generating_vector_equals_parts_array_basis(m, d, alpha):
     z = [int(v) for v in (2 * rng.integers(1, 2 ** (m - 1), size=d) + 1)]
     shift = torch.rand((1, d), dtype=torch.float64, generator=torch.Generator().manual_seed(d)).to(DEV)
     gen = LatticePartsGen(z, [alpha] * d, shift)
-    got = spec_basis_gen(gen, n, torch.device(DEV))
+    got = spec_basis_gen(gen, n, torch.device(DEV), force=True)
     assert got is not None
     ref = spec_basis(0, ops.lattice_parts_gen(gen.z, gen.shift[0], gen.alphas, n), n)
     assert got.shape == ref.shape
     assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("m", [17, 20])
+def test_persistent_fit_launch_equals_launch_per_iteration(m, monkeypatch):
+    """The persistent k_spec_tile (FGP_SPEC_PERSIST=1: every iteration of an fgp_fit_run call and the last step in
+    ONE launch, the launch boundary replaced by a wait on the published group sums) against one launch per
+    iteration: the bench's C4 batch (8 shifted lattice GPs, d = 5), loss histories and fitted parameters bit for
+    bit; with the spectra built from the generating vector (FGP_SPEC_BASIS_GEN=1) as well."""
+    import argparse
+    import bench
+    d, n, P = 5, 2 ** m, 8
+    dev = torch.device(DEV, 0)
+    g = torch.Generator().manual_seed(17)
+    xm, xv = torch.rand((8, d), generator=g).to(dev), torch.rand((2, d), generator=g).to(dev)
+    out = {}
+    for persist, bgen in (("0", "0"), ("1", "0"), ("1", "1")):
+        monkeypatch.setenv("FGP_SPEC_PERSIST", persist)
+        monkeypatch.setenv("FGP_SPEC_BASIS_GEN", bgen)
+        sh = bench.Shifts(F, d, n, bench.shard_seeds(0, 1, P), dev)
+        data, pm, pv = bench.step_batched(sh, argparse.Namespace(fit_iters=12), xm, xv, store_loss_hist=True)
+        out[(persist, bgen)] = ([dd["loss_hist"] for dd in data], sh.batch.raw().cpu().clone(), pm.cpu(), pv.cpu())
+    ref = out[("0", "0")]
+    for key in (("1", "0"), ("1", "1")):
+        got = out[key]
+        assert all(torch.equal(a, b) for a, b in zip(got[0], ref[0])), key
+        assert torch.equal(got[1], ref[1]) and torch.equal(got[2], ref[2]) and torch.equal(got[3], ref[3]), key
+        assert torch.isfinite(got[1]).all()

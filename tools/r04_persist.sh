@@ -5,7 +5,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-r04p}
 mkdir -p $OUT
 rc=0
-timeout -k 10 400 python -u -m pytest tests/test_gpu_bench_path.py tests/test_gpu_spectral.py -m gpu -q --maxfail=5 --timeout 150 --timeout-method thread > $OUT/pytest.log 2>&1 || rc=$?
+timeout -k 10 500 python -u -m pytest tests/test_gpu_bench_path.py tests/test_gpu_spectral.py -m gpu -q --maxfail=5 --timeout 150 --timeout-method thread > $OUT/pytest.log 2>&1 || rc=$?
 tail -15 $OUT/pytest.log
 if [ $rc -gt 1 ]; then echo "pytest rc=$rc"; exit $rc; fi
 set -e
@@ -16,12 +16,10 @@ for rep in 1 2; do
   done
 done
 cat $OUT/ab.jsonl
-for P in 1 0; do
-  FGP_SPEC_PERSIST=$P timeout -k 10 300 python -u bench.py --no-secondary --no-multitask --no-paper --no-cpu-baseline > $OUT/bench_p$P.json 2> $OUT/bench_p$P.err
-  python -c "import json;d=json.load(open('$OUT/bench_p$P.json'));print($P, d['value'], d['ms_per_step'], d.get('phases_ms'))"
+for PG in 00 10 11; do
+  FGP_SPEC_PERSIST=${PG:0:1} FGP_SPEC_BASIS_GEN=${PG:1:1} timeout -k 10 300 python -u bench.py --no-secondary --no-multitask --no-paper --no-cpu-baseline > $OUT/bench_$PG.json 2> $OUT/bench_$PG.err
+  python -c "import json;d=json.load(open('$OUT/bench_$PG.json'));print('persist,gen=$PG', d['value'], d['ms_per_step'], d.get('phases_ms'), d.get('graph'))"
 done
-FGP_SPEC_BASIS_GEN=0 timeout -k 10 300 python -u bench.py --no-secondary --no-multitask --no-paper --no-cpu-baseline > $OUT/bench_nogen.json 2> $OUT/bench_nogen.err
-python -c "import json;d=json.load(open('$OUT/bench_nogen.json'));print('basis_gen=0', d['value'], d['ms_per_step'], d.get('phases_ms'))"
 if [ -n "$PERSIST_STAMPS" ]; then timeout -k 10 200 python -u tools/exp_persist_stamps.py > $OUT/persist.jsonl 2> $OUT/persist.err; cat $OUT/persist.jsonl; fi
 if [ -n "$LIBAB" ]; then
   for v in $LIBAB; do
