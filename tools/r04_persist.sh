@@ -27,5 +27,12 @@ if [ -n "$LIBAB" ]; then
     python -c "import json;d=json.load(open('$OUT/bench_$v.json'));print('$v', d['value'], d['ms_per_step'], d.get('phases_ms'))"
   done
 fi
+if [ -n "$STEPTRACE" ]; then
+  timeout -k 10 200 python -u tools/step_trace.py $STEPTRACE > $OUT/step_host_$STEPTRACE.txt 2>&1
+  timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/st -o t -- python3 tools/step_trace.py $STEPTRACE > /dev/null 2> $OUT/st.err
+  python tools/step_trace.py --trace $OUT/st/t_kernel_trace.csv > $OUT/step_trace_$STEPTRACE.txt 2>&1
+  head -12 $OUT/step_host_$STEPTRACE.txt; tail -3 $OUT/step_trace_$STEPTRACE.txt
+fi
+if [ -n "$PROF_SMALL" ]; then timeout -k 10 200 python -u tools/prof_fit_small.py > $OUT/prof_small.txt 2>&1; head -40 $OUT/prof_small.txt; fi
 if [ $rc -eq 1 ]; then echo "pytest: failures"; exit 1; fi
 echo done
