@@ -56,8 +56,8 @@ def parse():
     p.add_argument("--no-secondary", dest="secondary", action="store_false",
                    help="skip the secondary BASELINE configs (C2, C3, C5) reported under 'secondary'")
     p.add_argument("--c5-outputs", type=int, default=512)
-    p.add_argument("--no-graph", dest="graph", action="store_false",
-                   help="time the eager enqueue of every step instead of replaying a hipGraph of it")
+    p.add_argument("--graph", dest="graph", action="store_true",
+                   help="replay a hipGraph capture of each step (experimental; default: the eager enqueue)")
     p.add_argument("--no-multitask", dest="multitask", action="store_false",
                    help="skip the docs/examples/multitask per-step timings reported under 'multitask'")
     p.add_argument("--no-paper", dest="paper", action="store_false",
