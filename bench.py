@@ -815,7 +815,9 @@ def capture_fn(fn):
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        # thread-local capture mode: the default (global) mode was invalidated on the device by an API call
+        # outside this thread's capture (every phase captures cleanly in thread-local mode, tools/diag_capture.py)
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             out = fn()
         g.replay()
         torch.cuda.synchronize()
@@ -847,7 +849,7 @@ def capture_step(sh, args, xm, xv):
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             out = step_batched(sh, args, xm, xv)
         g.replay()
         torch.cuda.synchronize()
