@@ -130,9 +130,38 @@ __device__ __forceinline__ void spec_values(const SpecAcc<D>& acc, double* v) {
 // (dL/dlambda = sqrt(n) dL/dev; dlambda/draw_scale = lambda, dlambda/draw_l_j = scale l_j dP/dl_j) and
 // one store per quantity by lane 0 (sc1 when handed to a last-workgroup reduction).  The single-frequency
 // corrections reload their spectra and Y from global memory, so every kernel computes the same values.
+// The lattice's single-frequency corrections (k = 0 and k = n/2) of a wave's first / last block, loaded at the
+// start of a launch (their latency then hides under the chunk stream instead of sitting in the block's
+// epilogue, the critical path of the group hand-off / grid barrier): one double per lane -- phi0[s] / phi1[s]
+// the spectra at k = 0 / n/2 (lane s), y[p] / y[32 + p] Y of the wave's problem g0 + p at k = 0 / n/2 --
+// read back by v_readlane.  on = false: spec_block_partials loads them itself.
+struct SpecCorr {
+  double phi0, phi1, y;
+  int g0;
+  bool on;
+};
+
+// load the wave's corrections (wave-uniform condition: the wave holds block 0 or the last block)
+template <int NS>
+__device__ __forceinline__ SpecCorr spec_corr_load(const Nll& a, int blk, int g0, int cnt) {
+  SpecCorr c{0.0, 0.0, 0.0, g0, false};
+  if (a.spec_net || !(blk == 0 || blk == a.nb - 1)) return c;
+  const int lane = tid_fresh() & 63;
+  const double* phib = a.basis + (int64_t)g0 * a.basis_stride;
+  if (lane < NS) {
+    c.phi0 = phib[spec_at<NS>(0, lane)];
+    c.phi1 = phib[spec_at<NS>(a.spec_main, lane)];
+  }
+  const int p = lane & 31;
+  if (p < cnt) c.y = a.ysq[ysq_at(a, g0 + p, lane < 32 ? 0 : a.spec_main)];
+  c.on = true;
+  return c;
+}
+
 template <int D, bool NET>
 __device__ __forceinline__ void spec_block_partials(const Nll& a, const Hyp& h, int g, int blk, double rootn, double wl,
-                                                    const SpecAcc<D>& acc, bool sc1, double* pbase) {
+                                                    const SpecAcc<D>& acc, bool sc1, double* pbase,
+                                                    const SpecCorr& corr = SpecCorr{0.0, 0.0, 0.0, 0, false}) {
   constexpr int NS = 1 << D, NV = 4 + D;
   const int lane = tid_fresh() & 63;
   double v[NV];
@@ -150,10 +179,13 @@ __device__ __forceinline__ void spec_block_partials(const Nll& a, const Hyp& h, 
       if (!here) continue;
       const int64_t k = side == 0 ? 0 : a.spec_main;
       double phi[NS];
+      // (v_readlane of the preloaded values: exec-independent, inside the lane-0 branch)
 #pragma unroll
-      for (int s = 0; s < NS; ++s) phi[s] = phib[spec_at<NS>(k, s)];
+      for (int s = 0; s < NS; ++s)
+        phi[s] = corr.on ? read_lane(side == 0 ? corr.phi0 : corr.phi1, s) : phib[spec_at<NS>(k, s)];
+      const double yk = corr.on ? read_lane(corr.y, (side == 0 ? 0 : 32) + g - corr.g0) : a.ysq[ysq_at(a, g, k)];
       SpecAcc<D> t;
-      spec_terms<D>(phi, h, rootn, wl, a.ysq[ysq_at(a, g, k)], t);
+      spec_terms<D>(phi, h, rootn, wl, yk, t);
       double tv[NV];
       spec_values<D>(t, tv);
       const double sg = side == 0 ? -1.0 : 1.0;   // k = 0: weight 2 -> 1; k = n/2: weight 1
@@ -590,6 +622,13 @@ __global__ __launch_bounds__(kWG) void k_spec_persist(Nll a, Fit f, int iters, d
   const double rootn = sqrt((double)((int64_t)1 << a.log2n)), wl = a.logdet_weight;
   const RpState st{st_raw, st_prev, st_step};
   const int64_t psize = (int64_t)a.nq * a.nb;      // one parity's partials (G = 1)
+  // the single-frequency corrections, loaded once for the whole fit by the wave holding block 0 / the last
+  // block (the blocks t = w, w + 4, ... of this workgroup)
+  SpecCorr corr{0.0, 0.0, 0.0, 0, false};
+  for (int t = w; t < bpw; t += kWG / 64) {
+    const int blk = blk0 + t;
+    if (blk < a.nb && (blk == 0 || blk == a.nb - 1)) corr = spec_corr_load<NS>(a, blk, 0, 1);
+  }
   // (a.stamps: workgroup 0's device clock per iteration -- start, partials stored, barrier passed, reduced,
   // stepped -- at stamps[5 it + phase]; tools/exp_persist_stamps.py)
   auto stamp = [&](int it, int ph) {
@@ -614,7 +653,7 @@ __global__ __launch_bounds__(kWG) void k_spec_persist(Nll a, Fit f, int iters, d
         for (int s = 0; s < NS; ++s) phi[s] = cb[64 * s];
         spec_terms<D>(phi, h, rootn, wl, cb[64 * NS], acc);
       }
-      spec_block_partials<D, NET>(a, h, 0, blk, rootn, wl, acc, true, pbase);
+      spec_block_partials<D, NET>(a, h, 0, blk, rootn, wl, acc, true, pbase, corr);
     }
     // grid barrier it + 1: every wave's sc1 partials retired, one add per workgroup, one bounded poller
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -903,6 +942,9 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
   SpecAcc<D> acc[PPW];
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // only the chunk loads below are counted
   if (persist) __syncthreads();                     // the previous iteration's ring / flag reads done; st_* loaded
+  // the single-frequency corrections of block 0 / the last block, loaded ahead of the chunk DMAs (older: a
+  // chunk's counted wait covers them too; first used in the epilogue)
+  const SpecCorr corr = active ? spec_corr_load<NS>(a, blk, goff + g0, min(PPW, GS - g0)) : SpecCorr{0.0, 0.0, 0.0, 0, false};
   // every ring slot filled before the loop (the prologue below runs under them): chunks 0 .. pre - 1
   const int pre = min(min(FGP_SPEC_PRE, RING), nc);
 #pragma unroll
@@ -985,7 +1027,8 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
 #pragma unroll
   for (int p = 0; p < PPW; ++p)
     if (on[p] && active)
-      spec_block_partials<D, NET>(a, h[p], goff + g0 + p, blk, rootn, wl, acc[p], fz.counters != nullptr, a.partials);
+      spec_block_partials<D, NET>(a, h[p], goff + g0 + p, blk, rootn, wl, acc[p], fz.counters != nullptr, a.partials,
+                                  corr);
   if (fz.check && fz.counters) handoff_check_store(a, fz, blk / kSpecGroup, g0, PPW, GS, blk, active);
   if (fz.counters) {
     // Level 1 of the fused reduction (MI355X_MICROARCH.md hand-off row 1: sc1 stores retired by every
