@@ -1454,7 +1454,10 @@ void spec_geometry(Nll& a) {
   // G / 4 times instead of G / 2 and each wave's loads serve 4 evaluations.  d <= 3 only: 156 VGPRs,
   // 3 waves / SIMD there; at d = 4, 5 the four accumulator sets spill (8 per wave spills at d = 3)
   const int64_t lanes = std::max<int64_t>(1, a.spec_main / 64);
-  a.nb = (int)std::min<int64_t>(kSpecBlocks, lanes);
+  // at least 4 chunks per block where the frequencies allow (>= 4 blocks): a block's epilogue (wave reduction of
+  // 4 + d partials, the corrections) costs ~1 us of latency, so small problems (C2 / C3, the paper's n = 2^10,
+  // whose single-launch fit runs one block per wave) no longer pay it per 64 frequencies; n >= 2^18 unchanged
+  a.nb = (int)std::min<int64_t>(kSpecBlocks, std::max<int64_t>(std::min<int64_t>(lanes, 4), lanes / 4));
   a.spec_kpl = (int)((a.spec_main + 64 * (int64_t)a.nb - 1) / (64 * (int64_t)a.nb));
   a.spec_tile = 0;
   a.spec_pgp = a.spec_ck = 0;
