@@ -803,6 +803,18 @@ def cpu_baseline(args, n, d):
             "seconds_per_gp": t_gp}
 
 
+def _clear_capture_error():
+    """After an invalidated capture the HIP error is reported by the next launch: take it here (a throwaway
+    op whose error is swallowed) so the eager fallback runs clean."""
+    for _ in range(3):
+        try:
+            torch.zeros(1, device="cuda").add_(1)
+            torch.cuda.synchronize()
+            return
+        except Exception:
+            continue
+
+
 def capture_fn(fn):
     """fn() (returning a tuple of device tensors) captured once into a hipGraph; (graph, info).  The replay's
     outputs must equal an eager call's bit for bit, else (None, info) and the caller times the eager calls."""
@@ -815,10 +827,12 @@ def capture_fn(fn):
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
-        # thread-local capture mode: the default (global) mode was invalidated on the device by an API call
-        # outside this thread's capture (every phase captures cleanly in thread-local mode, tools/diag_capture.py)
-        with torch.cuda.graph(g, capture_error_mode="thread_local"):
-            out = fn()
+        # thread-local capture mode on an explicit stream (every phase captures cleanly this way,
+        # tools/diag_capture.py)
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
+                out = fn()
+        torch.cuda.current_stream().wait_stream(s)
         g.replay()
         torch.cuda.synchronize()
         got = [t.clone() for t in out]
@@ -830,41 +844,19 @@ def capture_fn(fn):
         info.update({"used": True, "check": "replay == eager call (post_mean, post_var bit for bit)"})
         return g, info
     except Exception as e:          # capture not possible here: time the eager enqueue
+        import traceback
         info["error"] = repr(e)[:300]
-        torch.cuda.synchronize()
+        info["where"] = [ln.strip() for ln in traceback.format_exc().splitlines() if "repo" in ln][-4:]
+        _clear_capture_error()
         return None, info
 
 
 def capture_step(sh, args, xm, xv):
     """The whole batched step (data re-ingest + parameter reset, ytilde, spectra, 50 fit iterations, coefficients,
-    post_mean, post_var) captured once into a hipGraph (torch.cuda.graph) and replayed per timed step: the same
-    device work, without the host's per-launch Python.  Checked on the spot: a replay's post_mean / post_var equal
-    an eager step's bit for bit, else the eager loop is timed (graph_info says why)."""
-    info = {"used": False}
-    try:
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            step_batched(sh, args, xm, xv)
-        torch.cuda.current_stream().wait_stream(s)
-        torch.cuda.synchronize()
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, capture_error_mode="thread_local"):
-            out = step_batched(sh, args, xm, xv)
-        g.replay()
-        torch.cuda.synchronize()
-        pm_g, pv_g = out[1].clone(), out[2].clone()
-        _, pm_e, pv_e = step_batched(sh, args, xm, xv)
-        torch.cuda.synchronize()
-        if not (torch.equal(pm_g, pm_e) and torch.equal(pv_g, pv_e)):
-            info["error"] = "replay differs from the eager step"
-            return None, info
-        info.update({"used": True, "check": "replay == eager step (post_mean, post_var bit for bit)"})
-        return g, info
-    except Exception as e:          # capture not possible here: time the eager enqueue
-        info["error"] = repr(e)[:300]
-        torch.cuda.synchronize()
-        return None, info
+    post_mean, post_var) captured once into a hipGraph and replayed per timed step: the same device work,
+    without the host's per-launch Python.  Checked on the spot: a replay's post_mean / post_var equal an eager
+    step's bit for bit, else the eager loop is timed (graph_info says why)."""
+    return capture_fn(lambda: step_batched(sh, args, xm, xv)[1:])
 
 
 def main():
