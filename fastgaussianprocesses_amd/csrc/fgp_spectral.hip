@@ -634,8 +634,12 @@ __global__ __launch_bounds__(kWG) void k_spec_persist(Nll a, Fit f, int iters, d
   auto stamp = [&](int it, int ph) {
     if (a.stamps && blockIdx.x == 0 && tid == 0) a.stamps[5 * it + ph] = wall_clock64();
   };
+  // one workgroup over at most one group of blocks (the paper's n = 2^10 fits): the block partials go through
+  // LDS and no barrier is needed -- the same values summed in the same order as the global hand-off
+  __shared__ double lpart[NQ * kSpecGroup];
+  const bool single = W == 1 && a.nb <= kSpecGroup;
   for (int it = 0; it <= iters; ++it) {
-    double* pbase = a.partials + (it & 1) * psize;
+    double* pbase = single ? static_cast<double*>(lpart) : a.partials + (it & 1) * psize;
     stamp(it, 0);
     Hyp h;
     load_hyp_wave(a, 0, h, st_raw);
@@ -653,13 +657,13 @@ __global__ __launch_bounds__(kWG) void k_spec_persist(Nll a, Fit f, int iters, d
         for (int s = 0; s < NS; ++s) phi[s] = cb[64 * s];
         spec_terms<D>(phi, h, rootn, wl, cb[64 * NS], acc);
       }
-      spec_block_partials<D, NET>(a, h, 0, blk, rootn, wl, acc, true, pbase, corr);
+      spec_block_partials<D, NET>(a, h, 0, blk, rootn, wl, acc, !single, pbase, corr);
     }
     // grid barrier it + 1: every wave's sc1 partials retired, one add per workgroup, one bounded poller
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     stamp(it, 1);
-    if (tid == 0) {
+    if (tid == 0 && !single) {
       __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const unsigned target = (unsigned)(it + 1) * (unsigned)W;
       long long polls = 0;
@@ -687,7 +691,7 @@ __global__ __launch_bounds__(kWG) void k_spec_persist(Nll a, Fit f, int iters, d
       const double* pp = pbase + (int64_t)q * a.nb + b0;
       double tv[kSpecGroup];
 #pragma unroll
-      for (int b = 0; b < kSpecGroup; ++b) tv[b] = ld_part<true>(pp + (b < nbg ? b : 0));
+      for (int b = 0; b < kSpecGroup; ++b) tv[b] = single ? pp[b < nbg ? b : 0] : ld_part<true>(pp + (b < nbg ? b : 0));
       double sgrp = 0.0;
 #pragma unroll
       for (int b = 0; b < kSpecGroup; ++b) sgrp += b < nbg ? tv[b] : 0.0;
