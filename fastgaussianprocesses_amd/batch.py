@@ -103,16 +103,28 @@ def _fit_loop(eng, iterations, stop_crit_improvement_threshold, stop_crit_wait_i
     return state
 
 
+_COLS = {}
+
+
+def _best_cols(device, P, S, L, dl):
+    """The raw-vector columns of every problem's (scale, lengthscales, noise), a device tensor made once per
+    shape (no host-to-device copy in a step: a hipGraph capture of the step cannot take one)."""
+    key = (str(device), P, S, L, dl)
+    if key not in _COLS:
+        cols = []
+        for p in range(P):
+            cols += [p] + [S + p * dl + j for j in range(dl)] + [S + L + p]
+        _COLS[key] = torch.tensor(cols, dtype=torch.int64).to(device)
+    return _COLS[key]
+
+
 def _best_raw(eng, state, dl):
     """[P, 2 + dl] = (raw scale, raw lengthscales, raw noise) of every problem at its best iteration
     (one gather from the per-iteration parameter history).  Best iterations decided on the device
     (best_i None: the first minimum of each loss history, = the host rule `lv < best`) stay there."""
     P = eng.G
     S, L, _ = eng.sizes
-    cols = []
-    for p in range(P):
-        cols += [p] + [S + p * dl + j for j in range(dl)] + [S + L + p]
-    idx_c = torch.tensor(cols, dtype=torch.int64).pin_memory().to(eng.device, non_blocking=True)
+    idx_c = _best_cols(eng.device, P, S, L, dl)
     if state[0]["best_i"] is None:
         total = state[0]["stop"] + 1
         lh = eng.loss_hist[:total, :, 0]

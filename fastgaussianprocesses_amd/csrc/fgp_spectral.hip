@@ -948,7 +948,9 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
   if (persist) __syncthreads();                     // the previous iteration's ring / flag reads done; st_* loaded
   // the single-frequency corrections of block 0 / the last block, loaded ahead of the chunk DMAs (older: a
   // chunk's counted wait covers them too; first used in the epilogue)
-  const SpecCorr corr = active ? spec_corr_load<NS>(a, blk, goff + g0, min(PPW, GS - g0)) : SpecCorr{0.0, 0.0, 0.0, 0, false};
+  // (k_spec_tile loads them in its epilogue: preloading them here, 6 VGPRs and their v_readlane broadcasts, cost
+  // SGPR spills through the chunk loop and measured no shorter tail, profiles/r04e_spec_stamps.jsonl)
+  const SpecCorr corr{0.0, 0.0, 0.0, 0, false};
   // every ring slot filled before the loop (the prologue below runs under them): chunks 0 .. pre - 1
   const int pre = min(min(FGP_SPEC_PRE, RING), nc);
 #pragma unroll
