@@ -56,8 +56,8 @@ def parse():
     p.add_argument("--no-secondary", dest="secondary", action="store_false",
                    help="skip the secondary BASELINE configs (C2, C3, C5) reported under 'secondary'")
     p.add_argument("--c5-outputs", type=int, default=512)
-    p.add_argument("--graph", dest="graph", action="store_true",
-                   help="replay a hipGraph capture of each step (experimental; default: the eager enqueue)")
+    p.add_argument("--no-graph", dest="graph", action="store_false",
+                   help="time the eager enqueue of each step instead of replaying its hipGraph capture")
     p.add_argument("--no-multitask", dest="multitask", action="store_false",
                    help="skip the docs/examples/multitask per-step timings reported under 'multitask'")
     p.add_argument("--no-paper", dest="paper", action="store_false",
@@ -698,9 +698,9 @@ def roofline_fit_kernels(F, shifts, iters):
 
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r03i_pmc_fit_kernels.json")
-PMC_SQ_SUMMARY = os.path.join(ROOT, "profiles", "r03i_pmc_sq_fit_kernels.json")
-ROCPROF_GRID_STATS = os.path.join(ROOT, "profiles", "r03i_bench_kernel_grid_stats.txt")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r04g_pmc_fit_kernels.json")
+PMC_SQ_SUMMARY = os.path.join(ROOT, "profiles", "r04h_pmc_sq_fit_kernels.json")
+ROCPROF_GRID_STATS = os.path.join(ROOT, "profiles", "r04g_bench_kernel_grid_stats.txt")
 # the read floor of the spectral iteration's footprint: tools/stream_microbench.hip over the same 168 MB,
 # re-read back to back, 24.0-24.3 us per pass (7.0 TB/s; profiles/r03v_stream_and_stamps.jsonl)
 STREAM_FLOOR_US = 24.0
