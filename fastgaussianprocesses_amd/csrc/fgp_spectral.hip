@@ -771,7 +771,7 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 #define FGP_SPEC_PRE 2
 #endif
 #ifndef FGP_SPEC_PF
-#define FGP_SPEC_PF 1
+#define FGP_SPEC_PF 0     // (1: ~100 more VALU per wave, no measurable gain: profiles/r04ab2_basis_gen_prefetch.txt)
 #endif
 
 // workgroup barrier that lets LDS-DMA loads stay in flight across it (__syncthreads() would drain them

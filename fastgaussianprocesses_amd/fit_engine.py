@@ -119,11 +119,11 @@ def spec_basis(family, parts, n):
 def spec_basis_gen(gen, n, device, force=False):
     """spec_basis of lattice parts regenerated from the generating vector inside the transform (fgp_spec_basis_gen,
     ABI 15): the basis of spec_basis(ops.lattice_parts_gen(gen...)) bit for bit, without the d x n parts array;
-    None outside its domain (17 <= log2 n <= 24, d <= 6, one smoothness) or unless FGP_SPEC_BASIS_GEN=1 (or
-    force)."""
+    None outside its domain (17 <= log2 n <= 24, d <= 6, one smoothness) or with FGP_SPEC_BASIS_GEN=0 (A/B).
+    C4: the spectra build 0.27 -> 0.20 ms per step (profiles/r04ab2_basis_gen_prefetch.txt)."""
     m = log2_exact(n)
     d = len(gen.z)
-    on = force or os.environ.get("FGP_SPEC_BASIS_GEN", "0")[:1] == "1"
+    on = force or os.environ.get("FGP_SPEC_BASIS_GEN", "1")[:1] != "0"
     if not on or not (17 <= m <= 24) or d > 6 or len(set(int(a) for a in gen.alphas)) != 1:
         return None
     Q = spec_chunks(LATTICE, n)
