@@ -1463,7 +1463,11 @@ void spec_geometry(Nll& a) {
   // at least 4 chunks per block where the frequencies allow (>= 4 blocks): a block's epilogue (wave reduction of
   // 4 + d partials, the corrections) costs ~1 us of latency, so small problems (C2 / C3, the paper's n = 2^10,
   // whose single-launch fit runs one block per wave) no longer pay it per 64 frequencies; n >= 2^18 unchanged
-  a.nb = (int)std::min<int64_t>(kSpecBlocks, std::max<int64_t>(std::min<int64_t>(lanes, 4), lanes / 4));
+  // (fewer chunks per block where a 4-chunk block of 2^d + 1 rows would not fit the single-launch fit's LDS:
+  // d = 6 takes 2)
+  int64_t minc = 4;
+  while (minc > 1 && ((((int64_t)1 << a.d) + 1) * minc * 512 > 96 * 1024)) minc /= 2;
+  a.nb = (int)std::min<int64_t>(kSpecBlocks, std::max<int64_t>(std::min<int64_t>(lanes, 4), lanes / minc));
   a.spec_kpl = (int)((a.spec_main + 64 * (int64_t)a.nb - 1) / (64 * (int64_t)a.nb));
   a.spec_tile = 0;
   a.spec_pgp = a.spec_ck = 0;
