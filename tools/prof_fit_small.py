@@ -52,9 +52,11 @@ def main():
     gp.fit(iterations=5000, verbose=0, store_loss_hist=True)
     torch.cuda.synchronize()
     pr.disable()
-    s = io.StringIO()
-    pstats.Stats(pr, stream=s).sort_stats("cumulative").print_stats(45)
-    print(s.getvalue())
+    st = pstats.Stats(pr).stats          # {(file, line, fn): (cc, nc, tottime, cumtime, callers)}
+    rows = sorted(st.items(), key=lambda kv: -kv[1][3])[:60]
+    print("%9s %9s %6s  %s" % ("cum_us", "self_us", "calls", "function"))
+    for (fn, ln, name), (cc, nc, tt, ct, _) in rows:
+        print("%9.1f %9.1f %6d  %s:%d(%s)" % (ct * 1e6, tt * 1e6, nc, os.path.basename(fn), ln, name))
 
 
 if __name__ == "__main__":
