@@ -217,7 +217,16 @@ def call(name, *args):
     return rc
 
 
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream_ptr(device):
+    """The current HIP stream of `device` (torch's raw-stream query: ~1 us instead of the ~7 us of building a
+    torch.cuda.Stream object per call)."""
+    if _RAW_STREAM is not None:
+        idx = device.index if isinstance(device, torch.device) and device.index is not None else \
+            torch.cuda.current_device() if not isinstance(device, int) else device
+        return ctypes.c_void_p(_RAW_STREAM(idx))
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 

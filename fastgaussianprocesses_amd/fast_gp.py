@@ -199,6 +199,12 @@ class AbstractFastGP(torch.nn.Module):
         lengthscales = _Hyper.make(lengthscales, shape_lengthscales, shape_batch, lambda v: v in (1, d),
                                    "lengthscales", "pos", dev)
         noise = _Hyper.make(noise, shape_noise, shape_batch, lambda v: v == 1, "noise", "pos", dev)
+        # the default task kernel (no factor columns, task noise 1 through the default transforms) is exactly 1:
+        # known here, so the first fit need not check it on the device (_task_unit)
+        unit_task = (shape_factor_task_kernel is None and not isinstance(factor_task_kernel, torch.Tensor)
+                     and not rank_factor_task_kernel and shape_noise_task_kernel is None
+                     and not isinstance(noise_task_kernel, torch.Tensor) and float(noise_task_kernel) == 1.0
+                     and tfs_noise_task_kernel is _DEFAULT_TFS)
         if shape_factor_task_kernel is None and not isinstance(factor_task_kernel, torch.Tensor):
             if rank_factor_task_kernel is None:
                 rank_factor_task_kernel = 0
@@ -223,6 +229,9 @@ class AbstractFastGP(torch.nn.Module):
                                                          requires_grad=bool(requires_grad_factor_task_kernel))
         self.raw_noise_task_kernel = torch.nn.Parameter(tfs_noise_task_kernel[0](noise_task_kernel),
                                                         requires_grad=bool(requires_grad_noise_task_kernel))
+        if unit_task:
+            self._task_unit_memo = (tuple((id(p), p._version, p.data_ptr()) for p in (
+                self.raw_factor_task_kernel, self.raw_noise_task_kernel)), True)
         self.adaptive_nugget = adaptive_nugget
         self.compile_fts, self.compile_fts_kwargs = compile_fts, compile_fts_kwargs   # accepted; HIP kernels are native
         # alpha (abstract_fast_gp.py:21-24)
