@@ -743,7 +743,8 @@ class AbstractFastGP(torch.nn.Module):
                         mll_const=mll_constant(d_out, n),
                         requires_grad=(self.raw_scale.requires_grad, self.raw_lengthscales.requires_grad,
                                        self.raw_noise.requires_grad),
-                        lr=lr, max_iters=min(iterations + 1, 64), gen=gen, basis=basis)
+                        lr=lr, max_iters=(iterations + 1 if G == 1 and iterations < 8192 else min(iterations + 1, 64)),
+                        gen=gen, basis=basis)
 
     def _fit_fused(self, iterations, lr, stop, hists, verbose, indent, ysq=None, d_out=None):
         """Device-resident MLL fit (the engine of _fused_engine; the reference's loop semantics: loss

@@ -201,9 +201,10 @@ class FusedMLL(object):
         cdt = torch.complex128 if self.family == 0 else torch.float64
         self.work = torch.empty((G, n), dtype=cdt, device=self.device) if (self.m > 12 and basis is None and
                                                                            mt is None) else None
-        self.prev = torch.zeros(self.n_params, dtype=torch.float64, device=self.device)
-        self.step = torch.full((self.n_params,), float(lr), dtype=torch.float64, device=self.device)
-        self.grad = torch.zeros(self.n_params, dtype=torch.float64, device=self.device)
+        # Rprop state (previous gradient, step sizes) and the gradient in one allocation
+        st = torch.zeros((3, self.n_params), dtype=torch.float64, device=self.device)
+        st[1].fill_(float(lr))
+        self.prev, self.step, self.grad = st[0], st[1], st[2]
         self.max_iters = 0
         self.loss_hist = None
         self.raw_hist = None
