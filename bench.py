@@ -832,6 +832,8 @@ def capture_fn(fn):
         with torch.cuda.stream(s):
             with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
                 out = fn()
+                if os.environ.get("FGP_BENCH_GRAPH_FAIL") == "1":      # test hook: the eager fallback
+                    torch.cuda.synchronize()                          # (a sync inside a capture invalidates it)
         torch.cuda.current_stream().wait_stream(s)
         g.replay()
         torch.cuda.synchronize()
