@@ -113,6 +113,26 @@ __device__ __forceinline__ void spec_terms(const double* phi, const Hyp& h, doub
   for (int j = 0; j < D; ++j) acc.gl[j] = __builtin_fma(g, dp[j], acc.gl[j]);
 }
 
+// One lane of a double through a DPP pattern (two 32-bit moves; every source lane valid for the patterns used)
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+// The sum over the 64 lanes of a wave in a fixed order (valid in every lane 0..63 of each 16-lane row, the total
+// from the four row sums): DPP quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror (VALU-latency moves
+// instead of six LDS-crossbar ds_bpermute rounds of a butterfly), then ((r0 + r16) + (r32 + r48)) by v_readlane.
+// Deterministic; the spectral kernels' per-block partials all use it, so they agree bit for bit.
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+  v += dpp_f64<0xB1>(v);    // quad_perm [1,0,3,2]: pairs
+  v += dpp_f64<0x4E>(v);    // quad_perm [2,3,0,1]: quads
+  v += dpp_f64<0x141>(v);   // row_half_mirror (lane i <-> 7 - i): 8 lanes
+  v += dpp_f64<0x140>(v);   // row_mirror (lane i <-> 15 - i): the 16-lane row
+  return (read_lane(v, 0) + read_lane(v, 16)) + (read_lane(v, 32) + read_lane(v, 48));
+}
+
 // v[0..3+D] of one accumulator set: norm, log|ev| sum, g sum, g P sum, g dP/dl_j sums
 template <int D>
 __device__ __forceinline__ void spec_values(const SpecAcc<D>& acc, double* v) {
@@ -196,9 +216,7 @@ __device__ __forceinline__ void spec_block_partials(const Nll& a, const Hyp& h, 
     }
   }
 #pragma unroll
-  for (int q = 0; q < NV; ++q)
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v[q] += __shfl_xor(v[q], o, 64);
+  for (int q = 0; q < NV; ++q) v[q] = wave_sum_dpp(v[q]);
   if (lane == 0) {
     const double gsc = rootn * h.scale;
     v[3] *= gsc;
