@@ -598,7 +598,7 @@ struct FitFuse {
 constexpr int kSpecStateMax = 64;                  // Rprop parameters of a persistent k_spec_tile (LDS copies)
 // parameters of a spectral fit (the raw vector's length: the noise block is last)
 __host__ __device__ __forceinline__ int spec_nparams(const Nll& a) { return a.noise_off + (a.noise_pp ? a.G : 1); }
-constexpr int kHandoffWords = 16 * 8 * 16;         // XOR words of the check buffer (groups x G x nq, at most)
+constexpr int kHandoffWords = 32 * 8 * 16;         // XOR words of the check buffer (groups x G x nq, at most)
 int launch_re_bwd_fused(const Nll& a, const FitFuse& fz, const Tables* tb, hipStream_t st);
 
 // spectral fit path (fgp_spectral.hip): d <= kSpecMaxD, at most kSpecBlocks k blocks per problem

@@ -359,7 +359,10 @@ __global__ __launch_bounds__(kWG) void k_spec_iter(Nll a) {
 // are bit-identical: level 1 sums the blocks of each group of kSpecGroup consecutive blocks (ascending),
 // level 2 sums the ng = ceil(nb / kSpecGroup) group sums (ascending).  One thread per (problem,
 // quantity): a group's block loads are issued together (one round trip, not a dependent chain).
-constexpr int kSpecGroup = 32;
+#ifndef FGP_SPEC_GROUP
+#define FGP_SPEC_GROUP 32
+#endif
+constexpr int kSpecGroup = FGP_SPEC_GROUP;
 
 __device__ __forceinline__ int spec_groups(const Nll& a) { return (a.nb + kSpecGroup - 1) / kSpecGroup; }
 
