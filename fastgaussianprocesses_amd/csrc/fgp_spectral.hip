@@ -769,14 +769,23 @@ __global__ __launch_bounds__(kWG) void k_spec_persist(Nll a, Fit f, int iters, d
       return;
     }
     stamp(it, 2);
-    // level 1 (groups of kSpecGroup blocks, ascending) and level 2 (groups ascending): k_spec_reduce_step's order
+    // level 1 (groups of kSpecGroup blocks, ascending) and level 2 (groups ascending): k_spec_reduce_step's order.
+    // One workgroup, one group: the partials are in LDS and level 2 adds the single group sum to 0.0 (exact), so
+    // thread q sums its row of lpart directly (typed LDS loads, one barrier) -- the same additions in the same order.
+    if (single) {
+      if (tid < NQ) {
+        double sq = 0.0;
+        for (int b = 0; b < a.nb; ++b) sq += lpart[tid * a.nb + b];
+        tot[tid] = sq;
+      }
+    } else {
     for (int e = tid; e < NQ * ng; e += kWG) {
       const int q = e / ng, grp = e - q * ng;
       const int b0 = grp * kSpecGroup, nbg = min(kSpecGroup, a.nb - b0);
       const double* pp = pbase + (int64_t)q * a.nb + b0;
       double tv[kSpecGroup];
 #pragma unroll
-      for (int b = 0; b < kSpecGroup; ++b) tv[b] = single ? pp[b < nbg ? b : 0] : ld_part<true>(pp + (b < nbg ? b : 0));
+      for (int b = 0; b < kSpecGroup; ++b) tv[b] = ld_part<true>(pp + (b < nbg ? b : 0));
       double sgrp = 0.0;
 #pragma unroll
       for (int b = 0; b < kSpecGroup; ++b) sgrp += b < nbg ? tv[b] : 0.0;
@@ -787,6 +796,7 @@ __global__ __launch_bounds__(kWG) void k_spec_persist(Nll a, Fit f, int iters, d
       double sq = 0.0;
       for (int grp = 0; grp < ng; ++grp) sq += gsum[tid * MAXG + grp];
       tot[tid] = sq;
+    }
     }
     __syncthreads();
     stamp(it, 3);
