@@ -1,5 +1,6 @@
 #!/bin/bash
 # the LDS-only-barrier patch (tools/exp/r04v_barrier_keep_vm.patch) as an experiment build: parity subset + stamps
+# build first (CPU): git apply tools/exp/r04v_barrier_keep_vm.patch && bash tools/build_exp.sh FGP_EXP_KEEPVM=1 keepvm fgp_spectral.hip && git checkout fastgaussianprocesses_amd/csrc/fgp_spectral.hip && python -c "import fastgaussianprocesses_amd.build as b; b.build()"
 export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-r04v}
 mkdir -p $OUT
