@@ -62,7 +62,37 @@ def parse():
                    help="skip the docs/examples/multitask per-step timings reported under 'multitask'")
     p.add_argument("--no-paper", dest="paper", action="store_false",
                    help="skip the probnum25 paper's n=2^10 per-step timings reported under 'paper'")
+    p.add_argument("--dump", default=None,
+                   help="directory: every rank writes its shifts' seeds, fitted raw parameters, post_mean and post_var "
+                        "after the timed steps to rank<r>.npz (the N-rank test compares them with N = 1 runs)")
     return p.parse_args()
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args, argv):
+    """`bench.py --gpus N` (N > 1) started without a launcher: run torch.distributed.run with N ranks over this
+    same command line as a CHILD process -- before this process makes any GPU call -- relay rank 0's JSON line
+    and return the child's exit code.  (The driver's own N-GPU runs start under torch.distributed.run, with
+    WORLD_SIZE set, and go straight to main.)"""
+    import subprocess
+    import sys
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True)
+    for line in proc.stdout:
+        if line.startswith("{"):
+            print(line.rstrip("\n"), flush=True)
+        else:
+            sys.stderr.write(line)
+    return proc.wait()
 
 
 def shard_seeds(rank, world, per_rank, base=1000):
@@ -304,6 +334,14 @@ def secondary_configs(F, args, device, rank=0, world=1, collect=None):
                 samples.append([ev[i].elapsed_time(ev[i + 1]) for i in range(4)])
             phases = {k: sorted(s[i] for s in samples)[1] for i, k in enumerate(keys)}
         total = getattr(sg, "total", 1)
+        roof_pm = None
+        if name.startswith("C5 per-output"):
+            # 512 outputs with their own kernels: k_post_mean<0, 3, 4, 4> over blocks of 4 outputs (128 launches of
+            # N x n x 4 output-pairs), priced on tools/predict_kernels.py's trace of the same call
+            roof_pm = roofline_post_mean("k_post_mean<0, 3, 4, 4>", None, args.n_mean * sg.n * 4, 3, 4,
+                                         stats=ROCPROF_PREDICT_STATS, sq=PMC_SQ_PREDICT,
+                                         live_ms=phases.get("post_mean") if phases else None,
+                                         launches=(sg.outputs + 3) // 4)
         out.append({"metric": "GP fit+predict points/sec" if total == 1 else
                     "multi-output GP fit+predict output-points/sec",
                     "value": sg.n * total / sec, "unit": "points/s" if total == 1 else "output-points/s",
@@ -312,7 +350,7 @@ def secondary_configs(F, args, device, rank=0, world=1, collect=None):
                     "config": {"workload": "%s: fit %d Rprop iters + post_mean N=%d + post_var N=%d"
                                            % (name, args.fit_iters, args.n_mean, args.n_var),
                                "n": sg.n, "outputs": total},
-                    "phases_ms": phases, "graph": ginfo})
+                    "phases_ms": phases, "graph": ginfo, "roofline_predict": roof_pm})
         del graph, sg
         torch.cuda.empty_cache()
     return out
@@ -708,6 +746,10 @@ STREAM_FLOOR_US = 24.0
 # (FP64 vector at half the FP32 vector rate of MI355X_MICROARCH.md, 157.3 TFLOP/s; 78.6 TFLOP/s FMA)
 FP64_LANE_OPS_PEAK = 256 * 4 * 16 * 2.4e9
 CPU_FIDELITY = os.path.join(ROOT, "profiles", "r02_cpu_fidelity.json")
+# the prediction kernels (tools/predict_kernels.py: C4's batched post_mean / post_var, C5 per-output's post_mean):
+# rocprofv3 kernel-trace summary and SQ counter pass
+ROCPROF_PREDICT_STATS = os.path.join(ROOT, "profiles", "r05_predict_kernel_grid_stats.txt")
+PMC_SQ_PREDICT = os.path.join(ROOT, "profiles", "r05_pmc_sq_predict.json")
 
 
 def pmc_traffic(kernel, grid):
@@ -725,26 +767,35 @@ def pmc_traffic(kernel, grid):
     return None
 
 
-def pmc_valu_insts(kernel, grid):
+def _kernel_match(name, kernel):
+    """`kernel` is a base name ("k_spec_tile": any template instance) or a full instance ("k_post_mean<0, 5, 1, 4>")."""
+    full = name.split("::")[-1] if "<" not in name else name[name.index("k_"):] if "k_" in name else name
+    if "<" in kernel:
+        return full.replace(" ", "") == kernel.replace(" ", "")
+    return name.split("<")[0].split("::")[-1] == kernel
+
+
+def pmc_valu_insts(kernel, grid, path=None):
     """VALU wave-instructions per launch (SQ_INSTS_VALU) of `kernel` at `grid` threads from the committed
-    SQ counter pass (tools/pmc_sq_summary.py over tools/fit_kernels.py), or None when absent."""
+    SQ counter pass (tools/pmc_sq_summary.py over tools/fit_kernels.py; `path`: another summary, e.g. the
+    prediction kernels' over tools/predict_kernels.py), or None when absent."""
     try:
-        summ = json.load(open(PMC_SQ_SUMMARY))
+        summ = json.load(open(path or PMC_SQ_SUMMARY))
     except (OSError, ValueError):
         return None
     for k, v in summ.items():
         name, _, g = k.partition("|grid=")
-        if name.split("<")[0].split("::")[-1] == kernel and g == str(grid) and "SQ_INSTS_VALU" in v:
+        if _kernel_match(name, kernel) and (grid is None or g == str(grid)) and "SQ_INSTS_VALU" in v:
             return v["SQ_INSTS_VALU"]
     return None
 
 
-def rocprof_avg_us(kernel, grid):
+def rocprof_avg_us(kernel, grid, path=None):
     """Average duration of `kernel` at `grid` threads in the committed rocprofv3 --kernel-trace summary
     of this bench command (tools/kstats_grid.py over `rocprofv3 --kernel-trace --stats -- python3
-    bench.py`), or None when absent."""
+    bench.py`; `path`: another summary), or None when absent."""
     try:
-        lines = open(ROCPROF_GRID_STATS).read().splitlines()[1:]
+        lines = open(path or ROCPROF_GRID_STATS).read().splitlines()[1:]
     except OSError:
         return None
     for ln in lines:
@@ -752,9 +803,44 @@ def rocprof_avg_us(kernel, grid):
         if len(f) < 6:
             continue
         name = " ".join(f[:-5])
-        if name.split("<")[0].split("::")[-1] == kernel and f[-5] == str(grid):
+        if _kernel_match(name, kernel) and (grid is None or f[-5] == str(grid)):
             return float(f[-3])
     return None
+
+
+def post_mean_ops_per_pair(d, nb):
+    """FP64 VALU instructions per (test point, training point, output) of k_post_mean's folded-B4 loop
+    (csrc/fgp_predict.hip; lattice, alpha = 2), read off its gfx950 ISA: per dimension v_add_f64 (x_t - z_i) and
+    v_fma_f64 (u = t^2 - |t|) shared by the kernel's nb outputs, then per output v_fma_f64 (u^2 + c') and v_mul_f64
+    into the product (less the first dimension's product by 1.0), and one v_fmac_f64 with the coefficient:
+    (2 d + 2 d nb) / nb -- 4 d for one output."""
+    return (2.0 * d + 2.0 * d * nb) / nb
+
+
+def roofline_post_mean(kernel, grid, pairs, d, nb, stats=None, sq=None, live_ms=None, launches=1):
+    """FP64-VALU roofline of a posterior-mean launch (abstract_gp.py:352-380; matrix-free cross-kernel
+    contraction): `pairs` (test point, training point, output) triples per launch x post_mean_ops_per_pair
+    lane-operations over the rocprofv3 average duration, against the FP64 VALU issue peak; beside it the
+    measured SQ_INSTS_VALU x 64 lanes over the same duration (every VALU instruction, address and loop
+    arithmetic included)."""
+    us = rocprof_avg_us(kernel, grid, stats)
+    ops = post_mean_ops_per_pair(d, nb)
+    out = {"bound": "fp64 valu", "kernel": kernel, "pairs_per_launch": pairs, "ops_per_pair": ops,
+           "op_model": "per dimension v_add_f64 + v_fma_f64 shared by %d output(s), v_fma_f64 + v_mul_f64 per output, "
+                       "one v_fmac_f64 per output (gfx950 ISA of the folded-B4 loop)" % nb,
+           "peak": FP64_LANE_OPS_PEAK, "unit": "FP64 lane-ops/s", "launches_per_step": launches,
+           "avg_us_source": "rocprofv3 --kernel-trace average, %s" % os.path.relpath(stats or ROCPROF_GRID_STATS, ROOT)}
+    if us is None:
+        return out
+    ach = pairs * ops / (us * 1e-6)
+    out.update({"avg_us": us, "achieved": ach, "frac": ach / FP64_LANE_OPS_PEAK})
+    vi = pmc_valu_insts(kernel, grid, sq)
+    if vi is not None:
+        out["valu"] = {"insts_per_launch": vi, "frac": vi * 64 / (us * 1e-6) / FP64_LANE_OPS_PEAK,
+                       "source": os.path.relpath(sq or PMC_SQ_SUMMARY, ROOT) + " (SQ_INSTS_VALU)"}
+    if live_ms is not None:
+        out["phase_ms_live"] = live_ms
+    return out
 
 
 def cpu_baseline(args, n, d):
@@ -862,15 +948,25 @@ def capture_step(sh, args, xm, xv):
 
 
 def main():
+    import sys
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # test overrides: every rank on one device (FGP_BENCH_DEVICE) and the gloo backend (the N-rank test on one GPU)
+    if os.environ.get("FGP_BENCH_DEVICE"):
+        local = int(os.environ["FGP_BENCH_DEVICE"])
     dist = world > 1
     if dist:
         import torch.distributed as tdist
         torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("FGP_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            tdist.init_process_group(backend)
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
     import fastgaussianprocesses_amd as F
@@ -913,6 +1009,13 @@ def main():
         torch.cuda.synchronize()
         graph_info["eager_ms_per_step"] = (time.perf_counter() - t0) / args.steps * 1e3
 
+    if args.dump:
+        # one more step's results (every step is the same computation from the same reset state)
+        data, pm, pv = step_batched(shifts, args, xm, xv)
+        torch.cuda.synchronize()
+        os.makedirs(args.dump, exist_ok=True)
+        np.savez(os.path.join(args.dump, "rank%d.npz" % rank), seeds=np.array(shard_seeds(rank, world, args.shifts)),
+                 raw=shifts.batch.raw().cpu().numpy(), post_mean=pm.cpu().numpy(), post_var=pv.cpu().numpy())
     phases = phase_breakdown(shifts, args.fit_iters, xm, xv)
     n_, variant, us, us_ev, t_iter, khz = roofline_fit_kernels(F, shifts, args.fit_iters)
     parts_array = variant not in ("spectral", "spectral_fused", "re")
@@ -969,8 +1072,14 @@ def main():
                     "path, which reads only the 2^d shared spectra and Y per iteration"}
         roof["read_floor"] = {"us": STREAM_FLOOR_US, "frac": STREAM_FLOOR_US / us_price,
                               "source": "tools/stream_microbench.hip, profiles/r03v_stream_and_stamps.jsonl"}
+    # the posterior mean (about a third of the step): FP64-VALU roofline of its one k_post_mean launch over the P
+    # shifts (fgp_post_mean_batched), priced on the same rocprofv3 trace as `roofline`
+    roof_pm = roofline_post_mean("k_post_mean<0, %d, 1, 4>" % d, None, P * args.n_mean * n, d, 1, sq=PMC_SQ_PREDICT,
+                                 live_ms=phases.get("post_mean"))
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:
+        # after the timed region on every N (rank 0 only; the other ranks wait at the next collective), so the
+        # N-GPU line carries the CPU baseline beside its scaling
         cpu = cpu_baseline(args, n, d)
     secondary = None
     if args.secondary:
@@ -993,7 +1102,13 @@ def main():
                                       "post_mean N=%d + post_var N=%d per shift" %
                                       (args.log2n, d, args.shifts, args.fit_iters, args.n_mean, args.n_var),
                           "global_shifts": args.shifts * world, "parallelism": "replicas%d" % world},
-               "roofline": roof, "cpu_baseline": cpu, "phases_ms": phases, "secondary": secondary,
+               "timing": {"value_from": "hipGraph replay of the whole step (captured once, replay checked bit-identical "
+                                        "to an eager step)" if graph is not None else "eager enqueue of every step",
+                          "value_eager": (args.shifts * n * world / (graph_info["eager_ms_per_step"] * 1e-3)
+                                          if graph is not None else value),
+                          "ms_per_step_eager": graph_info.get("eager_ms_per_step", sec_step * 1e3)},
+               "roofline": roof, "roofline_predict": roof_pm,
+               "cpu_baseline": cpu, "phases_ms": phases, "secondary": secondary,
                "paper": paper, "multitask": multitask, "graph": graph_info}
         print(json.dumps(out))
     if dist:

@@ -1973,6 +1973,11 @@ int fgp_fit_persist(const fgp_nll_desc* nll, const fgp_fit_desc* fit, int iters,
                              (hipStream_t)stream);
 }
 
+int fgp_set_persist_poll_max(long long polls) {
+  set_persist_poll_max(polls);
+  return kOk;
+}
+
 int fgp_handoff_check(int enable, unsigned long long* out) {
   const size_t bytes = sizeof(unsigned long long) * (kHandoffWords + 2);
   if (enable) {

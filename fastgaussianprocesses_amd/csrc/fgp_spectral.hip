@@ -668,7 +668,7 @@ constexpr long long kPersistPollMax = 1ll << 22;
 
 template <int D, bool NET>
 __global__ __launch_bounds__(kWG) void k_spec_persist(Nll a, Fit f, int iters, double logtol, int wait_max, int bpw,
-                                                      unsigned* counter, int* out) {
+                                                      unsigned* counter, int* out, long long poll_max) {
   constexpr int NS = 1 << D, NQ = 4 + D, MAXG = kSpecBlocks / kSpecGroup;
   extern __shared__ double lds[];                  // [bpw][kpl][NS + 1][64] spectra + Y of this workgroup's blocks
   __shared__ double st_raw[kSpecScratch], st_prev[kSpecScratch], st_step[kSpecScratch];
@@ -754,7 +754,7 @@ __global__ __launch_bounds__(kWG) void k_spec_persist(Nll a, Fit f, int iters, d
       long long polls = 0;
       while (__hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
         __builtin_amdgcn_s_sleep(2);
-        if (++polls > kPersistPollMax) {
+        if (++polls > poll_max) {
           fail_s = 1;
           break;
         }
@@ -763,9 +763,13 @@ __global__ __launch_bounds__(kWG) void k_spec_persist(Nll a, Fit f, int iters, d
     __syncthreads();
     if (fail_s) {
       // a barrier gave up (every workgroup's next wait then fails too, so no final state is written): the
-      // fit's parameters become NaN -- visible downstream even when the caller never reads `out`
+      // fit's parameters and every parameter-history row become NaN -- whichever row the caller restores as the
+      // best iterate, the failure shows downstream even when `out` is never read (a hipGraph replay).  Rprop's
+      // prev / step are untouched: with the caller's copy of the entry raw parameters the fit can be re-run.
       if (tid == 0) out[1] = 1;
       for (int p = tid; p < np; p += kWG) f.raw[p] = NAN;
+      if (f.raw_hist)
+        for (int64_t e = tid; e < (int64_t)(iters + 1) * f.n_params; e += kWG) f.raw_hist[e] = NAN;
       return;
     }
     stamp(it, 2);
@@ -1741,6 +1745,47 @@ int launch_spec_reduce_step(const Nll& a, const Fit& f, int iter, int do_update,
   });
 }
 
+// The k_spec_persist instance of a desc (D, NET), for the residency query.
+static const void* spec_persist_kernel(const Nll& a) {
+  const void* kp = nullptr;
+  (void)with_spec_d(a.d, [&](auto dc) {
+    constexpr int D = decltype(dc)::value;
+    kp = a.spec_net ? reinterpret_cast<const void*>(k_spec_persist<D, true>)
+                    : reinterpret_cast<const void*>(k_spec_persist<D, false>);
+    return kOk;
+  });
+  return kp;
+}
+
+// Workgroups of `kp` at `shm` bytes of dynamic LDS that can be resident at once on the current device
+// (workgroups per CU x CUs), queried once per (kernel, LDS size) and remembered -- so a launch inside a hipGraph
+// capture makes no query.  0 when the query fails.
+static int64_t persist_resident(const void* kp, size_t shm) {
+  static const void* rk[64];
+  static size_t rshm[64];
+  static int64_t rres[64];
+  static int nr = 0;
+  for (int i = 0; i < nr; ++i)
+    if (rk[i] == kp && rshm[i] == shm) return rres[i];
+  (void)hipFuncSetAttribute(kp, hipFuncAttributeMaxDynamicSharedMemorySize, kPersistLdsMax);
+  int per_cu = 0, dev = 0, cus = 0;
+  const int64_t resident = (hipGetDevice(&dev) == hipSuccess &&
+                            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+                            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kp, kWG, shm) == hipSuccess)
+                               ? (int64_t)per_cu * cus : 0;
+  if (nr < 64) {
+    rk[nr] = kp;
+    rshm[nr] = shm;
+    rres[nr++] = resident;
+  }
+  return resident;
+}
+
+// Test hook (fgp_set_persist_poll_max): the bound of k_spec_persist's barrier polls (default 2^22).
+static long long g_persist_poll_max = kPersistPollMax;
+
+void set_persist_poll_max(long long v) { g_persist_poll_max = v < 0 ? kPersistPollMax : v; }
+
 int spec_persist_geometry(const Nll& a, int* W, int* bpw, size_t* shm) {
   if (!a.spec || a.G != 1 || a.basis_stride != 0 || a.d > kSpecMaxD || !a.ysq_chunked)
     return set_error(kErrUnsupported, "fgp_fit_persist: one problem on the spectral path only");
@@ -1749,6 +1794,10 @@ int spec_persist_geometry(const Nll& a, int* W, int* bpw, size_t* shm) {
   for (int w = 1; w <= kPersistMaxW && w <= a.nb; w *= 2) {
     const int b = (a.nb + w - 1) / w;
     if ((size_t)b * per_blk <= (size_t)kPersistLdsMax) {
+      // the workgroups wait on each other at the in-kernel grid barrier: all W must be resident at once
+      // (a partitioned device, or CUs held by other work, would otherwise turn every barrier into a give-up)
+      if (w > 1 && persist_resident(spec_persist_kernel(a), (size_t)b * per_blk) < (int64_t)w)
+        return set_error(kErrUnsupported, "fgp_fit_persist: %d workgroups are not co-resident", w);
       *W = w;
       *bpw = b;
       *shm = (size_t)b * per_blk;
@@ -1771,7 +1820,7 @@ int launch_spec_persist(const Nll& a, const Fit& f, int iters, double logtol, in
     auto go = [&](auto kern) {
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 kPersistLdsMax);
-      kern<<<(unsigned)W, kWG, shm, st>>>(a, f, iters, logtol, wait_max, bpw, counter, out);
+      kern<<<(unsigned)W, kWG, shm, st>>>(a, f, iters, logtol, wait_max, bpw, counter, out, g_persist_poll_max);
     };
     if (a.spec_net) go(k_spec_persist<D, true>);
     else go(k_spec_persist<D, false>);

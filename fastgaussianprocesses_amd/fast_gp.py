@@ -230,8 +230,7 @@ class AbstractFastGP(torch.nn.Module):
         self.raw_noise_task_kernel = torch.nn.Parameter(tfs_noise_task_kernel[0](noise_task_kernel),
                                                         requires_grad=bool(requires_grad_noise_task_kernel))
         if unit_task:
-            self._task_unit_memo = (tuple((id(p), p._version, p.data_ptr()) for p in (
-                self.raw_factor_task_kernel, self.raw_noise_task_kernel)), True)
+            self._task_unit_memo = (self._task_unit_key(), True)
         self.adaptive_nugget = adaptive_nugget
         self.compile_fts, self.compile_fts_kwargs = compile_fts, compile_fts_kwargs   # accepted; HIP kernels are native
         # alpha (abstract_fast_gp.py:21-24)
@@ -341,12 +340,18 @@ class AbstractFastGP(torch.nn.Module):
     def _task_unit(self):
         """gram_matrix_tasks == 1 (a single-task GP's unit task kernel).  Checked again only when the
         task-kernel parameters change: the check synchronises with the device."""
-        key = tuple((id(p), p._version, p.data_ptr()) for p in (self.raw_factor_task_kernel, self.raw_noise_task_kernel))
+        key = self._task_unit_key()
         hit = getattr(self, "_task_unit_memo", None)
-        if hit is None or hit[0] != key:
+        if hit is None or len(hit[0]) != len(key) or not all(
+                a[0] is b[0] and a[1:] == b[1:] for a, b in zip(hit[0], key)):
             kt = self.gram_matrix_tasks.detach()
             hit = self._task_unit_memo = (key, bool(torch.equal(kt, torch.ones_like(kt))))
         return hit[1]
+
+    def _task_unit_key(self):
+        """The task-kernel Parameters THEMSELVES (held by the memo, so a replaced Parameter's id / address cannot
+        be reused by a new one while the memo refers to it), their version counters and data pointers."""
+        return tuple((p, p._version, p.data_ptr()) for p in (self.raw_factor_task_kernel, self.raw_noise_task_kernel))
 
     def _task_scalar(self):
         if not self._task_unit():
@@ -759,25 +764,27 @@ class AbstractFastGP(torch.nn.Module):
         done = False
         losses = []
         if getattr(eng, "persist_ok", lambda: False)():
-            # the whole fit in one launch (fgp_fit_persist: the early-stopping rule on the device).  Without a
-            # possible early stop nothing is read back (every iteration runs; the best iterate is found on the
-            # device, as below); otherwise the last iteration and the host rule on the loss history.
+            # the whole fit in one launch (fgp_fit_persist: the early-stopping rule on the device); the last
+            # iteration and the failure word are read back.  A barrier give-up (None) restored the entry state:
+            # the fit then runs below on the launch per iteration (the same trajectory bit for bit).
             no_stop = wait_max > iterations
-            i = eng.run_persist(iterations, logtol, wait_max, sync=not no_stop)
-            done = True
-            if no_stop:
-                l0 = eng.loss_hist[:total, 0, 0]
-                best_i = torch.where(torch.isnan(l0), torch.full_like(l0, math.inf), l0).argmin()
-            if not no_stop or verbose or hists["loss"]:
-                rows = eng.loss_hist[:i + 1, 0].cpu().tolist()
-                for r, row in enumerate(rows):
-                    lv = float(row[0])
-                    losses.append((lv, float(row[1]), float(row[2])))
-                    if lv < best and not no_stop:
-                        best, best_i = lv, r
-                    if verbose and (r % verbose == 0 or r == i):
-                        self._log_row(r, lv, row[1], row[2], indent)
-        elif wait_max > iterations:
+            ip = eng.run_persist(iterations, logtol, wait_max)
+            if ip is not None:
+                i = ip
+                done = True
+                if no_stop:
+                    l0 = eng.loss_hist[:total, 0, 0]
+                    best_i = torch.where(torch.isnan(l0), torch.full_like(l0, math.inf), l0).argmin()
+                if not no_stop or verbose or hists["loss"]:
+                    rows = eng.loss_hist[:i + 1, 0].cpu().tolist()
+                    for r, row in enumerate(rows):
+                        lv = float(row[0])
+                        losses.append((lv, float(row[1]), float(row[2])))
+                        if lv < best and not no_stop:
+                            best, best_i = lv, r
+                        if verbose and (r % verbose == 0 or r == i):
+                            self._log_row(r, lv, row[1], row[2], indent)
+        if not done and wait_max > iterations:
             # no early stop is possible: every iteration runs, the best iterate is the first minimum of
             # the loss history (the host rule `lv < best`; NaN never best), found on the device -- one
             # enqueue, no host sync unless losses are logged or returned

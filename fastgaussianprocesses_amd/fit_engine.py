@@ -307,28 +307,46 @@ class FusedMLL(object):
     def persist_ok(self):
         """fgp_fit_persist applies (one problem on the spectral path whose spectra fit the LDS of at most 64
         workgroups: the whole fit in one launch); FGP_FIT_PERSIST=0 keeps the launch per iteration."""
+        return self.persist_workgroups() > 0
+
+    def persist_workgroups(self):
+        """Workgroups of the single-launch fit (fgp_fit_persist_ok: 0 outside its domain, or when they would not
+        all be co-resident on this device)."""
         if os.environ.get("FGP_FIT_PERSIST", "1")[:1] == "0" or self.G != 1 or self.basis is None:
-            return False
+            return 0
         ok = ctypes.c_int(0)
         N.call("fgp_fit_persist_ok", self._nll, ctypes.byref(ok))
-        return ok.value > 0
+        return ok.value
 
-    def run_persist(self, iterations, logtol, wait_max, sync=True):
+    def run_persist(self, iterations, logtol, wait_max):
         """AbstractGP.fit's iterations 0 .. iterations with its early-stopping rule, in one launch
-        (fgp_fit_persist); returns the last iteration evaluated (its row applied no update).  sync=False (no
-        early stop possible): nothing is read back and `iterations` is returned; the barrier flag is checked at
-        the next synchronising call (check_persist)."""
+        (fgp_fit_persist); returns the last iteration evaluated (its row applied no update).
+
+        The 4-int control word is read back at once (one small device-to-host read): when an in-kernel barrier
+        gave up (the workgroups were not co-resident after all -- e.g. CUs taken by other work), the entry
+        parameters are restored (the kernel leaves Rprop's state untouched and sets the parameters to NaN) and
+        None is returned, so the caller re-runs the fit on the launch per iteration, which gives the same
+        trajectory bit for bit.  Inside a hipGraph capture nothing can be read: the word is kept for
+        check_persist at the next eager call, and a failure shows as NaN parameters and parameter history."""
         self.check_persist()
         self.ensure_history(iterations + 1)
         ctrl = torch.zeros((4,), dtype=torch.int32, device=self.device)
+        capturing = torch.cuda.is_current_stream_capturing()
+        raw0 = None if capturing else self.raw.clone()
         N.call("fgp_fit_persist", self._nll, self._fit, int(iterations), float(logtol), int(wait_max),
                ctrl.data_ptr(), self.stream())
-        self._ctrl = ctrl
-        if not sync:
+        if capturing:
+            self._ctrl = ctrl
             return int(iterations)
-        return self.check_persist()
+        c = ctrl.cpu().tolist()
+        if c[2]:
+            self.raw.copy_(raw0)
+            self.persist_failures = getattr(self, "persist_failures", 0) + 1
+            return None
+        return int(c[1])
 
     def check_persist(self):
+        """Raise for a failed fgp_fit_persist whose control word could not be read when it ran (a capture)."""
         ctrl = getattr(self, "_ctrl", None)
         if ctrl is None:
             return None

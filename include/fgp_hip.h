@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define FGP_ABI_VERSION 15
+#define FGP_ABI_VERSION 16
 
 #define FGP_OK 0
 #define FGP_ERR_INVALID (-1)     /* bad argument (shape, stride, null pointer) */
@@ -563,6 +563,13 @@ int fgp_mt_fit_run(const fgp_mt_fit_desc* desc, int iter0, int iters, int final_
  * mismatch.  enable == 0 synchronises the device, disarms it and returns out[0] = group hand-offs checked,
  * out[1] = mismatches (0 when every arriver saw every stored partial). */
 int fgp_handoff_check(int enable, unsigned long long* out);
+
+/* ABI 16 -- test hook (no reference counterpart): the bound of fgp_fit_persist's in-kernel barrier polls (a
+ * negative value restores the default 2^22).  0 makes every barrier wait that does not find the grid complete
+ * give up at once, so the failure path (fit parameters and parameter history set to NaN, ((int*)ctrl)[2] = 1)
+ * and the host's fallback to the launch per iteration can be tested.  fgp_fit_persist_ok / fgp_fit_persist
+ * also report unsupported (0 / an error) when the workgroups would not all be co-resident. */
+int fgp_set_persist_poll_max(long long polls);
 
 #ifdef __cplusplus
 }

@@ -70,3 +70,49 @@ def test_path_choice():
     assert F.fit_engine.spectral_wanted(0, 2 ** 18, 3, 512)               # C5 per-output hyper-parameters
     assert not F.fit_engine.spectral_wanted(0, 2 ** 22, 5, 1)
     assert not F.fit_engine.spectral_wanted(0, 2 ** 20, 7, 8)             # d > 6
+
+
+def test_gpus_flag_starts_a_launcher_child(monkeypatch, capsys):
+    """bench.py --gpus N (N > 1, no WORLD_SIZE): the parent runs torch.distributed.run with N ranks over the same
+    arguments as a child process and relays only rank 0's JSON line (no GPU call in the parent)."""
+    import io
+    import subprocess
+    import sys
+    seen = {}
+
+    class FakeProc(object):
+        def __init__(self, cmd, stdout=None, env=None, text=None):
+            seen["cmd"], seen["env"] = cmd, env
+            self.stdout = io.StringIO('some launcher chatter\n{"metric": "m", "n_gpus": 3}\n')
+
+        def wait(self):
+            return 0
+    monkeypatch.setattr(subprocess, "Popen", FakeProc)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "3", "--steps", "2"])
+    try:
+        bench.main()
+    except SystemExit as e:
+        assert e.code == 0
+    cmd = seen["cmd"]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert cmd[cmd.index("--nproc-per-node") + 1] == "3"
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-4:] == ["--gpus", "3", "--steps", "2"]
+    assert capsys.readouterr().out.strip() == '{"metric": "m", "n_gpus": 3}'
+
+
+def test_c4_fixture_inputs_are_the_benched_shifts():
+    """tests/golden/c4_m20_d5_it50.npz (the real reference over bench.py's exact C4 work) holds the inputs bench.py
+    generates: the shift seeds of rank 0, the package's default generating vector, the shifts of seqs.Lattice
+    (default_rng(seed)), 51 loss-history rows per shift (50 Rprop iterations + the final evaluation)."""
+    import os
+    import numpy as np
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "c4_m20_d5_it50.npz"))
+    d = int(g["d"])
+    assert list(g["seeds"]) == bench.shard_seeds(0, 1, 8)[:2]
+    for p, seed in enumerate(g["seeds"]):
+        s = F.Lattice(d, seed=int(seed), randomize="SHIFT")
+        assert np.array_equal(s.z, g["z"]) and np.array_equal(s.shift, g["shift"][p])
+    assert g["loss_hist"].shape == (2, int(g["its"]) + 1)
+    assert np.isfinite(g["pmean"]).all() and (g["pvar"] >= 0).all()

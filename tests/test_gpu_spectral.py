@@ -305,6 +305,43 @@ def test_single_launch_fit_equals_launch_per_iteration(family, m, d, wait, monke
     assert torch.equal(sa, sb) and torch.equal(la, lb)
 
 
+@pytest.mark.parametrize("family,wait", [("lattice", 60), ("net", 10)])
+def test_single_launch_fit_barrier_give_up_falls_back(family, wait, monkeypatch):
+    """A give-up of fgp_fit_persist's in-kernel grid barrier (forced by the test hook fgp_set_persist_poll_max(0):
+    every wait that does not find the grid complete gives up at once) is detected in the SAME fit call: the
+    kernel leaves NaN parameters and history, the host reads the control word, restores the entry parameters and
+    re-runs the fit on the launch per iteration -- the result equals the normal single-launch fit bit for bit,
+    with early stopping impossible (C2's bench step) and possible."""
+    from fastgaussianprocesses_amd import _native as N
+    from fastgaussianprocesses_amd.fit_engine import FusedMLL
+    monkeypatch.setenv("FGP_FIT_PATH", "spectral")
+    monkeypatch.setenv("FGP_FIT_PERSIST", "1")
+    runs, fails = {}, []
+    orig = FusedMLL.run_persist
+
+    def spy(self, *a, **k):
+        r = orig(self, *a, **k)
+        fails.append(r is None)
+        return r
+    monkeypatch.setattr(FusedMLL, "run_persist", spy)
+    for poll in (-1, 0):
+        gp, _, _ = _gp(family, 3, 16)
+        assert gp._fused_engine(1, 0.1).persist_workgroups() >= 2, "C2 / C3 run the single-launch fit over >= 2 workgroups"
+        N.call("fgp_set_persist_poll_max", poll)
+        try:
+            data = gp.fit(iterations=50, store_hists=True, verbose=0, stop_crit_wait_iterations=wait)
+        finally:
+            N.call("fgp_set_persist_poll_max", -1)
+        runs[poll] = (data, gp.raw_scale.detach().cpu().clone(), gp.raw_lengthscales.detach().cpu().clone())
+    assert fails == [False, True], fails
+    (a, sa, la), (b, sb, lb) = runs[-1], runs[0]
+    assert a["iterations"] == b["iterations"]
+    assert torch.equal(a["loss_hist"], b["loss_hist"])
+    assert torch.equal(a["lengthscales_hist"], b["lengthscales_hist"])
+    assert torch.equal(sa, sb) and torch.equal(la, lb)
+    assert bool(torch.isfinite(sb).all()) and bool(torch.isfinite(lb).all())
+
+
 @pytest.mark.parametrize("m,d,alpha", [(17, 1, 2), (17, 5, 2), (18, 3, 1), (18, 6, 2), (17, 2, 4)])
 def test_basis_from_generating_vector_equals_parts_array_basis(m, d, alpha):
     """fgp_spec_basis_gen (ABI 15: the lattice parts regenerated in the transform's row pass) against

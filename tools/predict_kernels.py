@@ -27,6 +27,9 @@ def main():
     p.add_argument("--n-mean", type=int, default=256)
     p.add_argument("--n-var", type=int, default=8)
     p.add_argument("--reps", type=int, default=2)
+    p.add_argument("--c5po", type=int, default=512,
+                   help="outputs of the C5 per-output GP (n = 2^18, d = 3, shape_scale = [B, 1]) whose post_mean at "
+                        "N = --n-mean also runs (0: skip)")
     a = p.parse_args()
     import bench
     import fastgaussianprocesses_amd as F
@@ -45,9 +48,18 @@ def main():
     xt = torch.rand((256, 3), generator=g).to(dev)
     for _ in range(a.reps):
         net.post_mean(xt)
+    if a.c5po:
+        # bench.py's C5 per-output case (secondary_configs): k_post_mean<0, 3, 4, 4> over blocks of 4 outputs
+        c5 = bench.MultiOutputGP(F, 18, 3, a.c5po, dev, per_output=True)
+        c5.reset()
+        xc = torch.rand((a.n_mean, 3), generator=g).to(dev)
+        with torch.no_grad():
+            c5.gp.coeffs
+        for _ in range(a.reps):
+            c5.gp.post_mean(xc)
     torch.cuda.synchronize()
-    print("ran %d x (post_mean N=%d + post_var N=%d) over %d problems, n=2^%d, d=%d; net post_mean n=2^16 N=256" %
-          (a.reps, a.n_mean, a.n_var, a.shifts, a.log2n, a.d))
+    print("ran %d x (post_mean N=%d + post_var N=%d) over %d problems, n=2^%d, d=%d; net post_mean n=2^16 N=256; "
+          "C5 per-output post_mean (%d outputs)" % (a.reps, a.n_mean, a.n_var, a.shifts, a.log2n, a.d, a.c5po))
 
 
 if __name__ == "__main__":
