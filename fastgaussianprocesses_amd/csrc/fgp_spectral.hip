@@ -666,6 +666,15 @@ constexpr long long kSpecPollMax = 1ll << 22;     // bounded waits of the persis
 constexpr int kPersistLdsMax = 96 * 1024;
 constexpr long long kPersistPollMax = 1ll << 22;
 
+// workgroup barrier that lets global loads / stores stay in flight across it (__syncthreads() drains them with
+// vmcnt(0)): LDS-DMA chunks, workgroup 0's history stores; the waves' LDS accesses retired (lgkmcnt), the raw
+// barrier, a compiler memory fence
+__device__ __forceinline__ void barrier_keep_vm() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 template <int D, bool NET>
 __global__ __launch_bounds__(kWG) void k_spec_persist(Nll a, Fit f, int iters, double logtol, int wait_max, int bpw,
                                                       unsigned* counter, int* out, long long poll_max) {
@@ -823,7 +832,9 @@ __global__ __launch_bounds__(kWG) void k_spec_persist(Nll a, Fit f, int iters, d
     __syncthreads();
     const int brk = brk_s;
     spec_finish<D>(a, f, tot, 0, 1, it, brk ? 0 : 1, st, st, blockIdx.x == 0, nullptr, 1);
-    __syncthreads();
+    // (the new state is in LDS; workgroup 0's history stores stay in flight -- drained by the next iteration's
+    // vmcnt(0) before its grid barrier, under its compute: a __syncthreads here cost ~1 us per iteration)
+    barrier_keep_vm();
     stamp(it, 4);
     if (brk) {
       if (blockIdx.x == 0) {
@@ -872,14 +883,6 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 #ifndef FGP_SPEC_PF
 #define FGP_SPEC_PF 0     // (1: ~100 more VALU per wave, no measurable gain: profiles/r04ab2_basis_gen_prefetch.txt)
 #endif
-
-// workgroup barrier that lets LDS-DMA loads stay in flight across it (__syncthreads() would drain them
-// with vmcnt(0)): the waves' LDS accesses retired (lgkmcnt), the raw barrier, a compiler memory fence
-__device__ __forceinline__ void barrier_keep_vm() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
 
 // fgp_handoff_check (a test hook, fz.check): lane 0 of each storing wave reads back the partials it stored
 // (its own retired stores) and XORs their bits into the group's words [grp][g][q] with agent-scope atomics,
@@ -1094,7 +1097,9 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
     spec_level2<D>(a, fz.par ^ 1, tot);
     __syncthreads();
     spec_finish<D>(a, fz.f, tot, 0, G, fz.iter - 1, 1, fz.sin, fz.sout, blockIdx.x == 0, nraw, -1, FGP_SPEC_PF ? pf : nullptr);
-    __syncthreads();
+    // (nraw is LDS; workgroup 0's history / state stores stay in flight: the chunk waits below count only the
+    // older DMA loads as landed -- loads retire in order, so extra stores only make them more conservative)
+    barrier_keep_vm();
 #pragma unroll
     for (int p = 0; p < PPW; ++p) load_hyp_wave(a, on[p] ? g0 + p : 0, h[p], nraw);
   } else {
