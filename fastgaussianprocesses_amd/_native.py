@@ -48,7 +48,11 @@ class NllDesc(ctypes.Structure):
         ("stamps", _c_vp),
         ("basis", _c_vp), ("basis_stride", _c_i64), ("ysq_chunked", _c_int),
         ("mt_tasks", _c_int), ("mt_basis", _c_vp), ("mt_ytilde", _c_vp), ("mt_kt", _c_vp),
+        ("loss_metric", _c_int), ("cv_weight", _c_dbl),
     ]
+
+
+LOSS_MLL, LOSS_GCV, LOSS_CV = 0, 1, 2       # fgp_nll_desc.loss_metric (include/fgp_hip.h, ABI 16)
 
 
 class FitDesc(ctypes.Structure):

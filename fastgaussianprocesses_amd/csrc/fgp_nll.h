@@ -56,6 +56,8 @@ struct Nll {
   const void* mt_ytilde;
   const double* mt_kt;
   int64_t out_stride;                // fgp_fftbr_real_half: row stride of the half spectra (grad_lam)
+  int loss;                          // FGP_LOSS_MLL / GCV / CV (ABI 16; GCV / CV: k_spec_loss_iter + k_spec_loss_step)
+  double cv_weight;
 };
 
 // Device-clock kernel timing (fgp_nll_desc.stamps; off when NULL -- a uniform branch on a kernel
@@ -64,7 +66,18 @@ struct Nll {
 // contended address serialises thousands of them and slows the kernel being timed).
 constexpr int kStampStride = 1 + kWG / 64;
 __device__ __forceinline__ void stamp_begin(const Nll& a) {
+#ifdef FGP_EXP_HWID
+  // (experiment build, tools/build_exp.sh: the start stamp carries where the workgroup runs -- XCC_ID in bits
+  // 56-63, HW_ID's se / sh / cu fields (bits 8-15) in bits 48-55; the clock stays below 2^48)
+  if (a.stamps && threadIdx.x == 0) {
+    const unsigned hw = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));       // HW_REG_HW_ID
+    const unsigned xcc = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11));     // HW_REG_XCC_ID
+    a.stamps[(int64_t)blockIdx.x * kStampStride] = (unsigned long long)wall_clock64() |
+        ((unsigned long long)((hw >> 8) & 0xFF) << 48) | ((unsigned long long)(xcc & 0xFF) << 56);
+  }
+#else
   if (a.stamps && threadIdx.x == 0) a.stamps[(int64_t)blockIdx.x * kStampStride] = (unsigned long long)wall_clock64();
+#endif
 }
 __device__ __forceinline__ void stamp_end(const Nll& a) {
   if (a.stamps && (threadIdx.x & 63) == 0)
@@ -617,7 +630,9 @@ constexpr int kSpecLdsMax = FGP_SPEC_LDS_KB * 1024;   // its dynamic LDS per wor
 constexpr int kSpecScratch = 256;                  // doubles of the deferred step's totals / parameters (ring slot RING-1)
 constexpr int kSpecMaxDma = 6;                     // LDS-DMA wave-instructions per wave and chunk (tile <= 3072 doubles;
                                                    // the per-wave source pointers live in registers)
-void spec_geometry(Nll& a);                        // nb and the spec_* fields of a spectral desc
+void spec_geometry(Nll& a, bool allow_tile = true);   // nb and the spec_* fields of a spectral desc
+int launch_spec_loss_iter(const Nll& a, hipStream_t st);   // GCV / CV partials (ABI 16)
+int launch_spec_loss_step(const Nll& a, const Fit& f, int iter, int do_update, hipStream_t st);
 int64_t spec_chunks(bool net, int log2n);          // 64-frequency chunks of the spectra (fgp_spec_basis layout)
 // one fit iteration (loss + gradient partials); with fz (tile kernel only) also the reduction + Rprop
 int launch_spec_iter(const Nll& a, hipStream_t st, const FitFuse* fz = nullptr);

@@ -1335,9 +1335,21 @@ static int to_nll(const fgp_nll_desc* d, Nll& a) {
   a.spec_K = a.spec_KS = a.spec_main = a.spec_kw = 0;
   a.spec_kpl = a.spec_ppw = a.spec_pg = a.spec_tile = a.spec_pgp = a.spec_ck = a.spec_ps = 0;
   a.spec_nsl = 1;
+  a.loss = d->loss_metric;
+  a.cv_weight = d->cv_weight;
+  if (a.loss != FGP_LOSS_MLL) {
+    if (a.loss != FGP_LOSS_GCV && a.loss != FGP_LOSS_CV) return set_error(kErrInvalid, "bad loss_metric %d", a.loss);
+    if (!d->basis || mt) return set_error(kErrUnsupported, "GCV / CV fits need the spectral path (basis), one task");
+  }
   if (a.spec) {
     a.re = a.r2c = 0;
-    spec_geometry(a);
+    spec_geometry(a, a.loss == FGP_LOSS_MLL);
+    if (a.loss != FGP_LOSS_MLL) {
+      // the alternative losses' per-wave kernel: one problem per wave, 2 + 2 (2 + d) quantities per block
+      a.spec_ppw = 1;
+      a.spec_pg = a.G;
+      a.nq = 6 + 2 * a.d;
+    }
   }
   a.mt = 0;
   a.mt_F = a.mt_cpb = 0;
@@ -1540,6 +1552,7 @@ static int check_per_problem(const Nll& a, const Fit& f) {
 }
 
 static int fit_step(const Nll& a, const Fit& f, int iter, int do_update, hipStream_t st, bool counter_zero = false) {
+  if (a.spec && a.loss != FGP_LOSS_MLL) return launch_spec_loss_step(a, f, iter, do_update, st);
   if (f.per_problem && a.spec) return launch_spec_reduce_step(a, f, iter, do_update, st);
   if (a.spec && a.nb <= kSpecBlocks && !getenv_off("FGP_SPEC_STEP_MANY")) {
     // one loss over many problems: the parallel step (k_spec_step_many); its counter is zeroed once per run

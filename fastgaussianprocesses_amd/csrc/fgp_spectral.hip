@@ -850,6 +850,235 @@ __global__ __launch_bounds__(kWG) void k_spec_persist(Nll a, Fit f, int iters, d
   }
 }
 
+// ---------------------------------------------------------------- GCV / CV fits (ABI 16)
+// The alternative losses of AbstractGP.fit (abstract_gp.py:242-273) for one task: with ev_k = sqrt(n) scale P_k +
+// noise, lambda'_k = sqrt(n) scale P_k (= ev_k - noise) and Y_k = sum_b |ytilde_bk|^2,
+//   GCV (util.py:371-380):  N1 = sum_k Y_k / ev_k^2 (= sum |z~|^2, z~ = ytilde / ev),  T = sum_k 1 / ev_k (the trace of
+//                           the inverse),  loss = N1 / (T / n)^2;
+//   CV  (util.py:381-385):  inv_diag I = (1/n) sum_k 1 / lambda'_k, coeffs = ift(ytilde / ev).real with
+//                           sum_i coeffs_i^2 = N1 (Parseval; ytilde / ev is Hermitian), loss = w N1 / I^2.
+// Both gradients are  dL/dtheta = c1 S1_theta + c2 S2_theta  with per-frequency sums
+//   S1_theta = sum_k (Y_k / ev_k^3) dev_k/dtheta,   S2_theta = sum_k w2_k dx_k/dtheta,
+//   GCV: w2 = 1 / ev^2, x = ev;  CV: w2 = 1 / lambda'^2, x = lambda' (no noise term),
+// and the global factors (GCV: c1 = -2 / D, c2 = 2 N1 T / (n^2 D^2), D = (T / n)^2; CV: c1 = -2 w / I^2,
+// c2 = 2 w N1 / (n I^3)) applied once the sums are reduced (k_spec_loss_step), the same way the MLL's weights are.
+// dev/draw_scale = sqrt(n) scale P, dev/draw_l_j = sqrt(n) scale l_j dP/dl_j, dev/draw_noise = noise.
+template <int D>
+struct LossAcc {
+  double n1 = 0.0, t = 0.0, s1n = 0.0, s1s = 0.0, s2n = 0.0, s2s = 0.0;
+  double s1l[D], s2l[D];
+  __device__ __forceinline__ LossAcc() {
+#pragma unroll
+    for (int j = 0; j < D; ++j) s1l[j] = s2l[j] = 0.0;
+  }
+};
+
+template <int D, bool CV>
+__device__ __forceinline__ void loss_terms(const double* phi, const Hyp& h, double rootn, double Y, LossAcc<D>& acc) {
+  double dp[D];
+  const double P = mlin<D>(phi, h.ls, dp);
+  const double lp = rootn * (h.scale * P);
+  const double e = lp + h.noise;
+  const double r = rcp_nr(e);
+  const double yr2 = Y * (r * r);
+  acc.n1 += yr2;
+  const double w1 = yr2 * r;
+  double w2;
+  if constexpr (CV) {
+    const double rl = rcp_nr(lp);
+    acc.t += rl;
+    w2 = rl * rl;
+  } else {
+    acc.t += r;
+    w2 = r * r;
+    acc.s2n += w2;
+  }
+  acc.s1n += w1;
+  acc.s1s = __builtin_fma(w1, P, acc.s1s);
+  acc.s2s = __builtin_fma(w2, P, acc.s2s);
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+    acc.s1l[j] = __builtin_fma(w1, dp[j], acc.s1l[j]);
+    acc.s2l[j] = __builtin_fma(w2, dp[j], acc.s2l[j]);
+  }
+}
+
+template <int D>
+__device__ __forceinline__ void loss_values(const LossAcc<D>& acc, double* v) {
+  v[0] = acc.n1;
+  v[1] = acc.t;
+  v[2] = acc.s1n;
+  v[3] = acc.s1s;
+#pragma unroll
+  for (int j = 0; j < D; ++j) v[4 + j] = acc.s1l[j];
+  v[4 + D] = acc.s2n;
+  v[5 + D] = acc.s2s;
+#pragma unroll
+  for (int j = 0; j < D; ++j) v[6 + D + j] = acc.s2l[j];
+}
+
+// Per-block partials of the alternative losses: wave task = (k block, problem), one problem per wave; lane l sums
+// k = block base + l + 64 i (ascending i); the lattice's fold (weight 2 for 0 < k < n/2, 1 at k = 0 and n/2) as in
+// spec_block_partials; the chain factors sqrt(n) scale (scale sums) and sqrt(n) scale l_j (lengthscale sums); fixed
+// wave-sum order.  Partials [G][6 + 2 d][nb] (part_ptr).
+template <int D, bool NET, bool CV>
+__global__ __launch_bounds__(kWG) void k_spec_loss_iter(Nll a) {
+  constexpr int NS = 1 << D, NV = 6 + 2 * D;
+  const int lane = threadIdx.x & 63;
+  const int task = (int)blockIdx.x * (kWG / 64) + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int kb = task / a.G, g = task - kb * a.G;
+  if (kb >= a.nb) return;
+  Hyp h;
+  load_hyp_wave(a, g, h);
+  const double rootn = sqrt((double)((int64_t)1 << a.log2n));
+  const double* phib = a.basis + (int64_t)g * a.basis_stride;
+  LossAcc<D> acc;
+  const int64_t kbase = (int64_t)kb * 64 * a.spec_kpl;
+  for (int i = 0; i < a.spec_kpl; ++i) {
+    const int64_t k = kbase + lane + 64 * i;
+    if (k >= a.spec_main) break;
+    double phi[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) phi[s] = phib[spec_at<NS>(k, s)];
+    loss_terms<D, CV>(phi, h, rootn, a.ysq[ysq_at(a, g, k)], acc);
+  }
+  double v[NV];
+  loss_values<D>(acc, v);
+  if (!NET) {
+#pragma unroll
+    for (int q = 0; q < NV; ++q) v[q] *= 2.0;
+    if (lane == 0 && (kb == 0 || kb == a.nb - 1)) {
+#pragma unroll
+      for (int side = 0; side < 2; ++side) {
+        if (side == 0 ? kb != 0 : kb != a.nb - 1) continue;
+        const int64_t k = side == 0 ? 0 : a.spec_main;
+        double phi[NS];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) phi[s] = phib[spec_at<NS>(k, s)];
+        LossAcc<D> t;
+        loss_terms<D, CV>(phi, h, rootn, a.ysq[ysq_at(a, g, k)], t);
+        double tv[NV];
+        loss_values<D>(t, tv);
+        const double sg = side == 0 ? -1.0 : 1.0;   // k = 0: weight 2 -> 1; k = n/2: weight 1
+#pragma unroll
+        for (int q = 0; q < NV; ++q) v[q] = __builtin_fma(sg, tv[q], v[q]);
+      }
+    }
+  }
+  const double gsc = rootn * h.scale;
+#pragma unroll
+  for (int q = 0; q < NV; ++q) {
+    double f = 1.0;
+    if (q == 3 || q == 5 + D) f = gsc;
+#pragma unroll
+    for (int j = 0; j < D; ++j)
+      if (q == 4 + j || q == 6 + D + j) f = gsc * h.ls[j];
+    const double sq = wave_sum_dpp(v[q]);
+    if (lane == 0) part_ptr(a, g, q, kb)[0] = sq * f;
+  }
+}
+
+// Reduction + loss + Rprop of the alternative losses: problems 16 b .. 16 b + 15 per workgroup (one workgroup when
+// the problems share one loss), the two-level block order of k_spec_reduce_step, then per problem the loss (GCV:
+// history [loss, numer, denom]; CV: [loss, nan, nan] -- abstract_gp.py:242-273's term1 / term2) and the gradient
+// c1 S1 + c2 S2 of every parameter it touches (a parameter shared by several problems sums theirs), then
+// torch.optim.Rprop (rprop_update).
+template <int D>
+__global__ __launch_bounds__(kWG) void k_spec_loss_step(Nll a, Fit f, int iter, int do_update) {
+  constexpr int NQ = 6 + 2 * D, MAXG = kSpecBlocks / kSpecGroup;
+  __shared__ double gs[16 * NQ * MAXG];
+  __shared__ double tot[16 * NQ];
+  __shared__ double lossg[16], c1s[16], c2s[16];
+  const int g0 = (int)blockIdx.x * 16, cnt = min(16, a.G - g0), ng = spec_groups(a);
+  for (int t = threadIdx.x; t < cnt * NQ * ng; t += kWG) {
+    const int pair = t / ng, grp = t % ng;
+    gs[pair * MAXG + grp] = spec_group_sum<false>(a, g0 + pair / NQ, pair % NQ, grp);
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < cnt * NQ) {
+    double s = 0.0;
+    for (int grp = 0; grp < ng; ++grp) s += gs[threadIdx.x * MAXG + grp];
+    tot[threadIdx.x] = s;
+  }
+  __syncthreads();
+  const double n = (double)((int64_t)1 << a.log2n);
+  const bool cv = a.loss == FGP_LOSS_CV;
+  if ((int)threadIdx.x < cnt) {
+    const int i = threadIdx.x;
+    const double N1 = tot[i * NQ + 0], T = tot[i * NQ + 1];
+    double L, c1, c2, t1, t2;
+    if (cv) {
+      const double I = T / n, w = a.cv_weight;
+      L = w * N1 / (I * I);
+      c1 = -2.0 * w / (I * I);
+      c2 = 2.0 * w * N1 / (n * I * I * I);
+      t1 = t2 = NAN;
+    } else {
+      const double Dn = (T / n) * (T / n);
+      L = N1 / Dn;
+      c1 = -2.0 / Dn;
+      c2 = 2.0 * N1 * T / (n * n * Dn * Dn);
+      t1 = N1;
+      t2 = Dn;
+    }
+    lossg[i] = L;
+    c1s[i] = c1;
+    c2s[i] = c2;
+    if (f.per_problem) {
+      double* lh = f.loss_hist + ((int64_t)iter * (f.hist_stride ? f.hist_stride : a.G) + f.hist_offset + g0 + i) * 3;
+      lh[0] = L;
+      lh[1] = t1;
+      lh[2] = t2;
+    }
+  }
+  __syncthreads();
+  if (!f.per_problem && threadIdx.x == 0) {
+    double L = 0.0;
+    for (int i = 0; i < cnt; ++i) L += lossg[i];
+    f.loss_hist[(int64_t)iter * 3 + 0] = L;
+    f.loss_hist[(int64_t)iter * 3 + 1] = cnt == 1 && !cv ? tot[0] : NAN;
+    f.loss_hist[(int64_t)iter * 3 + 2] = cnt == 1 && !cv ? (tot[1] / n) * (tot[1] / n) : NAN;
+  }
+  // every parameter slot of this workgroup's problems: thread t takes raw index t and sums the gradient of every
+  // (problem, slot) mapped to it, problems ascending
+  const int dl = a.ls_pd ? a.d : 1, np = spec_nparams(a);
+  for (int p = threadIdx.x; p < np; p += kWG) {
+    double gp = 0.0;
+    int rg = -1;
+    for (int i = 0; i < cnt; ++i) {
+      const int g = g0 + i;
+      const double* v = tot + i * NQ;
+      for (int k = 0; k < 2 + dl; ++k) {
+        if (spec_slot_param(a, g, k, dl) != p) continue;
+        double s1, s2;
+        if (k == 0) {
+          s1 = v[3];
+          s2 = v[5 + D];
+          rg = f.scale_rg;
+        } else if (k <= dl) {
+          s1 = s2 = 0.0;
+          for (int j = 0; j < D; ++j)
+            if (a.ls_pd ? j == k - 1 : true) {
+              s1 += v[4 + j];
+              s2 += v[6 + D + j];
+            }
+          rg = f.ls_rg;
+        } else {
+          const double nz = exp(a.raw[p]);
+          s1 = nz * v[2];
+          s2 = nz * v[4 + D];
+          rg = f.noise_rg;
+        }
+        gp += c1s[i] * s1 + c2s[i] * s2;
+      }
+    }
+    if (rg < 0) continue;                  // not a parameter of these problems
+    f.raw_hist[(int64_t)iter * f.n_params + p] = f.raw[p];
+    f.grad_out[p] = gp;
+    if (do_update && rg) rprop_update(f, p, gp);
+  }
+}
+
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void glb_void;
 
@@ -1107,6 +1336,19 @@ __global__ __launch_bounds__(kWG, 2) void k_spec_tile(Nll a, FitFuse fz) {
     for (int p = 0; p < PPW; ++p) load_hyp_wave(a, on[p] ? goff + g0 + p : 0, h[p]);
   }
   for (int c = 0; c < nc; ++c) {
+#ifdef FGP_SPEC_PRIO
+    // (experiment: issue priority falling with progress -- the workgroup behind on its CU wins the SIMDs' arbitration)
+    if (FGP_SPEC_PRIO == 4) {
+      const int q = (4 * c) / nc;
+      if (q == 0) __builtin_amdgcn_s_setprio(3);
+      else if (q == 1) __builtin_amdgcn_s_setprio(2);
+      else if (q == 2) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+    } else {
+      if (2 * c < nc) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+    }
+#endif
     // this wave's loads of chunk c have landed (chunks c + 1 .. issued - 1 may stay in flight)
     wait_vmcnt(cnt_w * (issued - 1 - c));
     barrier_keep_vm();                              // ... every wave's; every wave done with chunk c - 1
@@ -1553,7 +1795,7 @@ static int with_spec_d(int d, Fn&& fn) {
 // PG <= 4, the chunk's tile <= 32 KB): workgroups of KW = max(CK, main / 512) frequencies, chunks of
 // CK = 64 (4 / PGP).  Otherwise (k_spec_iter): nb k blocks of 64 kpl frequencies covering [0, main)
 // (lattice main = n/2, plus k = n/2; net main = n), PPW problems per wave.
-void spec_geometry(Nll& a) {
+void spec_geometry(Nll& a, bool allow_tile) {
   const int64_t n = (int64_t)1 << a.log2n;
   const bool net = a.spec_net;
   a.spec_main = net ? n : n / 2;
@@ -1579,7 +1821,7 @@ void spec_geometry(Nll& a) {
   a.spec_ps = 0;
   a.spec_nsl = 1;
   const char* te = getenv("FGP_SPEC_TILE");   // 0: the per-wave kernel only (A/B experiments)
-  const bool tile_ok = !(te && te[0] == '0');
+  const bool tile_ok = allow_tile && !(te && te[0] == '0');
   // Tile kernel (one shared set of spectra, d <= 5): 2 problems per wave (1 for G = 1), problem groups
   // PG <= 4 in the 4 waves of a workgroup.  (4 problems per wave at G = 8 -- 233 VGPRs, 2 blocks per
   // workgroup, 1024 blocks -- measured slower: 51.7 vs 42.0 us per C4 iteration, profiles/r03x_*.)
@@ -1639,12 +1881,44 @@ void spec_geometry(Nll& a) {
   a.spec_pg = (a.G + a.spec_ppw - 1) / a.spec_ppw;
 }
 
+int launch_spec_loss_iter(const Nll& a, hipStream_t st) {
+  const int64_t tasks = (int64_t)a.nb * a.G;
+  const unsigned grid = (unsigned)((tasks + kWG / 64 - 1) / (kWG / 64));
+  return with_spec_d(a.d, [&](auto dc) {
+    constexpr int D = decltype(dc)::value;
+    auto go = [&](auto net, auto cv) {
+      k_spec_loss_iter<D, decltype(net)::value, decltype(cv)::value><<<grid, kWG, 0, st>>>(a);
+    };
+    if (a.spec_net) {
+      if (a.loss == FGP_LOSS_CV) go(std::true_type{}, std::true_type{});
+      else go(std::true_type{}, std::false_type{});
+    } else {
+      if (a.loss == FGP_LOSS_CV) go(std::false_type{}, std::true_type{});
+      else go(std::false_type{}, std::false_type{});
+    }
+    return check_launch("k_spec_loss_iter");
+  });
+}
+
+int launch_spec_loss_step(const Nll& a, const Fit& f, int iter, int do_update, hipStream_t st) {
+  if (!f.per_problem && a.G > 16) return set_error(kErrUnsupported, "GCV / CV fits: one loss over at most 16 problems");
+  if (a.nb > kSpecBlocks) return set_error(kErrInvalid, "k_spec_loss_step: nb > %d", kSpecBlocks);
+  return with_spec_d(a.d, [&](auto dc) {
+    k_spec_loss_step<decltype(dc)::value><<<(unsigned)((a.G + 15) / 16), kWG, 0, st>>>(a, f, iter, do_update);
+    return check_launch("k_spec_loss_step");
+  });
+}
+
 int64_t spec_chunks(bool net, int log2n) {
   const int64_t n = (int64_t)1 << log2n, K = net ? n : n / 2 + 1;
   return (K + 63) / 64;
 }
 
 int launch_spec_iter(const Nll& a, hipStream_t st, const FitFuse* fz) {
+  if (a.loss != FGP_LOSS_MLL) {
+    if (fz) return set_error(kErrUnsupported, "GCV / CV fits: no fused spectral step");
+    return launch_spec_loss_iter(a, st);
+  }
   if (a.spec_tile) {
     if (a.spec_ppw > 4) return set_error(kErrInvalid, "spectral tile kernel: %d problems per wave", a.spec_ppw);
     if (fz && a.spec_ps) return set_error(kErrInvalid, "spectral tile kernel: no fused step over problem slices");
@@ -1653,7 +1927,12 @@ int launch_spec_iter(const Nll& a, hipStream_t st, const FitFuse* fz) {
     const FitFuse& f = fz ? *fz : none;
     bool persist_ok = false;
     const int trows = (1 << a.d) + (a.spec_ps ? a.spec_ps : a.G);
+#ifdef FGP_SPEC_SHM_MIN
+    // (experiment build: at least this much dynamic LDS per workgroup -- fewer co-resident workgroups per CU)
+    const size_t shm = std::max(sizeof(double) * (size_t)kSpecRing * (size_t)(trows * a.spec_ck), (size_t)FGP_SPEC_SHM_MIN);
+#else
     const size_t shm = sizeof(double) * (size_t)kSpecRing * (size_t)(trows * a.spec_ck);
+#endif
     const unsigned grid = (unsigned)(a.nb / (4 / a.spec_pgp) * a.spec_nsl);
     return with_spec_d(a.d, [&](auto dc) {
       constexpr int D = decltype(dc)::value;
@@ -1792,7 +2071,7 @@ static long long g_persist_poll_max = kPersistPollMax;
 void set_persist_poll_max(long long v) { g_persist_poll_max = v < 0 ? kPersistPollMax : v; }
 
 int spec_persist_geometry(const Nll& a, int* W, int* bpw, size_t* shm) {
-  if (!a.spec || a.G != 1 || a.basis_stride != 0 || a.d > kSpecMaxD || !a.ysq_chunked)
+  if (!a.spec || a.G != 1 || a.basis_stride != 0 || a.d > kSpecMaxD || !a.ysq_chunked || a.loss != FGP_LOSS_MLL)
     return set_error(kErrUnsupported, "fgp_fit_persist: one problem on the spectral path only");
   if (spec_nparams(a) > kSpecScratch) return set_error(kErrUnsupported, "fgp_fit_persist: parameters");
   const size_t per_blk = (size_t)a.spec_kpl * (((size_t)1 << a.d) + 1) * 64 * sizeof(double);

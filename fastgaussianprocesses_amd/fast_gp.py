@@ -28,7 +28,8 @@ import torch
 from . import _native
 from . import ops
 from . import seqs as _seqs
-from .fit_engine import FusedMLL, LatticePartsGen, mll_constant, spec_basis, spec_basis_gen, spec_inv_eig, spec_post_var, spectral_wanted
+from .fit_engine import (SPEC_MAX_D, FusedMLL, LatticePartsGen, mll_constant, spec_basis, spec_basis_gen, spec_inv_eig,
+                         spec_post_var, spectral_wanted)
 
 
 def _log(x):
@@ -509,11 +510,15 @@ class AbstractFastGP(torch.nn.Module):
                         self.raw_noise.detach().reshape(-1), G, gen=gen, n=n, basis=basis)
         return lam.reshape(tuple(pb) + (n,))
 
-    def _spec_basis(self, n, G=1):
+    def _spec_basis(self, n, G=1, force=False):
         """Part-product spectra Phi_S = ft(prod_{j in S} parts_j) of the first n points (fgp_spec_basis)
-        when the spectral fit path is the cheaper one for G eigen-problems (fit_engine.spectral_wanted),
+        when the spectral fit path is the cheaper one for G eigen-problems (fit_engine.spectral_wanted), or
+        with `force` whenever it applies (d <= 6, the spectra <= 16 GiB: the GCV / CV fits, which only it runs),
         else None.  Hyper-parameter independent; cached with the data (dropped by add_y_next)."""
-        if not spectral_wanted(self._FAMILY, n, self.d, G):
+        if force:
+            if self.d > SPEC_MAX_D or n < 16 or (2 ** self.d) * (n // 2 + 1) * 8 > (16 << 30):
+                return None
+        elif not spectral_wanted(self._FAMILY, n, self.d, G):
             return None
 
         def f():
@@ -676,19 +681,23 @@ class AbstractFastGP(torch.nn.Module):
                      task_kernel=store_hists or (store_task_kernel_hist and (
                          self.raw_factor_task_kernel.requires_grad or self.raw_noise_task_kernel.requires_grad)))
         stop = (np.log(1 + stop_crit_improvement_threshold), stop_crit_wait_iterations)
-        fused = (loss_metric == "MLL" and optimizer is None and masks is None and self._fused_ok())
+        fused = optimizer is None and masks is None and self._fused_ok() and (
+            loss_metric == "MLL" or self._alt_loss_ok(loss_metric, cv_weights))
         if optimizer is None:
             optimizer = None if fused else self.get_default_optimizer(lr)
         else:
             assert isinstance(optimizer, torch.optim.Optimizer)
         if fused:
-            return self._fit_fused(iterations, 1e-1 if lr is None else lr, stop, hists, verbose, verbose_indent)
+            return self._fit_fused(iterations, 1e-1 if lr is None else lr, stop, hists, verbose, verbose_indent,
+                                   loss_metric=loss_metric, cv_weight=float(cv_weights) if loss_metric == "CV" else 1.0)
         return self._fit_generic(loss_metric, iterations, optimizer, stop, hists, verbose, verbose_indent, masks,
                                  cv_weights)
 
     def _fused_ok(self):
+        # (the adaptive nugget of ONE task is the plain one: noise |tr_00 / tr_00| = noise, util.py:286-290 -- the
+        # trace sqrt(n) sum_k lambda_k = n k1[0] > 0 for these positive kernels)
         n = self._nh
-        if n < 16 or self.d > 8 or self.adaptive_nugget:
+        if n < 16 or self.d > 8:
             return False
         if self._tfs["scale"][1] is not _exp or self._tfs["lengthscales"][1] is not _exp or \
                 self._tfs["noise"][1] is not _exp:
@@ -699,6 +708,22 @@ class AbstractFastGP(torch.nn.Module):
             return False
         pb = self._problem_batch()
         return pb is not None
+
+    def _alt_loss_ok(self, loss_metric, cv_weights):
+        """fit(loss_metric="GCV" / "CV") on the device (fgp_nll_desc.loss_metric, ABI 16): the spectral path
+        (d <= 6), one loss over at most 16 eigen-problems, a scalar cv_weights (the Parseval form of CV's
+        sum_i (coeffs_i / inv_diag)^2 w needs one weight for every point); FGP_ALT_LOSS_DEVICE=0 keeps the generic
+        autograd loop (A/B, tests)."""
+        if os.environ.get("FGP_ALT_LOSS_DEVICE", "1")[:1] == "0" or self.d > SPEC_MAX_D:
+            return False
+        if loss_metric == "CV":
+            if torch.is_tensor(cv_weights):
+                if cv_weights.numel() != 1:
+                    return False
+            elif not np.isscalar(cv_weights):
+                return False
+        pb = self._problem_batch()
+        return pb is not None and pb[1] <= 16 and self._spec_basis(self._nh, pb[1], force=True) is not None
 
     def _problem_batch(self):
         """G and the per-problem flags for the fused layout (None when shapes need broadcasting)."""
@@ -729,15 +754,16 @@ class AbstractFastGP(torch.nn.Module):
     def _log_row(self, i, loss, t1, t2, indent):
         print(" " * indent + "%16.2e | %-10.2e | %-10.2e | %-10.2e" % (i, loss, t1, t2))
 
-    def _fused_engine(self, iterations, lr, ysq=None, d_out=None):
+    def _fused_engine(self, iterations, lr, ysq=None, d_out=None, loss_metric="MLL", cv_weight=1.0):
         """The FusedMLL of this GP's fit: G eigen-problems from the part-product spectra, the regenerated
         lattice parts or the parts array; `ysq` / `d_out` override Y = sum_b |ytilde_b|^2 and the output
-        count (distributed.fit_sharded: Y all-reduced over the ranks' output shards)."""
+        count (distributed.fit_sharded: Y all-reduced over the ranks' output shards); loss_metric GCV / CV: the
+        spectral path's alternative losses (FusedMLL)."""
         n = self._nh
         pb_shape, G = self._problem_batch()
         if d_out is None:
             d_out = math.prod(self.shape_batch)
-        basis = self._spec_basis(n, G)
+        basis = self._spec_basis(n, G, force=loss_metric != "MLL")
         gen = self._parts_gen(n) if basis is None else None
         parts = self._k1parts(n) if (gen is None and basis is None) else None
         ls_raw = self.raw_lengthscales.detach()
@@ -749,13 +775,16 @@ class AbstractFastGP(torch.nn.Module):
                         requires_grad=(self.raw_scale.requires_grad, self.raw_lengthscales.requires_grad,
                                        self.raw_noise.requires_grad),
                         lr=lr, max_iters=(iterations + 1 if G == 1 and iterations < 8192 else min(iterations + 1, 64)),
-                        gen=gen, basis=basis)
+                        gen=gen, basis=basis, loss_metric=loss_metric, cv_weight=cv_weight)
 
-    def _fit_fused(self, iterations, lr, stop, hists, verbose, indent, ysq=None, d_out=None):
-        """Device-resident MLL fit (the engine of _fused_engine; the reference's loop semantics: loss
-        history, early stopping, best iterate)."""
+    def _fit_fused(self, iterations, lr, stop, hists, verbose, indent, ysq=None, d_out=None, loss_metric="MLL",
+                   cv_weight=1.0):
+        """Device-resident fit (the engine of _fused_engine; the reference's loop semantics: loss history, early
+        stopping, best iterate) of the MLL, or of the GCV / CV loss (abstract_gp.py:242-273, whose history holds
+        the loss itself where the MLL's holds -loss)."""
         logtol, wait_max = stop
-        eng = self._fused_engine(iterations, lr, ysq, d_out)
+        eng = (self._fused_engine(iterations, lr, ysq, d_out) if loss_metric == "MLL" else
+               self._fused_engine(iterations, lr, ysq, d_out, loss_metric=loss_metric, cv_weight=cv_weight))
         self._iters_for_log = iterations
         self._log_header(verbose, indent)
         best, save, waited = math.inf, math.inf, 0
@@ -839,7 +868,8 @@ class AbstractFastGP(torch.nn.Module):
         self._snap = None
         data = {"iterations": i}
         if hists["loss"]:
-            data["loss_hist"] = torch.tensor([-v[0] for v in losses])
+            sgn = -1.0 if loss_metric == "MLL" else 1.0        # metric_val: -loss (MLL), loss (GCV, CV)
+            data["loss_hist"] = torch.tensor([sgn * v[0] for v in losses])
         if hists["scale"]:
             data["scale_hist"] = self.tf_scale(s_raw.reshape((-1,) + self.raw_scale.shape)).cpu()
         if hists["lengthscales"]:

@@ -142,7 +142,7 @@ def spec_basis_gen(gen, n, device, force=False):
 class FusedMLL(object):
     def __init__(self, family, parts, ysq, raw_scale, raw_lengthscales, raw_noise, logdet_weight, mll_const,
                  requires_grad=(True, True, False), lr=0.1, max_iters=1, parts_per_problem=False, per_problem=None,
-                 gen=None, basis=None, mt=None):
+                 gen=None, basis=None, mt=None, loss_metric="MLL", cv_weight=1.0):
         """
         family: 0 lattice (FFT) / 1 net (FWHT)
         basis:  part-product spectra (spec_basis) [Q, 2^d, 64] shared or [G, Q, 2^d, 64]: the spectral fit path
@@ -155,7 +155,11 @@ class FusedMLL(object):
         raw_noise [S_n] with S_n in {1, G}
         mt:     multitask spectral fit (include/fgp_hip.h mt_tasks; G = 1, ysq only gives n): dict with
                 `basis` the pair spectra [T (T+1)/2, 2^d, n], `ytilde` [T, n], `kt` the task kernel [T, T]
+        loss_metric: "MLL" (default), or "GCV" / "CV" (fgp_nll_desc.loss_metric, ABI 16: the spectral path only;
+                cv_weight the scalar cv_weights of AbstractGP.fit); their loss history holds [loss, numer, denom]
         """
+        if loss_metric != "MLL" and basis is None:
+            raise ValueError("GCV / CV fits run on the spectral path only (basis)")
         require_device(ysq, "FusedMLL")
         self.device = ysq.device
         self.family = int(family)
@@ -217,6 +221,9 @@ class FusedMLL(object):
             logdet_weight=float(logdet_weight),
             grad_lam=0, work=(self.work.data_ptr() if self.work is not None else 0),
             partials=0, **self.layout)
+        self.loss_metric = loss_metric
+        self._nll.loss_metric = {"MLL": N.LOSS_MLL, "GCV": N.LOSS_GCV, "CV": N.LOSS_CV}[loss_metric]
+        self._nll.cv_weight = float(cv_weight)
         if gen is not None:
             gen.apply(self._nll, n)
         self.ysq_rows = self.ysq

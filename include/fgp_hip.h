@@ -236,7 +236,23 @@ typedef struct fgp_nll_desc {
   const void* mt_basis;       /* [T (T + 1) / 2][2^d][n] pair spectra, pairs (k, l), k <= l, row-major */
   const void* mt_ytilde;      /* [T][n] ytilde of every task (complex128 lattice / float64 net) */
   const double* mt_kt;        /* device [T][T] task kernel */
+  /* ABI 16 -- the alternative fit losses of AbstractGP.fit (abstract_gp.py:242-273) on the spectral path:
+   * loss_metric FGP_LOSS_MLL (0, the default: everything above), FGP_LOSS_GCV (1) or FGP_LOSS_CV (2).  With
+   * ev_k = sqrt(n) lambda_k + noise (lambda from the spectra, basis non-NULL, mt_tasks = 0) and Y = ysq:
+   *   GCV (util.py:371-380):  numer = sum_k Y_k / ev_k^2,  denom = (sum_k 1 / ev_k / n)^2,  loss = numer / denom;
+   *   CV  (util.py:381-385, abstract_gp.py:262-273, one task): inv_diag = mean_k 1 / (sqrt(n) lambda_k) and, by
+   *       Parseval, sum_i coeffs_i^2 = numer, so loss = cv_weight numer / inv_diag^2 (a scalar cv_weights),
+   * summed over the problems (or per problem with a per_problem fit desc), gradients in closed form.  Every
+   * iteration is the per-wave partials kernel (2 + 2 (2 + d) quantities per problem and k block) plus the
+   * reduction / step kernel; the tile, single-launch and persistent kernels are MLL-only.  A desc that is not
+   * per_problem holds at most 16 problems. */
+  int loss_metric;
+  double cv_weight;
 } fgp_nll_desc;
+
+#define FGP_LOSS_MLL 0
+#define FGP_LOSS_GCV 1
+#define FGP_LOSS_CV 2
 
 /* A = 1/ev, ev = sqrt(n) lambda + exp(raw_noise), of the G problems of a spectral desc (basis non-NULL;
  * util.py:285,292-300 with lambda = scale sum_S l^S Phi_S, real): wa [G][n] float64 (lattice: the even

@@ -1,0 +1,78 @@
+"""GPU parity of fits with the adaptive nugget (adaptive_nugget=True: _FastInverseLogDetCache.__call__,
+util.py:286-290 -- lams[l, l] += noise |tr_ll / tr_00|) against the REAL reference's fit trajectories
+(tests/golden/make_golden_adaptive.py -> tests/golden/adaptive/*.npz).
+
+One task: the ratio is tr_00 / tr_00 = 1 exactly, so the device-resident spectral fit (the plain nugget) runs; the
+test checks that it does and matches the reference.  Multitask (T = 2, the learned task kernel): the ratio
+|tr_11 / tr_00| scales the second task's nugget (generic path).
+Tolerances as the golden fits (tests/test_gpu_gp.py): loss history 2e-7 relative, parameters 1e-10, post_mean
+1e-8 relative, post_var 1e-8 K(x, x).
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import fastgaussianprocesses_amd as F
+from tests.gpu_fixtures import DEV, rel_err
+
+pytestmark = pytest.mark.gpu
+torch.set_default_dtype(torch.float64)
+
+ADIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "adaptive")
+NAMES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(ADIR, "*.npz")))
+
+
+def build(g):
+    fam, d, alpha = str(g["family"]), int(g["d"]), int(g["alpha"])
+    ns = [int(v) for v in g["ns"]]
+    T = len(ns)
+    kw = dict(alpha=alpha, adaptive_nugget=True, noise=float(g["noise"]), device=DEV)
+    if T > 1:
+        kw["num_tasks"] = T
+    if fam == "lattice":
+        seqs = [F.Lattice(d, randomize="SHIFT", generating_vector=g["z"], shift=g["shifts"][l]) for l in range(T)]
+        gp = F.FastGPLattice(seqs if T > 1 else seqs[0], **kw)
+    else:
+        seqs = [F.DigitalNetB2(d, randomize="DS", generating_matrices=g["C"].astype(np.uint64), t=int(g["t"]),
+                               shift=g["shifts"][l].astype(np.uint64)) for l in range(T)]
+        gp = F.FastGPDigitalNetB2(seqs if T > 1 else seqs[0], **kw)
+    if T > 1:
+        xs = gp.get_x_next(torch.tensor(ns))
+        for l in range(T):
+            assert np.array_equal(xs[l].cpu().numpy(), g["x_%d" % l])
+        gp.add_y_next([torch.from_numpy(g["y_%d" % l]).to(DEV) for l in range(T)])
+    else:
+        x = gp.get_x_next(ns[0])
+        assert np.array_equal(x.cpu().numpy(), g["x_0"])
+        gp.add_y_next(torch.from_numpy(g["y_0"]).to(DEV))
+    return gp
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_adaptive_nugget_fit_matches_reference(name, monkeypatch):
+    from fastgaussianprocesses_amd import fit_engine
+    g = np.load(os.path.join(ADIR, name + ".npz"))
+    engines = []
+    orig = fit_engine.FusedMLL.__init__
+
+    def init(self, *a, **k):
+        engines.append(1)
+        return orig(self, *a, **k)
+    monkeypatch.setattr(fit_engine.FusedMLL, "__init__", init)
+    gp = build(g)
+    its = len(g["fit_loss_hist"]) - 1
+    data = gp.fit(iterations=its, store_hists=True, verbose=0, stop_crit_wait_iterations=its + 5)
+    if len(g["ns"]) == 1:
+        assert engines, "a single-task adaptive-nugget fit runs the device-resident fit"
+    assert rel_err(data["loss_hist"], g["fit_loss_hist"]) <= 2e-7
+    assert rel_err(gp.raw_lengthscales, g["fit_raw_lengthscales"]) <= 1e-10
+    assert rel_err(data["lengthscales_hist"], g["fit_lengthscales_hist"]) <= 1e-10
+    assert rel_err(gp.raw_scale, g["fit_raw_scale"]) <= 1e-10
+    xt = torch.from_numpy(g["x_test"]).to(DEV)
+    assert rel_err(gp.post_mean(xt), g["fit_pmean"]) <= 1e-8
+    pv = gp.post_var(xt).cpu()
+    kxx = float(np.abs(g["fit_pvar"]).max()) + float(torch.exp(gp.raw_scale.detach()).max())
+    assert float((pv - torch.from_numpy(g["fit_pvar"])).abs().max()) <= 1e-8 * kxx

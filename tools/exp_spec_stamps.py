@@ -20,9 +20,50 @@ sys.path.insert(0, ROOT)
 torch.set_default_dtype(torch.float64)
 
 
+def placement(st, grid):
+    """FGP_EXP_HWID builds (tools/build_exp.sh): the start stamp's bits 48-63 hold the workgroup's XCC and
+    se / sh / cu ids -> per launch, how many workgroups shared each CU, and the mean workgroup duration by that
+    count (is the spread of the durations the CUs' uneven loading?)"""
+    ids = (st[:, :grid, 0] >> 48)
+    if not bool((ids != 0).any()):
+        return None
+    clk = st[:, :grid].clone()
+    clk[:, :, 0] &= (1 << 48) - 1
+    dur = (clk[:, :, 1:].amax(2) - clk[:, :, 0]).double()
+    by = {}
+    for i in range(st.shape[0]):
+        row = ids[i].tolist()
+        cnt = {}
+        for v in row:
+            cnt[v] = cnt.get(v, 0) + 1
+        for w, v in enumerate(row):
+            by.setdefault(cnt[v], []).append(float(dur[i, w]))
+    # the workgroups sharing a CU, by start order (the older one wins the SIMDs' issue arbitration), and by XCD
+    first, second, xcd = [], [], {}
+    for i in range(st.shape[0]):
+        grp = {}
+        for w, v in enumerate(ids[i].tolist()):
+            grp.setdefault(v, []).append(w)
+            xcd.setdefault(v >> 8, []).append(float(dur[i, w]))
+        for v, ws in grp.items():
+            if len(ws) == 2:
+                a, b = sorted(ws, key=lambda w: int(clk[i, w, 0]))
+                first.append(float(dur[i, a]))
+                second.append(float(dur[i, b]))
+    mean = lambda v: sum(v) / max(1, len(v))
+    return {"cus_used_per_launch": float(sum(len(set(ids[i].tolist())) for i in range(st.shape[0])) / st.shape[0]),
+            "wg_dur_ticks_by_wgs_per_cu": {k: (len(v), sum(v) / len(v)) for k, v in sorted(by.items())},
+            "dur_ticks_first_started_on_cu": mean(first), "dur_ticks_second_started_on_cu": mean(second),
+            "frac_second_longer": mean([1.0 if b > a else 0.0 for a, b in zip(first, second)]),
+            "dur_ticks_by_xcd": {k: round(mean(v), 1) for k, v in sorted(xcd.items())}}
+
+
 def summarize(st, grid, khz, name, extra=None):
     """st [iters, grid, 5] raw wall-clock stamps -> offsets in us"""
-    st = st[:, :grid].double()
+    pl = placement(st, grid)
+    st = st[:, :grid].clone()
+    st[:, :, 0] &= (1 << 48) - 1
+    st = st.double()
     t0 = st[:, :, 0].amin(1, keepdim=True)
     start = (st[:, :, 0] - t0) * (1e3 / khz)
     end = (st[:, :, 1:].amax(2) - t0) * (1e3 / khz)
@@ -37,6 +78,8 @@ def summarize(st, grid, khz, name, extra=None):
            # the 17 latest workgroups include the 16 level-1 group finishers and the level-2 finisher
            "end_18th_latest_us": float(se[:, -18].mean()), "end_2nd_latest_us": float(se[:, -2].mean())}
     out["tail_us"] = out["span_us"] - out["end_18th_latest_us"]
+    if pl is not None:
+        out["placement"] = pl
     if extra:
         out.update(extra)
     return out
