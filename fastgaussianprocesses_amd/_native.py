@@ -143,6 +143,7 @@ _SIGNATURES = {
     "fgp_kernel_rows": [_c_int, _c_vp, _c_i64, _c_vp, _c_i64, _c_int, _c_int, _c_pi, _c_pd, _c_vp, _c_int, _c_vp,
                         _c_vp],
     "fgp_post_mean_batched": [_P_PRED, _c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp],
+    "fgp_post_mean_batched_work": [_P_PRED, _c_i64, _c_pl],
     "fgp_post_var_batched": [_P_PRED, _c_vp, _c_i64, _c_i64, _c_pd, _c_vp, _c_vp, _c_vp, _c_vp],
     "fgp_net_points": [_c_vp, _c_int, _c_vp, _c_i64, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_vp],
     "fgp_double_update": [_c_int, _c_vp, _c_i64, _c_vp, _c_i64, _c_i64, _c_int, _c_vp, _c_i64, _c_vp],

@@ -11,6 +11,7 @@ own methods return: the stopping rule is applied per GP on its own loss history,
 parameters are restored, and the GP objects hold the fitted parameters and data afterwards.
 """
 import collections
+import ctypes
 import math
 
 import torch
@@ -467,10 +468,12 @@ class GPBatch(object):
         """[P, N] posterior means (AbstractGP.post_mean of every GP, abstract_gp.py:352-380)."""
         self.coeffs()
         x, xs, Nt = self._points(x)
-        nchunks = (self.n + 1023) // 1024
-        work = torch.empty(nchunks * self.P * Nt, dtype=torch.float64, device=self.device)
+        desc = self._desc()
+        wl = ctypes.c_int64(0)
+        N.call("fgp_post_mean_batched_work", desc, Nt, ctypes.byref(wl))
+        work = torch.empty(wl.value, dtype=torch.float64, device=self.device)
         out = torch.empty((self.P, Nt), dtype=torch.float64, device=self.device)
-        N.call("fgp_post_mean_batched", self._desc(), N.ptr(x), xs, Nt, N.ptr(out), N.ptr(work),
+        N.call("fgp_post_mean_batched", desc, N.ptr(x), xs, Nt, N.ptr(out), N.ptr(work),
                N.stream_ptr(self.device))
         return out
 

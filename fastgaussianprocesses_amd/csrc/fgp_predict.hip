@@ -738,6 +738,68 @@ static void post_mean_d(dim3 grid, hipStream_t st, bool uniform4, int B, const d
   }
 }
 
+// The k_post_mean instance post_mean_d launches (for the residency query)
+template <int FAM, int D>
+static const void* post_mean_kernel(bool uniform4, int B) {
+  if (B == 1) return (FAM == 1 || uniform4) ? reinterpret_cast<const void*>(k_post_mean<FAM, D, 1, 4>)
+                                            : reinterpret_cast<const void*>(k_post_mean<FAM, D, 1, 0>);
+  return (FAM == 1 || uniform4) ? reinterpret_cast<const void*>(k_post_mean<FAM, D, kPmB, 4>)
+                                : reinterpret_cast<const void*>(k_post_mean<FAM, D, kPmB, 0>);
+}
+
+// Workgroups of a post_mean instance resident at once on the current device (workgroups per CU x CUs), queried
+// once per instance and remembered (no query inside a hipGraph capture after the first eager call); 0 if unknown.
+static int64_t post_mean_resident(const void* kp) {
+  static const void* rk[256];
+  static int64_t rres[256];
+  static int nr = 0;
+  for (int i = 0; i < nr; ++i)
+    if (rk[i] == kp) return rres[i];
+  int per_cu = 0, dev = 0, cus = 0;
+  const int64_t res = (hipGetDevice(&dev) == hipSuccess &&
+                       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+                       hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kp, kWG, 0) == hipSuccess)
+                          ? (int64_t)per_cu * cus : 0;
+  if (nr < 256) {
+    rk[nr] = kp;
+    rres[nr++] = res;
+  }
+  return res;
+}
+
+// Training points per workgroup of a batched launch: the workgroups of an FP64-VALU-bound launch run in rounds of
+// `resident`; with W workgroups the last round is W / resident - floor(W / resident) full, so of the chunks
+// {2048, 1024, 512} (whole 256-point slabs; a workgroup's prologue ~1 % of a 512-point chunk) the one whose launch
+// fills its rounds best is taken, the larger on a tie (C4: 8 problems x 2^20 points, 5 workgroups per CU:
+// 1024 -> 6.4 rounds, 91 % filled; 512 -> 12.8 rounds, 98.5 %).  Unknown residency: kChunk.
+template <int FAM>
+static int64_t post_mean_chunk(int d, const PredSpec& spec, int64_t n, int64_t N, int64_t P, int B) {
+  bool uniform4 = true;
+  for (int j = 0; j < d; ++j) uniform4 = uniform4 && spec.order[j] == 4;
+  const void* kp = nullptr;
+  switch (d) {
+#define FGP_C(DD) case DD: kp = post_mean_kernel<FAM, DD>(uniform4, B); break;
+    FGP_C(1) FGP_C(2) FGP_C(3) FGP_C(4) FGP_C(5) FGP_C(6) FGP_C(7) FGP_C(8)
+#undef FGP_C
+    default: return kChunk;
+  }
+  const int64_t res = post_mean_resident(kp);
+  if (res <= 0) return kChunk;
+  const int64_t tiles = (N + kWG - 1) / kWG;
+  int64_t best = kChunk;
+  double best_fill = -1.0;
+  for (int64_t c = 2048; c >= 512; c /= 2) {
+    const int64_t w = P * tiles * ((n + c - 1) / c);
+    const double rounds = (double)w / (double)res;
+    const double fill = rounds / std::ceil(rounds);
+    if (fill > best_fill + 1e-9) {
+      best_fill = fill;
+      best = c;
+    }
+  }
+  return best;
+}
+
 template <int FAM>
 static int launch_post_mean(int d, const double* xt, int64_t N, const void* z, int64_t n, const PredSpec& spec, int tbits,
                             const double* hyp, int Gk, const double* coeffs, int64_t cstride, int B, double* out,
@@ -801,6 +863,30 @@ extern "C" {
 int fgp_post_mean(int family, const double* xt, int64_t N, const void* z, int64_t n, int d, int tbits, const int* order,
                   const double* coef, const double* hyp, int Gk, const double* coeffs, int64_t coeff_stride, int B,
                   double* out, int64_t out_stride, double* work, int64_t chunk, void* stream) {
+  if (B > kPmB && Gk == B && N > 0) {
+    // every output with its own hyper-parameters (per-output batches, e.g. C5 per-output: 512 outputs): the
+    // blocks of kPmB outputs as the problems of ONE launch (blockIdx.z; the arithmetic of one block per launch),
+    // the B mod kPmB remaining outputs in a second
+    if (N < 0 || n < 1 || d < 1 || d > FGP_MAX_D || chunk < 1 || !xt || !z || !hyp || !coeffs || !out || !work)
+      return set_error(kErrInvalid, "fgp_post_mean: bad sizes / null pointer");
+    if (out_stride != N) return set_error(kErrInvalid, "fgp_post_mean: B > %d needs out_stride == N", kPmB);
+    PredSpec spec;
+    int rc = make_spec(family, d, order, coef, spec);
+    if (rc != kOk) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    const int nblk = B / kPmB, rem = B - nblk * kPmB;
+    const ProbStrides ps{0, 0, (int64_t)kPmB * (1 + d), (int64_t)kPmB * coeff_stride};
+    rc = family == FGP_FAMILY_LATTICE
+             ? launch_post_mean<0>(d, xt, N, z, n, spec, tbits, hyp, kPmB, coeffs, coeff_stride, kPmB, out, N, work, st,
+                                   nblk, ps, chunk)
+             : launch_post_mean<1>(d, xt, N, z, n, spec, tbits, hyp, kPmB, coeffs, coeff_stride, kPmB, out, N, work, st,
+                                   nblk, ps, chunk);
+    if (rc != kOk || rem == 0) return rc;
+    const int b0 = nblk * kPmB;
+    return fgp_post_mean(family, xt, N, z, n, d, tbits, order, coef, hyp + (int64_t)b0 * (1 + d), rem,
+                         coeffs + (int64_t)b0 * coeff_stride, coeff_stride, rem, out + (int64_t)b0 * N, N, work, chunk,
+                         stream);
+  }
   if (N < 0 || n < 1 || d < 1 || d > FGP_MAX_D || B < 1 || B > kPmB || Gk < 1 || chunk < 1)
     return set_error(kErrInvalid, "fgp_post_mean: bad sizes (N=%lld n=%lld d=%d B=%d Gk=%d)", (long long)N,
                      (long long)n, d, B, Gk);
@@ -961,11 +1047,27 @@ int fgp_post_mean_batched(const fgp_pred_desc* pd, const double* xt, int64_t xt_
   if (rc != kOk) return rc;
   const ProbStrides ps{xt_stride, pd->z_stride, pd->hyp_stride, pd->coeff_stride};
   hipStream_t st = (hipStream_t)stream;
-  if (pd->family == FGP_FAMILY_LATTICE)
+  if (pd->family == FGP_FAMILY_LATTICE) {
+    const int64_t chunk = post_mean_chunk<0>(d, spec, pd->n, N, pd->P, 1);
     return launch_post_mean<0>(d, xt, N, pd->z, pd->n, spec, pd->tbits, pd->hyp, 1, pd->coeffs, pd->n, 1, out, N, work,
-                               st, pd->P, ps);
+                               st, pd->P, ps, chunk);
+  }
+  const int64_t chunk = post_mean_chunk<1>(d, spec, pd->n, N, pd->P, 1);
   return launch_post_mean<1>(d, xt, N, pd->z, pd->n, spec, pd->tbits, pd->hyp, 1, pd->coeffs, pd->n, 1, out, N, work, st,
-                             pd->P, ps);
+                             pd->P, ps, chunk);
+}
+
+int fgp_post_mean_batched_work(const fgp_pred_desc* pd, int64_t N, int64_t* work) {
+  if (!pd || !work) return set_error(kErrInvalid, "fgp_post_mean_batched_work: null pointer");
+  if (N < 0 || pd->n < 1 || pd->d < 1 || pd->d > FGP_MAX_D || pd->P < 1)
+    return set_error(kErrInvalid, "fgp_post_mean_batched_work: bad sizes");
+  PredSpec spec;
+  int rc = make_spec(pd->family, pd->d, pd->order, pd->coef, spec);
+  if (rc != kOk) return rc;
+  const int64_t chunk = pd->family == FGP_FAMILY_LATTICE ? post_mean_chunk<0>(pd->d, spec, pd->n, N, pd->P, 1)
+                                                         : post_mean_chunk<1>(pd->d, spec, pd->n, N, pd->P, 1);
+  *work = std::max<int64_t>(1, ((pd->n + chunk - 1) / chunk) * pd->P * N);
+  return kOk;
 }
 
 int fgp_post_var_batched(const fgp_pred_desc* pd, const double* xt, int64_t xt_stride, int64_t N, const double* part0,

@@ -445,6 +445,17 @@ def post_mean_matfree(family, xt, z_dn, hyp, coeffs, alphas=None, tbits=0, chunk
         coeffs = coeffs.contiguous()
     out = torch.empty((B, Nt), dtype=torch.float64, device=xt.device)
     order, coef = _pred_args(family, alphas, d)
+    if Gk == B and B > 4:
+        # every output with its own hyper-parameters (C5 per-output): ONE launch over the blocks of 4 outputs
+        # (fgp_post_mean, ABI 16) instead of one per block -- no launch gaps, the rounds of resident workgroups filled
+        if chunk is None:
+            chunk = post_mean_chunk(n, Nt * (B // 4))
+        nchunks = (n + chunk - 1) // chunk
+        work = torch.empty((nchunks * B * Nt,), dtype=torch.float64, device=xt.device)
+        hyp_c = hyp.contiguous()
+        N.call("fgp_post_mean", family, N.ptr(xt), Nt, N.ptr(z_dn), n, d, int(tbits), order, coef, N.ptr(hyp_c), B,
+               N.ptr(coeffs), coeffs.stride(0), B, N.ptr(out), Nt, N.ptr(work), chunk, _stream(xt))
+        return out
     if chunk is None:
         chunk = post_mean_chunk(n, Nt)
     nchunks = (n + chunk - 1) // chunk

@@ -364,8 +364,9 @@ int fgp_fit_run(const fgp_nll_desc* nll, const fgp_fit_desc* fit, int iter0, int
  * lattice: part_j = coef[j] B_{order[j]}((x_j - z_j) % 1), z float64 [d][n];
  * net:     part_j = walsh part of order order[j] (1..4, as fgp_net_parts; order = NULL: 1) of
  *          floor((x_j % 1) 2^tbits) XOR z_j, z int64 [d][n] (coef unused).
- * xt: [N, d] float64 contiguous; coeffs: [B][n] with row stride coeff_stride; 1 <= B <= 4;
- * out: [B][N] row stride out_stride; work: float64 scratch of ceil(n/chunk) * B * N entries. */
+ * xt: [N, d] float64 contiguous; coeffs: [B][n] with row stride coeff_stride; 1 <= B <= 4, or (ABI 16) any B
+ * when Gk == B (every output its own hyper-parameters: the blocks of 4 outputs run as one launch; out_stride
+ * must then be N); out: [B][N] row stride out_stride; work: float64 scratch of ceil(n/chunk) * B * N entries. */
 int fgp_post_mean(int family, const double* xt, int64_t N, const void* z, int64_t n, int d, int tbits, const int* order,
                   const double* coef, const double* hyp, int Gk, const double* coeffs, int64_t coeff_stride, int B,
                   double* out, int64_t out_stride, double* work, int64_t chunk, void* stream);
@@ -412,9 +413,11 @@ typedef struct fgp_pred_desc {
 } fgp_pred_desc;
 
 /* out[p, t] = sum_i K_p(xt_p[t], z_p[:, i]) coeffs_p[i]; xt_p = xt + p*xt_stride ([N, d]; stride 0 =
- * shared test points); out [P][N]; work: float64 scratch of ceil(n/1024) * P * N entries. */
+ * shared test points); out [P][N]; work: float64 scratch of fgp_post_mean_batched_work entries (ABI 16: the
+ * training points per workgroup are chosen so that the launch fills its rounds of resident workgroups). */
 int fgp_post_mean_batched(const fgp_pred_desc* desc, const double* xt, int64_t xt_stride, int64_t N, double* out,
                           double* work, void* stream);
+int fgp_post_mean_batched_work(const fgp_pred_desc* desc, int64_t N, int64_t* work);
 
 /* Posterior variance, 13 <= log2(n) <= 24 (AbstractGP.post_var, abstract_gp.py:381-416, n = the GP's n):
  *   out[p, t] = max(K_p(x, x) - sum_k wa_p[k] |ft(K_p(x_t, z_p))_k|^2, 0)  (negatives set to 0, :413)

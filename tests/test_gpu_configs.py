@@ -186,3 +186,27 @@ def test_post_mean_chunk_sizes_agree(family):
                        t=getattr(gp, "t", None))
     opm = o.post_mean(xt.cpu())
     assert float((pm.cpu() - opm).abs().max()) <= 1e-7 * float(opm.abs().max())
+
+
+@pytest.mark.parametrize("family", ["lattice", "net"])
+def test_post_mean_output_blocks_in_one_launch_equal_block_launches(family):
+    """fgp_post_mean with every output its own hyper-parameters and B > 4 (ABI 16: the blocks of 4 outputs as the
+    problems of ONE launch, the remainder in a second) against one launch per block of <= 4 outputs at the same
+    training chunk: the same arithmetic, bit for bit (B = 10: two full blocks and a block of 2)."""
+    n, d, B = 2 ** 14, 3, 10
+    if family == "lattice":
+        gp = F.FastGPLattice(F.Lattice(d, seed=3), device=DEV)
+    else:
+        gp = F.FastGPDigitalNetB2(F.DigitalNetB2(d, seed=3), device=DEV)
+    gp.get_x_next(n)
+    g = torch.Generator().manual_seed(9)
+    xt = torch.rand((300, d), generator=g).to(DEV)
+    z = gp._points_T(n)
+    hyp = torch.cat([torch.rand((B, 1), generator=g) + 0.5, torch.rand((B, d), generator=g) + 0.3], 1).to(DEV)
+    coeffs = torch.randn((B, n), generator=g).to(DEV)
+    kw = dict(alphas=gp._alphas, tbits=gp._tbits(), chunk=512)
+    one = F.ops.post_mean_matfree(gp._FAMILY, xt, z, hyp, coeffs, **kw)
+    blocks = torch.cat([F.ops.post_mean_matfree(gp._FAMILY, xt, z, hyp[b:b + 4], coeffs[b:b + 4], **kw)
+                        for b in range(0, B, 4)])
+    assert one.shape == (B, 300)
+    assert torch.equal(one, blocks)
