@@ -86,7 +86,7 @@ class MtLayout(ctypes.Structure):
 
 
 class MtFitDesc(ctypes.Structure):
-    """Mirror of fgp_mt_fit_desc (include/fgp_hip.h, ABI 14)."""
+    """Mirror of fgp_mt_fit_desc (include/fgp_hip.h, ABI 14; parameter batches ABI 16)."""
     _fields_ = [
         ("family", _c_int), ("d", _c_int), ("B", _c_int),
         ("layout", MtLayout), ("task", _c_int * 16),
@@ -99,6 +99,7 @@ class MtFitDesc(ctypes.Structure):
         ("logdet_weight", _c_dbl), ("mll_const", _c_dbl), ("eta_minus", _c_dbl), ("eta_plus", _c_dbl),
         ("step_min", _c_dbl), ("step_max", _c_dbl),
         ("work", _c_vp),
+        ("G", _c_int), ("rows", _c_vp), ("nrows", _c_int * 5),
     ]
 
 

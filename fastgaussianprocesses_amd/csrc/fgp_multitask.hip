@@ -314,6 +314,9 @@ __global__ __launch_bounds__(kWG) void k_mt_mll_grad(const double2* __restrict__
 struct MtFit {
   MtLay lay;
   int family, d, B, T_all, rank, dl, vtask_exp, P;
+  int G;                          // problems (parameter batch, ABI 16); rows: their parameter rows ([5][G], or NULL)
+  const int* rows;
+  int l_off, n_off;               // raw offsets of the lengthscale / noise blocks (scale rows at 0)
   int task[FGP_MT_MAX_TASKS];
   int rg_scale, rg_ls, rg_noise, rg_factor, rg_vtask;
   const double2* spec;
@@ -332,14 +335,25 @@ struct MtFit {
 
 constexpr int kMtgQ = 4 + FGP_MAX_D;   // norm, logdet, dnoise (/ noise), draw_scale, draw_l[FGP_MAX_D]
 
-__device__ __forceinline__ double mtg_scale(const MtFit& m) { return exp(m.raw[0]); }
-__device__ __forceinline__ double mtg_ls(const MtFit& m, int j) { return exp(m.raw[1 + (m.dl > 1 ? j : 0)]); }
-__device__ __forceinline__ double mtg_noise(const MtFit& m) { return exp(m.raw[1 + m.dl]); }
+// problem g's row of parameter block q (0 scale, 1 lengthscales, 2 noise, 3 task factor, 4 task noise)
+__device__ __forceinline__ int mtg_row(const MtFit& m, int q, int g) { return m.rows ? m.rows[q * m.G + g] : 0; }
+// raw indices of problem g's parameters
+__device__ __forceinline__ int mtg_is(const MtFit& m, int g) { return mtg_row(m, 0, g); }
+__device__ __forceinline__ int mtg_il(const MtFit& m, int g, int j) {
+  return m.l_off + mtg_row(m, 1, g) * m.dl + (m.dl > 1 ? j : 0);
+}
+__device__ __forceinline__ int mtg_in(const MtFit& m, int g) { return m.n_off + mtg_row(m, 2, g); }
+__device__ __forceinline__ int mtg_if(const MtFit& m, int g) { return m.f_off + mtg_row(m, 3, g) * m.T_all * m.rank; }
+__device__ __forceinline__ int mtg_iv(const MtFit& m, int g) { return m.v_off + mtg_row(m, 4, g) * m.T_all; }
+__device__ __forceinline__ double mtg_scale(const MtFit& m, int g) { return exp(m.raw[mtg_is(m, g)]); }
+__device__ __forceinline__ double mtg_ls(const MtFit& m, int g, int j) { return exp(m.raw[mtg_il(m, g, j)]); }
+__device__ __forceinline__ double mtg_noise(const MtFit& m, int g) { return exp(m.raw[mtg_in(m, g)]); }
 // K_task[a, b] = sum_r F[a, r] F[b, r] + [a == b] v_a  (util.py:157-162; F identity, v exp / identity)
-__device__ __forceinline__ double mtg_kt(const MtFit& m, int a, int b) {
+__device__ __forceinline__ double mtg_kt(const MtFit& m, int g, int a, int b) {
+  const int fo = mtg_if(m, g), vo = mtg_iv(m, g);
   double s = 0.0;
-  for (int r = 0; r < m.rank; ++r) s += m.raw[m.f_off + a * m.rank + r] * m.raw[m.f_off + b * m.rank + r];
-  if (a == b) s += m.vtask_exp ? exp(m.raw[m.v_off + a]) : m.raw[m.v_off + a];
+  for (int r = 0; r < m.rank; ++r) s += m.raw[fo + a * m.rank + r] * m.raw[fo + b * m.rank + r];
+  if (a == b) s += m.vtask_exp ? exp(m.raw[vo + a]) : m.raw[vo + a];
   return s;
 }
 
@@ -389,57 +403,62 @@ __device__ __forceinline__ double2 mtg_poly(const MtFit& m, int p, int64_t nk, i
 }
 
 template <int D>
-__device__ __forceinline__ void mtg_lpow(const MtFit& m, double* lpow) {
+__device__ __forceinline__ void mtg_lpow(const MtFit& m, int g, double* lpow) {
 #pragma unroll
   for (int S = 0; S < (1 << D); ++S) {
     double w = 1.0;
 #pragma unroll
     for (int j = 0; j < D; ++j)
-      if ((S >> j) & 1) w *= mtg_ls(m, j);
+      if ((S >> j) & 1) w *= mtg_ls(m, g, j);
     lpow[S] = w;
   }
 }
 
+// (problem g = the launch's y index: entry / class / block-row g of a parameter batch; 0 when unbatched)
 template <int D>
 __global__ __launch_bounds__(kWG) void k_mtg_lams(MtFit m) {
   const int64_t e = (int64_t)blockIdx.x * kWG + threadIdx.x;
+  const int g = blockIdx.y;
   if (e >= m.lay.L) return;
   double lpow[1 << D];
-  mtg_lpow<D>(m, lpow);
+  mtg_lpow<D>(m, g, lpow);
   int k, l, p;
   int64_t i;
   mtg_entry(m, e, k, l, p, i);
   const double2 P = mtg_poly<D, false>(m, p, m.lay.n[k], i, lpow, nullptr);
-  const double sc = mtg_scale(m), rn = sqrt((double)m.lay.n[l]);
+  const double sc = mtg_scale(m, g), rn = sqrt((double)m.lay.n[l]);
   // lams = K_task (sqrt(n_l) lam + noise [k == l]),  lam = scale P  (util.py:284-298)
   double2 v = make_double2(rn * (sc * P.x), rn * (sc * P.y));
-  if (k == l) v.x += mtg_noise(m);
-  const double kt = mtg_kt(m, m.task[k], m.task[l]);
-  m.lams[e] = make_double2(v.x * kt, v.y * kt);
+  if (k == l) v.x += mtg_noise(m, g);
+  const double kt = mtg_kt(m, g, m.task[k], m.task[l]);
+  m.lams[(int64_t)g * m.lay.L + e] = make_double2(v.x * kt, v.y * kt);
 }
 
 __global__ __launch_bounds__(kWG) void k_mtg_factor_grad(MtFit m) {
   const int64_t j = (int64_t)blockIdx.x * kWG + threadIdx.x;
+  const int g = blockIdx.y;
   const MtLay& lay = m.lay;
   if (j >= lay.nmin) return;
+  const int64_t go = (int64_t)g * lay.L, rn = (int64_t)lay.R * lay.nmin, gy = (int64_t)g * m.B * rn;
   bool bad = false;
-  m.logdet[j] = mt_ldl_class(m.lams + j, m.fac + j, lay, &bad);
+  m.logdet[(int64_t)g * lay.nmin + j] = mt_ldl_class(m.lams + go + j, m.fac + go + j, lay, &bad);
   if (bad) m.info[0] = 1;
-  const int64_t rn = (int64_t)lay.R * lay.nmin;
-  for (int b = 0; b < m.B; ++b) mt_solve_class(m.fac + j, lay, m.y + b * rn + j, m.z + b * rn + j);
-  mt_selinv_class(m.fac + j, lay, m.zinv + j);
+  for (int b = 0; b < m.B; ++b) mt_solve_class(m.fac + go + j, lay, m.y + gy + b * rn + j, m.z + gy + b * rn + j);
+  mt_selinv_class(m.fac + go + j, lay, m.zinv + go + j);
   const double gn = m.gn;
-  mt_grad_class(m.zinv + j, m.z, [&](int64_t) { return gn; }, m.gl, m.B, 1, 0, j, lay, m.glp + j);
+  mt_grad_class(m.zinv + go + j, m.z + gy, [&](int64_t) { return gn; }, m.gl, m.B, 1, 0, j, lay, m.glp + go + j);
 }
 
 template <int D>
 __global__ __launch_bounds__(kWG) void k_mtg_contract(MtFit m) {
   __shared__ double red[kWG / 64];
   const int64_t t0 = (int64_t)blockIdx.x * kWG + threadIdx.x, nt = (int64_t)gridDim.x * kWG;
+  const int g = blockIdx.y;
   const MtLay& lay = m.lay;
+  const int64_t go = (int64_t)g * lay.L, rnm = (int64_t)lay.R * lay.nmin;
   double lpow[1 << D];
-  mtg_lpow<D>(m, lpow);
-  const double sc = mtg_scale(m);
+  mtg_lpow<D>(m, g, lpow);
+  const double sc = mtg_scale(m, g);
   double acc[4 + D];
 #pragma unroll
   for (int q = 0; q < 4 + D; ++q) acc[q] = 0.0;
@@ -450,29 +469,30 @@ __global__ __launch_bounds__(kWG) void k_mtg_contract(MtFit m) {
     double2 dp[D];
     const double2 P = mtg_poly<D, true>(m, p, lay.n[k], i, lpow, dp);
     const double rn = sqrt((double)lay.n[l]);
-    const double kt = mtg_kt(m, m.task[k], m.task[l]);
-    const double2 c = m.glp[e];            // dL/dRe + i dL/dIm of lams[e]: dL/dtheta = Re(conj(c) dlams/dtheta)
+    const double kt = mtg_kt(m, g, m.task[k], m.task[l]);
+    const double2 c = m.glp[go + e];       // dL/dRe + i dL/dIm of lams[e]: dL/dtheta = Re(conj(c) dlams/dtheta)
     const double f = kt * rn * sc;
     acc[3] = __builtin_fma(f, __builtin_fma(c.x, P.x, c.y * P.y), acc[3]);             // draw_scale
 #pragma unroll
     for (int j = 0; j < D; ++j) acc[4 + j] = __builtin_fma(f, __builtin_fma(c.x, dp[j].x, c.y * dp[j].y), acc[4 + j]);
     double bx = rn * (sc * P.x), by = rn * (sc * P.y);
     if (k == l) {
-      bx += mtg_noise(m);
+      bx += mtg_noise(m, g);
       acc[2] = __builtin_fma(kt, c.x, acc[2]);                                         // dnoise / noise
     }
-    m.dkt[e] = __builtin_fma(c.x, bx, c.y * by);                                       // dL/dK_task of entry e
+    m.dkt[go + e] = __builtin_fma(c.x, bx, c.y * by);                                  // dL/dK_task of entry e
   }
-  const int64_t rnm = (int64_t)lay.R * lay.nmin;
+  const double2* yg = m.y + (int64_t)g * m.B * rnm;
+  const double2* zg = m.z + (int64_t)g * m.B * rnm;
   for (int64_t e = t0; e < (int64_t)m.B * rnm; e += nt) {
-    const double2 yv = m.y[e], zv = m.z[e];
+    const double2 yv = yg[e], zv = zg[e];
     acc[0] = __builtin_fma(yv.x, zv.x, __builtin_fma(yv.y, zv.y, acc[0]));             // Re(conj(y) z)
   }
-  for (int64_t j = t0; j < lay.nmin; j += nt) acc[1] += m.logdet[j];
+  for (int64_t j = t0; j < lay.nmin; j += nt) acc[1] += m.logdet[(int64_t)g * lay.nmin + j];
 #pragma unroll
   for (int q = 0; q < 4 + D; ++q) {
     const double s = block_sum(acc[q], red);
-    if (threadIdx.x == 0) m.part[(int64_t)blockIdx.x * kMtgQ + q] = s;
+    if (threadIdx.x == 0) m.part[((int64_t)g * m.nblk + blockIdx.x) * kMtgQ + q] = s;
   }
 }
 
@@ -489,58 +509,68 @@ __global__ __launch_bounds__(kWG) void k_mtg_step(MtFit m, int iter, int do_upda
   __shared__ double red[kWG / 64];
   __shared__ double tot[kMtgQ];
   __shared__ double gkt[FGP_MT_MAX_TASKS * (FGP_MT_MAX_TASKS + 1) / 2];
-  __shared__ double grad[FGP_MT_MAX_TASKS * FGP_MT_MAX_TASKS + FGP_MT_MAX_TASKS + 3 + FGP_MAX_D];
+  __shared__ double term[2];
+  extern __shared__ double grad[];                 // [n_params]
   const int tid = threadIdx.x;
   const MtLay& lay = m.lay;
-  for (int q = 0; q < 4 + D; ++q) {
-    const double s = mtg_sum(m.nblk, [&](int64_t b) { return m.part[b * kMtgQ + q]; }, red);
-    if (tid == 0) tot[q] = s;
-  }
-  for (int k = 0, p = 0; k < lay.T; ++k)
-    for (int l = k; l < lay.T; ++l, ++p) {
-      const int64_t o = lay.off[k * FGP_MT_MAX_TASKS + l];
-      const double s = mtg_sum(lay.n[k], [&](int64_t i) { return m.dkt[o + i]; }, red);
-      if (tid == 0) gkt[p] = s;
-    }
+  for (int q = tid; q < m.n_params; q += kWG) grad[q] = 0.0;
+  if (tid == 0) term[0] = term[1] = 0.0;
   __syncthreads();
-  if (tid == 0) {
-    const double term2 = m.logdet_weight * tot[1];
-    double* lh = m.loss_hist + (int64_t)iter * 3;
-    lh[0] = 0.5 * (tot[0] + term2 + m.mll_const);
-    lh[1] = tot[0];
-    lh[2] = term2;
-    // gradients in the raw vector's order
-    grad[0] = tot[3];
-    if (m.dl > 1) {
-      for (int j = 0; j < m.d; ++j) grad[1 + j] = tot[4 + j];
-    } else {
-      double g = 0.0;
-      for (int j = 0; j < m.d; ++j) g += tot[4 + j];
-      grad[1] = g;
+  // problem by problem (ascending): its fixed-order reductions, its gradient added into its parameter rows
+  for (int g = 0; g < m.G; ++g) {
+    for (int q = 0; q < 4 + D; ++q) {
+      const double s = mtg_sum(m.nblk, [&](int64_t b) { return m.part[((int64_t)g * m.nblk + b) * kMtgQ + q]; }, red);
+      if (tid == 0) tot[q] = s;
     }
-    grad[1 + m.dl] = mtg_noise(m) * tot[2];
-    for (int q = m.f_off; q < m.n_params; ++q) grad[q] = 0.0;
-    // K_task[a, b] = sum_r F[a, r] F[b, r] + [a == b] v_a:  dF[c, r] += g_ab (F[b, r] [a == c] + F[a, r] [b == c])
     for (int k = 0, p = 0; k < lay.T; ++k)
       for (int l = k; l < lay.T; ++l, ++p) {
-        const int a = m.task[k], b = m.task[l];
-        const double g = gkt[p];
-        for (int r = 0; r < m.rank; ++r) {
-          grad[m.f_off + a * m.rank + r] += g * m.raw[m.f_off + b * m.rank + r];
-          grad[m.f_off + b * m.rank + r] += g * m.raw[m.f_off + a * m.rank + r];
-        }
-        if (a == b) grad[m.v_off + a] += m.vtask_exp ? g * exp(m.raw[m.v_off + a]) : g;
+        const int64_t o = (int64_t)g * lay.L + lay.off[k * FGP_MT_MAX_TASKS + l];
+        const double s = mtg_sum(lay.n[k], [&](int64_t i) { return m.dkt[o + i]; }, red);
+        if (tid == 0) gkt[p] = s;
       }
+    __syncthreads();
+    if (tid == 0) {
+      term[0] += tot[0];
+      term[1] += tot[1];
+      grad[mtg_is(m, g)] += tot[3];
+      if (m.dl > 1) {
+        for (int j = 0; j < m.d; ++j) grad[mtg_il(m, g, j)] += tot[4 + j];
+      } else {
+        double s = 0.0;
+        for (int j = 0; j < m.d; ++j) s += tot[4 + j];
+        grad[mtg_il(m, g, 0)] += s;
+      }
+      grad[mtg_in(m, g)] += mtg_noise(m, g) * tot[2];
+      // K_task[a, b] = sum_r F[a, r] F[b, r] + [a == b] v_a:  dF[c, r] += g_ab (F[b, r] [a == c] + F[a, r] [b == c])
+      const int fo = mtg_if(m, g), vo = mtg_iv(m, g);
+      for (int k = 0, p = 0; k < lay.T; ++k)
+        for (int l = k; l < lay.T; ++l, ++p) {
+          const int a = m.task[k], b = m.task[l];
+          const double gv = gkt[p];
+          for (int r = 0; r < m.rank; ++r) {
+            grad[fo + a * m.rank + r] += gv * m.raw[fo + b * m.rank + r];
+            grad[fo + b * m.rank + r] += gv * m.raw[fo + a * m.rank + r];
+          }
+          if (a == b) grad[vo + a] += m.vtask_exp ? gv * exp(m.raw[vo + a]) : gv;
+        }
+    }
+    __syncthreads();
   }
-  __syncthreads();
+  if (tid == 0) {
+    const double term2 = m.logdet_weight * term[1];
+    double* lh = m.loss_hist + (int64_t)iter * 3;
+    lh[0] = 0.5 * (term[0] + term2 + m.mll_const);
+    lh[1] = term[0];
+    lh[2] = term2;
+  }
   for (int q = tid; q < m.n_params; q += kWG) {
     const double gp = grad[q];
     m.raw_hist[(int64_t)iter * m.n_params + q] = m.raw[q];
     m.grad[q] = gp;
     int rg;
-    if (q == 0) rg = m.rg_scale;
-    else if (q <= m.dl) rg = m.rg_ls;
-    else if (q == 1 + m.dl) rg = m.rg_noise;
+    if (q < m.l_off) rg = m.rg_scale;
+    else if (q < m.n_off) rg = m.rg_ls;
+    else if (q < m.f_off) rg = m.rg_noise;
     else if (q < m.v_off) rg = m.rg_factor;
     else rg = m.rg_vtask;
     if (!(do_update && rg)) continue;
@@ -629,23 +659,33 @@ static int to_mtfit(const fgp_mt_fit_desc* d, MtFit* m, int64_t* work_bytes) {
   m->eta_plus = d->eta_plus;
   m->step_min = d->step_min;
   m->step_max = d->step_max;
-  m->f_off = 2 + m->dl;
-  m->v_off = m->f_off + m->T_all * m->rank;
-  m->n_params = m->v_off + m->T_all;
-  const int64_t L = m->lay.L, rn = (int64_t)m->lay.R * m->lay.nmin;
+  // problems of a parameter batch (ABI 16; G = 0: 1) and the row counts of the parameter blocks
+  m->G = d->G > 0 ? d->G : 1;
+  if (m->G > 65535) return set_error(kErrUnsupported, "fgp_mt_fit: G = %d problems > 65535", m->G);
+  m->rows = d->rows;
+  int nr[5];
+  for (int q = 0; q < 5; ++q) nr[q] = d->nrows[q] > 0 ? d->nrows[q] : 1;
+  if (m->G > 1 && !m->rows) return set_error(kErrInvalid, "fgp_mt_fit: G = %d problems without parameter rows", m->G);
+  m->l_off = nr[0];
+  m->n_off = m->l_off + nr[1] * m->dl;
+  m->f_off = m->n_off + nr[2];
+  m->v_off = m->f_off + nr[3] * m->T_all * m->rank;
+  m->n_params = m->v_off + nr[4] * m->T_all;
+  if (m->n_params > 8192) return set_error(kErrUnsupported, "fgp_mt_fit: %d parameters > 8192", m->n_params);
+  const int64_t G = m->G, L = m->lay.L, rn = (int64_t)m->lay.R * m->lay.nmin;
   const int64_t cover = std::max<int64_t>(std::max<int64_t>(L, (int64_t)m->B * rn), m->lay.nmin);
   m->nblk = (int)std::min<int64_t>(1024, (cover + kWG - 1) / kWG);
-  // workspace: lams, fac, zinv, glp [L] double2; z [B][R nmin] double2; logdet [nmin]; dkt [L]; part
-  // [nblk][kMtgQ]; info
+  // workspace: lams, fac, zinv, glp [G][L] double2; z [G][B][R nmin] double2; logdet [G][nmin]; dkt [G][L]; part
+  // [G][nblk][kMtgQ]; info
   size_t off = 0;
-  const size_t o_lams = off; off += mtg_align(16 * (size_t)L);
-  const size_t o_fac = off; off += mtg_align(16 * (size_t)L);
-  const size_t o_zinv = off; off += mtg_align(16 * (size_t)L);
-  const size_t o_glp = off; off += mtg_align(16 * (size_t)L);
-  const size_t o_z = off; off += mtg_align(16 * (size_t)m->B * rn);
-  const size_t o_ld = off; off += mtg_align(8 * (size_t)m->lay.nmin);
-  const size_t o_dkt = off; off += mtg_align(8 * (size_t)L);
-  const size_t o_part = off; off += mtg_align(8 * (size_t)m->nblk * kMtgQ);
+  const size_t o_lams = off; off += mtg_align(16 * (size_t)(G * L));
+  const size_t o_fac = off; off += mtg_align(16 * (size_t)(G * L));
+  const size_t o_zinv = off; off += mtg_align(16 * (size_t)(G * L));
+  const size_t o_glp = off; off += mtg_align(16 * (size_t)(G * L));
+  const size_t o_z = off; off += mtg_align(16 * (size_t)(G * m->B * rn));
+  const size_t o_ld = off; off += mtg_align(8 * (size_t)(G * m->lay.nmin));
+  const size_t o_dkt = off; off += mtg_align(8 * (size_t)(G * L));
+  const size_t o_part = off; off += mtg_align(8 * (size_t)(G * m->nblk * kMtgQ));
   const size_t o_info = off; off += 256;
   if (work_bytes) *work_bytes = (int64_t)off;
   char* w = static_cast<char*>(d->work);
@@ -777,15 +817,17 @@ int fgp_mt_fit_run(const fgp_mt_fit_desc* desc, int iter0, int iters, int final_
     return set_error(kErrInvalid, "fgp_mt_fit_run: null pointer");
   if (iter0 < 0 || iters < 0) return set_error(kErrInvalid, "fgp_mt_fit_run: iter0 / iters");
   hipStream_t st = (hipStream_t)stream;
-  const unsigned ge = (unsigned)((m.lay.L + kWG - 1) / kWG), gc = (unsigned)((m.lay.nmin + kWG - 1) / kWG);
+  const dim3 ge((unsigned)((m.lay.L + kWG - 1) / kWG), (unsigned)m.G), gc((unsigned)((m.lay.nmin + kWG - 1) / kWG), (unsigned)m.G);
+  const dim3 gb((unsigned)m.nblk, (unsigned)m.G);
+  const size_t shm = sizeof(double) * (size_t)m.n_params;
   return mtg_with_d(m.d, [&](auto dc) {
     constexpr int D = decltype(dc)::value;
     for (int it = 0; it < iters; ++it) {
       const int upd = !(final_no_update && it == iters - 1);
       k_mtg_lams<D><<<ge, kWG, 0, st>>>(m);
       k_mtg_factor_grad<<<gc, kWG, 0, st>>>(m);
-      k_mtg_contract<D><<<(unsigned)m.nblk, kWG, 0, st>>>(m);
-      k_mtg_step<D><<<1, kWG, 0, st>>>(m, iter0 + it, upd);
+      k_mtg_contract<D><<<gb, kWG, 0, st>>>(m);
+      k_mtg_step<D><<<1, kWG, shm, st>>>(m, iter0 + it, upd);
       const int r = check_launch("fgp_mt_fit_run");
       if (r != kOk) return r;
     }

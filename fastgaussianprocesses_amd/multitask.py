@@ -356,12 +356,38 @@ class MultiTaskFastGP(AbstractFastGP):
         return tuple(self.raw_scale.shape) == (1,) and tuple(self.raw_noise.shape) == (1,) and \
             tuple(self.raw_lengthscales.shape) in ((1,), (self.d,))
 
+    def _mt_param_rows(self):
+        """Parameter batches (docs/examples/batch_multitask/fgp_lattice.ipynb cell 6; abstract_gp.py:73-139: each
+        parameter's batch dimensions are the TRAILING dimensions of shape_batch): None when no parameter has batch
+        dimensions (one problem, the data batch sharing the parameters), else the [5, d_out] int tensor of every
+        output's row in each parameter block (scale, lengthscales, noise, task factor, task noise) and the blocks'
+        row counts -- each output its own eigen-problem (fgp_mt_fit_desc.G / rows, ABI 16)."""
+        tails = ((self.raw_scale, 1), (self.raw_lengthscales, 1), (self.raw_noise, 1), (self.raw_factor_task_kernel, 2),
+                 (self.raw_noise_task_kernel, 1))
+        bshapes = [tuple(p.shape[:p.dim() - t]) for p, t in tails]
+        if not any(bshapes):
+            return None
+        sb = tuple(int(v) for v in self.shape_batch)
+        d_out = int(np.prod(sb)) if sb else 1
+        grid = np.stack(np.meshgrid(*[np.arange(v) for v in sb], indexing="ij"), -1).reshape(d_out, len(sb)) \
+            if sb else np.zeros((1, 0), dtype=np.int64)
+        rows, nrows = [], []
+        for bs in bshapes:
+            k = len(bs)
+            if k > len(sb) or tuple(sb[len(sb) - k:]) != bs:
+                return False
+            sub = grid[:, len(sb) - k:]
+            rows.append(np.ravel_multi_index(tuple(sub.T), bs) if k else np.zeros(d_out, dtype=np.int64))
+            nrows.append(int(np.prod(bs)) if k else 1)
+        return np.stack(rows).astype(np.int32), nrows
+
     def _mt_general_ok(self):
         """The device-resident fit of the GENERAL case (fgp_mt_fit_run, ABI 14: MtGeneralEngine) -- the reference's
         default multitask setting (abstract_gp.py:116-139: the task kernel F F^T + diag(v) learned), any n per
-        task (util.py:273-323), a data batch sharing the hyper-parameters: at most 16 active tasks, d <= 6, no
-        parameter batch, exp transforms for scale / lengthscales / noise, the identity for the task factor and
-        exp or the identity for the task noise, no adaptive nugget, pair spectra within MT_SPECTRA_CAP bytes."""
+        task (util.py:273-323), a data batch sharing the hyper-parameters or (ABI 16) parameter batches broadcast
+        over shape_batch (every output its own eigen-problem, at most 4096): at most 16 active tasks, d <= 6, exp
+        transforms for scale / lengthscales / noise, the identity for the task factor and exp or the identity for
+        the task noise (one per task), no adaptive nugget, pair spectra within MT_SPECTRA_CAP bytes."""
         if os.environ.get("FGP_MT_FUSED", "1")[:1] == "0":
             return False
         lo_ns = [v for v in self._ns if v > 0]
@@ -372,13 +398,22 @@ class MultiTaskFastGP(AbstractFastGP):
         if self.tf_factor_task_kernel is not _identity or self.tf_noise_task_kernel not in (_exp, _identity):
             return False
         T = self.num_tasks
-        if tuple(self.raw_scale.shape) != (1,) or tuple(self.raw_noise.shape) != (1,) or \
-                tuple(self.raw_lengthscales.shape) not in ((1,), (self.d,)) or \
-                self.raw_factor_task_kernel.dim() != 2 or tuple(self.raw_noise_task_kernel.shape) != (T,):
+        if self.raw_scale.shape[-1] != 1 or self.raw_noise.shape[-1] != 1 or \
+                self.raw_lengthscales.shape[-1] not in (1, self.d) or self.raw_factor_task_kernel.dim() < 2 or \
+                self.raw_factor_task_kernel.shape[-2] != T or self.raw_noise_task_kernel.shape[-1] != T:
+            return False
+        pr = self._mt_param_rows()
+        if pr is False or (pr is not None and (len(pr[0][0]) > 4096 or
+                                              sum(n * w for n, w in zip(pr[1], self._mt_row_widths())) > 8192)):
             return False
         srt = sorted(lo_ns, reverse=True)
         spec = sum(srt[k] for k in range(len(srt)) for _ in range(k, len(srt))) * (1 << self.d) * 16
         return spec <= MT_SPECTRA_CAP
+
+    def _mt_row_widths(self):
+        """Raw elements per row of each parameter block (scale, lengthscales, noise, task factor, task noise)."""
+        return (1, int(self.raw_lengthscales.shape[-1]), 1,
+                int(self.raw_factor_task_kernel.shape[-1]) * self.num_tasks, self.num_tasks)
 
     def _mt_spectra(self, n):
         """Pair spectra Phi^{kl}_S = ft(B^{kl}_S) [T (T+1)/2, 2^d, n] (pairs k <= l row-major): with the
@@ -1045,10 +1080,21 @@ class MtGeneralEngine(object):
         Y = lo.pack([gp.get_ytilde(l).to(torch.complex128) for l in range(T)])
         B = int(np.prod(tuple(Y.shape[:-1]))) if Y.dim() > 1 else 1
         self.y = Y.reshape(B, -1).resolve_conj().contiguous()
-        self.B = B
-        dl = gp.raw_lengthscales.numel()
+        # parameter batches (ABI 16): every output its own problem (G = d_out, one data vector each), its
+        # parameters the rows of _mt_param_rows
+        pr = gp._mt_param_rows()
+        G = 1 if pr is None else B
+        if G > 1:
+            B = 1
+            self.rows = torch.from_numpy(np.ascontiguousarray(pr[0])).to(dev)
+            nrows = pr[1]
+        else:
+            self.rows = None
+            nrows = [1] * 5
+        self.G, self.B = G, B
+        dl = int(gp.raw_lengthscales.shape[-1])
         r = int(gp.raw_factor_task_kernel.shape[-1])
-        self.sizes = (1, dl, 1, T * r, T)
+        self.sizes = tuple(n * w for n, w in zip(nrows, gp._mt_row_widths()))
         self.raw = torch.cat([gp.raw_scale.detach().reshape(-1), gp.raw_lengthscales.detach().reshape(-1),
                               gp.raw_noise.detach().reshape(-1), gp.raw_factor_task_kernel.detach().reshape(-1),
                               gp.raw_noise_task_kernel.detach().reshape(-1)]).to(dev, torch.float64).contiguous()
@@ -1059,6 +1105,10 @@ class MtGeneralEngine(object):
         d_out = int(torch.tensor(tuple(gp.shape_batch)).prod()) if len(gp.shape_batch) else 1
         desc = N.MtFitDesc()
         desc.family, desc.d, desc.B = int(gp._FAMILY), int(d), B
+        desc.G = G
+        desc.rows = self.rows.data_ptr() if self.rows is not None else None
+        for q in range(5):
+            desc.nrows[q] = int(nrows[q])
         desc.layout = lo.lay
         for k, a in enumerate(lo.active):
             desc.task[k] = int(a)
@@ -1073,9 +1123,13 @@ class MtGeneralEngine(object):
                                                     int(gp.raw_noise.requires_grad))
         desc.rg_factor, desc.rg_vtask = int(gp.raw_factor_task_kernel.requires_grad), int(gp.raw_noise_task_kernel.requires_grad)
         desc.rprop_prev, desc.rprop_step, desc.grad_out = self.prev.data_ptr(), self.step.data_ptr(), self.grad.data_ptr()
+        # logdet weight d_out / numel(logdet) (abstract_gp.py:256): one problem's logdet stands for the d_out outputs
+        # sharing it; with a parameter batch every output is its own problem (weight 1: a parameter row shared by k
+        # outputs has its logdet counted k times, as the reference's broadcast replicates it)
+        w = 1.0 if G > 1 else float(d_out)
         desc.grad_norm = 0.5
-        desc.grad_logdet = 0.5 * d_out
-        desc.logdet_weight = float(d_out)
+        desc.grad_logdet = 0.5 * w
+        desc.logdet_weight = w
         desc.mll_const = float(mll_constant(d_out, sum(gp._ns)))
         desc.eta_minus, desc.eta_plus = RPROP_ETAS
         desc.step_min, desc.step_max = RPROP_STEPS
@@ -1124,5 +1178,5 @@ class MtGeneralEngine(object):
         gp = self.gp
         f, v = self.split_task(raw_rows)
         F = gp.tf_factor_task_kernel(f.reshape((-1,) + tuple(gp.raw_factor_task_kernel.shape)))
-        vv = gp.tf_noise_task_kernel(v.reshape(-1, gp.num_tasks))
+        vv = gp.tf_noise_task_kernel(v.reshape((-1,) + tuple(gp.raw_noise_task_kernel.shape)))
         return torch.einsum("...il,...kl->...ik", F, F) + torch.diag_embed(vv)

@@ -568,6 +568,16 @@ typedef struct fgp_mt_fit_desc {
   double grad_norm, grad_logdet;      /* dL/dnorm_b (1/2), dL/dlogdet (1/2 d_out / numel(logdet)) */
   double logdet_weight, mll_const, eta_minus, eta_plus, step_min, step_max;
   void* work;                         /* fgp_mt_fit_work bytes */
+  /* ABI 16 -- PARAMETER batches (docs/examples/batch_multitask/fgp_lattice.ipynb: scale / lengthscales / noise / task
+   * factor / task noise with batch dimensions broadcast to shape_batch, abstract_gp.py:73-139).  G >= 1 problems
+   * (0 = 1), each with its own B data vectors at y + g B R nmin; problem g's parameters are row prow of each
+   * parameter block, rows[q * G + g] (q = scale, lengthscales, noise, task factor, task noise; device int array;
+   * NULL: every problem row 0) of nrows[q] rows (0 = 1).  raw = [scale rows, lengthscale rows (dl each), noise rows,
+   * task-factor rows (T_all x rank each), task-noise rows (T_all each)].  The loss is the sum over the problems'
+   * MLLs with logdet_weight; a parameter row shared by several problems gets the sum of their gradients. */
+  int G;
+  const int* rows;
+  int nrows[5];
 } fgp_mt_fit_desc;
 
 int fgp_mt_fit_nparams(const fgp_mt_fit_desc* desc, int* n_params);
