@@ -1179,4 +1179,9 @@ class MtGeneralEngine(object):
         f, v = self.split_task(raw_rows)
         F = gp.tf_factor_task_kernel(f.reshape((-1,) + tuple(gp.raw_factor_task_kernel.shape)))
         vv = gp.tf_noise_task_kernel(v.reshape((-1,) + tuple(gp.raw_noise_task_kernel.shape)))
-        return torch.einsum("...il,...kl->...ik", F, F) + torch.diag_embed(vv)
+        FF, V = torch.einsum("...il,...kl->...ik", F, F), torch.diag_embed(vv)
+        # batch dims broadcast right-aligned after the leading history dim
+        nb = max(FF.dim(), V.dim())
+        FF = FF.reshape(FF.shape[:1] + (1,) * (nb - FF.dim()) + FF.shape[1:])
+        V = V.reshape(V.shape[:1] + (1,) * (nb - V.dim()) + V.shape[1:])
+        return FF + V

@@ -65,7 +65,7 @@ def gen(fg, qmcpy, family, d, alpha, seed=7):
         out["shifts"] = shifts.astype(np.int64)
         gp = fg.FastGPDigitalNetB2(seqs, **kw)
     for nm in PNAMES:
-        out["init_" + nm] = _np(getattr(gp, nm))
+        out["init_" + nm] = _np(getattr(gp, nm)).copy()     # the fit steps the parameters in place
     ns = [int(v) for v in 2 ** torch.arange(T + 1, 1, -1)]
     out["ns"] = np.array(ns, dtype=np.int64)
     xs = gp.get_x_next(n=torch.tensor(ns))
@@ -92,7 +92,7 @@ def gen(fg, qmcpy, family, d, alpha, seed=7):
     data = gp.fit(iterations=ITS, store_hists=True, verbose=0, stop_crit_wait_iterations=ITS + 5)
     out["fit_loss_hist"] = _np(data["loss_hist"])
     for nm in PNAMES:
-        out["fit_" + nm] = _np(getattr(gp, nm))
+        out["fit_" + nm] = _np(getattr(gp, nm)).copy()
     xt = torch.rand((12, d), generator=torch.Generator().manual_seed(17))
     out["x_test"] = _np(xt)
     out["fit_pmean"] = _np(gp.post_mean(xt))
