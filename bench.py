@@ -487,6 +487,54 @@ def multitask_configs(F, device, iterations=40):
                     os.environ["FGP_MT_FUSED"] = old
         row["speedup"] = row["generic_s_per_step"] / row["device_s_per_step"]
         out.append(row)
+    out += batch_multitask_configs(F, device, iterations)
+    return out
+
+
+def batch_multitask_configs(F, device, iterations):
+    """The reference's parameter-batched multitask setting (docs/examples/batch_multitask/fgp_lattice.ipynb
+    cells 4-7: d = 6, shape_batch = [2, 3, 4], 5 tasks at n = 2^[6, 5, 4, 3, 2], scale / lengthscales / noise /
+    task factor / task noise batched as in cell 6) and the same at 16x the points: 24 eigen-problems per
+    optimisation step through the device fit (fgp_mt_fit_run, G = 24) and through the generic autograd loop."""
+    d, T, sb = 6, 5, [2, 3, 4]
+    consts = torch.arange(24, device=device, dtype=torch.float64).reshape(sb)
+    out = []
+    for scale in (1, 16):
+        ns = [scale * 2 ** k for k in range(T + 1, 1, -1)]
+        row = {"workload": "docs/examples/batch_multitask: FastGPLattice d=6, 5 tasks, n=%s, shape_batch=%s, "
+                           "batched scale / lengthscales / noise / task kernel" % (ns, sb), "iterations": iterations}
+        for path in ("device", "generic"):
+            old = os.environ.get("FGP_MT_FUSED")
+            os.environ["FGP_MT_FUSED"] = "1" if path == "device" else "0"
+            try:
+                times = []
+                for rep in range(2 if path == "device" else 1):
+                    gp = F.FastGPLattice(d, seed_for_seq=7, num_tasks=T, shape_batch=sb, shape_scale=sb + [1],
+                                         shape_lengthscales=sb[1:] + [d], shape_noise=sb[2:] + [1],
+                                         shape_factor_task_kernel=sb + [T, T], shape_noise_task_kernel=sb[1:] + [T],
+                                         device=device)
+                    xs = gp.get_x_next(n=torch.tensor(ns))
+                    g = torch.Generator(device=device).manual_seed(11)
+                    gp.add_y_next([(consts[..., None, None] * xs[l] ** torch.arange(1, d + 1, device=device)).sum(-1)
+                                   + torch.randn(sb + [xs[l].shape[0]], generator=g, device=device) / (3 + l)
+                                   for l in range(T)])
+                    torch.cuda.synchronize()
+                    t0 = time.perf_counter()
+                    data = gp.fit(iterations=iterations, verbose=0, stop_crit_wait_iterations=iterations + 1,
+                                  store_loss_hist=True)
+                    torch.cuda.synchronize()
+                    times.append((time.perf_counter() - t0) / max(1, int(data["iterations"])))
+                row[path + "_s_per_step"] = min(times)
+                row[path + "_final_loss"] = float(-data["loss_hist"][-1])
+                if path == "device":
+                    row["device_path"] = "general, G=%d (fgp_mt_fit_run)" % 24 if gp._mt_general_ok() else "generic"
+            finally:
+                if old is None:
+                    os.environ.pop("FGP_MT_FUSED", None)
+                else:
+                    os.environ["FGP_MT_FUSED"] = old
+        row["speedup"] = row["generic_s_per_step"] / row["device_s_per_step"]
+        out.append(row)
     return out
 
 

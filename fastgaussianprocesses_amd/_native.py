@@ -163,6 +163,7 @@ _SIGNATURES = {
     "fgp_mt_fit_run": [_P_MTFIT, _c_int, _c_int, _c_int, _c_vp],
     "fgp_handoff_check": [_c_int, ctypes.POINTER(ctypes.c_ulonglong)],
     "fgp_set_persist_poll_max": [_c_i64],
+    "fgp_set_mt_class_kernel": [_c_int],
     "fgp_nll_partials_len": [_P_NLL, _c_pl],
     "fgp_spec_basis": [_c_int, _c_vp, _c_i64, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_i64, _c_vp],
     "fgp_spec_basis_work": [_c_int, _c_int, _c_int, _c_pl],

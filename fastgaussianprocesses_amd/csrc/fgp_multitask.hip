@@ -302,15 +302,18 @@ __global__ __launch_bounds__(kWG) void k_mt_mll_grad(const double2* __restrict__
 }
 
 // ------------------------------------------------------------------------------------------------
-// Device-resident fit of a general multitask GP (ABI 14, fgp_mt_fit_run).  One iteration = four launches:
+// Device-resident fit of a general multitask GP (ABI 14, fgp_mt_fit_run).  One iteration = five launches, each
+// over the G problems of a parameter batch (ABI 16) as its y index:
 //   k_mtg_lams          packed lams from the pair spectra and the current parameters (thread per entry)
 //   k_mtg_factor_grad   per frequency class: structured LDL^H, solves of the B data vectors, selected inverse,
-//                       dL/dlams (thread per class: mt_ldl_class / mt_solve_class / mt_selinv_class /
-//                       mt_grad_class, the generic path's kernels' bodies)
+//   / k_mtg_class       dL/dlams (thread per class: mt_ldl_class / mt_solve_class / mt_selinv_class /
+//                       mt_grad_class, the generic path's kernels' bodies; or a wave per class when they are few)
 //   k_mtg_contract      dL/dlams contracted with dlams/dtheta (thread per entry): block partials of the norm,
 //                       logdet, dL/dnoise, dL/draw_scale, dL/draw_l_m; the per-entry dL/dK_task terms
-//   k_mtg_step          one workgroup: fixed-order reductions, loss history, dL/d(task factor / noise) by
-//                       the chain rule through K_task = F F^T + diag(v), torch.optim.Rprop on every element
+//   k_mtg_reduce        the fixed-order totals of those, a wave per (total, problem)
+//   k_mtg_step          one workgroup: loss history, dL/d(task factor / noise) by the chain rule through
+//                       K_task = F F^T + diag(v), the problems' gradients summed into their parameter rows,
+//                       torch.optim.Rprop on every element
 struct MtFit {
   MtLay lay;
   int family, d, B, T_all, rank, dl, vtask_exp, P;
@@ -328,7 +331,7 @@ struct MtFit {
   int n_params, f_off, v_off;
   // workspace
   double2 *lams, *fac, *zinv, *glp, *z;
-  double *logdet, *dkt, *part;
+  double *logdet, *dkt, *part, *sums;
   int* info;
   int nblk;
 };
@@ -404,12 +407,15 @@ __device__ __forceinline__ double2 mtg_poly(const MtFit& m, int p, int64_t nk, i
 
 template <int D>
 __device__ __forceinline__ void mtg_lpow(const MtFit& m, int g, double* lpow) {
+  double ls[D];
+#pragma unroll
+  for (int j = 0; j < D; ++j) ls[j] = mtg_ls(m, g, j);
 #pragma unroll
   for (int S = 0; S < (1 << D); ++S) {
     double w = 1.0;
 #pragma unroll
     for (int j = 0; j < D; ++j)
-      if ((S >> j) & 1) w *= mtg_ls(m, g, j);
+      if ((S >> j) & 1) w *= ls[j];
     lpow[S] = w;
   }
 }
@@ -447,6 +453,183 @@ __global__ __launch_bounds__(kWG) void k_mtg_factor_grad(MtFit m) {
   mt_selinv_class(m.fac + go + j, lay, m.zinv + go + j);
   const double gn = m.gn;
   mt_grad_class(m.zinv + go + j, m.z + gy, [&](int64_t) { return gn; }, m.gl, m.B, 1, 0, j, lay, m.glp + go + j);
+}
+
+// The same per class with ONE WAVE per (class j, problem g) -- for few classes (G nmin small: the thread per
+// class above is then a single dependent chain of global read-modify-writes, ~0.1 us each).  The class's packed
+// entries (E = L / nmin), its selected inverse and its B vectors live in LDS; the rows of a task form a diagonal
+// block, so every step of the elimination / substitutions / Takahashi recurrence runs over a task's rows (or the
+// entries they update) in parallel.  A value is produced by the same operation sequence as in mt_*_class (the
+// updates of one target in ascending q, the logdet summed in row order), so both kernels agree bit for bit.
+constexpr int kMtcWG = 64;
+constexpr int kMtcMaxLds = 60 * 1024;
+constexpr int64_t kMtcMaxClasses = 8192;         // G nmin above this: the thread per class has the parallelism
+
+__device__ __forceinline__ double2 mtc_zpat(const double2* Z, const int* oe, int l, int pl, int m, int pm) {
+  return l <= m ? Z[oe[l * FGP_MT_MAX_TASKS + m] + pl] : conj2(Z[oe[m * FGP_MT_MAX_TASKS + l] + pm]);
+}
+
+__global__ __launch_bounds__(kMtcWG) void k_mtg_class(MtFit m) {
+  extern __shared__ double2 sm[];
+  __shared__ int oe[FGP_MT_MAX_TASKS * FGP_MT_MAX_TASKS];     // packed offset / nmin of block (k, l)
+  __shared__ int qn[FGP_MT_MAX_TASKS], rs[FGP_MT_MAX_TASKS];
+  __shared__ int bad;
+  const MtLay& lay = m.lay;
+  const int t = threadIdx.x, T = lay.T, R = lay.R, B = m.B;
+  const int64_t nm = lay.nmin, j = blockIdx.x, g = blockIdx.y;
+  const int E = (int)(lay.L / nm);
+  double2* F = sm;
+  double2* Z = sm + E;
+  double2* o = sm + 2 * E;
+  double* lg = reinterpret_cast<double*>(o + B * R);       // log |pivot| of every row
+  double* ip = lg + R;                                      // 1 / pivot of every row
+  constexpr int MT = FGP_MT_MAX_TASKS;
+  for (int u = t; u < T * T; u += kMtcWG) {
+    const int k = u / T, l = u - k * T;
+    oe[k * MT + l] = k <= l ? (int)(lay.off[k * MT + l] / nm) : 0;
+  }
+  for (int k = t; k < T; k += kMtcWG) {
+    qn[k] = (int)(lay.n[k] / nm);
+    rs[k] = lay.rs[k];
+  }
+  if (t == 0) bad = 0;
+  const int64_t go = g * lay.L, rn = (int64_t)R * nm, gy = g * B * rn;
+  for (int e = t; e < E; e += kMtcWG) F[e] = m.lams[go + e * nm + j];
+  for (int u = t; u < B * R; u += kMtcWG) {
+    const int b = u / R, r = u - b * R;
+    o[u] = m.y[gy + b * rn + (int64_t)r * nm + j];
+  }
+  __syncthreads();
+#if defined(FGP_MTC_EXP_STOP) && FGP_MTC_EXP_STOP == 1
+  return;     // timing experiment (tools/build_exp.sh): the load only
+#endif
+  // LDL^H (mt_ldl_class): pivots of task k, the updates of the later tasks' blocks, the couplings scaled
+  for (int k = 0; k < T; ++k) {
+    const int qk = qn[k], dk = oe[k * MT + k];
+    for (int q = t; q < qk; q += kMtcWG) {
+      const double dq = F[dk + q].x;
+      if (!(dq > 0.0)) bad = 1;
+      lg[rs[k] + q] = log(fabs(dq));
+      ip[rs[k] + q] = 1.0 / dq;
+      F[dk + q] = make_double2(dq, 0.0);
+    }
+    __syncthreads();
+    int tot = 0;
+    for (int l = k + 1; l < T; ++l) tot += (T - l) * qn[l];
+    for (int u = t; u < tot; u += kMtcWG) {
+      int l = k + 1, mm = l, rem = u;                  // target (l, mm, p)
+      for (;; ) {
+        if (rem < qn[l]) break;
+        rem -= qn[l];
+        if (++mm == T) mm = ++l;
+      }
+      const int ql = qn[l], p = rem;
+      double2 acc = F[oe[l * MT + mm] + p];
+      for (int q = p; q < qk; q += ql) {
+        const double2 ul = F[oe[k * MT + l] + q] * ip[rs[k] + q];
+        acc -= cmul_cj(ul, F[oe[k * MT + mm] + q]);
+      }
+      F[oe[l * MT + mm] + p] = acc;
+    }
+    __syncthreads();
+    for (int u = t; u < (T - 1 - k) * qk; u += kMtcWG) {
+      const int l = k + 1 + u / qk, q = u % qk;
+      double2* c = F + oe[k * MT + l] + q;
+      *c = *c * ip[rs[k] + q];
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    double ld = 0.0;
+    for (int r = 0; r < R; ++r) ld += lg[r];
+    m.logdet[g * nm + j] = ld;
+    if (bad) m.info[0] = 1;
+  }
+#if defined(FGP_MTC_EXP_STOP) && FGP_MTC_EXP_STOP == 2
+  return;
+#endif
+  // solves (mt_solve_class): w = L^-1 v by task, w /= D, z = L^-H w by task (backwards)
+  for (int k = 0; k < T; ++k) {
+    const int qk = qn[k];
+    int S = 0;
+    for (int l = k + 1; l < T; ++l) S += qn[l];
+    for (int u = t; u < B * S; u += kMtcWG) {
+      const int b = u / S;
+      int l = k + 1, p = u - b * S;
+      while (p >= qn[l]) p -= qn[l++];
+      const int ql = qn[l];
+      double2 acc = o[b * R + rs[l] + p];
+      for (int q = p; q < qk; q += ql) acc -= cmul_cj(F[oe[k * MT + l] + q], o[b * R + rs[k] + q]);
+      o[b * R + rs[l] + p] = acc;
+    }
+    __syncthreads();
+  }
+  for (int u = t; u < B * R; u += kMtcWG) o[u] = o[u] * ip[u % R];
+  __syncthreads();
+  for (int k = T - 1; k >= 0; --k) {
+    const int qk = qn[k];
+    for (int u = t; u < B * qk; u += kMtcWG) {
+      const int b = u / qk, q = u - b * qk;
+      double2 s = o[b * R + rs[k] + q];
+      for (int l = k + 1; l < T; ++l) s -= cmul(F[oe[k * MT + l] + q], o[b * R + rs[l] + q % qn[l]]);
+      o[b * R + rs[k] + q] = s;
+    }
+    __syncthreads();
+  }
+#if defined(FGP_MTC_EXP_STOP) && FGP_MTC_EXP_STOP == 3
+  return;
+#endif
+  // selected inverse (mt_selinv_class), task by task from the last: a row's couplings, then its diagonal
+  for (int k = T - 1; k >= 0; --k) {
+    const int qk = qn[k];
+    for (int q = t; q < qk; q += kMtcWG) {
+      for (int mm = k + 1; mm < T; ++mm) {
+        const int pm = q % qn[mm];
+        double2 s = make_double2(0.0, 0.0);
+        for (int l = k + 1; l < T; ++l) s -= cmul(F[oe[k * MT + l] + q], mtc_zpat(Z, oe, l, q % qn[l], mm, pm));
+        Z[oe[k * MT + mm] + q] = s;
+      }
+      double s = ip[rs[k] + q];
+      for (int l = k + 1; l < T; ++l) {
+        const double2 u = F[oe[k * MT + l] + q], zc = Z[oe[k * MT + l] + q];
+        s -= __builtin_fma(u.x, zc.x, u.y * zc.y);
+      }
+      Z[oe[k * MT + k] + q] = make_double2(s, 0.0);
+    }
+    __syncthreads();
+  }
+#if defined(FGP_MTC_EXP_STOP) && FGP_MTC_EXP_STOP == 4
+  return;
+#endif
+  // dL/dlams (mt_grad_class) and the solutions out
+  for (int k = 0; k < T; ++k)
+    for (int l = k; l < T; ++l)
+      for (int q = t; q < qn[k]; q += kMtcWG) {
+        const int e = oe[k * MT + l] + q, r = rs[k] + q, c = rs[l] + q % qn[l];
+        double2 w = make_double2(0.0, 0.0);
+        for (int b = 0; b < B; ++b) {
+          const double2 p = cmulc(o[b * R + r], o[b * R + c]);
+          w.x = __builtin_fma(m.gn, p.x, w.x);
+          w.y = __builtin_fma(m.gn, p.y, w.y);
+        }
+        const double2 a = Z[e];
+        m.glp[go + e * nm + j] = r == c ? make_double2(__builtin_fma(m.gl, a.x, -w.x), 0.0)
+                                        : make_double2(2.0 * __builtin_fma(m.gl, a.x, -w.x),
+                                                       2.0 * __builtin_fma(m.gl, a.y, -w.y));
+      }
+  for (int u = t; u < B * R; u += kMtcWG) {
+    const int b = u / R, r = u - b * R;
+    m.z[gy + b * rn + (int64_t)r * nm + j] = o[u];
+  }
+}
+
+static int g_mt_class_mode = 0;            // fgp_set_mt_class_kernel
+
+// LDS bytes of k_mtg_class for this layout (0: does not fit)
+static size_t mtc_lds(const MtLay& lay, int B) {
+  const size_t E = (size_t)(lay.L / lay.nmin);
+  const size_t b = (2 * E + (size_t)B * lay.R) * 16 + (size_t)lay.R * 16;
+  return b <= (size_t)kMtcMaxLds ? b : 0;
 }
 
 template <int D>
@@ -496,66 +679,138 @@ __global__ __launch_bounds__(kWG) void k_mtg_contract(MtFit m) {
   }
 }
 
-// fixed-order workgroup sum of v(t) over t < cnt (thread-strided, wave shuffles, waves in order)
-template <typename F>
-__device__ __forceinline__ double mtg_sum(int64_t cnt, F v, double* red) {
-  double s = 0.0;
-  for (int64_t t = threadIdx.x; t < cnt; t += kWG) s += v(t);
-  return block_sum(s, red);
+// the per-problem totals the step needs: sums[g][q] = the workgroup-order sum of block partial q (q < 4 + D) and of
+// dL/dK_task over the entries of pair p (q = 4 + D + p).  One wave per total, reproducing block_sum's order
+// (thread t's strided sum, the wave butterfly, the four waves added in order) so the totals are those of a
+// 256-thread reduction, bit for bit
+template <int D>
+__global__ __launch_bounds__(kWG) void k_mtg_reduce(MtFit m) {
+  const int ln = threadIdx.x & 63, q = (int)blockIdx.x * (kWG / 64) + (threadIdx.x >> 6), g = blockIdx.y;
+  if (q >= 4 + D + m.P) return;
+  const MtLay& lay = m.lay;
+  const double* src;
+  int64_t cnt, stride;
+  if (q < 4 + D) {
+    src = m.part + (int64_t)g * m.nblk * kMtgQ + q;
+    cnt = m.nblk;
+    stride = kMtgQ;
+  } else {
+    int k = 0, l = 0;
+    for (int kk = 0, p = 0; kk < lay.T; ++kk)
+      for (int ll = kk; ll < lay.T; ++ll, ++p)
+        if (p == q - 4 - D) {
+          k = kk;
+          l = ll;
+        }
+    src = m.dkt + (int64_t)g * lay.L + lay.off[k * FGP_MT_MAX_TASKS + l];
+    cnt = lay.n[k];
+    stride = 1;
+  }
+  double tot = 0.0;
+#pragma unroll
+  for (int w = 0; w < kWG / 64; ++w) {
+    double s = 0.0;
+    for (int64_t t = w * 64 + ln; t < cnt; t += kWG) s += src[t * stride];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    tot += s;
+  }
+  if (ln == 0) m.sums[(int64_t)g * (kMtgQ + m.P) + q] = tot;
 }
 
-template <int D>
-__global__ __launch_bounds__(kWG) void k_mtg_step(MtFit m, int iter, int do_update) {
-  __shared__ double red[kWG / 64];
-  __shared__ double tot[kMtgQ];
-  __shared__ double gkt[FGP_MT_MAX_TASKS * (FGP_MT_MAX_TASKS + 1) / 2];
+// one element per thread (the elements' sums are chains of LDS reads: latency, hidden by 16 waves)
+constexpr int kMtgStepWG = 1024;
+
+template <int D, bool STAGE>
+__global__ __launch_bounds__(kMtgStepWG) void k_mtg_step(MtFit m, int iter, int do_update) {
   __shared__ double term[2];
-  extern __shared__ double grad[];                 // [n_params]
-  const int tid = threadIdx.x;
+  // LDS: the gradient [n_params]; with STAGE, copies of the raw parameters [n_params], the problems' totals
+  // [G][NQs] and their rows [5][G] (the element loops below then run on LDS latency, not a chain of global loads)
+  extern __shared__ double grad[];
+  const int tid = threadIdx.x, G = m.G, NQs = kMtgQ + m.P;
   const MtLay& lay = m.lay;
-  for (int q = tid; q < m.n_params; q += kWG) grad[q] = 0.0;
-  if (tid == 0) term[0] = term[1] = 0.0;
-  __syncthreads();
-  // problem by problem (ascending): its fixed-order reductions, its gradient added into its parameter rows
-  for (int g = 0; g < m.G; ++g) {
-    for (int q = 0; q < 4 + D; ++q) {
-      const double s = mtg_sum(m.nblk, [&](int64_t b) { return m.part[((int64_t)g * m.nblk + b) * kMtgQ + q]; }, red);
-      if (tid == 0) tot[q] = s;
-    }
-    for (int k = 0, p = 0; k < lay.T; ++k)
-      for (int l = k; l < lay.T; ++l, ++p) {
-        const int64_t o = (int64_t)g * lay.L + lay.off[k * FGP_MT_MAX_TASKS + l];
-        const double s = mtg_sum(lay.n[k], [&](int64_t i) { return m.dkt[o + i]; }, red);
-        if (tid == 0) gkt[p] = s;
-      }
-    __syncthreads();
-    if (tid == 0) {
-      term[0] += tot[0];
-      term[1] += tot[1];
-      grad[mtg_is(m, g)] += tot[3];
-      if (m.dl > 1) {
-        for (int j = 0; j < m.d; ++j) grad[mtg_il(m, g, j)] += tot[4 + j];
-      } else {
-        double s = 0.0;
-        for (int j = 0; j < m.d; ++j) s += tot[4 + j];
-        grad[mtg_il(m, g, 0)] += s;
-      }
-      grad[mtg_in(m, g)] += mtg_noise(m, g) * tot[2];
-      // K_task[a, b] = sum_r F[a, r] F[b, r] + [a == b] v_a:  dF[c, r] += g_ab (F[b, r] [a == c] + F[a, r] [b == c])
-      const int fo = mtg_if(m, g), vo = mtg_iv(m, g);
-      for (int k = 0, p = 0; k < lay.T; ++k)
-        for (int l = k; l < lay.T; ++l, ++p) {
-          const int a = m.task[k], b = m.task[l];
-          const double gv = gkt[p];
-          for (int r = 0; r < m.rank; ++r) {
-            grad[fo + a * m.rank + r] += gv * m.raw[fo + b * m.rank + r];
-            grad[fo + b * m.rank + r] += gv * m.raw[fo + a * m.rank + r];
-          }
-          if (a == b) grad[vo + a] += m.vtask_exp ? gv * exp(m.raw[vo + a]) : gv;
-        }
-    }
+  double* sraw = grad + m.n_params;
+  double* ssum = sraw + m.n_params;
+  int* srows = reinterpret_cast<int*>(ssum + (int64_t)G * NQs);
+  if constexpr (STAGE) {
+    for (int u = tid; u < m.n_params; u += kMtgStepWG) sraw[u] = m.raw[u];
+    for (int u = tid; u < G * NQs; u += kMtgStepWG) ssum[u] = m.sums[u];
+    if (m.rows)
+      for (int u = tid; u < 5 * G; u += kMtgStepWG) srows[u] = m.rows[u];
     __syncthreads();
   }
+  const double* raw = STAGE ? sraw : m.raw;
+  const double* sums = STAGE ? ssum : m.sums;
+  const int* rw = m.rows ? (STAGE ? srows : m.rows) : nullptr;
+  if (tid == 0) {
+    double t0 = 0.0, t1 = 0.0;
+    for (int g = 0; g < G; ++g) {
+      t0 += sums[(int64_t)g * NQs];
+      t1 += sums[(int64_t)g * NQs + 1];
+    }
+    term[0] = t0;
+    term[1] = t1;
+  }
+  auto row = [&](int q, int g) { return rw ? rw[q * G + g] : 0; };
+  // element by element: the problems' contributions to the element's parameter row in ascending problem order
+  // (pairs ascending within a problem, the (a, .) term of a pair before its (b, .) term) -- the order of a
+  // single-threaded pass over the problems
+#ifdef FGP_MTG_EXP_NOELEM
+  for (int x = tid; x < m.n_params; x += kMtgStepWG) grad[x] = 0.0;   // timing experiment: no element sums
+  if (false)
+#endif
+  for (int x = tid; x < m.n_params; x += kMtgStepWG) {
+    double gs = 0.0;
+    if (x < m.l_off) {
+      for (int g = 0; g < G; ++g)
+        if (row(0, g) == x) gs += sums[(int64_t)g * NQs + 3];
+    } else if (x < m.n_off) {
+      const int rr = (x - m.l_off) / m.dl, j = (x - m.l_off) - rr * m.dl;
+      for (int g = 0; g < G; ++g) {
+        if (row(1, g) != rr) continue;
+        const double* tot = sums + (int64_t)g * NQs;
+        if (m.dl > 1) {
+          gs += tot[4 + j];
+        } else {
+          double s = 0.0;
+          for (int jj = 0; jj < m.d; ++jj) s += tot[4 + jj];
+          gs += s;
+        }
+      }
+    } else if (x < m.f_off) {
+      const double nz = exp(raw[x]);
+      for (int g = 0; g < G; ++g)
+        if (row(2, g) == x - m.n_off) gs += nz * sums[(int64_t)g * NQs + 2];
+    } else if (x < m.v_off) {
+      // K_task[a, b] = sum_r F[a, r] F[b, r] + [a == b] v_a:  dF[c, r] += g_ab (F[b, r] [a == c] + F[a, r] [b == c])
+      const int TR = m.T_all * m.rank, rr = (x - m.f_off) / TR, u = (x - m.f_off) - rr * TR;
+      const int c = u / m.rank, r = u - c * m.rank, fo = m.f_off + rr * TR;
+      for (int g = 0; g < G; ++g) {
+        if (row(3, g) != rr) continue;
+        const double* gkt = sums + (int64_t)g * NQs + 4 + D;
+        for (int k = 0, p = 0; k < lay.T; ++k)
+          for (int l = k; l < lay.T; ++l, ++p) {
+            const int a = m.task[k], b = m.task[l];
+            if (a == c) gs += gkt[p] * raw[fo + b * m.rank + r];
+            if (b == c) gs += gkt[p] * raw[fo + a * m.rank + r];
+          }
+      }
+    } else {
+      const int rr = (x - m.v_off) / m.T_all, c = (x - m.v_off) - rr * m.T_all;
+      const double ev = m.vtask_exp ? exp(raw[x]) : 1.0;
+      for (int g = 0; g < G; ++g) {
+        if (row(4, g) != rr) continue;
+        const double* gkt = sums + (int64_t)g * NQs + 4 + D;
+        for (int k = 0; k < lay.T; ++k)
+          if (m.task[k] == c) {
+            const double gv = gkt[k * lay.T - k * (k - 1) / 2];      // the diagonal pair (k, k)
+            gs += m.vtask_exp ? gv * ev : gv;
+          }
+      }
+    }
+    grad[x] = gs;
+  }
+  __syncthreads();
   if (tid == 0) {
     const double term2 = m.logdet_weight * term[1];
     double* lh = m.loss_hist + (int64_t)iter * 3;
@@ -563,7 +818,7 @@ __global__ __launch_bounds__(kWG) void k_mtg_step(MtFit m, int iter, int do_upda
     lh[1] = term[0];
     lh[2] = term2;
   }
-  for (int q = tid; q < m.n_params; q += kWG) {
+  for (int q = tid; q < m.n_params; q += kMtgStepWG) {
     const double gp = grad[q];
     m.raw_hist[(int64_t)iter * m.n_params + q] = m.raw[q];
     m.grad[q] = gp;
@@ -686,6 +941,7 @@ static int to_mtfit(const fgp_mt_fit_desc* d, MtFit* m, int64_t* work_bytes) {
   const size_t o_ld = off; off += mtg_align(8 * (size_t)(G * m->lay.nmin));
   const size_t o_dkt = off; off += mtg_align(8 * (size_t)(G * L));
   const size_t o_part = off; off += mtg_align(8 * (size_t)(G * m->nblk * kMtgQ));
+  const size_t o_sums = off; off += mtg_align(8 * (size_t)(G * (kMtgQ + m->P)));
   const size_t o_info = off; off += 256;
   if (work_bytes) *work_bytes = (int64_t)off;
   char* w = static_cast<char*>(d->work);
@@ -698,6 +954,7 @@ static int to_mtfit(const fgp_mt_fit_desc* d, MtFit* m, int64_t* work_bytes) {
     m->logdet = reinterpret_cast<double*>(w + o_ld);
     m->dkt = reinterpret_cast<double*>(w + o_dkt);
     m->part = reinterpret_cast<double*>(w + o_part);
+    m->sums = reinterpret_cast<double*>(w + o_sums);
     m->info = reinterpret_cast<int*>(w + o_info);
   }
   return kOk;
@@ -793,6 +1050,12 @@ int fgp_mt_mll_grad(const fgp_mt_layout* layout, const void* zinv, const void* z
 }
 
 
+int fgp_set_mt_class_kernel(int mode) {
+  if (mode < 0 || mode > 2) return set_error(kErrInvalid, "fgp_set_mt_class_kernel: mode %d", mode);
+  g_mt_class_mode = mode;
+  return kOk;
+}
+
 int fgp_mt_fit_nparams(const fgp_mt_fit_desc* desc, int* n_params) {
   MtFit m;
   int rc = to_mtfit(desc, &m, nullptr);
@@ -819,15 +1082,27 @@ int fgp_mt_fit_run(const fgp_mt_fit_desc* desc, int iter0, int iters, int final_
   hipStream_t st = (hipStream_t)stream;
   const dim3 ge((unsigned)((m.lay.L + kWG - 1) / kWG), (unsigned)m.G), gc((unsigned)((m.lay.nmin + kWG - 1) / kWG), (unsigned)m.G);
   const dim3 gb((unsigned)m.nblk, (unsigned)m.G);
-  const size_t shm = sizeof(double) * (size_t)m.n_params;
+  // the step's LDS: the gradient, and copies of the parameters / totals / rows when they fit beside it
+  const size_t shm0 = sizeof(double) * (size_t)m.n_params;
+  const size_t shm1 = shm0 * 2 + sizeof(double) * (size_t)m.G * (kMtgQ + m.P) + 20 * (size_t)m.G;
+  const int stage = shm1 <= 65536;
+  const size_t shm = stage ? shm1 : shm0;
+  // one wave per (class, problem) while the classes are few (and the class fits LDS), else a thread per class
+  const size_t lds = mtc_lds(m.lay, m.B);
+  const bool wave_class = lds > 0 && (g_mt_class_mode == 2 || (g_mt_class_mode == 0 && (int64_t)m.G * m.lay.nmin <= kMtcMaxClasses));
+  const dim3 gw((unsigned)m.lay.nmin, (unsigned)m.G);
   return mtg_with_d(m.d, [&](auto dc) {
     constexpr int D = decltype(dc)::value;
+    const dim3 gr((unsigned)((4 + D + m.P + kWG / 64 - 1) / (kWG / 64)), (unsigned)m.G);
     for (int it = 0; it < iters; ++it) {
       const int upd = !(final_no_update && it == iters - 1);
       k_mtg_lams<D><<<ge, kWG, 0, st>>>(m);
-      k_mtg_factor_grad<<<gc, kWG, 0, st>>>(m);
+      if (wave_class) k_mtg_class<<<gw, kMtcWG, lds, st>>>(m);
+      else k_mtg_factor_grad<<<gc, kWG, 0, st>>>(m);
       k_mtg_contract<D><<<gb, kWG, 0, st>>>(m);
-      k_mtg_step<D><<<1, kWG, shm, st>>>(m, iter0 + it, upd);
+      k_mtg_reduce<D><<<gr, kWG, 0, st>>>(m);
+      if (stage) k_mtg_step<D, true><<<1, kMtgStepWG, shm, st>>>(m, iter0 + it, upd);
+      else k_mtg_step<D, false><<<1, kMtgStepWG, shm, st>>>(m, iter0 + it, upd);
       const int r = check_launch("fgp_mt_fit_run");
       if (r != kOk) return r;
     }

@@ -600,6 +600,11 @@ int fgp_handoff_check(int enable, unsigned long long* out);
  * also report unsupported (0 / an error) when the workgroups would not all be co-resident. */
 int fgp_set_persist_poll_max(long long polls);
 
+/* ABI 16 -- test hook (no reference counterpart): the per-class kernel of fgp_mt_fit_run: 0 automatic (a wave per
+ * frequency class while problems x classes <= 8192 and a class fits 60 KB of LDS, else a thread per class), 1 a
+ * thread per class, 2 a wave per class where it fits.  Both give the same results bit for bit. */
+int fgp_set_mt_class_kernel(int mode);
+
 #ifdef __cplusplus
 }
 #endif

@@ -11,7 +11,7 @@ committed vector and explicit shifts per task; the notebook's lattice GP otherwi
 variant of the same shapes (d = 3, alpha = 2).  Writes tests/golden/batch_mt/*.npz: inputs (generating vector /
 matrices, shifts, every task's observations [2, 3, 4, n_l], the initial raw parameters) and the reference's
 outputs: the MLL and its gradient at the initial parameters, fit(iterations=4) (early stopping off) loss history and
-every fitted raw parameter, post_mean / post_var at 12 test points after the fit.
+every fitted raw parameter, post_mean / post_var at 12 test points and post_cov between 4 and 5 of them after the fit.
 """
 import os
 import sys
@@ -97,6 +97,7 @@ def gen(fg, qmcpy, family, d, alpha, seed=7):
     out["x_test"] = _np(xt)
     out["fit_pmean"] = _np(gp.post_mean(xt))
     out["fit_pvar"] = _np(gp.post_var(xt))
+    out["fit_pcov"] = _np(gp.post_cov(xt[:4], xt[4:9]))
     return out
 
 

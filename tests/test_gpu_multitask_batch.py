@@ -8,7 +8,7 @@ The device-resident fit (fgp_mt_fit_run over G = 24 eigen-problems, ABI 16: ever
 parameters the rows of each parameter block, a row shared by several outputs summing their gradients) and the
 generic autograd loop (FGP_MT_FUSED=0) against the reference's 4-iteration trajectory: loss history 2e-7 relative (the
 multitask golden tolerance), every fitted raw parameter 1e-9 (sign-driven Rprop: the trajectory is the reference's),
-post_mean / post_var after the fit 1e-8 relative / 1e-8 of the largest variance scale.
+post_mean / post_var / post_cov after the fit 1e-8 relative / 1e-8 of the largest variance scale.
 """
 import glob
 import os
@@ -72,6 +72,9 @@ def test_parameter_batched_multitask_fit_matches_reference(name, path, monkeypat
     assert rel_err(gp.post_mean(xt), g["fit_pmean"]) <= 1e-8
     pv = gp.post_var(xt).cpu()
     assert float((pv - torch.from_numpy(g["fit_pvar"])).abs().max()) <= 1e-8 * max(1.0, float(np.abs(g["fit_pvar"]).max()))
+    pc = gp.post_cov(xt[:4], xt[4:9]).cpu()
+    assert tuple(pc.shape) == g["fit_pcov"].shape          # shape_batch + [T, T, 4, 5]
+    assert float((pc - torch.from_numpy(g["fit_pcov"])).abs().max()) <= 1e-8 * max(1.0, float(np.abs(g["fit_pcov"]).max()))
 
 
 @pytest.mark.parametrize("name", NAMES)
@@ -94,3 +97,37 @@ def test_parameter_batched_multitask_loss_and_gradient(name, monkeypatch):
         if "grad_" + nm in g.files:
             ref = torch.from_numpy(g["grad_" + nm]).reshape(-1)
             assert rel_err(gv, ref) <= 2e-7, (nm, gv[:4], ref[:4])
+
+
+def _general_fit_rows(gp, mode, its=6):
+    """fit rows (loss history, raw parameter history) of the general device fit with the per-class kernel forced
+    (fgp_set_mt_class_kernel: 1 thread per class, 2 wave per class)."""
+    from fastgaussianprocesses_amd import _native as N
+    from fastgaussianprocesses_amd.multitask import MtGeneralEngine
+    N.call("fgp_set_mt_class_kernel", mode)
+    try:
+        eng = MtGeneralEngine(gp, 0.1, its + 1)
+        eng.run(0, its + 1, final_no_update=True)
+        torch.cuda.synchronize()
+        return eng.loss_hist[:its + 1].cpu(), eng.raw_hist[:its + 1].cpu()
+    finally:
+        N.call("fgp_set_mt_class_kernel", 0)
+
+
+@pytest.mark.parametrize("name", NAMES + ["mt:" + nm for nm in ("mt_lattice_d1_a2_T3", "mt_net_d2_a2_T3",
+                                                                 "mt_lattice_d2_a2_T2_b2", "deriv_lattice_d2_a2")])
+def test_wave_per_class_kernel_equals_thread_per_class(name, monkeypatch):
+    """k_mtg_class (a wave per frequency class, the class in LDS) against k_mtg_factor_grad (a thread per class,
+    the generic path's bodies): the whole fit trajectory bit for bit, on the parameter batch and on the
+    unbatched multitask fixtures."""
+    monkeypatch.setenv("FGP_MT_GENERAL", "1")
+    if name.startswith("mt:"):
+        from tests.golden_util import load_golden
+        from tests.test_gpu_multitask import product_mt
+        gp = product_mt(load_golden(name[3:]))
+    else:
+        gp = build(np.load(os.path.join(BDIR, name + ".npz")))
+    la, ra = _general_fit_rows(gp, 1)
+    lb, rb = _general_fit_rows(gp, 2)
+    assert torch.isfinite(la).all()
+    assert torch.equal(la, lb) and torch.equal(ra, rb)
