@@ -1757,7 +1757,7 @@ int fgp_nll_partials_len(const fgp_nll_desc* desc, int64_t* len) {
     int cnt;
     spec_counters_offset(a, &off, &cnt);
     *len = std::max<int64_t>(*len, off + cnt + 1);
-    *len = std::max<int64_t>(*len, 2 * (int64_t)a.G * a.nq * a.nb);   // fgp_fit_persist's two partial parities
+    *len = std::max<int64_t>(*len, 3 * (int64_t)a.G * a.nq * a.nb);   // fgp_fit_persist's three partial buffers
   }
   return kOk;
 }

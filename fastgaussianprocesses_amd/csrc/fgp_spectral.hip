@@ -226,6 +226,14 @@ __device__ __forceinline__ SpecCorr spec_corr_load(const Nll& a, int blk, int g0
   return c;
 }
 
+// global (address space 1) views of the partial buffers: the agent-scope accesses of the cross-workgroup hand-offs
+// become global_load / global_store ... sc1 (MI355X_MICROARCH.md: sc1 loads to registers, never flat_)
+typedef __attribute__((address_space(1))) double gdouble;
+__device__ __forceinline__ gdouble* gptr(const double* p) { return (gdouble*)(const_cast<double*>(p)); }
+__device__ __forceinline__ void st_part_sc1(double* p, double v) {
+  __hip_atomic_store(gptr(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int D, bool NET>
 __device__ __forceinline__ void spec_block_partials(const Nll& a, const Hyp& h, int g, int blk, double rootn, double wl,
                                                     const SpecAcc<D>& acc, bool sc1, double* pbase,
@@ -281,7 +289,7 @@ __device__ __forceinline__ void spec_block_partials(const Nll& a, const Hyp& h, 
       if (q8 == 4 + j) f = gsc * h.ls[j];
     double* dst = pbase + ((int64_t)g * a.nq + q8) * a.nb + blk;
     const double val = q8 < 3 ? s8 : s8 * f;
-    if (sc1) __hip_atomic_store(dst, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (sc1) st_part_sc1(dst, val);
     else *dst = val;
   }
   if (lane == 0) {
@@ -289,7 +297,7 @@ __device__ __forceinline__ void spec_block_partials(const Nll& a, const Hyp& h, 
     for (int q = 8; q < NV; ++q) {
       double* dst = pbase + ((int64_t)g * a.nq + q) * a.nb + blk;
       const double val = v[q] * (gsc * h.ls[q - 4]);
-      if (sc1) __hip_atomic_store(dst, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (sc1) st_part_sc1(dst, val);
       else *dst = val;
     }
   }
@@ -383,7 +391,7 @@ __host__ __device__ __forceinline__ RpState spec_state(const Nll& a, int par) {
 
 template <bool SC1>
 __device__ __forceinline__ double ld_part(const double* p) {
-  return SC1 ? __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *p;
+  return SC1 ? __hip_atomic_load(gptr(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *p;
 }
 
 // level 1: sum of problem g's quantity q over the blocks of group grp
@@ -655,16 +663,20 @@ __global__ __launch_bounds__(kWG) void k_spec_finish_step(Nll a, FitFuse fz) {
 // (fgp_fit_persist, ABI 14).  A single GP whose spectra and Y fit the LDS of kPersistMaxW workgroups (C2 / C3 at
 // n = 2^16, the probnum25 paper's n = 2^10): workgroup b loads the blocks [b bpw, (b + 1) bpw) of k_spec_iter's
 // geometry into LDS once, then every Rprop iteration is
-//   block partials (spec_terms / spec_block_partials: k_spec_iter's arithmetic) -> sc1 stores -> grid barrier
-//   (one agent-scope counter, MI355X_MICROARCH.md hand-off row 1; a bounded poll) -> every workgroup sums the
-//   partials in the two-level order of k_spec_reduce_step and applies the same Rprop step to its own LDS copy of
-//   the state -> AbstractGP.fit's early-stopping rule (abstract_gp.py:276-284) evaluated on the same loss values
+//   block partials (spec_terms / spec_block_partials: k_spec_iter's arithmetic) -> agent-scope stores into one of
+//   three rotating buffers whose empty slots hold a sentinel -> every workgroup polls the slots it sums until
+//   none is empty (the grid barrier and the partial read in one round trip; bounded polls) and sums them in the
+//   two-level order of k_spec_reduce_step -> the same Rprop step on each workgroup's own LDS copy of the state
+//   -> AbstractGP.fit's early-stopping rule (abstract_gp.py:276-284) evaluated on the same loss values
 // so the trajectory is the multi-launch fit's bit for bit, without a launch per iteration.  Workgroup 0 writes
 // the histories and the final state; out[0] = the last iteration, out[1] = 1 if a barrier poll gave up.
 constexpr int kPersistMaxW = 64;
 constexpr long long kSpecPollMax = 1ll << 22;     // bounded waits of the persistent k_spec_tile
 constexpr int kPersistLdsMax = 96 * 1024;
 constexpr long long kPersistPollMax = 1ll << 22;
+// an empty partial slot of the single-launch fit (all ones: a NaN payload no arithmetic produces; the buffers are
+// filled with it before the launch)
+constexpr long long kPartEmpty = -1ll;
 
 // workgroup barrier that lets global loads / stores stay in flight across it (__syncthreads() drains them with
 // vmcnt(0)): LDS-DMA chunks, workgroup 0's history stores; the waves' LDS accesses retired (lgkmcnt), the raw
@@ -733,10 +745,15 @@ __global__ __launch_bounds__(kWG) void k_spec_persist(Nll a, Fit f, int iters, d
   __shared__ double lpart[NQ * kSpecGroup];
   const bool single = W == 1 && a.nb <= kSpecGroup;
   for (int it = 0; it <= iters; ++it) {
-    double* pbase = single ? static_cast<double*>(lpart) : a.partials + (it & 1) * psize;
+    // three rotating partial buffers, empty slots holding kPartEmpty: iteration it writes buffer it % 3, and a slot
+    // is emptied again by its writer once every workgroup has read it (see the reset below)
+    double* pbase = single ? static_cast<double*>(lpart) : a.partials + (it % 3) * psize;
     stamp(it, 0);
     Hyp h;
     load_hyp_wave(a, 0, h, st_raw);
+    // the previous iteration's slot resets (and workgroup 0's history stores) retired before this iteration's
+    // partials can be seen
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     for (int t = w; t < bpw; t += kWG / 64) {
       const int blk = blk0 + t;
       if (blk >= a.nb) break;
@@ -753,63 +770,70 @@ __global__ __launch_bounds__(kWG) void k_spec_persist(Nll a, Fit f, int iters, d
       }
       spec_block_partials<D, NET>(a, h, 0, blk, rootn, wl, acc, !single, pbase, corr);
     }
-    // grid barrier it + 1: every wave's sc1 partials retired, one add per workgroup, one bounded poller
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
     stamp(it, 1);
-    if (tid == 0 && !single) {
-      __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned target = (unsigned)(it + 1) * (unsigned)W;
-      long long polls = 0;
-      while (__hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++polls > poll_max) {
-          fail_s = 1;
-          break;
-        }
-      }
-    }
-    __syncthreads();
-    if (fail_s) {
-      // a barrier gave up (every workgroup's next wait then fails too, so no final state is written): the
-      // fit's parameters and every parameter-history row become NaN -- whichever row the caller restores as the
-      // best iterate, the failure shows downstream even when `out` is never read (a hipGraph replay).  Rprop's
-      // prev / step are untouched: with the caller's copy of the entry raw parameters the fit can be re-run.
-      if (tid == 0) out[1] = 1;
-      for (int p = tid; p < np; p += kWG) f.raw[p] = NAN;
-      if (f.raw_hist)
-        for (int64_t e = tid; e < (int64_t)(iters + 1) * f.n_params; e += kWG) f.raw_hist[e] = NAN;
-      return;
-    }
-    stamp(it, 2);
     // level 1 (groups of kSpecGroup blocks, ascending) and level 2 (groups ascending): k_spec_reduce_step's order.
     // One workgroup, one group: the partials are in LDS and level 2 adds the single group sum to 0.0 (exact), so
     // thread q sums its row of lpart directly (typed LDS loads, one barrier) -- the same additions in the same order.
     if (single) {
+      __syncthreads();
+      stamp(it, 2);
       if (tid < NQ) {
         double sq = 0.0;
         for (int b = 0; b < a.nb; ++b) sq += lpart[tid * a.nb + b];
         tot[tid] = sq;
       }
     } else {
-    for (int e = tid; e < NQ * ng; e += kWG) {
-      const int q = e / ng, grp = e - q * ng;
-      const int b0 = grp * kSpecGroup, nbg = min(kSpecGroup, a.nb - b0);
-      const double* pp = pbase + (int64_t)q * a.nb + b0;
-      double tv[kSpecGroup];
+      // the grid barrier IS the read: each (quantity, group) thread polls its group's 32 slots (one round trip
+      // per poll, the loads issued together) until none is empty -- no counter, no separate re-read
+      for (int e = tid; e < NQ * ng; e += kWG) {
+        const int q = e / ng, grp = e - q * ng;
+        const int b0 = grp * kSpecGroup, nbg = min(kSpecGroup, a.nb - b0);
+        const double* pp = pbase + (int64_t)q * a.nb + b0;
+        double tv[kSpecGroup];
+        long long polls = 0;
+        for (;;) {
 #pragma unroll
-      for (int b = 0; b < kSpecGroup; ++b) tv[b] = ld_part<true>(pp + (b < nbg ? b : 0));
-      double sgrp = 0.0;
+          for (int b = 0; b < kSpecGroup; ++b) tv[b] = ld_part<true>(pp + (b < nbg ? b : 0));
+          bool full = true;
 #pragma unroll
-      for (int b = 0; b < kSpecGroup; ++b) sgrp += b < nbg ? tv[b] : 0.0;
-      gsum[q * MAXG + grp] = sgrp;
-    }
-    __syncthreads();
-    if (tid < NQ) {
-      double sq = 0.0;
-      for (int grp = 0; grp < ng; ++grp) sq += gsum[tid * MAXG + grp];
-      tot[tid] = sq;
-    }
+          for (int b = 0; b < kSpecGroup; ++b) full = full && __double_as_longlong(tv[b]) != kPartEmpty;
+          if (full) break;
+          __builtin_amdgcn_s_sleep(1);
+          if (++polls > poll_max) {
+            fail_s = 1;
+            break;
+          }
+        }
+        double sgrp = 0.0;
+#pragma unroll
+        for (int b = 0; b < kSpecGroup; ++b) sgrp += b < nbg ? tv[b] : 0.0;
+        gsum[q * MAXG + grp] = sgrp;
+      }
+      __syncthreads();
+      stamp(it, 2);
+      if (fail_s) {
+        // a wait gave up (every workgroup's next wait then fails too, so no final state is written): the fit's
+        // parameters and every parameter-history row become NaN -- whichever row the caller restores as the best
+        // iterate, the failure shows downstream even when `out` is never read (a hipGraph replay).  Rprop's prev /
+        // step are untouched: with the caller's copy of the entry raw parameters the fit can be re-run.
+        if (tid == 0) out[1] = 1;
+        for (int p = tid; p < np; p += kWG) f.raw[p] = NAN;
+        if (f.raw_hist)
+          for (int64_t e = tid; e < (int64_t)(iters + 1) * f.n_params; e += kWG) f.raw_hist[e] = NAN;
+        return;
+      }
+      // every workgroup has read iteration it - 1's buffer ((it + 2) % 3: each wrote its iteration-it partials after
+      // its own reads of it - 1 returned), so this workgroup empties its slots there for iteration it + 2
+      double* pnext = a.partials + ((it + 2) % 3) * psize;
+      for (int e = tid; e < NQ * bpw; e += kWG) {
+        const int q = e / bpw, blk = blk0 + (e - q * bpw);
+        if (blk < a.nb) st_part_sc1(pnext + (int64_t)q * a.nb + blk, __longlong_as_double(kPartEmpty));
+      }
+      if (tid < NQ) {
+        double sq = 0.0;
+        for (int grp = 0; grp < ng; ++grp) sq += gsum[tid * MAXG + grp];
+        tot[tid] = sq;
+      }
     }
     __syncthreads();
     stamp(it, 3);
@@ -2097,8 +2121,11 @@ int launch_spec_persist(const Nll& a, const Fit& f, int iters, double logtol, in
   size_t shm;
   int rc = spec_persist_geometry(a, &W, &bpw, &shm);
   if (rc != kOk) return rc;
-  if (hipMemsetAsync(counter, 0, sizeof(unsigned), st) != hipSuccess || hipMemsetAsync(out, 0, 2 * sizeof(int), st) != hipSuccess)
-    return set_error(kErrHip, "fgp_fit_persist: counter reset failed");
+  // the three partial buffers empty (kPartEmpty: all bytes 0xff), the control word cleared
+  (void)counter;
+  if (hipMemsetAsync(a.partials, 0xff, 3 * sizeof(double) * (size_t)a.nq * (size_t)a.nb, st) != hipSuccess ||
+      hipMemsetAsync(out, 0, 2 * sizeof(int), st) != hipSuccess)
+    return set_error(kErrHip, "fgp_fit_persist: workspace reset failed");
   return with_spec_d(a.d, [&](auto dc) {
     constexpr int D = decltype(dc)::value;
     auto go = [&](auto kern) {
