@@ -333,6 +333,8 @@ def secondary_configs(F, args, device, rank=0, world=1, collect=None):
                 torch.cuda.synchronize()
                 samples.append([ev[i].elapsed_time(ev[i + 1]) for i in range(4)])
             phases = {k: sorted(s[i] for s in samples)[1] for i, k in enumerate(keys)}
+            if graph is not None:
+                ginfo["phases_ms"] = graph_phases(F, sg, args, xm, xv, device)
         total = getattr(sg, "total", 1)
         roof_pm = None
         if name.startswith("C5 per-output"):
@@ -953,6 +955,45 @@ def _clear_capture_error():
             return
         except Exception:
             continue
+
+
+def graph_phases(F, sg, args, xm, xv, device, reps=5):
+    """Device time of each phase of a single-GP / multi-output step REPLAYED from a hipGraph: the step captured
+    with a device-clock stamp kernel (fgp_clock_stamp) between its phases (ytilde+fit, coeffs, post_mean,
+    post_var), replayed `reps` times, the median of the stamp differences per phase (ms).  The eager
+    `phases_ms` also hold the host's enqueue time; these do not (each stamp adds one ~2 us launch).  None when
+    the capture fails."""
+    st = torch.zeros(5, dtype=torch.int64, device=device)
+    call = F._native.call
+
+    def stamp(i):
+        call("fgp_clock_stamp", st[i:i + 1].data_ptr(), torch.cuda.current_stream().cuda_stream)
+
+    def fn():
+        sg.reset()
+        stamp(0)
+        sg.gp.fit(iterations=args.fit_iters, stop_crit_wait_iterations=args.fit_iters + 1, verbose=0)
+        stamp(1)
+        with torch.no_grad():
+            sg.gp.coeffs
+        stamp(2)
+        pm = sg.gp.post_mean(xm)
+        stamp(3)
+        pv = sg.gp.post_var(xv)
+        stamp(4)
+        return pm, pv
+    g, info = capture_fn(fn)
+    if g is None:
+        return None
+    khz = wall_clock_khz(F, torch.device(device))
+    rows = []
+    for _ in range(reps):
+        g.replay()
+        torch.cuda.synchronize()
+        t = st.cpu().tolist()
+        rows.append([(t[i + 1] - t[i]) / khz for i in range(4)])
+    keys = ("ytilde+fit", "coeffs", "post_mean", "post_var")
+    return {k: sorted(r[i] for r in rows)[reps // 2] for i, k in enumerate(keys)}
 
 
 def capture_fn(fn):

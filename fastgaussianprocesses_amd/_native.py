@@ -113,6 +113,7 @@ _P_PRED = ctypes.POINTER(PredDesc)
 _SIGNATURES = {
     "fgp_init": [_c_vp],
     "fgp_wall_clock_khz": [_c_int, _c_pi],
+    "fgp_clock_stamp": [_c_vp, _c_vp],
     "fgp_fftbr": [_c_vp, _c_i64, _c_int, _c_vp, _c_i64, _c_int, _c_int, _c_vp],
     "fgp_ifftbr": [_c_vp, _c_i64, _c_vp, _c_int, _c_vp, _c_i64, _c_int, _c_int, _c_vp],
     "fgp_fwht": [_c_vp, _c_i64, _c_vp, _c_i64, _c_int, _c_int, _c_vp],

@@ -66,6 +66,10 @@ const Tables* get_tables(hipStream_t stream) {
 
 }  // namespace fgp
 
+namespace fgp {
+__global__ void k_clock_stamp(unsigned long long* dst) { *dst = (unsigned long long)wall_clock64(); }
+}  // namespace fgp
+
 extern "C" {
 
 const char* fgp_last_error(void) { return fgp::g_err; }
@@ -77,6 +81,12 @@ int fgp_wall_clock_khz(int device, int* khz) {
   if (hipDeviceGetAttribute(khz, hipDeviceAttributeWallClockRate, device) != hipSuccess)
     return fgp::set_error(fgp::kErrHip, "fgp_wall_clock_khz: hipDeviceGetAttribute failed");
   return fgp::kOk;
+}
+
+int fgp_clock_stamp(unsigned long long* dst, void* stream) {
+  if (!dst) return fgp::set_error(fgp::kErrInvalid, "fgp_clock_stamp: null destination");
+  fgp::k_clock_stamp<<<1, 1, 0, (hipStream_t)stream>>>(dst);
+  return fgp::check_launch("k_clock_stamp");
 }
 
 int fgp_init(void* stream) {

@@ -40,6 +40,10 @@ const char* fgp_last_error(void);
 int fgp_init(void* stream);
 /* Frequency (kHz) of the device wall clock that fgp_nll_desc.stamps records (hipDeviceAttributeWallClockRate). */
 int fgp_wall_clock_khz(int device, int* khz);
+/* ABI 16 -- measurement hook (no reference counterpart): one single-lane kernel on `stream` that stores the device
+ * wall clock (fgp_wall_clock_khz ticks) into *dst when it runs; placed between the launches of a hipGraph capture,
+ * the differences of such stamps are the replayed phases' device time. */
+int fgp_clock_stamp(unsigned long long* dst, void* stream);
 
 /* Orthonormal DFT of bit-reversed-order input along the last axis:
  *   out[b, k] = n^-1/2 * sum_i in[b, brev_m(i)] exp(-2 pi i k i / n),  n = 2^log2n, 0 <= log2n <= 24.

@@ -1,5 +1,6 @@
 """cProfile of one eager C2 / C3 fit (bench.SingleGP, 50 iterations): where the host time of ytilde+fit goes."""
 import cProfile
+import os
 import pstats
 import sys
 
@@ -22,5 +23,8 @@ pr.enable()
 sg.gp.fit(iterations=50, stop_crit_wait_iterations=51, verbose=0)
 pr.disable()
 torch.cuda.synchronize()
-pstats.Stats(pr).sort_stats("cumulative").print_stats(45)
-pstats.Stats(pr).sort_stats("tottime").print_stats(25)
+st = pstats.Stats(pr)
+rows = sorted(st.stats.items(), key=lambda kv: -kv[1][3])
+print("cumulative us  tottime us  calls  function")
+for (fn, line, name), (cc, nc, tt, ct, _) in rows[:60]:
+    print("%12.1f %11.1f %6d  %s:%d(%s)" % (ct * 1e6, tt * 1e6, nc, os.path.basename(fn), line, name))
