@@ -86,7 +86,7 @@ class MtLayout(ctypes.Structure):
 
 
 class MtFitDesc(ctypes.Structure):
-    """Mirror of fgp_mt_fit_desc (include/fgp_hip.h, ABI 14; parameter batches ABI 16)."""
+    """Mirror of fgp_mt_fit_desc (include/fgp_hip.h, ABI 14; parameter batches and the adaptive nugget ABI 16)."""
     _fields_ = [
         ("family", _c_int), ("d", _c_int), ("B", _c_int),
         ("layout", MtLayout), ("task", _c_int * 16),
@@ -100,6 +100,7 @@ class MtFitDesc(ctypes.Structure):
         ("step_min", _c_dbl), ("step_max", _c_dbl),
         ("work", _c_vp),
         ("G", _c_int), ("rows", _c_vp), ("nrows", _c_int * 5),
+        ("nugget_coef", _c_vp), ("nugget_ref", _c_int),
     ]
 
 

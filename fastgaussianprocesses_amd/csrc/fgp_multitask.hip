@@ -333,6 +333,8 @@ struct MtFit {
   double2 *lams, *fac, *zinv, *glp, *z;
   double *logdet, *dkt, *part, *sums;
   int* info;
+  const double2* nug_coef;        // adaptive nugget (ABI 16): [T][2^d] sqrt(n_k) sum_i Phi^{kk}_S[i], or NULL
+  int nug_ref;
   int nblk;
 };
 
@@ -420,6 +422,48 @@ __device__ __forceinline__ void mtg_lpow(const MtFit& m, int g, double* lpow) {
   }
 }
 
+// The adaptive nugget's ratio of sorted task k (util.py:286-290): r = |A_k| / |A_ref| with A_k = sqrt(n_k) sum_S l^S c_kS
+// (the trace of the block's sqrt(n_k) lam over scale), and with DER dr[j] = l_j dr/dl_j (log-lengthscale derivative:
+// l_j dA/dl_j = sum_{S containing j} l^S c_S).
+template <int D, bool DER>
+__device__ __forceinline__ double mtg_nug_ratio(const MtFit& m, int k, const double* lpow, double* dr) {
+  constexpr int NS = 1 << D;
+  double2 A[2] = {make_double2(0.0, 0.0), make_double2(0.0, 0.0)};
+  double2 Aj[2][DER ? D : 1];
+  const int kk[2] = {k, m.nug_ref};
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+#pragma unroll
+    for (int j = 0; j < (DER ? D : 1); ++j) Aj[u][j] = make_double2(0.0, 0.0);
+    const double2* c = m.nug_coef + (int64_t)kk[u] * NS;
+#pragma unroll
+    for (int S = 0; S < NS; ++S) {
+      const double2 cs = c[S];
+      A[u].x = __builtin_fma(lpow[S], cs.x, A[u].x);
+      A[u].y = __builtin_fma(lpow[S], cs.y, A[u].y);
+      if constexpr (DER) {
+#pragma unroll
+        for (int j = 0; j < D; ++j)
+          if ((S >> j) & 1) {
+            Aj[u][j].x = __builtin_fma(lpow[S], cs.x, Aj[u][j].x);
+            Aj[u][j].y = __builtin_fma(lpow[S], cs.y, Aj[u][j].y);
+          }
+      }
+    }
+  }
+  const double a2 = __builtin_fma(A[0].x, A[0].x, A[0].y * A[0].y), b2 = __builtin_fma(A[1].x, A[1].x, A[1].y * A[1].y);
+  const double r = sqrt(a2) / sqrt(b2);
+  if constexpr (DER) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      const double ga = __builtin_fma(A[0].x, Aj[0][j].x, A[0].y * Aj[0][j].y) / a2;
+      const double gb = __builtin_fma(A[1].x, Aj[1][j].x, A[1].y * Aj[1][j].y) / b2;
+      dr[j] = r * (ga - gb);
+    }
+  }
+  return r;
+}
+
 // (problem g = the launch's y index: entry / class / block-row g of a parameter batch; 0 when unbatched)
 template <int D>
 __global__ __launch_bounds__(kWG) void k_mtg_lams(MtFit m) {
@@ -435,7 +479,7 @@ __global__ __launch_bounds__(kWG) void k_mtg_lams(MtFit m) {
   const double sc = mtg_scale(m, g), rn = sqrt((double)m.lay.n[l]);
   // lams = K_task (sqrt(n_l) lam + noise [k == l]),  lam = scale P  (util.py:284-298)
   double2 v = make_double2(rn * (sc * P.x), rn * (sc * P.y));
-  if (k == l) v.x += mtg_noise(m, g);
+  if (k == l) v.x += m.nug_coef ? mtg_noise(m, g) * mtg_nug_ratio<D, false>(m, k, lpow, nullptr) : mtg_noise(m, g);
   const double kt = mtg_kt(m, g, m.task[k], m.task[l]);
   m.lams[(int64_t)g * m.lay.L + e] = make_double2(v.x * kt, v.y * kt);
 }
@@ -660,8 +704,19 @@ __global__ __launch_bounds__(kWG) void k_mtg_contract(MtFit m) {
     for (int j = 0; j < D; ++j) acc[4 + j] = __builtin_fma(f, __builtin_fma(c.x, dp[j].x, c.y * dp[j].y), acc[4 + j]);
     double bx = rn * (sc * P.x), by = rn * (sc * P.y);
     if (k == l) {
-      bx += mtg_noise(m, g);
-      acc[2] = __builtin_fma(kt, c.x, acc[2]);                                         // dnoise / noise
+      if (m.nug_coef) {
+        // adaptive nugget noise r_k: d/dnoise = r_k, d/draw_l_j = noise l_j dr_k/dl_j (on the diagonal entries)
+        double dr[D];
+        const double r = mtg_nug_ratio<D, true>(m, k, lpow, dr);
+        const double nz = mtg_noise(m, g);
+        bx += nz * r;
+        acc[2] = __builtin_fma(kt * r, c.x, acc[2]);                                   // dnoise / noise
+#pragma unroll
+        for (int j = 0; j < D; ++j) acc[4 + j] = __builtin_fma(kt * c.x, nz * dr[j], acc[4 + j]);
+      } else {
+        bx += mtg_noise(m, g);
+        acc[2] = __builtin_fma(kt, c.x, acc[2]);                                       // dnoise / noise
+      }
     }
     m.dkt[go + e] = __builtin_fma(c.x, bx, c.y * by);                                  // dL/dK_task of entry e
   }
@@ -915,6 +970,10 @@ static int to_mtfit(const fgp_mt_fit_desc* d, MtFit* m, int64_t* work_bytes) {
   m->step_min = d->step_min;
   m->step_max = d->step_max;
   // problems of a parameter batch (ABI 16; G = 0: 1) and the row counts of the parameter blocks
+  m->nug_coef = static_cast<const double2*>(d->nugget_coef);
+  m->nug_ref = d->nugget_ref;
+  if (m->nug_coef && (m->nug_ref < 0 || m->nug_ref >= m->lay.T))
+    return set_error(kErrInvalid, "fgp_mt_fit: nugget_ref = %d", m->nug_ref);
   m->G = d->G > 0 ? d->G : 1;
   if (m->G > 65535) return set_error(kErrUnsupported, "fgp_mt_fit: G = %d problems > 65535", m->G);
   m->rows = d->rows;

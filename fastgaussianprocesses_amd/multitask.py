@@ -387,11 +387,12 @@ class MultiTaskFastGP(AbstractFastGP):
         task (util.py:273-323), a data batch sharing the hyper-parameters or (ABI 16) parameter batches broadcast
         over shape_batch (every output its own eigen-problem, at most 4096): at most 16 active tasks, d <= 6, exp
         transforms for scale / lengthscales / noise, the identity for the task factor and exp or the identity for
-        the task noise (one per task), no adaptive nugget, pair spectra within MT_SPECTRA_CAP bytes."""
+        the task noise (one per task), the plain or (ABI 16) the adaptive nugget, pair spectra within MT_SPECTRA_CAP
+        bytes."""
         if os.environ.get("FGP_MT_FUSED", "1")[:1] == "0":
             return False
         lo_ns = [v for v in self._ns if v > 0]
-        if not lo_ns or self.d > 6 or len(lo_ns) > N.MT_MAX_TASKS or self.adaptive_nugget:
+        if not lo_ns or self.d > 6 or len(lo_ns) > N.MT_MAX_TASKS:
             return False
         if any(self._tfs[k][1] is not _exp for k in ("scale", "lengthscales", "noise")):
             return False
@@ -1131,6 +1132,20 @@ class MtGeneralEngine(object):
         desc.grad_logdet = 0.5 * w
         desc.logdet_weight = w
         desc.mll_const = float(mll_constant(d_out, sum(gp._ns)))
+        # adaptive nugget (util.py:286-290): sorted task k's trace coefficients sqrt(n_k) sum_i Phi^{kk}_S[i] and the
+        # sorted position of task 0 (as _lams_blocks)
+        self.nug = None
+        if gp.adaptive_nugget:
+            NS = 1 << d
+            rows_c = []
+            for k in range(lo.T):
+                p = k * lo.T - k * (k - 1) // 2
+                nk = lo.nsrt[k]
+                blk = self.spec[offs[p]:offs[p] + NS * nk].reshape(NS, nk)
+                rows_c.append(blk.sum(-1) * math.sqrt(nk))
+            self.nug = torch.stack(rows_c).to(torch.complex128).contiguous()
+            desc.nugget_coef = self.nug.data_ptr()
+            desc.nugget_ref = lo.active.index(0) if 0 in lo.active else 0
         desc.eta_minus, desc.eta_plus = RPROP_ETAS
         desc.step_min, desc.step_max = RPROP_STEPS
         wb = ctypes.c_int64(0)

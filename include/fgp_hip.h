@@ -582,6 +582,13 @@ typedef struct fgp_mt_fit_desc {
   int G;
   const int* rows;
   int nrows[5];
+  /* ABI 16 -- the ADAPTIVE nugget (adaptive_nugget=True, util.py:286-290): sorted task k's diagonal block gets
+   * noise |tr_kk / tr_ref| instead of noise, tr_kk = sum_i sqrt(n_k) lam_kk[i] = scale sqrt(n_k) sum_S l^S c_kS with
+   * nugget_coef[k][S] = sum_i Phi^{kk}_S[i] (complex128 [T][2^d], the pair spectra's sums; NULL: the plain nugget)
+   * and ref = the sorted position of task 0 (nugget_ref) -- its gradient w.r.t. the noise and the lengthscales
+   * included. */
+  const void* nugget_coef;
+  int nugget_ref;
 } fgp_mt_fit_desc;
 
 int fgp_mt_fit_nparams(const fgp_mt_fit_desc* desc, int* n_params);

@@ -4,7 +4,9 @@ util.py:286-290 -- lams[l, l] += noise |tr_ll / tr_00|) against the REAL referen
 
 One task: the ratio is tr_00 / tr_00 = 1 exactly, so the device-resident spectral fit (the plain nugget) runs; the
 test checks that it does and matches the reference.  Multitask (T = 2, the learned task kernel): the ratio
-|tr_11 / tr_00| scales the second task's nugget (generic path).
+|tr_11 / tr_00| scales the second task's nugget -- through the device-resident general multitask fit
+(fgp_mt_fit_desc.nugget_coef, ABI 16: the ratio from the pair spectra's sums, its noise and lengthscale
+derivatives in closed form) and through the generic autograd loop (FGP_MT_FUSED=0).
 Tolerances as the golden fits (tests/test_gpu_gp.py): loss history 2e-7 relative, parameters 1e-10, post_mean
 1e-8 relative, post_var 1e-8 K(x, x).
 """
@@ -51,22 +53,36 @@ def build(g):
     return gp
 
 
-@pytest.mark.parametrize("name", NAMES)
-def test_adaptive_nugget_fit_matches_reference(name, monkeypatch):
-    from fastgaussianprocesses_amd import fit_engine
-    g = np.load(os.path.join(ADIR, name + ".npz"))
+def _spy(monkeypatch):
+    """Count the device engines the fits build (FusedMLL: single task; MtGeneralEngine: multitask)."""
+    from fastgaussianprocesses_amd import fit_engine, multitask
     engines = []
-    orig = fit_engine.FusedMLL.__init__
+    for cls in (fit_engine.FusedMLL, multitask.MtGeneralEngine):
+        orig = cls.__init__
 
-    def init(self, *a, **k):
-        engines.append(1)
-        return orig(self, *a, **k)
-    monkeypatch.setattr(fit_engine.FusedMLL, "__init__", init)
+        def init(self, *a, _orig=orig, **k):
+            engines.append(type(self).__name__)
+            return _orig(self, *a, **k)
+        monkeypatch.setattr(cls, "__init__", init)
+    return engines
+
+
+@pytest.mark.parametrize("path", ["device", "generic"])
+@pytest.mark.parametrize("name", NAMES)
+def test_adaptive_nugget_fit_matches_reference(name, path, monkeypatch):
+    g = np.load(os.path.join(ADIR, name + ".npz"))
+    T = len(g["ns"])
+    if path == "generic" and T == 1:
+        pytest.skip("one task: the plain nugget (device fit) -- no separate generic case")
+    monkeypatch.setenv("FGP_MT_FUSED", "1" if path == "device" else "0")
+    engines = _spy(monkeypatch)
     gp = build(g)
     its = len(g["fit_loss_hist"]) - 1
     data = gp.fit(iterations=its, store_hists=True, verbose=0, stop_crit_wait_iterations=its + 5)
-    if len(g["ns"]) == 1:
-        assert engines, "a single-task adaptive-nugget fit runs the device-resident fit"
+    if path == "device":
+        assert engines == (["FusedMLL"] if T == 1 else ["MtGeneralEngine"]), engines
+    else:
+        assert not engines, engines
     assert rel_err(data["loss_hist"], g["fit_loss_hist"]) <= 2e-7
     assert rel_err(gp.raw_lengthscales, g["fit_raw_lengthscales"]) <= 1e-10
     assert rel_err(data["lengthscales_hist"], g["fit_lengthscales_hist"]) <= 1e-10
@@ -76,3 +92,39 @@ def test_adaptive_nugget_fit_matches_reference(name, monkeypatch):
     pv = gp.post_var(xt).cpu()
     kxx = float(np.abs(g["fit_pvar"]).max()) + float(torch.exp(gp.raw_scale.detach()).max())
     assert float((pv - torch.from_numpy(g["fit_pvar"])).abs().max()) <= 1e-8 * kxx
+
+
+@pytest.mark.parametrize("family", ["lattice", "net"])
+def test_multitask_adaptive_nugget_device_equals_generic(family, monkeypatch):
+    """Three tasks of unequal n (the reference's multitask example sizes [64, 8, 256]), the task kernel learned, the
+    adaptive nugget: the device fit (its first loss against a one-iteration MtGeneralEngine evaluation) and the
+    generic autograd loop, 8 iterations each: loss histories 5e-7 relative, lengthscales / task factor / noise
+    1e-9 (sign-driven Rprop)."""
+    from fastgaussianprocesses_amd.multitask import MtGeneralEngine
+    d, T, ns = 2, 3, [64, 8, 256]
+
+    def make():
+        if family == "lattice":
+            gp = F.FastGPLattice(d, seed_for_seq=5, num_tasks=T, adaptive_nugget=True, noise=1e-4, device=DEV)
+        else:
+            gp = F.FastGPDigitalNetB2(d, seed_for_seq=5, num_tasks=T, adaptive_nugget=True, noise=1e-4, device=DEV)
+        xs = gp.get_x_next(n=torch.tensor(ns))
+        gp.add_y_next([torch.sin(3 * xs[l]).sum(1) * (1 + l) + torch.cos(7 * xs[l][:, 0]) for l in range(T)])
+        return gp
+    gp = make()
+    assert gp._mt_general_ok()
+    eng = MtGeneralEngine(gp, 0.1, 2)
+    eng.run(0, 1, final_no_update=True)
+    torch.cuda.synchronize()
+    loss = float(eng.loss_hist[0, 0, 0])
+    out = {}
+    for path in ("device", "generic"):
+        monkeypatch.setenv("FGP_MT_FUSED", "1" if path == "device" else "0")
+        gpp = make()
+        data = gpp.fit(iterations=8, store_hists=True, verbose=0, stop_crit_wait_iterations=20)
+        out[path] = (data["loss_hist"], gpp.raw_lengthscales.detach().cpu().clone(),
+                     gpp.raw_factor_task_kernel.detach().cpu().clone(), gpp.raw_noise.detach().cpu().clone())
+    (la, sa, fa, na), (lb, sb, fb, nb) = out["device"], out["generic"]
+    assert abs(float(-la[0]) - loss) <= 1e-12 * abs(loss)
+    assert rel_err(la, lb) <= 5e-7, (la, lb)
+    assert rel_err(sa, sb) <= 1e-9 and rel_err(fa, fb) <= 1e-9 and rel_err(na, nb) <= 1e-9
