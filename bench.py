@@ -282,8 +282,8 @@ def secondary_configs(F, args, device, rank=0, world=1, collect=None):
                   % (B, B, B, ", replicas over %d ranks" % world if world > 1 else ""),
                   lambda: MultiOutputGP(F, 18, 3, B, device, shard=sh, per_output=True), 3))
     if world == 1:
-        cases.append(("C5 mixed: FastGPLattice n=2^18 d=3 x %d outputs, fp32 observations + complex64 "
-                      "ytilde for the MLL, fp64 eigenvalues / coefficients / posteriors" % B,
+        cases.append(("C5 mixed: FastGPLattice n=2^18 d=3 x %d outputs, fp32 observations widened on load into "
+                      "one fp64 half-spectrum transform (Y and coefficients), fp64 eigenvalues / posteriors" % B,
                       lambda: MultiOutputGP(F, 18, 3, B, device, torch.float32), 3))
     out = []
     for name, make, d in cases:

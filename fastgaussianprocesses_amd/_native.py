@@ -157,6 +157,7 @@ _SIGNATURES = {
     "fgp_mt_selinv": [_P_MT, _c_vp, _c_i64, _c_vp, _c_vp],
     "fgp_mt_mll_grad": [_P_MT, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_i64, _c_vp, _c_vp],
     "fgp_fftbr_real_half": [_c_vp, _c_i64, _c_vp, _c_i64, _c_vp, _c_i64, _c_int, _c_vp],
+    "fgp_fftbr_real_half_f32": [_c_vp, _c_i64, _c_vp, _c_i64, _c_vp, _c_i64, _c_int, _c_vp],
     "fgp_sum_sq_half": [_c_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp],
     "fgp_fit_persist_ok": [_P_NLL, _c_pi],
     "fgp_fit_persist": [_P_NLL, _P_FIT, _c_int, _c_dbl, _c_int, _c_vp, _c_vp],

@@ -487,8 +487,9 @@ __global__ __launch_bounds__(kWG) void k_fwd_rows_r2c(Nll a, const double2* __re
 }
 
 // The same row pass on a REAL input array (fgp_fftbr_real): x[:n/2] + i x[n/2:] of problem g read as
-// 16-byte pairs instead of generated k1.
-__global__ __launch_bounds__(kWG) void k_fwd_rows_r2c_in(const double* __restrict__ in, int64_t in_stride, int log2n,
+// 16-byte pairs instead of generated k1 (T = float: fp32 rows widened exactly on load, fgp_fftbr_real_half_f32).
+template <typename T>
+__global__ __launch_bounds__(kWG) void k_fwd_rows_r2c_in(const T* __restrict__ in, int64_t in_stride, int log2n,
                                                          double2* __restrict__ work, const double2* __restrict__ tw,
                                                          const double2* __restrict__ twm) {
   constexpr int P2 = 12, N2 = 1 << P2;
@@ -500,15 +501,27 @@ __global__ __launch_bounds__(kWG) void k_fwd_rows_r2c_in(const double* __restric
   const int64_t g = blockIdx.x / tiles;
   const int row0 = (int)(blockIdx.x % tiles);
   const int tid = threadIdx.x;
-  const double* x = in + g * in_stride + (int64_t)row0 * N2 + 16 * tid;
+  const T* x = in + g * in_stride + (int64_t)row0 * N2 + 16 * tid;
   double2 v[16];
   double2 sum = make_double2(0.0, 0.0);
+  if constexpr (sizeof(T) == 8) {
 #pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    const double2 lo = *reinterpret_cast<const double2*>(x + 2 * u);
-    const double2 hi = *reinterpret_cast<const double2*>(x + nt + 2 * u);
-    v[2 * u] = make_double2(lo.x, hi.x);
-    v[2 * u + 1] = make_double2(lo.y, hi.y);
+    for (int u = 0; u < 8; ++u) {
+      const double2 lo = *reinterpret_cast<const double2*>(x + 2 * u);
+      const double2 hi = *reinterpret_cast<const double2*>(x + nt + 2 * u);
+      v[2 * u] = make_double2(lo.x, hi.x);
+      v[2 * u + 1] = make_double2(lo.y, hi.y);
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float4 lo = *reinterpret_cast<const float4*>(x + 4 * u);
+      const float4 hi = *reinterpret_cast<const float4*>(x + nt + 4 * u);
+      v[4 * u] = make_double2((double)lo.x, (double)hi.x);
+      v[4 * u + 1] = make_double2((double)lo.y, (double)hi.y);
+      v[4 * u + 2] = make_double2((double)lo.z, (double)hi.z);
+      v[4 * u + 3] = make_double2((double)lo.w, (double)hi.w);
+    }
   }
 #pragma unroll
   for (int t = 0; t < 16; ++t) sum += v[t];
@@ -1776,8 +1789,11 @@ int fgp_nll_bwd(const fgp_nll_desc* desc, void* stream) {
   return nll_bwd(a, (hipStream_t)stream, desc->family == FGP_FAMILY_LATTICE);
 }
 
-static int fftbr_real_any(const double* in, int64_t in_batch_stride, void* out, int64_t out_stride, bool half,
+extern "C++" {
+template <typename T>
+static int fftbr_real_any(const T* in, int64_t in_batch_stride, void* out, int64_t out_stride, bool half,
                           void* work, int64_t batch, int log2n, void* stream);
+}
 
 int fgp_fftbr_real(const double* in, int64_t in_batch_stride, void* out, void* work, int64_t batch, int log2n,
                    void* stream) {
@@ -1791,14 +1807,24 @@ int fgp_fftbr_real_half(const double* in, int64_t in_batch_stride, void* out, in
   return fftbr_real_any(in, in_batch_stride, out, out_batch_stride, true, work, batch, log2n, stream);
 }
 
-static int fftbr_real_any(const double* in, int64_t in_batch_stride, void* out, int64_t out_stride, bool half,
+int fgp_fftbr_real_half_f32(const float* in, int64_t in_batch_stride, void* out, int64_t out_batch_stride, void* work,
+                            int64_t batch, int log2n, void* stream) {
+  if (log2n >= 1 && batch > 1 && out_batch_stride < ((int64_t)1 << (log2n - 1)) + 1)
+    return set_error(kErrInvalid, "fgp_fftbr_real_half_f32: out row stride below n/2 + 1");
+  return fftbr_real_any(in, in_batch_stride, out, out_batch_stride, true, work, batch, log2n, stream);
+}
+
+extern "C++" {
+template <typename T>
+static int fftbr_real_any(const T* in, int64_t in_batch_stride, void* out, int64_t out_stride, bool half,
                           void* work, int64_t batch, int log2n, void* stream) {
   if (log2n < 17 || log2n > 24 || batch < 0) return set_error(kErrInvalid, "fgp_fftbr_real: needs 17 <= log2n <= 24");
   if (batch == 0) return kOk;
   if (!in || !out || !work) return set_error(kErrInvalid, "fgp_fftbr_real: null pointer");
   if (in_batch_stride < ((int64_t)1 << log2n) && batch > 1)
     return set_error(kErrInvalid, "fgp_fftbr_real: batch stride below n");
-  if (((uintptr_t)in & 15) || (in_batch_stride & 1)) return set_error(kErrInvalid, "fgp_fftbr_real: in must be 16-byte aligned rows");
+  if (((uintptr_t)in & 15) || (in_batch_stride & (16 / sizeof(T) - 1)))
+    return set_error(kErrInvalid, "fgp_fftbr_real: in must be 16-byte aligned rows");
   const int64_t tiles = (int64_t)1 << (log2n - 1 - kTileLog);
   if (batch * tiles >= ((int64_t)1 << 31)) return set_error(kErrUnsupported, "fgp_fftbr_real: batch too large");
   hipStream_t st = (hipStream_t)stream;
@@ -1806,7 +1832,8 @@ static int fftbr_real_any(const double* in, int64_t in_batch_stride, void* out, 
   if (!tb) return set_error(kErrHip, "twiddle table initialisation failed");
   const int mt = log2n - 1, p1 = mt - 12;
   const unsigned grid = (unsigned)(batch * tiles);
-  k_fwd_rows_r2c_in<<<grid, kWG, 0, st>>>(in, in_batch_stride, log2n, static_cast<double2*>(work), tb->tw4096, tb->twm[mt]);
+  k_fwd_rows_r2c_in<T><<<grid, kWG, 0, st>>>(in, in_batch_stride, log2n, static_cast<double2*>(work), tb->tw4096,
+                                             tb->twm[mt]);
   int rc = check_launch("k_fwd_rows_r2c_in");
   if (rc != kOk) return rc;
   Nll a{};
@@ -1828,6 +1855,7 @@ static int fftbr_real_any(const double* in, int64_t in_batch_stride, void* out, 
   }
   return check_launch("k_fwd_cols_r2c");
 }
+}  // extern "C++"
 
 static int ifftbr_real_any(const void* in, int64_t in_batch_stride, const void* f, bool freal, int64_t f_batch_stride,
                            double* out, int64_t out_batch_stride, void* work, int64_t batch, int log2n, void* stream) {

@@ -540,7 +540,7 @@ class AbstractFastGP(torch.nn.Module):
         def f():
             y = self._y[0]
             st = getattr(self, "_yt_state", None)
-            half = self._cache.get(("ytilde_half", n, False, False))
+            half = self._cache.get(("ytilde_half", n, False, False)) if y.dtype == torch.float64 else None
             if half is not None:
                 # the fused consumers took only the Hermitian half (_ytilde_half): the full spectrum is its mirror
                 yt = ops.hermitian_full(half, n)
@@ -556,13 +556,17 @@ class AbstractFastGP(torch.nn.Module):
         return self._cached(("ytilde", n), f, grad_sensitive=False)
 
     def _ytilde_half(self):
-        """The Hermitian half (k <= n/2) of ytilde = ft(y) of real float64 lattice observations, 2^17 <= n <= 2^24
+        """The Hermitian half (k <= n/2) of ytilde = ft(y) of real float64 / float32 lattice observations, 2^17 <= n <= 2^24
         (ops.fftbr_real_half): all that Y = sum |ytilde|^2 and the spectral coefficient solve read, at half the
         bytes written; a view of the full ytilde when that is cached already.  None when it does not apply."""
         n = self._nh
         y = self._y[0]
         if self._FAMILY != ops.LATTICE or n < 2 or not ops.half_spectrum_ok(y):
             return None
+        if y.dtype == torch.float32:
+            # data_dtype=float32: the fp32 rows widened exactly on load (fgp_fftbr_real_half_f32) -- Y and the
+            # coefficients in fp64 from one transform; get_ytilde keeps the API's complex64 ft(y)
+            return self._cached(("ytilde_half64", n), lambda: ops.fftbr_real_half(y), grad_sensitive=False)
         full = self._cache.get(("ytilde", n, False, False))
         if full is not None:
             return full[..., :n // 2 + 1]
@@ -614,7 +618,7 @@ class AbstractFastGP(torch.nn.Module):
         if (pb is not None and self._FAMILY == ops.LATTICE and 17 <= n.bit_length() - 1 <= 24
                 and pb[1] in (1, rows_y)):
             basis = self._spec_basis(n, pb[1])
-        half = self._ytilde_half() if (basis is not None and self.data_dtype == torch.float64) else None
+        half = self._ytilde_half() if basis is not None else None
         if half is not None:
             yt = half                     # the Hermitian half is all fgp_ifftbr_real_rf reads
         elif self.data_dtype != torch.float64:

@@ -90,10 +90,11 @@ def fftbr_raw(x, stable=True):
 
 
 def half_spectrum_ok(x):
-    """fgp_fftbr_real_half applies to x: real float64 rows, 2^17 <= n <= 2^24 (FGP_YT_HALF=0 / FGP_R2C=0 off)."""
+    """fgp_fftbr_real_half applies to x: real float64 (or float32: widened on load) rows, 2^17 <= n <= 2^24
+    (FGP_YT_HALF=0 / FGP_R2C=0 off)."""
     n = x.shape[-1]
-    return (x.dtype == torch.float64 and n >= 2 and (n & (n - 1)) == 0 and 17 <= n.bit_length() - 1 <= 24
-            and rows_ok_env() and os.environ.get("FGP_YT_HALF", "1")[:1] != "0")
+    return (x.dtype in (torch.float64, torch.float32) and n >= 2 and (n & (n - 1)) == 0
+            and 17 <= n.bit_length() - 1 <= 24 and rows_ok_env() and os.environ.get("FGP_YT_HALF", "1")[:1] != "0")
 
 
 def fftbr_real_half(x):
@@ -103,14 +104,16 @@ def fftbr_real_half(x):
     shape = x.shape
     n = shape[-1]
     m = log2_exact(n)
-    assert x.dtype == torch.float64 and 17 <= m <= 24, "fftbr_real_half: float64 rows, 2^17 <= n <= 2^24"
+    f32 = x.dtype == torch.float32
+    assert (x.dtype == torch.float64 or f32) and 17 <= m <= 24, "fftbr_real_half: float64 / float32 rows, 2^17 <= n <= 2^24"
     rows, bs = _as_rows(x)
-    if rows.data_ptr() % 16 or bs % 2:
+    if rows.data_ptr() % 16 or bs % (4 if f32 else 2):
         rows, bs = rows.contiguous(), n
     H = n // 2 + 1
     out = torch.empty((rows.size(0), H), dtype=torch.complex128, device=x.device)
     work = torch.empty((rows.size(0), n), dtype=torch.complex128, device=x.device)
-    N.call("fgp_fftbr_real_half", N.ptr(rows), bs, N.ptr(out), H, N.ptr(work), rows.size(0), m, _stream(x))
+    N.call("fgp_fftbr_real_half_f32" if f32 else "fgp_fftbr_real_half", N.ptr(rows), bs, N.ptr(out), H, N.ptr(work),
+           rows.size(0), m, _stream(x))
     return out.reshape(shape[:-1] + (H,))
 
 

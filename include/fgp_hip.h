@@ -522,6 +522,10 @@ int fgp_mt_mll_grad(const fgp_mt_layout* layout, const void* zinv, const void* z
  * values bit for bit. */
 int fgp_fftbr_real_half(const double* in, int64_t in_batch_stride, void* out, int64_t out_batch_stride, void* work,
                         int64_t batch, int log2n, void* stream);
+/* ABI 16 -- the same of float32 rows (16-byte aligned, stride a multiple of 4), widened to float64 exactly on load:
+ * fgp_fftbr_real_half of the widened rows bit for bit (data_dtype=float32 observations, BASELINE config C5). */
+int fgp_fftbr_real_half_f32(const float* in, int64_t in_batch_stride, void* out, int64_t out_batch_stride, void* work,
+                            int64_t batch, int log2n, void* stream);
 int fgp_sum_sq_half(const void* x, int64_t x_row_stride, int64_t R, int64_t G, int64_t n, double* out, void* stream);
 
 /* ABI 14 -- the WHOLE fit of one small problem on the spectral path in ONE launch (G = 1, the part-product

@@ -51,9 +51,9 @@ def test_benched_c5_regime_matches_reference(mixed):
     """The C5 configuration bench.py times: n = 2^18, d = 3, 512 outputs sharing the default hyper-parameters,
     the default nugget 1e-8, fit(iterations=3) (early stopping off), post_mean at 16 and post_var at 2 test
     points -- against the REAL reference's results on the same points and data (tests/golden/
-    c5_m18_d3_b512*.npz).  mixed: float32 observations (complex64 ytilde for the MLL's Y, fp64 from there)
-    against the reference on the same float32-rounded data; its loss tolerance adds 1e-6 for the complex64
-    ytilde's rounding of Y (~1e-7 relative per frequency, test_mixed_precision_multi_output_matches_oracle)."""
+    c5_m18_d3_b512*.npz).  mixed: float32 observations (widened exactly into the fp64 half-spectrum transform
+    that feeds Y and the coefficients, ABI 16) against the reference on the same float32-rounded data; its loss
+    tolerance keeps the 1e-6 allowance of the earlier complex64 Y (now fp64: the allowance is unused)."""
     import numpy as np
     g = np.load(os.path.join(os.path.dirname(__file__), "golden",
                              "c5_m18_d3_b512%s.npz" % ("_f32data" if mixed else "")))
@@ -149,11 +149,11 @@ def test_multi_output_fit_and_predict_match_oracle(per_output):
 
 
 def test_mixed_precision_multi_output_matches_oracle():
-    """data_dtype=float32 (the mixed-precision C5 path): fp32 observations, complex64 ytilde for the
-    MLL's Y (fgp_fftbr_c64 + fgp_sum_sq in fp64), fp64 eigenvalues / fit / coefficients / posteriors.
-    Against the fp64 oracle on the same fp32-rounded observations: loss trajectory 2e-6 relative
-    (measured 2.1e-7 at this nugget: the complex64 ytilde's rounding in Y), fitted lengthscales 1e-10,
-    posterior mean 1e-7, posterior variance 1e-8 K(x,x)."""
+    """data_dtype=float32 (the fp32 C5 path): fp32 observations stored, widened exactly on load into ONE fp64
+    Hermitian-half transform (fgp_fftbr_real_half_f32, ABI 16) that feeds the MLL's Y and the coefficients; fp64
+    eigenvalues / fit / posteriors; get_ytilde keeps the API's complex64 ft(y).  Against the fp64 oracle on the same
+    fp32-rounded observations: loss trajectory 2e-6 relative, fitted lengthscales 1e-10, posterior mean 1e-7,
+    posterior variance 1e-8 K(x,x)."""
     m, d, B, its = 18, 3, 16, 4
     n = 2 ** m
     gp = F.FastGPLattice(F.Lattice(d, seed=7), shape_batch=[B], noise=1e-3, device=DEV, data_dtype=torch.float32)

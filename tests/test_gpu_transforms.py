@@ -307,6 +307,18 @@ def test_ifftbr_real_half_length_matches_full_length(monkeypatch, m, batch, shar
         _close(half, O.ft_stable(x.cpu(), O.ifftbr).real, m)
 
 
+@pytest.mark.parametrize("m,rows", [(17, 3), (18, 4)])
+def test_float32_rows_widened_on_load_equal_float64_half(m, rows):
+    """fgp_fftbr_real_half_f32 (ABI 16: data_dtype=float32 observations) equals fgp_fftbr_real_half of the rows
+    widened to float64 bit for bit (the widening is exact), also for rows with a padded stride."""
+    from fastgaussianprocesses_amd import ops
+    n = 2 ** m
+    g = torch.Generator().manual_seed(m + 1)
+    y32 = (torch.randn((rows, n + 8), generator=g) + 3.0).float().to(DEV)
+    for y in (y32[:, :n].contiguous(), y32[:, :n]):
+        assert torch.equal(ops.fftbr_real_half(y), ops.fftbr_real_half(y.double()))
+
+
 @pytest.mark.parametrize("m,rows", [(17, 3), (18, 5), (20, 2)])
 def test_hermitian_half_spectra_equal_full_length_ones(m, rows):
     """fgp_fftbr_real_half (ABI 14) writes fgp_fftbr_real's values at k <= n/2 only: bit for bit, and the
