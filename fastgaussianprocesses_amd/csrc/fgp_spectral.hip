@@ -670,7 +670,7 @@ __global__ __launch_bounds__(kWG) void k_spec_finish_step(Nll a, FitFuse fz) {
 //   -> AbstractGP.fit's early-stopping rule (abstract_gp.py:276-284) evaluated on the same loss values
 // so the trajectory is the multi-launch fit's bit for bit, without a launch per iteration.  Workgroup 0 writes
 // the histories and the final state; out[0] = the last iteration, out[1] = 1 if a barrier poll gave up.
-constexpr int kPersistMaxW = 64;
+constexpr int kPersistMaxW = 256;
 constexpr long long kSpecPollMax = 1ll << 22;     // bounded waits of the persistent k_spec_tile
 constexpr int kPersistLdsMax = 96 * 1024;
 constexpr long long kPersistPollMax = 1ll << 22;

@@ -284,12 +284,14 @@ def test_real_factor_inverse_reads_half_of_hermitian_input(m, rows):
 
 
 @pytest.mark.parametrize("family,m,d,wait", [("lattice", 16, 3, 60), ("net", 16, 3, 60), ("lattice", 10, 6, 10),
-                                             ("net", 10, 2, 10), ("lattice", 12, 1, 4)])
+                                             ("net", 10, 2, 10), ("lattice", 12, 1, 4), ("lattice", 18, 3, 60),
+                                             ("net", 17, 2, 10)])
 def test_single_launch_fit_equals_launch_per_iteration(family, m, d, wait, monkeypatch):
     """fgp_fit_persist (the whole fit of one small spectral problem in one launch: LDS-resident spectra, an
     in-kernel grid barrier per iteration, the early-stopping rule on the device) against the launch per
     iteration (FGP_FIT_PERSIST=0): the same iterations, loss history and fitted parameters bit for bit --
-    with early stopping impossible (wait 60 > 50 iterations: C2 / C3's bench step) and possible."""
+    with early stopping impossible (wait 60 > 50 iterations: C2 / C3's bench step) and possible; n = 2^17 / 2^18
+    spread the spectra over 128 workgroups (the C5 shared-parameter fit's geometry)."""
     monkeypatch.setenv("FGP_FIT_PATH", "spectral")
     out = {}
     for persist in ("1", "0"):
