@@ -1385,23 +1385,28 @@ class AbstractFastGP(torch.nn.Module):
                 add.append([float(v) for v in a.tolist()])
         return order, coef, add
 
-    def _kargs(self, x):
-        """points as the parts kernel takes them: float64 lattice points, int64 t-bit net points."""
+    def _kargs(self, x, check=True):
+        """points as the parts kernel takes them: float64 lattice points, int64 t-bit net points.  check: the
+        reference's [0, 1] range assertion (fast_gp_lattice.py:264-265; a device->host sync) -- skipped for the
+        GP's own point sets (get_xb), which are in range by construction."""
         if self._FAMILY == ops.LATTICE:
             x = x.to(device=self.device, dtype=torch.float64)
-            assert bool(((0 <= x) & (x <= 1)).all()), "x should have all elements in [0,1]"
+            if check:
+                assert bool(((0 <= x) & (x <= 1)).all()), "x should have all elements in [0,1]"
             return x
         if torch.is_floating_point(x):
             x = x.to(self.device)
-            assert bool(((0 <= x) & (x <= 1)).all()), "x should have all elements in [0,1]"
+            if check:
+                assert bool(((0 <= x) & (x <= 1)).all()), "x should have all elements in [0,1]"
             return torch.floor((x % 1) * 2 ** self.t).to(torch.int64)
         return x.to(device=self.device, dtype=torch.int64)
 
-    def _parts_pairs(self, x, z, beta0, beta1, zip_pairs=False):
+    def _parts_pairs(self, x, z, beta0, beta1, zip_pairs=False, check=True):
         """_kernel_parts (abstract_fast_gp.py:173-180) for all (x_i, z_k) pairs -> [N, M, p0, p1, d]
         (or the (x_i, z_i) pairs -> [N, p0, p1, d])."""
         order, coef, add = self._pair_spec(beta0, beta1)
-        p = ops.mt_parts(self._FAMILY, self._kargs(x), self._kargs(z), order, coef, add, self._tbits(), zip_pairs)
+        p = ops.mt_parts(self._FAMILY, self._kargs(x, check), self._kargs(z, check), order, coef, add, self._tbits(),
+                         zip_pairs)
         return p.reshape(p.shape[:-2] + (len(beta0), len(beta1), self.d))
 
     def _kernel_from_parts(self, parts, beta0, beta1, c0, c1):

@@ -460,13 +460,18 @@ class MultiTaskFastGP(AbstractFastGP):
                 t0, t1 = (a, b) if a <= b else (b, a)
                 nk = lo.nsrt[k]
                 parts = self.get_k1parts(t0, t1, nk)                              # [nk, p0, p1, d]
-                b0, b1 = self._derivs_h[t0], self._derivs_h[t1]
-                need = (b0[:, None, :] + b1[None, :, :]) > 0
-                valid = (~need[None] | ins[:, None, None, :]).all(-1)
-                cc = self.derivatives_coeffs[t0][:, None] * self.derivatives_coeffs[t1][None, :]
-                prod = torch.where(insd[:, None, None, None, :], parts[None], 1.0).prod(-1)
-                w = cc[None] * valid.to(device=dev, dtype=torch.float64)
-                B = (prod * w[:, None]).sum((-1, -2))                            # [NS, nk]
+                if not self._deriv_mode:
+                    # no derivatives (one (b0, b1) = (0, 0) term, coefficient 1): B_S = prod_{j in S} parts_j -- the
+                    # same values as the weighted sum below (x * 1.0, one-term sums), without its host-side mask copy
+                    B = torch.where(insd[:, None, :], parts[None, :, 0, 0, :], 1.0).prod(-1)   # [NS, nk]
+                else:
+                    b0, b1 = self._derivs_h[t0], self._derivs_h[t1]
+                    need = (b0[:, None, :] + b1[None, :, :]) > 0
+                    valid = (~need[None] | ins[:, None, None, :]).all(-1)
+                    cc = self.derivatives_coeffs[t0][:, None] * self.derivatives_coeffs[t1][None, :]
+                    prod = torch.where(insd[:, None, None, None, :], parts[None], 1.0).prod(-1)
+                    w = cc[None] * valid.to(device=dev, dtype=torch.float64)
+                    B = (prod * w[:, None]).sum((-1, -2))                        # [NS, nk]
                 spec = self.ft(B).to(torch.complex128)
                 if a > b:
                     spec = spec.conj()
@@ -523,7 +528,8 @@ class MultiTaskFastGP(AbstractFastGP):
         if key not in self._parts_cache:
             xa = self.get_xb(task0, n)
             zb = self.get_xb(task1, 1)
-            self._parts_cache[key] = self._parts_pairs(xa, zb, self._derivs_h[task0], self._derivs_h[task1])[:, 0]
+            self._parts_cache[key] = self._parts_pairs(xa, zb, self._derivs_h[task0], self._derivs_h[task1],
+                                                       check=False)[:, 0]
         return self._parts_cache[key]
 
     def get_lam(self, task0, task1, n=None):
@@ -544,7 +550,7 @@ class MultiTaskFastGP(AbstractFastGP):
                 # _LamCaches doubling (util.py:113-132): one DIT stage from the cached lam at n/2 and ft
                 # of the first-column kernel over the new half of task0's points
                 new = self._parts_pairs(self.get_xb(task0, n)[n // 2:], self.get_xb(task1, 1),
-                                        self._derivs_h[task0], self._derivs_h[task1])[:, 0]
+                                        self._derivs_h[task0], self._derivs_h[task1], check=False)[:, 0]
                 return ops.double_update(self._FAMILY, half, self.ft(k1_of(new)))
             return self.ft(k1_of(self.get_k1parts(task0, task1, n)))
         return self._cached(("lam", (task0, task1, n)), f)

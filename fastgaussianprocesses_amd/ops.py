@@ -571,6 +571,9 @@ def mt_layout(ns_sorted):
     return lay
 
 
+_MT_SPEC = {}
+
+
 def mt_parts(family, x, z, order, coef, add, tbits=0, zip_pairs=False):
     """Derivative kernel parts (fgp_mt_parts): x [N, d], z [M, d] (float64 lattice / int64 net points);
     order / coef / add [P, d] host lists -> [N, M, P, d] (or [N, P, d] with zip_pairs, N == M)."""
@@ -584,9 +587,17 @@ def mt_parts(family, x, z, order, coef, add, tbits=0, zip_pairs=False):
     M = z.shape[0]
     P = len(order)
     dev = x.device
-    o = torch.tensor(order, dtype=torch.int32, device=dev).reshape(P, d).contiguous()
-    c = torch.tensor(coef, dtype=torch.float64, device=dev).reshape(P, d).contiguous()
-    a = torch.tensor(add, dtype=torch.float64, device=dev).reshape(P, d).contiguous()
+    # the [P, d] spec arrays on the device, made once per spec (a host list -> device tensor is a blocking copy)
+    key = (str(dev), int(family), tuple(map(tuple, order)), tuple(map(tuple, coef)), tuple(map(tuple, add)))
+    spec = _MT_SPEC.get(key)
+    if spec is None:
+        spec = (torch.tensor(order, dtype=torch.int32, device=dev).reshape(P, d).contiguous(),
+                torch.tensor(coef, dtype=torch.float64, device=dev).reshape(P, d).contiguous(),
+                torch.tensor(add, dtype=torch.float64, device=dev).reshape(P, d).contiguous())
+        if len(_MT_SPEC) > 256:
+            _MT_SPEC.clear()
+        _MT_SPEC[key] = spec
+    o, c, a = spec
     shape = (Nx, P, d) if zip_pairs else (Nx, M, P, d)
     out = torch.empty(shape, dtype=torch.float64, device=dev)
     N.call("fgp_mt_parts", int(family), N.ptr(x), x.stride(0) if Nx > 1 else d, Nx, N.ptr(z),
