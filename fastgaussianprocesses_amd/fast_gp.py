@@ -1363,7 +1363,16 @@ class AbstractFastGP(torch.nn.Module):
     # ------------------------------------------------------------------ kernel parts with derivative orders
     def _pair_spec(self, beta0, beta1):
         """(order, coef, add) [p0 p1, d] for fgp_mt_parts (fast_gp_lattice.py:267-273,
-        fast_gp_digital_net_b2.py:289-301); coefficients evaluated with the reference's own ops."""
+        fast_gp_digital_net_b2.py:289-301); coefficients evaluated with the reference's own ops (memoised per
+        (beta0, beta1): the multitask pair spectra ask for the same derivative orders pair after pair)."""
+        key = (tuple(beta0.shape), tuple(beta0.reshape(-1).tolist()), tuple(beta1.shape),
+               tuple(beta1.reshape(-1).tolist()), tuple(self._alphas))
+        memo = self.__dict__.setdefault("_pair_spec_memo", {})
+        if key not in memo:
+            memo[key] = self._pair_spec_eval(beta0, beta1)
+        return memo[key]
+
+    def _pair_spec_eval(self, beta0, beta1):
         alpha = torch.tensor(self._alphas, dtype=torch.int64)
         order, coef, add = [], [], []
         for b0 in beta0:

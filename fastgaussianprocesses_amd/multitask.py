@@ -454,7 +454,7 @@ class MultiTaskFastGP(AbstractFastGP):
             NS = 1 << d
             ins = torch.tensor([[bool((S >> j) & 1) for j in range(d)] for S in range(NS)])
             insd = ins.to(dev)
-            rows, offs, off = [], [], 0
+            Bs, conj, offs, off = [], [], [], 0
             for (k, l) in lo.pairs:
                 a, b = lo.active[k], lo.active[l]
                 t0, t1 = (a, b) if a <= b else (b, a)
@@ -472,13 +472,20 @@ class MultiTaskFastGP(AbstractFastGP):
                     prod = torch.where(insd[:, None, None, None, :], parts[None], 1.0).prod(-1)
                     w = cc[None] * valid.to(device=dev, dtype=torch.float64)
                     B = (prod * w[:, None]).sum((-1, -2))                        # [NS, nk]
-                spec = self.ft(B).to(torch.complex128)
-                if a > b:
-                    spec = spec.conj()
-                rows.append(spec.resolve_conj().reshape(-1))
+                Bs.append(B)
+                conj.append(a > b)
                 offs.append(off)
                 off += NS * nk
-            return torch.cat(rows).contiguous(), offs
+            # one transform per distinct n over the pairs of that length (rows are transformed independently: the
+            # same values as pair by pair)
+            specs = [None] * len(Bs)
+            for nk in sorted(set(int(B.shape[-1]) for B in Bs)):
+                idx = [i for i, B in enumerate(Bs) if int(B.shape[-1]) == nk]
+                ft = self.ft(torch.cat([Bs[i] for i in idx])).to(torch.complex128)
+                for r, i in enumerate(idx):
+                    sp = ft[r * NS:(r + 1) * NS]
+                    specs[i] = (sp.conj() if conj[i] else sp).resolve_conj().reshape(-1)
+            return torch.cat(specs).contiguous(), offs
         return self._cached(("mt_pair_spec", tuple(lo.nsrt), tuple(lo.active)), f, grad_sensitive=False)
 
     def _fused_engine(self, iterations, lr, ysq=None, d_out=None):

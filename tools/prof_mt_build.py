@@ -20,4 +20,8 @@ pr.enable()
 MtGeneralEngine(gp, 0.1, 41)
 torch.cuda.synchronize()
 pr.disable()
-pstats.Stats(pr).sort_stats("cumulative").print_stats(35)
+st = pstats.Stats(pr)
+rows = sorted(st.stats.items(), key=lambda kv: -kv[1][3])
+print("cumulative us  tottime us  calls  function")
+for (fn, line, name), (cc, nc, tt, ct, _) in rows[:45]:
+    print("%12.1f %11.1f %6d  %s:%d(%s)" % (ct * 1e6, tt * 1e6, nc, fn.split("/")[-1], line, name))
