@@ -389,19 +389,27 @@ __device__ __forceinline__ double2 mtg_poly(const MtFit& m, int p, int64_t nk, i
   double2 P = make_double2(0.0, 0.0);
 #pragma unroll
   for (int j = 0; j < (DER ? D : 0); ++j) dp[j] = make_double2(0.0, 0.0);
+  // S = sh + t in groups of 8: the bits of t resolve at compile time, the higher bits (D > 3) are uniform per group
+  // (a fully unrolled 2^6-term loop with its derivative sums spilled hundreds of VGPRs; a plain partial unroll
+  // tested every bit per term).  Every sum in ascending S, as before.
+  constexpr int U = NS < 8 ? NS : 8;
+#pragma unroll 1
+  for (int sh = 0; sh < NS; sh += U) {
 #pragma unroll
-  for (int S = 0; S < NS; ++S) {
-    const double2 f = ph[(int64_t)S * nk];
-    const double w = lpow[S];
-    P.x = __builtin_fma(w, f.x, P.x);
-    P.y = __builtin_fma(w, f.y, P.y);
-    if constexpr (DER) {
+    for (int t = 0; t < U; ++t) {
+      const int S = sh + t;
+      const double2 f = ph[(int64_t)S * nk];
+      const double w = lpow[S];
+      P.x = __builtin_fma(w, f.x, P.x);
+      P.y = __builtin_fma(w, f.y, P.y);
+      if constexpr (DER) {
 #pragma unroll
-      for (int j = 0; j < D; ++j)
-        if ((S >> j) & 1) {
-          dp[j].x = __builtin_fma(w, f.x, dp[j].x);
-          dp[j].y = __builtin_fma(w, f.y, dp[j].y);
-        }
+        for (int j = 0; j < D; ++j)
+          if (j < 3 ? ((t >> j) & 1) : ((sh >> j) & 1)) {
+            dp[j].x = __builtin_fma(w, f.x, dp[j].x);
+            dp[j].y = __builtin_fma(w, f.y, dp[j].y);
+          }
+      }
     }
   }
   return P;
@@ -422,6 +430,20 @@ __device__ __forceinline__ void mtg_lpow(const MtFit& m, int g, double* lpow) {
   }
 }
 
+// The same products for the launch's problem g in LDS (lp: __shared__ [2^D]), the threads < 2^D forming one each
+// (mtg_lpow's order) -- every thread of the workgroup then reads them instead of holding 2^D registers
+template <int D>
+__device__ __forceinline__ void mtg_lpow_lds(const MtFit& m, int g, double* lp) {
+  if ((int)threadIdx.x < (1 << D)) {
+    const int S = threadIdx.x;
+    double w = 1.0;
+    for (int j = 0; j < D; ++j)
+      if ((S >> j) & 1) w *= mtg_ls(m, g, j);
+    lp[S] = w;
+  }
+  __syncthreads();
+}
+
 // The adaptive nugget's ratio of sorted task k (util.py:286-290): r = |A_k| / |A_ref| with A_k = sqrt(n_k) sum_S l^S c_kS
 // (the trace of the block's sqrt(n_k) lam over scale), and with DER dr[j] = l_j dr/dl_j (log-lengthscale derivative:
 // l_j dA/dl_j = sum_{S containing j} l^S c_S).
@@ -436,7 +458,7 @@ __device__ __forceinline__ double mtg_nug_ratio(const MtFit& m, int k, const dou
 #pragma unroll
     for (int j = 0; j < (DER ? D : 1); ++j) Aj[u][j] = make_double2(0.0, 0.0);
     const double2* c = m.nug_coef + (int64_t)kk[u] * NS;
-#pragma unroll
+#pragma unroll 4
     for (int S = 0; S < NS; ++S) {
       const double2 cs = c[S];
       A[u].x = __builtin_fma(lpow[S], cs.x, A[u].x);
@@ -467,11 +489,11 @@ __device__ __forceinline__ double mtg_nug_ratio(const MtFit& m, int k, const dou
 // (problem g = the launch's y index: entry / class / block-row g of a parameter batch; 0 when unbatched)
 template <int D>
 __global__ __launch_bounds__(kWG) void k_mtg_lams(MtFit m) {
+  __shared__ double lpow[1 << D];
   const int64_t e = (int64_t)blockIdx.x * kWG + threadIdx.x;
   const int g = blockIdx.y;
+  mtg_lpow_lds<D>(m, g, lpow);
   if (e >= m.lay.L) return;
-  double lpow[1 << D];
-  mtg_lpow<D>(m, g, lpow);
   int k, l, p;
   int64_t i;
   mtg_entry(m, e, k, l, p, i);
@@ -569,6 +591,7 @@ __global__ __launch_bounds__(kMtcWG) void k_mtg_class(MtFit m) {
       }
       const int ql = qn[l], p = rem;
       double2 acc = F[oe[l * MT + mm] + p];
+#pragma unroll 4
       for (int q = p; q < qk; q += ql) {
         const double2 ul = F[oe[k * MT + l] + q] * ip[rs[k] + q];
         acc -= cmul_cj(ul, F[oe[k * MT + mm] + q]);
@@ -603,6 +626,7 @@ __global__ __launch_bounds__(kMtcWG) void k_mtg_class(MtFit m) {
       while (p >= qn[l]) p -= qn[l++];
       const int ql = qn[l];
       double2 acc = o[b * R + rs[l] + p];
+#pragma unroll 4
       for (int q = p; q < qk; q += ql) acc -= cmul_cj(F[oe[k * MT + l] + q], o[b * R + rs[k] + q]);
       o[b * R + rs[l] + p] = acc;
     }
@@ -615,6 +639,7 @@ __global__ __launch_bounds__(kMtcWG) void k_mtg_class(MtFit m) {
     for (int u = t; u < B * qk; u += kMtcWG) {
       const int b = u / qk, q = u - b * qk;
       double2 s = o[b * R + rs[k] + q];
+#pragma unroll 4
       for (int l = k + 1; l < T; ++l) s -= cmul(F[oe[k * MT + l] + q], o[b * R + rs[l] + q % qn[l]]);
       o[b * R + rs[k] + q] = s;
     }
@@ -630,6 +655,7 @@ __global__ __launch_bounds__(kMtcWG) void k_mtg_class(MtFit m) {
       for (int mm = k + 1; mm < T; ++mm) {
         const int pm = q % qn[mm];
         double2 s = make_double2(0.0, 0.0);
+#pragma unroll 4
         for (int l = k + 1; l < T; ++l) s -= cmul(F[oe[k * MT + l] + q], mtc_zpat(Z, oe, l, q % qn[l], mm, pm));
         Z[oe[k * MT + mm] + q] = s;
       }
@@ -683,8 +709,8 @@ __global__ __launch_bounds__(kWG) void k_mtg_contract(MtFit m) {
   const int g = blockIdx.y;
   const MtLay& lay = m.lay;
   const int64_t go = (int64_t)g * lay.L, rnm = (int64_t)lay.R * lay.nmin;
-  double lpow[1 << D];
-  mtg_lpow<D>(m, g, lpow);
+  __shared__ double lpow[1 << D];
+  mtg_lpow_lds<D>(m, g, lpow);
   const double sc = mtg_scale(m, g);
   double acc[4 + D];
 #pragma unroll
@@ -843,12 +869,17 @@ __global__ __launch_bounds__(kMtgStepWG) void k_mtg_step(MtFit m, int iter, int 
       for (int g = 0; g < G; ++g) {
         if (row(3, g) != rr) continue;
         const double* gkt = sums + (int64_t)g * NQs + 4 + D;
-        for (int k = 0, p = 0; k < lay.T; ++k)
-          for (int l = k; l < lay.T; ++l, ++p) {
-            const int a = m.task[k], b = m.task[l];
-            if (a == c) gs += gkt[p] * raw[fo + b * m.rank + r];
-            if (b == c) gs += gkt[p] * raw[fo + a * m.rank + r];
+        for (int k = 0, p = 0; k < lay.T; ++k) {
+          const int a = m.task[k];
+#pragma unroll 4
+          for (int l = k; l < lay.T; ++l) {
+            const int b = m.task[l];
+            const double gv = gkt[p + l - k];
+            if (a == c) gs += gv * raw[fo + b * m.rank + r];
+            if (b == c) gs += gv * raw[fo + a * m.rank + r];
           }
+          p += lay.T - k;
+        }
       }
     } else {
       const int rr = (x - m.v_off) / m.T_all, c = (x - m.v_off) - rr * m.T_all;
