@@ -1549,11 +1549,17 @@ __global__ __launch_bounds__(kWG) void k_mt_spec_iter(Nll a) {
       mt_pair_kl(p, T, k, l);
       const int64_t base = (int64_t)p * NS * n + j0 + f;
       double2 P = make_double2(0.0, 0.0);
+      // the subsets in groups of 8, the group loop rolled (a fully unrolled 2^6-term loop spilled), S ascending
+      constexpr int U = NS < 8 ? NS : 8;
+#pragma unroll 1
+      for (int sh = 0; sh < NS; sh += U) {
 #pragma unroll
-      for (int S = 0; S < NS; ++S) {
-        const double2 ph = mt_phi(a, base + (int64_t)S * n);
-        P.x = __builtin_fma(ls_pow[S], ph.x, P.x);
-        P.y = __builtin_fma(ls_pow[S], ph.y, P.y);
+        for (int t = 0; t < U; ++t) {
+          const int S = sh + t;
+          const double2 ph = mt_phi(a, base + (int64_t)S * n);
+          P.x = __builtin_fma(ls_pow[S], ph.x, P.x);
+          P.y = __builtin_fma(ls_pow[S], ph.y, P.y);
+        }
       }
       const double q = kt[k * T + l];
       double2 v = make_double2(sn * P.x, sn * P.y);
@@ -1651,14 +1657,19 @@ __global__ __launch_bounds__(kWG) void k_mt_spec_iter(Nll a) {
       const double2 w = wv[f][p];
       const double cx = wgt * w.x, cy = wgt * w.y;
       const int64_t base = (int64_t)p * NS * n + j0 + f;
+      constexpr int U = NS < 8 ? NS : 8;
+#pragma unroll 1
+      for (int sh = 0; sh < NS; sh += U) {
 #pragma unroll
-      for (int S = 0; S < NS; ++S) {
-        const double2 ph = mt_phi(a, base + (int64_t)S * n);
-        const double r = ls_pow[S] * (cx * ph.x - cy * ph.y);
-        acc_sc += r;
+        for (int t = 0; t < U; ++t) {
+          const int S = sh + t;
+          const double2 ph = mt_phi(a, base + (int64_t)S * n);
+          const double r = ls_pow[S] * (cx * ph.x - cy * ph.y);
+          acc_sc += r;
 #pragma unroll
-        for (int m = 0; m < D; ++m)
-          if ((S >> m) & 1) acc_l[m] += r;
+          for (int m = 0; m < D; ++m)
+            if (m < 3 ? ((t >> m) & 1) : ((sh >> m) & 1)) acc_l[m] += r;
+        }
       }
     }
   }
