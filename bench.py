@@ -338,12 +338,13 @@ def secondary_configs(F, args, device, rank=0, world=1, collect=None):
         total = getattr(sg, "total", 1)
         roof_pm = None
         if name.startswith("C5 per-output"):
-            # 512 outputs with their own kernels: k_post_mean<0, 3, 4, 4> over blocks of 4 outputs (128 launches of
-            # N x n x 4 output-pairs), priced on tools/predict_kernels.py's trace of the same call
-            roof_pm = roofline_post_mean("k_post_mean<0, 3, 4, 4>", None, args.n_mean * sg.n * 4, 3, 4,
+            # 512 outputs with their own kernels: k_post_mean<0, 3, 4, 4> over the outputs in blocks of 4, ONE launch
+            # (fgp_post_mean over output blocks: N x n x 4 output-pairs per block, B / 4 blocks), priced on
+            # tools/predict_kernels.py's trace of the same call
+            roof_pm = roofline_post_mean("k_post_mean<0, 3, 4, 4>", None, args.n_mean * sg.n * 4 * (sg.outputs // 4), 3, 4,
                                          stats=ROCPROF_PREDICT_STATS, sq=PMC_SQ_PREDICT,
                                          live_ms=phases.get("post_mean") if phases else None,
-                                         launches=(sg.outputs + 3) // 4)
+                                         launches=1 + (1 if sg.outputs % 4 else 0))
         out.append({"metric": "GP fit+predict points/sec" if total == 1 else
                     "multi-output GP fit+predict output-points/sec",
                     "value": sg.n * total / sec, "unit": "points/s" if total == 1 else "output-points/s",
@@ -792,9 +793,9 @@ def roofline_fit_kernels(F, shifts, iters):
 
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r05m_pmc_fit_kernels.json")
-PMC_SQ_SUMMARY = os.path.join(ROOT, "profiles", "r05m_pmc_sq_fit_kernels.json")
-ROCPROF_GRID_STATS = os.path.join(ROOT, "profiles", "r05m_bench_kernel_grid_stats.txt")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r05t_pmc_fit_kernels.json")
+PMC_SQ_SUMMARY = os.path.join(ROOT, "profiles", "r05t_pmc_sq_fit_kernels.json")
+ROCPROF_GRID_STATS = os.path.join(ROOT, "profiles", "r05t_bench_kernel_grid_stats.txt")
 # the read floor of the spectral iteration's footprint: tools/stream_microbench.hip over the same 168 MB,
 # re-read back to back, 24.0-24.3 us per pass (7.0 TB/s; profiles/r03v_stream_and_stamps.jsonl)
 STREAM_FLOOR_US = 24.0
@@ -804,8 +805,8 @@ FP64_LANE_OPS_PEAK = 256 * 4 * 16 * 2.4e9
 CPU_FIDELITY = os.path.join(ROOT, "profiles", "r02_cpu_fidelity.json")
 # the prediction kernels (tools/predict_kernels.py: C4's batched post_mean / post_var, C5 per-output's post_mean):
 # rocprofv3 kernel-trace summary and SQ counter pass
-ROCPROF_PREDICT_STATS = os.path.join(ROOT, "profiles", "r05m_predict_kernel_grid_stats.txt")
-PMC_SQ_PREDICT = os.path.join(ROOT, "profiles", "r05m_pmc_sq_predict.json")
+ROCPROF_PREDICT_STATS = os.path.join(ROOT, "profiles", "r05t_predict_kernel_grid_stats.txt")
+PMC_SQ_PREDICT = os.path.join(ROOT, "profiles", "r05t_pmc_sq_predict.json")
 
 
 def pmc_traffic(kernel, grid):
