@@ -448,6 +448,11 @@ __device__ __forceinline__ int64_t work_pos_pair(int64_t u, int64_t k, int P1, i
   return (tile << kTileLog) + (u << CL) + slot;
 }
 
+// A row of N2 = 16 kWG reals staged in the row kernels' ldsd (kTile + kTile/16 doubles): element p at
+// run_pad(p), each thread's run of 16 padded to 17 (thread t's run starts at kRunPad t).
+constexpr int kRunPad = 17;
+__device__ __forceinline__ int run_pad(int p) { return p + (p >> 4); }
+
 template <int PG, int D>
 __global__ __launch_bounds__(kWG) void k_fwd_rows_r2c(Nll a, const double2* __restrict__ tw, const double2* __restrict__ twm) {
   constexpr int P2 = 12, N2 = 1 << P2;
@@ -501,27 +506,43 @@ __global__ __launch_bounds__(kWG) void k_fwd_rows_r2c_in(const T* __restrict__ i
   const int64_t g = blockIdx.x / tiles;
   const int row0 = (int)(blockIdx.x % tiles);
   const int tid = threadIdx.x;
-  const T* x = in + g * in_stride + (int64_t)row0 * N2 + 16 * tid;
+  const T* x = in + g * in_stride + (int64_t)row0 * N2;
   double2 v[16];
   double2 sum = make_double2(0.0, 0.0);
-  if constexpr (sizeof(T) == 8) {
+  // thread t takes elements 16 t .. 16 t + 15 of x[:n/2] (Re) and x[n/2:] (Im); both halves are loaded
+  // lane-consecutive (16 B per lane) and handed over through LDS (loading a thread's run directly puts the
+  // lanes 128 B apart)
+  constexpr int VW = 16 / sizeof(T), NL = 16 / VW;   // elements per 16-B load, loads per half
+  using VT = typename std::conditional<sizeof(T) == 8, double2, float4>::type;
+  VT lo[NL], hi[NL];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const double2 lo = *reinterpret_cast<const double2*>(x + 2 * u);
-      const double2 hi = *reinterpret_cast<const double2*>(x + nt + 2 * u);
-      v[2 * u] = make_double2(lo.x, hi.x);
-      v[2 * u + 1] = make_double2(lo.y, hi.y);
-    }
-  } else {
+  for (int u = 0; u < NL; ++u) {
+    lo[u] = *reinterpret_cast<const VT*>(x + VW * (tid + kWG * u));
+    hi[u] = *reinterpret_cast<const VT*>(x + nt + VW * (tid + kWG * u));
+  }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const float4 lo = *reinterpret_cast<const float4*>(x + 4 * u);
-      const float4 hi = *reinterpret_cast<const float4*>(x + nt + 4 * u);
-      v[4 * u] = make_double2((double)lo.x, (double)hi.x);
-      v[4 * u + 1] = make_double2((double)lo.y, (double)hi.y);
-      v[4 * u + 2] = make_double2((double)lo.z, (double)hi.z);
-      v[4 * u + 3] = make_double2((double)lo.w, (double)hi.w);
+  for (int half = 0; half < 2; ++half) {
+#pragma unroll
+    for (int u = 0; u < NL; ++u) {
+      const int a = run_pad(VW * (tid + kWG * u));
+      const VT w = half ? hi[u] : lo[u];
+      if constexpr (sizeof(T) == 8) {
+        ldsd[a] = w.x;
+        ldsd[a + 1] = w.y;
+      } else {
+        ldsd[a] = (double)w.x;
+        ldsd[a + 1] = (double)w.y;
+        ldsd[a + 2] = (double)w.z;
+        ldsd[a + 3] = (double)w.w;
+      }
     }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      if (half) v[k].y = ldsd[kRunPad * tid + k];
+      else v[k].x = ldsd[kRunPad * tid + k];
+    }
+    __syncthreads();
   }
 #pragma unroll
   for (int t = 0; t < 16; ++t) sum += v[t];
@@ -903,11 +924,10 @@ __global__ __launch_bounds__(kWG, 2) void k_inv_cols_c2r(const double2* __restri
 #ifndef FGP_C2R_UNROLL
 #define FGP_C2R_UNROLL 8   // measured: 1501 vs 1533 us at 512 x 2^18 (profiles/r02i_exp_half_length_transforms.jsonl)
 #endif
-#pragma unroll FGP_C2R_UNROLL
-  for (int j = 0; j < JOBS; ++j) {
+  // pair job j: its (row, column) of the tile and of the mirrored partner (column 0 of tile 0 folds its
+  // own mirror image: rows r and N1 - r of column 0, and column N2/2)
+  auto job = [&](int j, int& sp, int& rp, int64_t& cp, int& ss, int& rs) {
     const int rr = rr0 + RSTEP * j;
-    int sp, rp, ss, rs;
-    int64_t cp;
     if (!col0) {
       sp = q; rp = rr; cp = cp_gen; ss = sp + HC; rs = N1 - 1 - rp;
     } else if (rr < N1 / 2) {
@@ -915,15 +935,55 @@ __global__ __launch_bounds__(kWG, 2) void k_inv_cols_c2r(const double2* __restri
     } else {
       sp = HC; rp = rr - N1 / 2; cp = N2 >> 1; ss = HC; rs = N1 - 1 - rp;
     }
+  };
+  // HERM: every job's two input values (and factors) are loaded before any is used, so the JOBS x 2
+  // loads of a thread are in flight together (the one-loop form waited for each job's loads in turn:
+  // the column pass is bound by these loads)
+  double2 av[HERM ? JOBS : 1], bv[HERM ? JOBS : 1], tv[HERM ? JOBS : 1], wv[HERM ? JOBS : 1];
+  double fa[HERM ? JOBS : 1], fb[HERM ? JOBS : 1];
+  if constexpr (HERM) {
+#pragma unroll
+    for (int j = 0; j < JOBS; ++j) {
+      int sp, rp, ss, rs;
+      int64_t cp;
+      job(j, sp, rp, cp, ss, rs);
+      const bool self = col0 && sp == 0 && rp == 0;
+      const int64_t kp = cp + (int64_t)rp * N2, kb = self ? nt : nt - kp;
+      tv[j] = tw[rp << (24 - m)];
+      wv[j] = col0 ? twmf[cp] : wcp;
+      av[j] = xg[kp];
+      bv[j] = xg[kb];
+      if (fr) {
+        fa[j] = fr[kp];
+        fb[j] = fr[kb];
+      }
+    }
+  }
+#pragma unroll FGP_C2R_UNROLL
+  for (int j = 0; j < JOBS; ++j) {
+    int sp, rp, ss, rs;
+    int64_t cp;
+    job(j, sp, rp, cp, ss, rs);
     const bool self = col0 && sp == 0 && rp == 0;   // frequencies 0, n/2 and (second element) n/4, 3n/4
-    const double2 wc = col0 ? twmf[cp] : wcp;
-    const double2 W = cmul(wc, tw[rp << (24 - m)]);                 // w_n^k, k = cp + N2 rp
+    double2 W;                                                        // w_n^k, k = cp + N2 rp
+    if constexpr (HERM) {
+      W = cmul(wv[j], tv[j]);
+    } else {
+      W = cmul(col0 ? twmf[cp] : wcp, tw[rp << (24 - m)]);
+    }
     const int64_t kp = cp + (int64_t)rp * N2;
     double2 h0, h1, vp, vs;
-    herm(kp, self ? 0 : nt - kp, h0, h1);
-    if (self) {   // partners of 0 and n/2 are themselves: the real parts
-      h0 = make_double2(xv(0).x, 0.0);
-      h1 = make_double2(xv(nt).x, 0.0);
+    if constexpr (HERM) {   // xv(kp), conj xv(nt - kp); self: the real parts of xv(0), xv(nt)
+      const double2 a = fr ? make_double2(av[j].x * fa[j], av[j].y * fa[j]) : av[j];
+      const double2 b = fr ? make_double2(bv[j].x * fb[j], bv[j].y * fb[j]) : bv[j];
+      h0 = self ? make_double2(a.x, 0.0) : a;
+      h1 = make_double2(b.x, self ? 0.0 : -b.y);
+    } else {
+      herm(kp, self ? 0 : nt - kp, h0, h1);
+      if (self) {   // partners of 0 and n/2 are themselves: the real parts
+        h0 = make_double2(xv(0).x, 0.0);
+        h1 = make_double2(xv(nt).x, 0.0);
+      }
     }
     vpack(h0, h1, W, vp, vs);
     lds[sp * CS + rp] = vp;
@@ -990,11 +1050,22 @@ __global__ __launch_bounds__(kWG) void k_inv_rows_c2r(const double2* __restrict_
   adj_reg_passes<P2, LastPass<P2>::S, true>(v, ldsd, tid, tw);
   if (tid == 0) v[0] += mean * (double)N2;
   const double gs = 1.0 / sqrt((double)n);
-  double* xo = out + g * out_stride + (int64_t)row0 * N2 + 16 * tid;
+  double* xo = out + g * out_stride + (int64_t)row0 * N2;
+  // v[k] is element 16 tid + k of the row: the Re (then Im) parts go through LDS so that a store
+  // instruction's lanes cover consecutive 16 B (direct stores put the lanes 128 B apart: 64 partial lines
+  // per instruction)
+  __syncthreads();
 #pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    *reinterpret_cast<double2*>(xo + 2 * u) = make_double2(v[2 * u].x * gs, v[2 * u + 1].x * gs);
-    *reinterpret_cast<double2*>(xo + nt + 2 * u) = make_double2(v[2 * u].y * gs, v[2 * u + 1].y * gs);
+  for (int half = 0; half < 2; ++half) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) ldsd[kRunPad * tid + k] = (half ? v[k].y : v[k].x) * gs;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int p = 2 * (tid + kWG * u), a = run_pad(p);
+      *reinterpret_cast<double2*>(xo + half * nt + p) = make_double2(ldsd[a], ldsd[a + 1]);
+    }
+    if (half == 0) __syncthreads();
   }
 }
 
