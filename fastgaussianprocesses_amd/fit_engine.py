@@ -205,13 +205,19 @@ class FusedMLL(object):
         cdt = torch.complex128 if self.family == 0 else torch.float64
         self.work = torch.empty((G, n), dtype=cdt, device=self.device) if (self.m > 12 and basis is None and
                                                                            mt is None) else None
-        # Rprop state (previous gradient, step sizes) and the gradient in one allocation
-        st = torch.zeros((3, self.n_params), dtype=torch.float64, device=self.device)
+        # Rprop state (previous gradient, step sizes), the gradient and the loss / parameter histories in ONE
+        # zeroed allocation (one fill kernel + the step sizes' fill: a graph-replayed small fit pays per node)
+        self.per_problem = bool(G == 1 if per_problem is None else per_problem)
+        hmax = max(int(max_iters), 16)                  # ensure_history's first size
+        hg = self.G if self.per_problem else 1
+        np_ = self.n_params
+        blob = torch.zeros((3 * np_ + hmax * hg * 3 + hmax * np_,), dtype=torch.float64, device=self.device)
+        st = blob[:3 * np_].view(3, np_)
         st[1].fill_(float(lr))
         self.prev, self.step, self.grad = st[0], st[1], st[2]
-        self.max_iters = 0
-        self.loss_hist = None
-        self.raw_hist = None
+        self.loss_hist = blob[3 * np_:3 * np_ + hmax * hg * 3].view(hmax, hg, 3)
+        self.raw_hist = blob[3 * np_ + hmax * hg * 3:].view(hmax, np_)
+        self.max_iters = hmax
         self._init_max_iters = max_iters
         self._nll = N.NllDesc(
             family=self.family, log2n=self.m, d=self.d, G=self.G,
@@ -234,8 +240,11 @@ class FusedMLL(object):
             # and every problem's Y of it are two contiguous runs
             Q = spec_chunks(self.family, n)
             w = min(n, Q * 64)
-            yp = torch.zeros((G, Q * 64), dtype=torch.float64, device=self.device)
-            yp[:, :w] = self.ysq[:, :w]
+            if w == Q * 64:                              # no padding: one copy (G = 1) or the transposing copy
+                yp = self.ysq[:, :w].clone() if G == 1 else self.ysq[:, :w]
+            else:
+                yp = torch.zeros((G, Q * 64), dtype=torch.float64, device=self.device)
+                yp[:, :w] = self.ysq[:, :w]
             self.ysq = yp.view(G, Q, 64).transpose(0, 1).contiguous()
             self._nll.ysq = self.ysq.data_ptr()
             self._nll.ysq_chunked = 1
@@ -253,10 +262,10 @@ class FusedMLL(object):
         N.call("fgp_nll_partials_len", self._nll, ctypes.byref(plen))
         self.partials = torch.empty((plen.value,), dtype=torch.float64, device=self.device)
         self._nll.partials = self.partials.data_ptr()
-        self.per_problem = bool(G == 1 if per_problem is None else per_problem)
         self.requires_grad = tuple(int(bool(r)) for r in requires_grad)
         self.mll_const = float(mll_const)
         self._fit = None
+        self._refresh_fit_desc()
         self.ensure_history(self._init_max_iters)
 
     def ensure_history(self, iters):
@@ -337,7 +346,7 @@ class FusedMLL(object):
         check_persist at the next eager call, and a failure shows as NaN parameters and parameter history."""
         self.check_persist()
         self.ensure_history(iterations + 1)
-        ctrl = torch.zeros((4,), dtype=torch.int32, device=self.device)
+        ctrl = torch.empty((4,), dtype=torch.int32, device=self.device)   # (the launch clears the words it reports)
         capturing = torch.cuda.is_current_stream_capturing()
         raw0 = None if capturing else self.raw.clone()
         N.call("fgp_fit_persist", self._nll, self._fit, int(iterations), float(logtol), int(wait_max),
