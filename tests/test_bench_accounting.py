@@ -116,3 +116,40 @@ def test_c4_fixture_inputs_are_the_benched_shifts():
         assert np.array_equal(s.z, g["z"]) and np.array_equal(s.shift, g["shift"][p])
     assert g["loss_hist"].shape == (2, int(g["its"]) + 1)
     assert np.isfinite(g["pmean"]).all() and (g["pvar"] >= 0).all()
+
+
+def test_timed_region_stats_takes_the_launches_between_the_markers(tmp_path):
+    """tools/timed_region_stats.py: only the kernels between the first two k_clock_stamp launches count (bench.py
+    brackets its timed loop with them), in kstats_grid's table format that bench.rocprof_avg_us reads."""
+    import csv
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    rows = []
+    t = 0
+
+    def add(name, dur, grid=131072):
+        nonlocal t
+        rows.append({"Kernel_Name": name, "Grid_Size_X": str(grid), "Start_Timestamp": str(t),
+                     "End_Timestamp": str(t + dur)})
+        t += dur
+
+    add("void fgp::k_spec_tile<5, 2, false, false>(fgp::Nll, fgp::FitFuse)", 40000)    # eager, before
+    add("fgp::k_clock_stamp(unsigned long long*)", 2000, 64)
+    for _ in range(3):
+        add("void fgp::k_spec_tile<5, 2, false, false>(fgp::Nll, fgp::FitFuse)", 37000)
+    add("fgp::k_clock_stamp(unsigned long long*)", 2000, 64)
+    add("void fgp::k_spec_tile<5, 2, false, false>(fgp::Nll, fgp::FitFuse)", 45000)    # eager, after
+    add("fgp::k_clock_stamp(unsigned long long*)", 2000, 64)
+    path = tmp_path / "trace.csv"
+    with open(path, "w", newline="") as fh:
+        w = csv.DictWriter(fh, fieldnames=list(rows[0].keys()))
+        w.writeheader()
+        w.writerows(rows)
+    out = subprocess.run([sys.executable, os.path.join(root, "tools", "timed_region_stats.py"), str(path)],
+                         capture_output=True, text=True, check=True).stdout
+    stats = tmp_path / "timed.txt"
+    stats.write_text(out)
+    assert bench.rocprof_avg_us("k_spec_tile<5, 2, false, false>", 131072, path=str(stats)) == 37.0
+    assert "timed region: 3 launches" in out

@@ -17,8 +17,10 @@ if [ -z "$NOBENCH" ]; then
   timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
   timeout -k 10 700 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err
   python -c "import json;d=json.load(open('$OUT/bench.json'));print(d['value'], d['ms_per_step'], d['phases_ms'], d['roofline']['frac'], d['roofline_predict'].get('frac'))"
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-secondary --no-multitask --no-paper --no-graph > $OUT/bench_prof.json 2> $OUT/bench_prof.err
+  # the bench command itself (graph replays in its timed region): every launch, and the timed region's alone
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-secondary --no-multitask --no-paper > $OUT/bench_prof.json 2> $OUT/bench_prof.err
   python tools/kstats_grid.py $OUT/prof/bench_kernel_trace.csv 60 > $OUT/grid_stats.txt; head -8 $OUT/grid_stats.txt
+  python tools/timed_region_stats.py $OUT/prof/bench_kernel_trace.csv 60 > $OUT/timed_stats.txt; head -6 $OUT/timed_stats.txt; tail -1 $OUT/timed_stats.txt
 fi
 if [ -z "$NOPMC" ]; then
   timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o fetch -- python3 tools/fit_kernels.py > $OUT/pmc_fetch.log 2>&1
