@@ -1,0 +1,13 @@
+#!/bin/bash
+# A/B of the spectral blocks' minimum chunk count (FGP_SPEC_MINC) on the C2 / C3 single-launch fits: kernel trace
+# of tools/prof_single.py per setting
+export TMPDIR=/tmp
+OUT=gpurun_out/minc
+mkdir -p $OUT
+set -e
+for m in 4 2 1 8; do
+  for fam in lattice net; do
+    FGP_SPEC_MINC=$m timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d $OUT/m${m}_$fam -o t -- python3 tools/prof_single.py --family $fam --reps 4 > $OUT/m${m}_$fam.log 2>&1
+  done
+done
+echo done
