@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B of the spectral blocks' minimum chunk count (FGP_SPEC_MINC) on the C2 / C3 single-launch fits: kernel trace
+# A/B of the spectral blocks' minimum chunk count on the C2 / C3 single-launch fits (needs the FGP_SPEC_MINC knob of the r05z A/B build, since reverted: profiles/r05z_persist_minc_ab.json): kernel trace
 # of tools/prof_single.py per setting
 export TMPDIR=/tmp
 OUT=gpurun_out/minc
