@@ -784,12 +784,41 @@ def roofline_fit_kernels(F, shifts, iters):
         e1.record()
         torch.cuda.synchronize()
         us_ev = {names[0]: 1e3 * e0.elapsed_time(e1) / iters}
+        # the same call replayed from a hipGraph, as the timed step runs it (a replayed launch skips the eager
+        # enqueue's per-packet work): HIP events around the replays, per iteration
+        us_ev[names[0] + "@graph"] = graph_fit_us(eng, iters)
     us = {name: float(dur_us[:, k].mean()) for k, name in enumerate(names)}
     if not fused:
         us_ev["k_fit_reduce_step"] = 1e3 * sum(e[ns].elapsed_time(e[ns + 1]) for e in ev) / iters
         us["k_fit_reduce_step"] = us_ev["k_fit_reduce_step"]
-    t_iter = sum(us_ev.values()) / 1e6
+    t_iter = sum(v for k, v in us_ev.items() if not k.endswith("@graph")) / 1e6
     return n, variant, us, us_ev, t_iter, khz
+
+
+def graph_fit_us(eng, iters, reps=5):
+    """Per-iteration time of eng.run(0, iters) (fgp_fit_run: one k_spec_tile per iteration + the final step)
+    captured once into a hipGraph and replayed `reps` times between two HIP events; None when the capture fails."""
+    try:
+        cur = torch.cuda.current_stream()
+        s = torch.cuda.Stream()
+        s.wait_stream(cur)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
+                eng.run(0, iters)
+        cur.wait_stream(s)
+        g.replay()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        return 1e3 * e0.elapsed_time(e1) / (reps * iters)
+    except Exception:                   # capture not possible here
+        _clear_capture_error()
+        return None
 
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -1145,6 +1174,9 @@ def main():
             "first workgroup start to last wave end, mean of %d launches" % (khz, args.fit_iters),
             "frac_device_clock": sb[dom] / (us[dom] * 1e-6) / 1e9 / HBM_PEAK_GBS,
             "avg_us_events": us_ev[dom],
+            "avg_us_graph_events": us_ev.get(dom + "@graph"),
+            "avg_us_graph_events_source": "this run: HIP events around hipGraph replays of the fit's launch sequence "
+                                          "(fgp_fit_run captured, as in the timed step), per iteration",
             "launch": "%d problems x n=2^%d (grid %d workgroups)" % (P, args.log2n, grid_wg),
             "transform": {"re": "real-even: n/2-point transform, columns [0, N2/2) (n/4 complex)",
                           "r2c": "half-length R2C (n/2 complex)", "full": "full-length (n complex)",
