@@ -12,7 +12,7 @@ import torch
 
 _LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
 LIB_PATH = os.environ.get("FGP_LIB_PATH") or os.path.join(_LIB_DIR, "libfgp_hip.so")   # override: experiments
-ABI_VERSION = 16
+ABI_VERSION = 17
 MT_MAX_TASKS = 16
 MAX_D = 8
 PARTS_ARRAY = 0
@@ -166,6 +166,7 @@ _SIGNATURES = {
     "fgp_mt_fit_run": [_P_MTFIT, _c_int, _c_int, _c_int, _c_vp],
     "fgp_handoff_check": [_c_int, ctypes.POINTER(ctypes.c_ulonglong)],
     "fgp_set_persist_poll_max": [_c_i64],
+    "fgp_persist_giveups": [ctypes.POINTER(ctypes.c_ulonglong), _c_int],
     "fgp_set_mt_class_kernel": [_c_int],
     "fgp_nll_partials_len": [_P_NLL, _c_pl],
     "fgp_spec_basis": [_c_int, _c_vp, _c_i64, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_i64, _c_vp],

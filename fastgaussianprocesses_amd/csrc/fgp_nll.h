@@ -651,6 +651,7 @@ int launch_spec_finish_step(const Nll& a, const FitFuse& fz, hipStream_t st);
 // the whole fit of one small spectral problem in one launch (fgp_fit_persist): geometry / applicability, launch
 int spec_persist_geometry(const Nll& a, int* W, int* bpw, size_t* shm);
 void set_persist_poll_max(long long v);
+int persist_giveups(unsigned long long* count, int reset);
 int launch_spec_persist(const Nll& a, const Fit& f, int iters, double logtol, int wait_max, unsigned* counter, int* out,
                         hipStream_t st);
 int launch_spec_lam(const Nll& a, hipStream_t st);    // lambda of the current parameters into grad_lam

@@ -2090,6 +2090,11 @@ int fgp_set_persist_poll_max(long long polls) {
   return kOk;
 }
 
+int fgp_persist_giveups(unsigned long long* count, int reset) {
+  if (!count) return set_error(kErrInvalid, "fgp_persist_giveups: null count");
+  return persist_giveups(count, reset);
+}
+
 int fgp_handoff_check(int enable, unsigned long long* out) {
   const size_t bytes = sizeof(unsigned long long) * (kHandoffWords + 2);
   if (enable) {

@@ -750,18 +750,22 @@ static const void* post_mean_kernel(bool uniform4, int B) {
 // Workgroups of a post_mean instance resident at once on the current device (workgroups per CU x CUs), queried
 // once per instance and remembered (no query inside a hipGraph capture after the first eager call); 0 if unknown.
 static int64_t post_mean_resident(const void* kp) {
+  // keyed by (instance, device): devices of one process may differ in CU count / partition mode
   static const void* rk[256];
+  static int rdev[256];
   static int64_t rres[256];
   static int nr = 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
   for (int i = 0; i < nr; ++i)
-    if (rk[i] == kp) return rres[i];
-  int per_cu = 0, dev = 0, cus = 0;
-  const int64_t res = (hipGetDevice(&dev) == hipSuccess &&
-                       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+    if (rk[i] == kp && rdev[i] == dev) return rres[i];
+  int per_cu = 0, cus = 0;
+  const int64_t res = (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
                        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kp, kWG, 0) == hipSuccess)
                           ? (int64_t)per_cu * cus : 0;
   if (nr < 256) {
     rk[nr] = kp;
+    rdev[nr] = dev;
     rres[nr++] = res;
   }
   return res;

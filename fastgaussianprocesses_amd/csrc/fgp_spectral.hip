@@ -233,6 +233,8 @@ __device__ __forceinline__ gdouble* gptr(const double* p) { return (gdouble*)(co
 __device__ __forceinline__ void st_part_sc1(double* p, double v) {
   __hip_atomic_store(gptr(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+typedef __attribute__((address_space(1))) unsigned guint;
+__device__ __forceinline__ guint* gptr_u(unsigned* p) { return (guint*)p; }
 
 template <int D, bool NET>
 __device__ __forceinline__ void spec_block_partials(const Nll& a, const Hyp& h, int g, int blk, double rootn, double wl,
@@ -674,6 +676,15 @@ constexpr int kPersistMaxW = 256;
 constexpr long long kSpecPollMax = 1ll << 22;     // bounded waits of the persistent k_spec_tile
 constexpr int kPersistLdsMax = 96 * 1024;
 constexpr long long kPersistPollMax = 1ll << 22;
+// the wall-clock bound of one barrier wait of the single-launch fit (device clock ticks: 5e6 = 50 ms at the 100 MHz
+// constant clock of fgp_wall_clock_khz) -- a give-up then costs milliseconds, not 2^22 polls of seconds
+constexpr unsigned long long kPersistWaitTicks = 5000000ull;
+// give-ups of k_spec_persist since load / the last reset (fgp_persist_giveups): never cleared by a launch, so a failure
+// inside a hipGraph replay is still visible after it
+__device__ unsigned long long g_persist_giveups = 0;
+// the poll bound of those waits (fgp_set_persist_poll_max): read by the kernel from device memory, so the test hook
+// also reaches launches replayed from a hipGraph captured before it was set
+__device__ long long g_persist_poll_max_dev = kPersistPollMax;
 // an empty partial slot of the single-launch fit (all ones: a NaN payload no arithmetic produces; the buffers are
 // filled with it before the launch)
 constexpr long long kPartEmpty = -1ll;
@@ -689,7 +700,7 @@ __device__ __forceinline__ void barrier_keep_vm() {
 
 template <int D, bool NET>
 __global__ __launch_bounds__(kWG) void k_spec_persist(Nll a, Fit f, int iters, double logtol, int wait_max, int bpw,
-                                                      unsigned* counter, int* out, long long poll_max) {
+                                                      unsigned* counter, int* out) {
   constexpr int NS = 1 << D, NQ = 4 + D, MAXG = kSpecBlocks / kSpecGroup;
   extern __shared__ double lds[];                  // [bpw][kpl][NS + 1][64] spectra + Y of this workgroup's blocks
   __shared__ double st_raw[kSpecScratch], st_prev[kSpecScratch], st_step[kSpecScratch];
@@ -701,6 +712,7 @@ __global__ __launch_bounds__(kWG) void k_spec_persist(Nll a, Fit f, int iters, d
   const int W = gridDim.x, kpl = a.spec_kpl, np = spec_nparams(a), ng = spec_groups(a);
   const int64_t main = a.spec_main, B = 64 * (int64_t)kpl;
   const int blk0 = (int)blockIdx.x * bpw;
+  const long long poll_max = g_persist_poll_max_dev;
   // the blocks' spectra and Y into LDS (chunked layouts: chunk q of the spectra at q NS 64, Y at q 64 for G = 1)
   const int per_blk = kpl * (NS + 1) * 64;
   for (int e = tid; e < bpw * per_blk; e += kWG) {
@@ -791,6 +803,7 @@ __global__ __launch_bounds__(kWG) void k_spec_persist(Nll a, Fit f, int iters, d
         const double* pp = pbase + (int64_t)q * a.nb + b0;
         double tv[kSpecGroup];
         long long polls = 0;
+        const unsigned long long t_wait = wall_clock64();
         for (;;) {
 #pragma unroll
           for (int b = 0; b < kSpecGroup; ++b) tv[b] = ld_part<true>(pp + (b < nbg ? b : 0));
@@ -798,11 +811,15 @@ __global__ __launch_bounds__(kWG) void k_spec_persist(Nll a, Fit f, int iters, d
 #pragma unroll
           for (int b = 0; b < kSpecGroup; ++b) full = full && __double_as_longlong(tv[b]) != kPartEmpty;
           if (full) break;
-          __builtin_amdgcn_s_sleep(1);
-          if (++polls > poll_max) {
+          // give up on the poll bound (test hook), the wall-clock bound, or another workgroup's give-up (the launch's
+          // fail word, ctrl[0]: a workgroup that starts only after the others exited stops at its first poll)
+          if (++polls > poll_max || wall_clock64() - t_wait > kPersistWaitTicks ||
+              __hip_atomic_load(gptr_u(counter), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+            __hip_atomic_store(gptr_u(counter), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             fail_s = 1;
             break;
           }
+          __builtin_amdgcn_s_sleep(1);
         }
         double sgrp = 0.0;
 #pragma unroll
@@ -816,7 +833,10 @@ __global__ __launch_bounds__(kWG) void k_spec_persist(Nll a, Fit f, int iters, d
         // parameters and every parameter-history row become NaN -- whichever row the caller restores as the best
         // iterate, the failure shows downstream even when `out` is never read (a hipGraph replay).  Rprop's prev /
         // step are untouched: with the caller's copy of the entry raw parameters the fit can be re-run.
-        if (tid == 0) out[1] = 1;
+        if (tid == 0) {
+          out[1] = 1;
+          atomicAdd(&g_persist_giveups, 1ull);        // the library's sticky count (fgp_persist_giveups)
+        }
         for (int p = tid; p < np; p += kWG) f.raw[p] = NAN;
         if (f.raw_hist)
           for (int64_t e = tid; e < (int64_t)(iters + 1) * f.n_params; e += kWG) f.raw_hist[e] = NAN;
@@ -1019,10 +1039,11 @@ __global__ __launch_bounds__(kWG) void k_spec_loss_step(Nll a, Fit f, int iter, 
     gs[pair * MAXG + grp] = spec_group_sum<false>(a, g0 + pair / NQ, pair % NQ, grp);
   }
   __syncthreads();
-  if ((int)threadIdx.x < cnt * NQ) {
+  // strided: cnt NQ reaches 16 (6 + 2 D) = 288 > kWG totals at D = 6
+  for (int u = threadIdx.x; u < cnt * NQ; u += kWG) {
     double s = 0.0;
-    for (int grp = 0; grp < ng; ++grp) s += gs[threadIdx.x * MAXG + grp];
-    tot[threadIdx.x] = s;
+    for (int grp = 0; grp < ng; ++grp) s += gs[u * MAXG + grp];
+    tot[u] = s;
   }
   __syncthreads();
   const double n = (double)((int64_t)1 << a.log2n);
@@ -2080,30 +2101,36 @@ static const void* spec_persist_kernel(const Nll& a) {
 // (workgroups per CU x CUs), queried once per (kernel, LDS size) and remembered -- so a launch inside a hipGraph
 // capture makes no query.  0 when the query fails.
 static int64_t persist_resident(const void* kp, size_t shm) {
+  // keyed by the device too: devices of one process may differ in CU count / partition mode
   static const void* rk[64];
   static size_t rshm[64];
+  static int rdev[64];
   static int64_t rres[64];
   static int nr = 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
   for (int i = 0; i < nr; ++i)
-    if (rk[i] == kp && rshm[i] == shm) return rres[i];
+    if (rk[i] == kp && rshm[i] == shm && rdev[i] == dev) return rres[i];
   (void)hipFuncSetAttribute(kp, hipFuncAttributeMaxDynamicSharedMemorySize, kPersistLdsMax);
-  int per_cu = 0, dev = 0, cus = 0;
-  const int64_t resident = (hipGetDevice(&dev) == hipSuccess &&
-                            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+  int per_cu = 0, cus = 0;
+  const int64_t resident = (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
                             hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kp, kWG, shm) == hipSuccess)
                                ? (int64_t)per_cu * cus : 0;
   if (nr < 64) {
     rk[nr] = kp;
     rshm[nr] = shm;
+    rdev[nr] = dev;
     rres[nr++] = resident;
   }
   return resident;
 }
 
-// Test hook (fgp_set_persist_poll_max): the bound of k_spec_persist's barrier polls (default 2^22).
-static long long g_persist_poll_max = kPersistPollMax;
-
-void set_persist_poll_max(long long v) { g_persist_poll_max = v < 0 ? kPersistPollMax : v; }
+// Test hook (fgp_set_persist_poll_max): the bound of k_spec_persist's barrier polls (default 2^22), in device memory.
+void set_persist_poll_max(long long v) {
+  const long long pm = v < 0 ? kPersistPollMax : v;
+  (void)hipDeviceSynchronize();
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_persist_poll_max_dev), &pm, sizeof(pm), 0, hipMemcpyHostToDevice);
+}
 
 int spec_persist_geometry(const Nll& a, int* W, int* bpw, size_t* shm) {
   if (!a.spec || a.G != 1 || a.basis_stride != 0 || a.d > kSpecMaxD || !a.ysq_chunked || a.loss != FGP_LOSS_MLL)
@@ -2126,23 +2153,36 @@ int spec_persist_geometry(const Nll& a, int* W, int* bpw, size_t* shm) {
   return set_error(kErrUnsupported, "fgp_fit_persist: the spectra do not fit %d workgroups' LDS", kPersistMaxW);
 }
 
+int persist_giveups(unsigned long long* count, int reset) {
+  if (hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpyFromSymbol(count, HIP_SYMBOL(g_persist_giveups), sizeof(unsigned long long), 0,
+                          hipMemcpyDeviceToHost) != hipSuccess)
+    return set_error(kErrHip, "fgp_persist_giveups: read failed");
+  if (reset) {
+    const unsigned long long z = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_persist_giveups), &z, sizeof(z), 0, hipMemcpyHostToDevice) != hipSuccess)
+      return set_error(kErrHip, "fgp_persist_giveups: reset failed");
+  }
+  return kOk;
+}
+
 int launch_spec_persist(const Nll& a, const Fit& f, int iters, double logtol, int wait_max, unsigned* counter, int* out,
                         hipStream_t st) {
   int W, bpw;
   size_t shm;
   int rc = spec_persist_geometry(a, &W, &bpw, &shm);
   if (rc != kOk) return rc;
-  // the three partial buffers empty (kPartEmpty: all bytes 0xff), the control word cleared
-  (void)counter;
+  // the three partial buffers empty (kPartEmpty: all bytes 0xff), the fail word (counter = ctrl[0]) and the control
+  // words out[0..1] (= ctrl[1..2]) cleared
   if (hipMemsetAsync(a.partials, 0xff, 3 * sizeof(double) * (size_t)a.nq * (size_t)a.nb, st) != hipSuccess ||
-      hipMemsetAsync(out, 0, 2 * sizeof(int), st) != hipSuccess)
+      hipMemsetAsync(counter, 0, 3 * sizeof(unsigned), st) != hipSuccess || out != reinterpret_cast<int*>(counter + 1))
     return set_error(kErrHip, "fgp_fit_persist: workspace reset failed");
   return with_spec_d(a.d, [&](auto dc) {
     constexpr int D = decltype(dc)::value;
     auto go = [&](auto kern) {
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 kPersistLdsMax);
-      kern<<<(unsigned)W, kWG, shm, st>>>(a, f, iters, logtol, wait_max, bpw, counter, out, g_persist_poll_max);
+      kern<<<(unsigned)W, kWG, shm, st>>>(a, f, iters, logtol, wait_max, bpw, counter, out);
     };
     if (a.spec_net) go(k_spec_persist<D, true>);
     else go(k_spec_persist<D, false>);

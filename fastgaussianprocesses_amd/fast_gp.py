@@ -29,7 +29,7 @@ from . import _native
 from . import ops
 from . import seqs as _seqs
 from .fit_engine import (SPEC_MAX_D, FusedMLL, LatticePartsGen, mll_constant, spec_basis, spec_basis_gen, spec_inv_eig,
-                         spec_post_var, spectral_wanted)
+                         spec_k, spec_post_var, spectral_wanted)
 
 
 def _log(x):
@@ -516,7 +516,7 @@ class AbstractFastGP(torch.nn.Module):
         with `force` whenever it applies (d <= 6, the spectra <= 16 GiB: the GCV / CV fits, which only it runs),
         else None.  Hyper-parameter independent; cached with the data (dropped by add_y_next)."""
         if force:
-            if self.d > SPEC_MAX_D or n < 16 or (2 ** self.d) * (n // 2 + 1) * 8 > (16 << 30):
+            if self.d > SPEC_MAX_D or n < 16 or (2 ** self.d) * spec_k(self._FAMILY, n) * 8 > (16 << 30):
                 return None
         elif not spectral_wanted(self._FAMILY, n, self.d, G):
             return None

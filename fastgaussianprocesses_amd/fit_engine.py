@@ -456,6 +456,24 @@ class FusedMLL(object):
         return raw_vec[..., :S], raw_vec[..., S:S + L], raw_vec[..., S + L:S + L + Nn]
 
 
+def persist_giveups(reset=False):
+    """The library's sticky count of single-launch-fit barrier give-ups (fgp_persist_giveups, ABI 17; synchronises)."""
+    c = ctypes.c_ulonglong(0)
+    N.call("fgp_persist_giveups", ctypes.byref(c), int(bool(reset)))
+    return int(c.value)
+
+
+def check_replayed_fits(before):
+    """Raise when a single-launch fit gave up since the count `before` (persist_giveups()) was read: after hipGraph
+    replays of captured fits, whose control words the capture could not read -- such a fit's parameters are NaN, not
+    a result (fit_engine.FusedMLL.run_persist)."""
+    now = persist_giveups()
+    if now != before:
+        raise RuntimeError("fgp_fit_persist: %d in-kernel barrier give-up(s) during replayed fits (their parameters are "
+                           "NaN; workgroups not co-resident?)" % (now - before))
+    return now
+
+
 def mll_constant(d_out, n):
     """d_out * n * log(2 pi) (fastgps/abstract_gp.py:235)."""
     return d_out * n * math.log(2 * math.pi)

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define FGP_ABI_VERSION 16
+#define FGP_ABI_VERSION 17
 
 #define FGP_OK 0
 #define FGP_ERR_INVALID (-1)     /* bad argument (shape, stride, null pointer) */
@@ -614,6 +614,12 @@ int fgp_handoff_check(int enable, unsigned long long* out);
  * and the host's fallback to the launch per iteration can be tested.  fgp_fit_persist_ok / fgp_fit_persist
  * also report unsupported (0 / an error) when the workgroups would not all be co-resident. */
 int fgp_set_persist_poll_max(long long polls);
+
+/* ABI 17 -- the library's sticky count of fgp_fit_persist barrier give-ups (a give-up counts once per workgroup that
+ * gave up; never cleared by a launch): read after hipGraph replays of captured fits, whose control words cannot be read
+ * during the capture (AbstractGP.fit's result would otherwise be NaN parameters nobody reported, abstract_gp.py:297-298).
+ * Synchronises the device; reset != 0 zeroes the count after reading it. */
+int fgp_persist_giveups(unsigned long long* count, int reset);
 
 /* ABI 16 -- test hook (no reference counterpart): the per-class kernel of fgp_mt_fit_run: 0 automatic (a wave per
  * frequency class while problems x classes <= 8192 and a class fits 60 KB of LDS, else a thread per class), 1 a

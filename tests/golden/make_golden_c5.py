@@ -6,6 +6,11 @@ reference's own FFT-backend sensitivity there (VERDICT r02 "Next round" item 1).
 
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_c5.py --per-output
 
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_c5.py [--per-output] --its 50
+
+--its 50 (round 6): the benched length, fit(iterations=50, stop_crit_wait_iterations=51), written to the *_it50.npz
+fixtures and profiles/r06_c5*_backend_spread.json.
+
 Writes tests/golden/c5_m18_d3_b512.npz (inputs: the point set's generating vector + shift and the data
 seed; outputs: the reference's fit(iterations=3) loss / parameter trajectory, post_mean at 16 test points,
 post_var at 2), tests/golden/c5_m18_d3_b512_f32data.npz (the same on the observations rounded to float32:
@@ -33,7 +38,12 @@ sys.path.insert(0, HERE)
 from oracle.refshim.load_reference import import_reference  # noqa: E402
 from make_golden import LATTICE_Z, f_ackley  # noqa: E402
 
-M, D, B, ITS, NM, NV = 18, 3, 512, 3, 16, 2
+M, D, B, NM, NV = 18, 3, 512, 16, 2
+# --its N: the fit length (3: the original fixtures; 50: the benched length, VERDICT r05 item 1 -- files and spread
+# records then carry the suffix _it50 / r06_)
+ITS = int(sys.argv[sys.argv.index("--its") + 1]) if "--its" in sys.argv else 3
+SUF = "" if ITS == 3 else "_it%d" % ITS
+STOP = ITS + 5 if ITS == 3 else ITS + 1      # early stopping off either way
 
 
 def c5_data(x, B, seed=5):
@@ -94,7 +104,7 @@ def run(fg, qmcpy, backend, f32_data=False):
     if f32_data:     # the mixed-precision C5 path's observations (data_dtype=float32), fp64 from there on
         y = y.float().double()
     gp.add_y_next(y)
-    data = gp.fit(iterations=ITS, store_hists=True, verbose=0, stop_crit_wait_iterations=ITS + 5)
+    data = gp.fit(iterations=ITS, store_hists=True, verbose=0, stop_crit_wait_iterations=STOP)
     xt = torch.rand((NM, D), generator=torch.Generator().manual_seed(17))
     pm = gp.post_mean(xt)
     pv = gp.post_var(xt[:NV])
@@ -133,7 +143,7 @@ def run_per_output(fg, qmcpy, backend):
         if yfull is None:
             yfull = c5_data(x, B)
         gp.add_y_next(yfull[a:a + Bc].clone())
-        data = gp.fit(iterations=ITS, store_hists=True, verbose=0, stop_crit_wait_iterations=ITS + 5)
+        data = gp.fit(iterations=ITS, store_hists=True, verbose=0, stop_crit_wait_iterations=STOP)
         xt = torch.rand((NM, D), generator=torch.Generator().manual_seed(17))
         pm = gp.post_mean(xt)
         pv = gp.post_var(xt[:NV])
@@ -152,7 +162,7 @@ def run_per_output(fg, qmcpy, backend):
 
 def main_per_output(fg, qmcpy):
     keep = (qmcpy.fftbr_torch, qmcpy.ifftbr_torch)
-    path = os.path.join(HERE, "c5_m18_d3_b512_po.npz")
+    path = os.path.join(HERE, "c5_m18_d3_b512_po%s.npz" % SUF)
     if "--reuse" in sys.argv and os.path.isfile(path):      # the torch-backend fixture of an earlier run
         ref = dict(np.load(path))
     else:
@@ -172,7 +182,7 @@ def main_per_output(fg, qmcpy):
               "raw_scale_abs": float(np.max(np.abs(alt["raw_scale"] - ref["raw_scale"]))),
               "pmean_rel": rel(alt["pmean"], ref["pmean"]),
               "pvar_abs_over_kxx": float(np.max(np.abs(alt["pvar"] - ref["pvar"]) / kdiag))}
-    with open(os.path.join(ROOT, "profiles", "r04_c5_po_backend_spread.json"), "w") as f:
+    with open(os.path.join(ROOT, "profiles", "r04_c5_po_backend_spread.json" if ITS == 3 else "r06_c5_po_backend_spread.json"), "w") as f:
         json.dump(spread, f, indent=1)
     print(json.dumps(spread, indent=1))
 
@@ -186,10 +196,10 @@ def main():
         return main_per_output(fg, qmcpy)
     keep = (qmcpy.fftbr_torch, qmcpy.ifftbr_torch)
     ref = run(fg, qmcpy, "torch")
-    np.savez_compressed(os.path.join(HERE, "c5_m18_d3_b512.npz"), m=np.array(M), d=np.array(D), B=np.array(B),
+    np.savez_compressed(os.path.join(HERE, "c5_m18_d3_b512%s.npz" % SUF), m=np.array(M), d=np.array(D), B=np.array(B),
                         its=np.array(ITS), **{k: np.asarray(v) for k, v in ref.items()})
     r32 = run(fg, qmcpy, "torch", f32_data=True)
-    np.savez_compressed(os.path.join(HERE, "c5_m18_d3_b512_f32data.npz"), m=np.array(M), d=np.array(D),
+    np.savez_compressed(os.path.join(HERE, "c5_m18_d3_b512_f32data%s.npz" % SUF), m=np.array(M), d=np.array(D),
                         B=np.array(B), its=np.array(ITS), **{k: np.asarray(v) for k, v in r32.items()})
     alt = run(fg, qmcpy, "numpy")
     qmcpy.fftbr_torch, qmcpy.ifftbr_torch = keep
@@ -202,7 +212,7 @@ def main():
               "raw_scale_abs": float(np.max(np.abs(alt["raw_scale"] - ref["raw_scale"]))),
               "pmean_rel": rel(alt["pmean"], ref["pmean"]),
               "pvar_abs_over_kxx": float(np.max(np.abs(alt["pvar"] - ref["pvar"])) / ref["kxx"])}
-    with open(os.path.join(ROOT, "profiles", "r03_c5_backend_spread.json"), "w") as f:
+    with open(os.path.join(ROOT, "profiles", "r03_c5_backend_spread.json" if ITS == 3 else "r06_c5_backend_spread.json"), "w") as f:
         json.dump(spread, f, indent=1)
     print(json.dumps(spread, indent=1))
 

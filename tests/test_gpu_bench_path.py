@@ -185,3 +185,55 @@ def test_bench_step_50_iterations_matches_reference(monkeypatch):
         assert np.abs(raw[p, 1:1 + d] - g["raw_lengthscales"][p]).max() <= C4_TOL["params"]
         assert np.abs(pm[p] - g["pmean"][p]).max() <= C4_TOL["pmean"] * np.abs(g["pmean"][p]).max()
         assert (np.abs(pv[p] - g["pvar"][p]) <= C4_TOL["pvar_kxx"] * g["kxx"][p]).all()
+
+
+# The benched C2 / C3 work (bench.SingleGP: n = 2^16, d = 3, alpha = 2, default nugget; 50 Rprop iterations with early
+# stopping off, post_mean, post_var) against the REAL reference (tests/golden/make_golden_c23.py -> c2_m16_d3_it50.npz,
+# c3_m16_d3_a2_it50.npz).  Tolerances = 5x the reference's own spread between two correct transforms over the same 50
+# iterations (profiles/r06_c23_backend_spread.json: C2 torch.fft vs pocketfft -- loss history 6.2e-8 of its largest
+# value, post_mean 2.6e-9, post_var 5.4e-16 K(x, x), parameters identical; C3 two FWHT butterfly orders -- loss 2.4e-14,
+# post_mean 1.4e-13, post_var 1.2e-15 K(x, x), parameters identical), with the floors of the golden tests where 5x the
+# spread is below them: fitted parameters 1e-10, post_var 1e-8 K(x, x); and for C3, whose MLL the two FWHTs round
+# identically to 2e-14, the loss / post_mean floors C23_FLOOR (the spectral fit sums lambda = scale sum_S l^S Phi_S in
+# another order than ft(k1): a rounding-level difference the reference's two transforms do not show).
+C23_TOL = {"c2_m16_d3_it50": dict(loss=3.1e-7, pmean=1.3e-8, pvar_kxx=1e-8, params=1e-10),
+           "c3_m16_d3_a2_it50": dict(loss=1.2e-13, pmean=7.2e-13, pvar_kxx=1e-8, params=1e-10)}
+C23_FLOOR = dict(loss=1e-11, pmean=1e-10)
+
+
+@pytest.mark.parametrize("name", sorted(C23_TOL))
+def test_bench_c2_c3_50_iterations_match_reference(name):
+    """bench.step_single exactly as timed for C2 (FastGPLattice) and C3 (FastGPDigitalNetB2, alpha = 2): fitted
+    parameters, post_mean at the fixture's 16 points and post_var at its first 2 against the reference after 50
+    iterations; the loss history of the same fit (store_loss_hist) against the reference's."""
+    import os
+    import numpy as np
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", name + ".npz"))
+    family, m, d, its = str(g["family"]), int(g["m"]), int(g["d"]), int(g["its"])
+    dev = torch.device(DEV, 0)
+    sg = bench.SingleGP(F, family, m, d, dev)
+    seq = sg.gp.seq if hasattr(sg.gp, "seq") else sg.gp.seqs[0]
+    if family == "lattice":
+        assert np.array_equal(np.asarray(seq.z)[:d], g["z"]) and np.array_equal(seq.shift, g["shift"])
+    else:
+        assert np.array_equal(np.asarray(seq.C, dtype=np.uint64)[:d, :g["C"].shape[1]], g["C"].astype(np.uint64))
+        assert np.array_equal(np.asarray(seq.shift, dtype=np.uint64), g["shift"].astype(np.uint64))
+    xt = torch.from_numpy(g["x_test"])
+    args = argparse.Namespace(fit_iters=its)
+    pm, pv = bench.step_single(sg, args, xt.to(dev), xt[:2].to(dev))
+    pm, pv = pm.cpu().numpy(), pv.cpu().numpy()
+    rs, rl = (sg.gp.raw_scale.detach().cpu().numpy().reshape(-1), sg.gp.raw_lengthscales.detach().cpu().numpy().reshape(-1))
+    sg.reset()
+    data = sg.gp.fit(iterations=its, stop_crit_wait_iterations=its + 1, verbose=0, store_loss_hist=True)
+    tol = C23_TOL[name]
+    lh, ref = data["loss_hist"].numpy(), g["loss_hist"]
+    assert data["iterations"] == its and lh.shape == ref.shape
+    e_loss = np.abs(lh - ref).max() / np.abs(ref).max()
+    e_pm = np.abs(pm - g["pmean"]).max() / np.abs(g["pmean"]).max()
+    errs = dict(loss=e_loss, pmean=e_pm, scale=np.abs(rs - g["raw_scale"]).max(),
+                lengthscales=np.abs(rl - g["raw_lengthscales"]).max(),
+                pvar_kxx=(np.abs(pv - g["pvar"]) / np.abs(g["kxx"])).max())
+    assert e_loss <= max(tol["loss"], C23_FLOOR["loss"]), errs
+    assert errs["scale"] <= tol["params"] and errs["lengthscales"] <= tol["params"], errs
+    assert e_pm <= max(tol["pmean"], C23_FLOOR["pmean"]), errs
+    assert errs["pvar_kxx"] <= tol["pvar_kxx"], errs

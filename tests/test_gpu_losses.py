@@ -106,3 +106,31 @@ def test_lattice_gcv_is_real():
     data = gp.fit(loss_metric="GCV", iterations=4, store_hists=True, verbose=0, stop_crit_wait_iterations=10)
     lh = data["loss_hist"]
     assert not torch.is_complex(lh) and torch.isfinite(lh).all()
+
+
+@pytest.mark.parametrize("metric", ["GCV", "CV"])
+def test_device_alternative_loss_d6_sixteen_problems_equals_generic(metric, monkeypatch):
+    """The widest device GCV / CV step: d = 6 (SPEC_MAX_D) and 16 per-output eigen-problems in one
+    k_spec_loss_step workgroup -- 16 (6 + 2 d) = 288 reduced totals, more than the workgroup's 256 threads (the
+    level-2 sum is a strided loop) -- against the generic autograd loop, tolerances as above."""
+    import fastgaussianprocesses_amd as F
+    from oracle import fgp_oracle as O
+    d, B, n = 6, 16, 2 ** 10
+    out = {}
+    for path in ("device", "generic"):
+        monkeypatch.setenv("FGP_ALT_LOSS_DEVICE", "1" if path == "device" else "0")
+        seen = _spy_engines(monkeypatch)
+        gp = F.FastGPLattice(F.Lattice(d, seed=13), shape_batch=[B], shape_scale=[B, 1], shape_lengthscales=[B, d],
+                             noise=1e-4, device="cuda")
+        x = gp.get_x_next(n).cpu()
+        f = O.f_ackley(x)
+        y = torch.stack([f * (1 + 0.1 * b) + 0.05 * b * torch.cos(2 * np.pi * x[:, b % d]) for b in range(B)])
+        gp.add_y_next(y.to(gp.device))
+        data = gp.fit(loss_metric=metric, iterations=4, store_hists=True, verbose=0, stop_crit_wait_iterations=20)
+        assert seen == ([metric] if path == "device" else []), (path, seen)
+        out[path] = (data["loss_hist"], data["lengthscales_hist"], data["iterations"])
+        monkeypatch.undo()
+    (la, ha, ia), (lb, hb, ib) = out["device"], out["generic"]
+    assert ia == ib
+    assert rel_err(la, lb) <= 5e-7, (la, lb)
+    assert rel_err(ha, hb) <= 1e-9

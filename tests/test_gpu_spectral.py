@@ -389,3 +389,39 @@ def test_persistent_fit_launch_equals_launch_per_iteration(m, monkeypatch):
         assert all(torch.equal(a, b) for a, b in zip(got[0], ref[0])), key
         assert torch.equal(got[1], ref[1]) and torch.equal(got[2], ref[2]) and torch.equal(got[3], ref[3]), key
         assert torch.isfinite(got[1]).all()
+
+
+def test_single_launch_fit_give_up_inside_replayed_graph_raises(monkeypatch):
+    """A give-up of fgp_fit_persist inside a hipGraph replay (the bench's C2 / C3 lines replay captured fits, whose
+    control word the capture cannot read) is counted by the library's sticky give-up count (fgp_persist_giveups, ABI
+    17) and fit_engine.check_replayed_fits raises -- instead of the replay silently returning NaN parameters."""
+    from fastgaussianprocesses_amd import _native as N
+    from fastgaussianprocesses_amd import fit_engine as E
+    monkeypatch.setenv("FGP_FIT_PATH", "spectral")
+    monkeypatch.setenv("FGP_FIT_PERSIST", "1")
+    gp, _, _ = _gp("lattice", 3, 16)
+    gp.fit(iterations=5, verbose=0, stop_crit_wait_iterations=60)          # spectra / ytilde cached, kernels loaded
+    before = E.persist_giveups()
+    E.check_replayed_fits(before)                                          # nothing since: no raise
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
+            gp.fit(iterations=50, verbose=0, stop_crit_wait_iterations=60)
+            out = gp.raw_lengthscales.detach().clone()
+    torch.cuda.current_stream().wait_stream(s)
+    g.replay()
+    torch.cuda.synchronize()
+    assert bool(torch.isfinite(out).all())
+    E.check_replayed_fits(before)                                          # a good replay: no raise
+    N.call("fgp_set_persist_poll_max", 0)
+    try:
+        g.replay()
+        torch.cuda.synchronize()
+    finally:
+        N.call("fgp_set_persist_poll_max", -1)
+    assert not bool(torch.isfinite(out).all())                             # what a replay leaves: NaN parameters
+    with pytest.raises(RuntimeError, match="give-up"):
+        E.check_replayed_fits(before)
+    E.persist_giveups(reset=True)

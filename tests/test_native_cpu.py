@@ -114,3 +114,17 @@ def test_lattice_coefficient_matches_reference_formula():
     for a in (1, 2, 3, 4):
         exact = (-1) ** (a + 1) * (2 * math.pi) ** (2 * a) / math.factorial(2 * a)
         assert abs(F.ops.lattice_coefficient(a) - exact) <= 1e-13 * abs(exact)
+
+
+def test_bench_c2_c3_point_sets_are_the_fixtures():
+    """bench.SingleGP's point sets -- Lattice(3, seed=7), DigitalNetB2(3, seed=7) -- are the ones the REAL reference ran
+    on in tests/golden/c2_m16_d3_it50.npz / c3_m16_d3_a2_it50.npz (generating vector / matrices and shifts)."""
+    import os
+    g2 = np.load(os.path.join(os.path.dirname(__file__), "golden", "c2_m16_d3_it50.npz"))
+    s = F.Lattice(3, seed=7)
+    assert np.array_equal(np.asarray(s.z)[:3], g2["z"]) and np.array_equal(s.shift, g2["shift"])
+    g3 = np.load(os.path.join(os.path.dirname(__file__), "golden", "c3_m16_d3_a2_it50.npz"))
+    s = F.DigitalNetB2(3, seed=7)
+    assert int(g3["t"]) == s.t
+    assert np.array_equal(s.C[:, :g3["C"].shape[1]], g3["C"].astype(np.uint64))
+    assert np.array_equal(s.shift, g3["shift"].astype(np.uint64))
