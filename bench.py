@@ -198,11 +198,13 @@ class MultiOutputGP(SingleGP):
         B = b - a
         extra = dict(shape_scale=[B, 1], shape_lengthscales=[B, d]) if per_output else {}
         self.gp = F.FastGPLattice(F.Lattice(d, seed=7), shape_batch=[B], device=device, data_dtype=data_dtype, **extra)
-        f = f_ackley(self.gp.get_x_next(n))
-        g = torch.Generator(device=device).manual_seed(5)
-        bb = torch.arange(outputs, device=device, dtype=torch.float64)[:, None]
-        noise = torch.randn((outputs, n), generator=g, device=device, dtype=torch.float64)
-        self.y = (f[None, :] * (1 + bb / outputs) + 0.01 * noise)[a:b].to(data_dtype).contiguous()
+        # the observations formed on the host (untimed set-up) exactly as tests/golden/make_golden_c5.py's c5_data, so the
+        # benched data are the REAL reference's fixture inputs bit for bit (tests/test_gpu_multioutput.py)
+        f = f_ackley(self.gp.get_x_next(n).cpu())
+        g = torch.Generator().manual_seed(5)
+        noise = torch.randn((outputs, n), generator=g, dtype=torch.float64)
+        bb = torch.arange(outputs, dtype=torch.float64)[:, None]
+        self.y = (f[None, :] * (1 + bb / outputs) + 0.01 * noise)[a:b].to(data_dtype).contiguous().to(device)
         del noise
         self.raw0 = [p.detach().clone() for p in (self.gp.raw_scale, self.gp.raw_lengthscales, self.gp.raw_noise)]
         self.n, self.outputs, self.total = n, B, outputs
@@ -1039,7 +1041,7 @@ def capture_fn(fn):
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         # thread-local capture mode on an explicit stream (every phase captures cleanly this way,
-        # tools/diag_capture.py)
+        # tools/diag_capture.py, removed in round 6: git show 1846d2f:tools/diag_capture.py)
         with torch.cuda.stream(s):
             with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
                 out = fn()

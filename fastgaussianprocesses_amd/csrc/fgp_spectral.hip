@@ -748,7 +748,7 @@ __global__ __launch_bounds__(kWG) void k_spec_persist(Nll a, Fit f, int iters, d
     if (blk < a.nb && (blk == 0 || blk == a.nb - 1)) corr = spec_corr_load<NS>(a, blk, 0, 1);
   }
   // (a.stamps: workgroup 0's device clock per iteration -- start, partials stored, barrier passed, reduced,
-  // stepped -- at stamps[5 it + phase]; tools/exp_persist_stamps.py)
+  // stepped -- at stamps[5 it + phase]; the round-5 tools/exp_persist_stamps.py, in git history: profiles/r05j_persist_stamps_sentinel.jsonl)
   auto stamp = [&](int it, int ph) {
     if (a.stamps && blockIdx.x == 0 && tid == 0) a.stamps[5 * it + ph] = wall_clock64();
   };

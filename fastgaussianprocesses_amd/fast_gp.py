@@ -611,7 +611,7 @@ class AbstractFastGP(torch.nn.Module):
         # first pass and its real part into the last (fgp_ifftbr_mul).  data_dtype=float32: the
         # coefficients still come from an fp64 transform of the (fp32) observations -- cond(K) ~ n /
         # noise makes fp32 coefficients useless for the posterior mean (measured O(1) relative error,
-        # tools/diag_mixed.py), so only the MLL's Y uses the complex64 ytilde.
+        # tools/diag_mixed.py of round 3, in git history), so only the MLL's Y uses the complex64 ytilde.
         rows_y = self._y[0].numel() // n
         pb = self._problem_batch() if (self._lam_fusable(n) and not self.adaptive_nugget) else None
         basis = None

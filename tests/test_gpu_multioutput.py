@@ -317,3 +317,44 @@ def test_bench_secondary_c5_lines_two_ranks_equal_one_rank():
             assert o["post_var"].shape == pv_ref.shape, case
             kxx = float(pr.abs().max()) + 1e-300
             assert float((o["post_var"] - pv_ref).abs().max()) <= 1e-9 * max(kxx, 1.0), case
+
+
+# The benched C5 work at its benched length (bench.MultiOutputGP: n = 2^18, d = 3, 512 outputs, shared hyper-parameters,
+# nugget 1e-8; bench.step_single: fit 50 Rprop iterations with early stopping off, post_mean, post_var) against the REAL
+# reference (tests/golden/make_golden_c5.py --its 50 -> c5_m18_d3_b512[_f32data]_it50.npz).  Tolerances = 5x the
+# reference's own torch.fft vs numpy-pocketfft spread over the same 50 iterations (profiles/r06_c5_backend_spread.json:
+# loss history 4.9e-7 relative, post_mean 1.7e-7 relative, post_var 1e-15 K(x,x), fitted parameters identical), with
+# the golden tests' floors: parameters 1e-10, post_var 1e-8 K(x,x).
+C5_50_TOL = dict(loss=2.5e-6, pmean=8.4e-7, pvar_kxx=1e-8, params=1e-10)
+
+
+@pytest.mark.parametrize("mixed", [False, True])
+def test_bench_c5_50_iterations_matches_reference(mixed):
+    """bench.step_single exactly as timed for the C5 line (mixed: the fp32-observation line) at the fixture's test
+    points: fitted parameters, post_mean (16 points), post_var (2 points); the loss history of the same 50-iteration
+    fit (store_loss_hist) -- the sign-driven Rprop trajectory pinned over the whole benched length."""
+    import argparse
+    import numpy as np
+    import bench
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden",
+                             "c5_m18_d3_b512%s_it50.npz" % ("_f32data" if mixed else "")))
+    m, d, B, its = int(g["m"]), int(g["d"]), int(g["B"]), int(g["its"])
+    dev = torch.device(DEV, 0)
+    sg = bench.MultiOutputGP(F, m, d, B, dev, data_dtype=torch.float32 if mixed else torch.float64)
+    assert np.array_equal(np.asarray(sg.gp.seq.z)[:d], g["z"]) and np.array_equal(sg.gp.seq.shift, g["shift"])
+    xt = torch.from_numpy(g["x_test"])
+    pm, pv = bench.step_single(sg, argparse.Namespace(fit_iters=its), xt.to(dev), xt[:g["pvar"].shape[-1]].to(dev))
+    rs, rl = sg.gp.raw_scale.detach().cpu(), sg.gp.raw_lengthscales.detach().cpu()
+    sg.reset()
+    data = sg.gp.fit(iterations=its, stop_crit_wait_iterations=its + 1, verbose=0, store_loss_hist=True)
+    assert data["iterations"] == its
+    errs = dict(loss=rel_err(data["loss_hist"], g["loss_hist"]),
+                scale=float((rs - torch.from_numpy(g["raw_scale"])).abs().max()),
+                lengthscales=float((rl - torch.from_numpy(g["raw_lengthscales"])).abs().max()),
+                pmean=rel_err(pm, g["pmean"]),
+                pvar_kxx=float((pv.cpu() - torch.from_numpy(g["pvar"])).abs().max()) / float(g["kxx"]))
+    assert pm.shape == tuple(g["pmean"].shape)
+    assert errs["loss"] <= C5_50_TOL["loss"], errs
+    assert errs["scale"] <= C5_50_TOL["params"] and errs["lengthscales"] <= C5_50_TOL["params"], errs
+    assert errs["pmean"] <= C5_50_TOL["pmean"], errs
+    assert errs["pvar_kxx"] <= C5_50_TOL["pvar_kxx"], errs
