@@ -227,6 +227,20 @@ def step_single(sg, args, xm, xv):
     return pm, pv
 
 
+def persist_giveups(F):
+    """The library's sticky count of single-launch-fit barrier give-ups (fgp_persist_giveups; synchronises)."""
+    return F.fit_engine.persist_giveups()
+
+
+def replay_giveup_error(F, before):
+    """None, or the message of fit_engine.check_replayed_fits when a single-launch fit gave up since `before`."""
+    try:
+        F.fit_engine.check_replayed_fits(before)
+        return None
+    except RuntimeError as e:
+        return str(e)
+
+
 def time_steps(fn, steps, warmup, device=None):
     """Seconds per step: warmup, then `steps` steps bracketed by a barrier + device sync on both sides,
     the max over the ranks when a process group is up."""
@@ -302,8 +316,12 @@ def secondary_configs(F, args, device, rank=0, world=1, collect=None):
                 one()
             graph, ginfo = capture_fn(one)
         run = graph.replay if graph is not None else one
+        gu0 = persist_giveups(F)
         wins = sorted(time_steps(run, max(5, args.steps), 2 if w == 0 else 0, device) for w in range(3))
         sec = wins[1]
+        # a single-launch fit that gave up inside a timed replay (its control word cannot be read in a capture) would
+        # have timed NaN parameters: the library's sticky give-up count must not have moved (fails the line)
+        giveup_err = replay_giveup_error(F, gu0)
         if graph is not None:
             ginfo["eager_ms_per_step"] = sorted(time_steps(one, max(5, args.steps), 0, device)
                                                 for _ in range(3))[1] * 1e3
@@ -349,7 +367,8 @@ def secondary_configs(F, args, device, rank=0, world=1, collect=None):
                                          launches=1 + (1 if sg.outputs % 4 else 0))
         out.append({"metric": "GP fit+predict points/sec" if total == 1 else
                     "multi-output GP fit+predict output-points/sec",
-                    "value": sg.n * total / sec, "unit": "points/s" if total == 1 else "output-points/s",
+                    "value": None if giveup_err else sg.n * total / sec, "error": giveup_err,
+                    "unit": "points/s" if total == 1 else "output-points/s",
                     "ms_per_step": sec * 1e3, "steps": max(5, args.steps), "n_gpus": world,
                     "dtype": "f64" if sg.gp.data_dtype == torch.float64 else "f32 data / f64 eigenvalues",
                     "config": {"workload": "%s: fit %d Rprop iters + post_mean N=%d + post_var N=%d"
@@ -1116,6 +1135,7 @@ def main():
     # two device-clock stamp kernels bracket the timed loop (outside the timed interval): the first two
     # k_clock_stamp launches of a rocprofv3 --kernel-trace of this command mark the timed region, whose launches
     # tools/timed_region_stats.py averages (the graph replays' per-kernel durations the roofline is priced on)
+    gu0 = persist_giveups(F)
     marks = torch.zeros(2, dtype=torch.int64, device=device)
     F._native.call("fgp_clock_stamp", marks[0:1].data_ptr(), torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
@@ -1134,6 +1154,9 @@ def main():
     F._native.call("fgp_clock_stamp", marks[1:2].data_ptr(), torch.cuda.current_stream().cuda_stream)
     sec_step = el / args.steps
     value = args.shifts * n * world / sec_step
+    giveup_err = replay_giveup_error(F, gu0)
+    if giveup_err:
+        raise RuntimeError("timed steps invalid: " + giveup_err)
     if graph is not None:
         # the same steps enqueued eagerly (host-side Python per launch), for comparison
         torch.cuda.synchronize()

@@ -233,8 +233,6 @@ __device__ __forceinline__ gdouble* gptr(const double* p) { return (gdouble*)(co
 __device__ __forceinline__ void st_part_sc1(double* p, double v) {
   __hip_atomic_store(gptr(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-typedef __attribute__((address_space(1))) unsigned guint;
-__device__ __forceinline__ guint* gptr_u(unsigned* p) { return (guint*)p; }
 
 template <int D, bool NET>
 __device__ __forceinline__ void spec_block_partials(const Nll& a, const Hyp& h, int g, int blk, double rootn, double wl,
@@ -811,11 +809,10 @@ __global__ __launch_bounds__(kWG) void k_spec_persist(Nll a, Fit f, int iters, d
 #pragma unroll
           for (int b = 0; b < kSpecGroup; ++b) full = full && __double_as_longlong(tv[b]) != kPartEmpty;
           if (full) break;
-          // give up on the poll bound (test hook), the wall-clock bound, or another workgroup's give-up (the launch's
-          // fail word, ctrl[0]: a workgroup that starts only after the others exited stops at its first poll)
-          if (++polls > poll_max || wall_clock64() - t_wait > kPersistWaitTicks ||
-              __hip_atomic_load(gptr_u(counter), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
-            __hip_atomic_store(gptr_u(counter), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          // give up on the poll bound (test hook) or the wall-clock bound
+          // (a fail word polled beside the slots -- a late workgroup stopping at its first poll -- made hipGraph replays
+          // give up: it read nonzero there, profiles/r06d_persist_failword_ab.jsonl; not kept)
+          if (++polls > poll_max || wall_clock64() - t_wait > kPersistWaitTicks) {
             fail_s = 1;
             break;
           }
@@ -2172,10 +2169,10 @@ int launch_spec_persist(const Nll& a, const Fit& f, int iters, double logtol, in
   size_t shm;
   int rc = spec_persist_geometry(a, &W, &bpw, &shm);
   if (rc != kOk) return rc;
-  // the three partial buffers empty (kPartEmpty: all bytes 0xff), the fail word (counter = ctrl[0]) and the control
-  // words out[0..1] (= ctrl[1..2]) cleared
+  // the three partial buffers empty (kPartEmpty: all bytes 0xff), the control words out[0..1] cleared
+  (void)counter;
   if (hipMemsetAsync(a.partials, 0xff, 3 * sizeof(double) * (size_t)a.nq * (size_t)a.nb, st) != hipSuccess ||
-      hipMemsetAsync(counter, 0, 3 * sizeof(unsigned), st) != hipSuccess || out != reinterpret_cast<int*>(counter + 1))
+      hipMemsetAsync(out, 0, 2 * sizeof(int), st) != hipSuccess)
     return set_error(kErrHip, "fgp_fit_persist: workspace reset failed");
   return with_spec_d(a.d, [&](auto dc) {
     constexpr int D = decltype(dc)::value;
