@@ -227,6 +227,14 @@ def step_single(sg, args, xm, xv):
     return pm, pv
 
 
+def fit_graph_stats(F):
+    """fgp_fit_graph_stats: [replays of a cached fit graph, captures, eager fallbacks] since the library loaded."""
+    import ctypes
+    out = (ctypes.c_longlong * 3)()
+    F._native.call("fgp_fit_graph_stats", out)
+    return list(out)
+
+
 def persist_giveups(F):
     """The library's sticky count of single-launch-fit barrier give-ups (fgp_persist_giveups; synchronises)."""
     return F.fit_engine.persist_giveups()
@@ -1160,11 +1168,14 @@ def main():
     if graph is not None:
         # the same steps enqueued eagerly (host-side Python per launch), for comparison
         torch.cuda.synchronize()
+        gs0 = fit_graph_stats(F)
         t0 = time.perf_counter()
         for _ in range(args.steps):
             step()
         torch.cuda.synchronize()
         graph_info["eager_ms_per_step"] = (time.perf_counter() - t0) / args.steps * 1e3
+        graph_info["eager_fit_graphs"] = dict(zip(("replays", "captures", "eager"),
+                                                  [b - a for a, b in zip(gs0, fit_graph_stats(F))]))
 
     if args.dump:
         # one more step's results (every step is the same computation from the same reset state)

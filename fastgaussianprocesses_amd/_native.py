@@ -167,6 +167,9 @@ _SIGNATURES = {
     "fgp_handoff_check": [_c_int, ctypes.POINTER(ctypes.c_ulonglong)],
     "fgp_set_persist_poll_max": [_c_i64],
     "fgp_persist_giveups": [ctypes.POINTER(ctypes.c_ulonglong), _c_int],
+    "fgp_fit_graph_stats": [ctypes.POINTER(ctypes.c_longlong)],
+    "fgp_fit_run_graph": [_P_NLL, _P_FIT, _c_int, _c_int, _c_int, _c_i64, _c_vp],
+    "fgp_fit_graph_release": [_c_i64],
     "fgp_set_mt_class_kernel": [_c_int],
     "fgp_nll_partials_len": [_P_NLL, _c_pl],
     "fgp_spec_basis": [_c_int, _c_vp, _c_i64, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_i64, _c_vp],

@@ -18,7 +18,7 @@ import torch
 
 from . import _native as N
 from . import ops
-from .fit_engine import FusedMLL, LatticePartsGen, fused_lam, mll_constant, spec_basis, spec_basis_gen, spec_inv_eig, spectral_wanted
+from .fit_engine import FusedMLL, LatticePartsGen, cached_engine, fused_lam, mll_constant, spec_basis, spec_basis_gen, spec_inv_eig, spectral_wanted
 
 
 class _LossReader(object):
@@ -198,10 +198,19 @@ def _basis_for(gps, n, parts, gen):
     return spec_basis(g0._FAMILY, p, n)
 
 
-def _engine(gps, n, ysq, parts, gen, lr, iterations, basis=None):
+def _engine(gps, n, ysq, parts, gen, lr, iterations, basis=None, cached=False):
     g0 = gps[0]
     dl = g0.raw_lengthscales.shape[-1]
-    d_out = int(torch.tensor(g0.shape_batch).prod())
+    d_out = int(math.prod(g0.shape_batch))
+    if cached and basis is not None:
+        # the batch's spectral engine, reused across fits of this geometry (fit_engine.cached_engine)
+        return cached_engine(g0._FAMILY, ysq, torch.stack([gp.raw_scale.detach().reshape(-1)[0] for gp in gps]),
+                             torch.stack([gp.raw_lengthscales.detach().reshape(dl) for gp in gps]),
+                             torch.stack([gp.raw_noise.detach().reshape(-1)[0] for gp in gps]),
+                             logdet_weight=float(d_out), mll_const=mll_constant(d_out, n),
+                             requires_grad=(g0.raw_scale.requires_grad, g0.raw_lengthscales.requires_grad,
+                                            g0.raw_noise.requires_grad),
+                             lr=1e-1 if lr is None else lr, max_iters=iterations + 1, basis=basis, per_problem=True)
     return FusedMLL(g0._FAMILY, parts, ysq,
                     torch.stack([gp.raw_scale.detach().reshape(-1)[0] for gp in gps]),
                     torch.stack([gp.raw_lengthscales.detach().reshape(dl) for gp in gps]),
@@ -381,12 +390,14 @@ class GPBatch(object):
         """Every GP's AbstractGP.fit(loss_metric="MLL", verbose=0) in one device loop; returns the list of
         per-GP data dicts."""
         parts, gen = self._source()
-        eng = _engine(self.gps, self.n, self.ysq(), parts, gen, lr, iterations, basis=self.basis())
+        eng = _engine(self.gps, self.n, self.ysq(), parts, gen, lr, iterations, basis=self.basis(), cached=True)
         state = _fit_loop(eng, iterations, stop_crit_improvement_threshold, stop_crit_wait_iterations)
         best = _best_raw(eng, state, self.dl)
         self.set_raw(best)
         self._st["raw"] = best
-        return _fit_data(state, store_hists or store_loss_hist)
+        out = _fit_data(state, store_hists or store_loss_hist)
+        eng.release_inputs()
+        return out
 
     # ---------------------------------------------------------------------------- predict
     def coeffs(self):

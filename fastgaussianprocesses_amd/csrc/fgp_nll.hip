@@ -27,6 +27,9 @@
 //   assembly, histories, Rprop update).
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <vector>
 
 #include "fgp_nll.h"
 
@@ -2116,8 +2119,10 @@ int fgp_handoff_check(int enable, unsigned long long* out) {
   return kOk;
 }
 
-int fgp_fit_run(const fgp_nll_desc* nll, const fgp_fit_desc* fit, int iter0, int iters, int final_no_update,
-                void* stream) {
+}  // extern "C"
+
+static int fit_run_enqueue(const fgp_nll_desc* nll, const fgp_fit_desc* fit, int iter0, int iters, int final_no_update,
+                           void* stream) {
   Nll a;
   Fit f;
   int rc = to_nll(nll, a);
@@ -2200,6 +2205,164 @@ int fgp_fit_run(const fgp_nll_desc* nll, const fgp_fit_desc* fit, int iter0, int
     if ((rc = nll_bwd(a, st, lat)) != kOk) return rc;
     if ((rc = fit_step(a, f, iter0 + it, upd, st, many)) != kOk) return rc;
   }
+  return kOk;
+}
+
+// ---------------------------------------------------------------- fgp_fit_run_graph (ABI 17)
+// An eager launch costs the device ~3 us more than the same launch replayed from a graph (the eager dispatch's
+// system-scope release: DESIGN.md section 8), i.e. ~150 us per C4 fit of 51 launches.  fgp_fit_run_graph captures the
+// launch sequence of fgp_fit_run (thread-local mode, on a library side stream: torch's default stream cannot capture)
+// into a hipGraph and replays it on the caller's stream.  Executable graphs are cached per caller token (one fit
+// engine: its buffers never move) and the call's exact arguments (the descriptors' bytes, the iteration range, the
+// device, the hand-off check hook, the library's A/B environment switches); a repeated call replays at once.  (Keyed
+// by the arguments alone, a replay for ANOTHER engine whose buffers happened to sit at the same addresses returned
+// garbage in the GPU suite -- not understood, so graphs are never shared between engines.)  Results are
+// bit-identical to the eager sequence: the same kernels with the same arguments.  A stream that is itself capturing
+// (bench.py's whole-step graph), a non-spectral desc or a capture error take the eager sequence.
+namespace {
+struct FitGraph {
+  long long token;
+  std::vector<unsigned char> key;
+  int dev;
+  hipGraph_t graph;
+  hipGraphExec_t exec;
+  hipEvent_t done;           // recorded after each launch: an evicted graph is destroyed only once it has finished
+  unsigned long long used;
+};
+std::mutex g_fg_mu;
+std::vector<FitGraph> g_fit_graphs;
+unsigned long long g_fg_clock = 0;
+hipStream_t g_fg_side[64] = {};
+long long g_fg_stats[3] = {0, 0, 0};         // replays of a cached graph, captures, eager calls
+constexpr size_t kFitGraphCache = 16;
+}  // namespace
+
+static void key_put(std::vector<unsigned char>& k, const void* p, size_t n) {
+  const unsigned char* b = static_cast<const unsigned char*>(p);
+  k.insert(k.end(), b, b + n);
+}
+
+static int fit_graph_wanted(const fgp_nll_desc* nll, hipStream_t st) {
+  if (!nll || !nll->basis || nll->mt_tasks > 0) return 0;      // the spectral single-task fits
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return cs == hipStreamCaptureStatusNone;
+}
+
+static void fit_graph_free(FitGraph& e) {
+  if (e.done) (void)hipEventSynchronize(e.done);
+  if (e.exec) (void)hipGraphExecDestroy(e.exec);
+  if (e.graph) (void)hipGraphDestroy(e.graph);
+  if (e.done) (void)hipEventDestroy(e.done);
+  e.exec = nullptr;
+  e.graph = nullptr;
+  e.done = nullptr;
+}
+
+static int fit_graph_launch(FitGraph& e, hipStream_t st) {
+  e.used = ++g_fg_clock;
+  if (hipGraphLaunch(e.exec, st) != hipSuccess || hipEventRecord(e.done, st) != hipSuccess)
+    return set_error(kErrHip, "fgp_fit_run_graph: hipGraphLaunch failed");
+  return kOk;
+}
+
+extern "C" {
+
+int fgp_fit_run(const fgp_nll_desc* nll, const fgp_fit_desc* fit, int iter0, int iters, int final_no_update,
+                void* stream) {
+  return fit_run_enqueue(nll, fit, iter0, iters, final_no_update, stream);
+}
+
+int fgp_fit_run_graph(const fgp_nll_desc* nll, const fgp_fit_desc* fit, int iter0, int iters, int final_no_update,
+                      long long token, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (!nll || !fit || !fit_graph_wanted(nll, st)) {
+    std::lock_guard<std::mutex> lock(g_fg_mu);
+    ++g_fg_stats[2];
+    return fit_run_enqueue(nll, fit, iter0, iters, final_no_update, stream);
+  }
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64)
+    return set_error(kErrHip, "fgp_fit_run_graph: hipGetDevice");
+  std::vector<unsigned char> key;
+  key.reserve(sizeof(*nll) + sizeof(*fit) + 128);
+  key_put(key, nll, sizeof(*nll));
+  key_put(key, fit, sizeof(*fit));
+  const int ints[4] = {iter0, iters, final_no_update, dev};
+  key_put(key, ints, sizeof(ints));
+  const void* hook = g_handoff_check;
+  key_put(key, &hook, sizeof(hook));
+  // the library's A/B switches that choose kernels / workspace layouts for a desc are inputs of the sequence too
+  for (const char* nm : {"FGP_SPEC_TILE", "FGP_SPEC_SLICE_NB", "FGP_SPEC_PERSIST", "FGP_SPEC_STEP_MANY", "FGP_R2C"}) {
+    const char* v = getenv(nm);
+    key_put(key, nm, strlen(nm));
+    if (v) key_put(key, v, strlen(v) + 1);
+    else key.push_back(0xff);
+  }
+  std::lock_guard<std::mutex> lock(g_fg_mu);
+  for (auto& e : g_fit_graphs)
+    if (e.token == token && e.dev == dev && e.key == key) {
+      ++g_fg_stats[0];
+      return fit_graph_launch(e, st);
+    }
+  if (!g_fg_side[dev] && hipStreamCreateWithFlags(&g_fg_side[dev], hipStreamNonBlocking) != hipSuccess) {
+    g_fg_side[dev] = nullptr;
+    return set_error(kErrHip, "fgp_fit_run_graph: side stream");
+  }
+  hipStream_t cap = g_fg_side[dev];
+  if (hipStreamBeginCapture(cap, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+    (void)hipGetLastError();
+    ++g_fg_stats[2];
+    return fit_run_enqueue(nll, fit, iter0, iters, final_no_update, stream);
+  }
+  const int rc = fit_run_enqueue(nll, fit, iter0, iters, final_no_update, cap);
+  hipGraph_t g = nullptr;
+  const hipError_t ec = hipStreamEndCapture(cap, &g);
+  hipGraphExec_t exec = nullptr;
+  hipEvent_t done = nullptr;
+  if (rc != kOk || ec != hipSuccess || !g || hipGraphInstantiate(&exec, g, nullptr, nullptr, 0) != hipSuccess ||
+      hipEventCreateWithFlags(&done, hipEventDisableTiming) != hipSuccess) {
+    if (exec) (void)hipGraphExecDestroy(exec);
+    if (g) (void)hipGraphDestroy(g);
+    (void)hipGetLastError();
+    if (rc != kOk) return rc;                       // an argument error: reported as the eager call would
+    ++g_fg_stats[2];
+    return fit_run_enqueue(nll, fit, iter0, iters, final_no_update, stream);
+  }
+  ++g_fg_stats[1];
+  FitGraph* slot = nullptr;
+  if (g_fit_graphs.size() >= kFitGraphCache) {       // evict a released engine's graph, else the least recently used
+    slot = &g_fit_graphs[0];
+    for (auto& e : g_fit_graphs)
+      if ((e.token < 0) > (slot->token < 0) || ((e.token < 0) == (slot->token < 0) && e.used < slot->used)) slot = &e;
+    fit_graph_free(*slot);
+  } else {
+    g_fit_graphs.push_back(FitGraph{});
+    slot = &g_fit_graphs.back();
+  }
+  slot->token = token;
+  slot->key = std::move(key);
+  slot->dev = dev;
+  slot->graph = g;
+  slot->exec = exec;
+  slot->done = done;
+  return fit_graph_launch(*slot, st);
+}
+
+int fgp_fit_graph_release(long long token) {
+  std::lock_guard<std::mutex> lock(g_fg_mu);
+  for (auto& e : g_fit_graphs)
+    if (e.token == token) e.token = -1;             // never launched again; freed when evicted
+  return kOk;
+}
+
+int fgp_fit_graph_stats(long long* out) {
+  if (!out) return set_error(kErrInvalid, "fgp_fit_graph_stats: null out");
+  std::lock_guard<std::mutex> lock(g_fg_mu);
+  for (int i = 0; i < 3; ++i) out[i] = g_fg_stats[i];
   return kOk;
 }
 

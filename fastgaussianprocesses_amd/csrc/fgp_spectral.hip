@@ -2134,6 +2134,8 @@ int spec_persist_geometry(const Nll& a, int* W, int* bpw, size_t* shm) {
     return set_error(kErrUnsupported, "fgp_fit_persist: one problem on the spectral path only");
   if (spec_nparams(a) > kSpecScratch) return set_error(kErrUnsupported, "fgp_fit_persist: parameters");
   const size_t per_blk = (size_t)a.spec_kpl * (((size_t)1 << a.d) + 1) * 64 * sizeof(double);
+  // (the fewest workgroups whose LDS holds the spectra: more of them -- 64, 128, 256 at C2 / C3 -- did not shorten the
+  // fit, profiles/r06f_persist_wg_sweep.jsonl: the iteration is bound by its barrier / reduce / step chain)
   for (int w = 1; w <= kPersistMaxW && w <= a.nb; w *= 2) {
     const int b = (a.nb + w - 1) / w;
     if ((size_t)b * per_blk <= (size_t)kPersistLdsMax) {

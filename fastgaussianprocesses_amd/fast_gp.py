@@ -28,8 +28,8 @@ import torch
 from . import _native
 from . import ops
 from . import seqs as _seqs
-from .fit_engine import (SPEC_MAX_D, FusedMLL, LatticePartsGen, mll_constant, spec_basis, spec_basis_gen, spec_inv_eig,
-                         spec_k, spec_post_var, spectral_wanted)
+from .fit_engine import (SPEC_MAX_D, FusedMLL, LatticePartsGen, cached_engine, mll_constant, spec_basis, spec_basis_gen,
+                         spec_inv_eig, spec_k, spec_post_var, spectral_wanted)
 
 
 def _log(x):
@@ -772,14 +772,21 @@ class AbstractFastGP(torch.nn.Module):
         parts = self._k1parts(n) if (gen is None and basis is None) else None
         ls_raw = self.raw_lengthscales.detach()
         ls2 = ls_raw.reshape(-1, ls_raw.shape[-1])
+        max_iters = iterations + 1 if G == 1 and iterations < 8192 else min(iterations + 1, 64)
+        rg = (self.raw_scale.requires_grad, self.raw_lengthscales.requires_grad, self.raw_noise.requires_grad)
+        if basis is not None:
+            # the spectral fit's engine, reused across fit() calls of this geometry (fit_engine.cached_engine)
+            return cached_engine(self._FAMILY, self._ysq(pb_shape, G) if ysq is None else ysq,
+                                 self.raw_scale.detach().reshape(-1), ls2, self.raw_noise.detach().reshape(-1),
+                                 logdet_weight=d_out / G, mll_const=mll_constant(d_out, n), requires_grad=rg, lr=lr,
+                                 max_iters=max_iters, basis=basis, loss_metric=loss_metric, cv_weight=cv_weight)
         return FusedMLL(self._FAMILY, parts, self._ysq(pb_shape, G) if ysq is None else ysq,
                         self.raw_scale.detach().reshape(-1), ls2,
                         self.raw_noise.detach().reshape(-1), logdet_weight=d_out / G,
                         mll_const=mll_constant(d_out, n),
                         requires_grad=(self.raw_scale.requires_grad, self.raw_lengthscales.requires_grad,
                                        self.raw_noise.requires_grad),
-                        lr=lr, max_iters=(iterations + 1 if G == 1 and iterations < 8192 else min(iterations + 1, 64)),
-                        gen=gen, basis=basis, loss_metric=loss_metric, cv_weight=cv_weight)
+                        lr=lr, max_iters=max_iters, gen=gen, basis=basis, loss_metric=loss_metric, cv_weight=cv_weight)
 
     def _fit_fused(self, iterations, lr, stop, hists, verbose, indent, ysq=None, d_out=None, loss_metric="MLL",
                    cv_weight=1.0):
@@ -870,6 +877,8 @@ class AbstractFastGP(torch.nn.Module):
                 setattr(self, name, torch.nn.Parameter(val.reshape(old.shape).clone(), requires_grad=old.requires_grad))
         self._cache = {k: v for k, v in self._cache.items() if not k[2]}    # keep data-only entries (ytilde, spectra)
         self._snap = None
+        if hasattr(eng, "release_inputs"):
+            eng.release_inputs()
         data = {"iterations": i}
         if hists["loss"]:
             sgn = -1.0 if loss_metric == "MLL" else 1.0        # metric_val: -loss (MLL), loss (GCV, CV)

@@ -9,6 +9,7 @@ One `FusedMLL` holds, for G eigen-problems of size n = 2^m:
 stream without any host synchronisation; the caller reads the histories back in chunks to apply
 AbstractGP.fit's early-stopping rule (fastgps/abstract_gp.py:276-284) exactly.
 """
+import collections
 import ctypes
 import math
 import os
@@ -50,6 +51,9 @@ class LatticePartsGen(object):
         desc.gen_shift = self.shift.data_ptr()
         desc.gen_shift_stride = d if self.shift.shape[0] > 1 else 0
 
+
+FIT_GRAPH_MIN_ITERS = 16       # fgp_fit_run_graph below this many iterations per call: eager launches
+_NEXT_TOKEN = 0
 
 SPEC_MAX_D = 6                 # fgp_spec_basis / the spectral fit kernels (include/fgp_hip.h, ABI 11)
 SPEC_WORK_CAP = 512 << 20      # scratch of one fgp_spec_basis call (subsets are transformed in chunks)
@@ -305,6 +309,13 @@ class FusedMLL(object):
         self.ensure_history(iter0 + iters)
         groups = self.groups()
         if groups <= 1:
+            if iters >= FIT_GRAPH_MIN_ITERS and os.environ.get("FGP_FIT_GRAPH", "1")[:1] != "0":
+                # the launch sequence replayed from a hipGraph of this engine (fgp_fit_run_graph, ABI 17): the
+                # replayed per-launch rate, bit-identical results; short runs (the early-stopping loop's first chunks)
+                # stay eager, a capture per call would not pay
+                N.call("fgp_fit_run_graph", self._nll, self._fit, int(iter0), int(iters), int(bool(final_no_update)),
+                       self._graph_token(), self.stream())
+                return
             N.call("fgp_fit_run", self._nll, self._fit, int(iter0), int(iters), int(bool(final_no_update)),
                    self.stream())
             return
@@ -320,6 +331,52 @@ class FusedMLL(object):
             done.record(st)
             cur.wait_event(done)
 
+    def refill(self, ysq, raw_scale, raw_lengthscales, raw_noise, lr, basis):
+        """Reuse this engine for a new fit of the same geometry (cached_engine): the new Y in the engine's own buffer,
+        the initial raw parameters, a fresh Rprop state (torch.optim.Rprop's: prev 0, step lr), the fit's spectra
+        (at the address the descriptors hold).  Histories are rewritten row by row by the fit."""
+        assert basis.data_ptr() == self._nll.basis
+        self.basis = basis
+        G, n = ysq.shape
+        if self._nll.ysq_chunked:
+            Q = spec_chunks(self.family, n)
+            w = min(n, Q * 64)
+            if w == Q * 64:
+                self.ysq.copy_(ysq[:, :w].view(G, Q, 64).transpose(0, 1))
+            else:
+                yp = torch.zeros((G, Q * 64), dtype=torch.float64, device=self.device)
+                yp[:, :w] = ysq[:, :w]
+                self.ysq.copy_(yp.view(G, Q, 64).transpose(0, 1))
+        else:
+            self.ysq.copy_(ysq)
+        self.ysq_rows = ysq
+        self.raw.copy_(torch.cat([raw_scale.reshape(-1), raw_lengthscales.reshape(-1), raw_noise.reshape(-1)]))
+        self.prev.zero_()
+        self.step.fill_(float(lr))
+
+    def release_inputs(self):
+        """Drop the references to the fit's inputs (spectra, Y rows) after the fit is enqueued: a cached engine must not
+        keep the caller's spectra alive (the next fit's spectra could then not take their address)."""
+        self.basis = None
+        self.ysq_rows = None
+
+    def _graph_token(self):
+        """This engine's token for fgp_fit_run_graph's cache (released when the engine is freed)."""
+        tok = getattr(self, "_token", None)
+        if tok is None:
+            global _NEXT_TOKEN
+            _NEXT_TOKEN += 1
+            tok = self._token = _NEXT_TOKEN
+        return tok
+
+    def __del__(self):
+        tok = getattr(self, "_token", None)
+        if tok is not None:
+            try:
+                N.call("fgp_fit_graph_release", tok)
+            except Exception:
+                pass
+
     def persist_ok(self):
         """fgp_fit_persist applies (one problem on the spectral path whose spectra fit the LDS of at most 64
         workgroups: the whole fit in one launch); FGP_FIT_PERSIST=0 keeps the launch per iteration."""
@@ -328,7 +385,7 @@ class FusedMLL(object):
     def persist_workgroups(self):
         """Workgroups of the single-launch fit (fgp_fit_persist_ok: 0 outside its domain, or when they would not
         all be co-resident on this device)."""
-        if os.environ.get("FGP_FIT_PERSIST", "1")[:1] == "0" or self.G != 1 or self.basis is None:
+        if os.environ.get("FGP_FIT_PERSIST", "1")[:1] == "0" or self.G != 1 or not self._nll.basis:
             return 0
         ok = ctypes.c_int(0)
         N.call("fgp_fit_persist_ok", self._nll, ctypes.byref(ok))
@@ -454,6 +511,38 @@ class FusedMLL(object):
     def split_raw(self, raw_vec):
         S, L, Nn = self.sizes
         return raw_vec[..., :S], raw_vec[..., S:S + L], raw_vec[..., S + L:S + L + Nn]
+
+
+_ENGINES = collections.OrderedDict()
+ENGINE_CACHE_SIZE = 4
+
+
+def cached_engine(family, ysq, raw_scale, raw_lengthscales, raw_noise, logdet_weight, mll_const, requires_grad, lr,
+                  max_iters, basis, per_problem=None, loss_metric="MLL", cv_weight=1.0):
+    """The FusedMLL of a spectral fit, reused across fit() calls of the same geometry (LRU of ENGINE_CACHE_SIZE): its
+    buffers keep their addresses, so fgp_fit_run_graph replays the engine's captured launch sequence instead of
+    capturing anew, and the host builds no engine per call (fit() at the replayed rate).  The spectra
+    must be at the same address (a rebuilt set usually is: the freed one's block).  FGP_ENGINE_CACHE=0: a new engine
+    per call."""
+    G, n = ysq.shape
+    S, (Sl, Dl), Sn = raw_scale.numel(), raw_lengthscales.shape, raw_noise.numel()
+    key = (str(ysq.device), int(family), int(G), int(n), basis.data_ptr(), tuple(basis.shape), S, Sl, Dl, Sn,
+           per_problem, float(logdet_weight), float(mll_const), tuple(bool(r) for r in requires_grad), int(max_iters),
+           loss_metric, float(cv_weight))
+    on = os.environ.get("FGP_ENGINE_CACHE", "1")[:1] != "0"
+    eng = _ENGINES.get(key) if on else None
+    if eng is not None:
+        _ENGINES.move_to_end(key)
+        eng.refill(ysq, raw_scale, raw_lengthscales, raw_noise, lr, basis)
+        return eng
+    eng = FusedMLL(family, None, ysq, raw_scale, raw_lengthscales, raw_noise, logdet_weight=logdet_weight,
+                   mll_const=mll_const, requires_grad=requires_grad, lr=lr, max_iters=max_iters,
+                   per_problem=per_problem, basis=basis, loss_metric=loss_metric, cv_weight=cv_weight)
+    if on:
+        _ENGINES[key] = eng
+        while len(_ENGINES) > ENGINE_CACHE_SIZE:
+            _ENGINES.popitem(last=False)
+    return eng
 
 
 def persist_giveups(reset=False):

@@ -353,9 +353,21 @@ typedef struct fgp_fit_desc {
 int fgp_fit_step(const fgp_nll_desc* nll, const fgp_fit_desc* fit, int iter, int do_update, void* stream);
 
 /* Run `iters` complete fit iterations starting at history index iter0 (fwd, bwd, step per iteration;
- * the last one without update when final_no_update=1). Stream-ordered, no host synchronisation. */
+ * the last one without update when final_no_update=1). Stream-ordered, no host synchronisation.
+ */
 int fgp_fit_run(const fgp_nll_desc* nll, const fgp_fit_desc* fit, int iter0, int iters, int final_no_update,
                 void* stream);
+
+/* ABI 17 -- fgp_fit_run through a hipGraph (AbstractGP.fit's loop at the replayed per-launch rate,
+ * abstract_gp.py:241-296): on the spectral path (basis set, single task) and a stream that is not capturing, the
+ * launch sequence is captured once per (token, arguments) and replayed; `token` names the caller's fit engine (its
+ * buffers must not move while the token is live; fgp_fit_graph_release(token) when they are freed).  Bit-identical
+ * to fgp_fit_run; other descs / a capturing stream run fgp_fit_run's eager sequence.  fgp_fit_graph_stats: out[0]
+ * replays of a cached graph, out[1] captures, out[2] eager calls (since load). */
+int fgp_fit_run_graph(const fgp_nll_desc* nll, const fgp_fit_desc* fit, int iter0, int iters, int final_no_update,
+                      long long token, void* stream);
+int fgp_fit_graph_release(long long token);
+int fgp_fit_graph_stats(long long* out);
 
 /* ---------------------------------------------------------------------------------------------
  * Prediction.

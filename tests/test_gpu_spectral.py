@@ -425,3 +425,72 @@ def test_single_launch_fit_give_up_inside_replayed_graph_raises(monkeypatch):
     with pytest.raises(RuntimeError, match="give-up"):
         E.check_replayed_fits(before)
     E.persist_giveups(reset=True)
+
+
+def _graph_stats():
+    import ctypes
+    from fastgaussianprocesses_amd import _native as N
+    out = (ctypes.c_longlong * 3)()
+    N.call("fgp_fit_graph_stats", out)
+    return list(out)
+
+
+@pytest.mark.parametrize("case", ["c4_batch", "c5_per_output", "c2_per_launch"])
+def test_fit_run_graph_replay_is_bit_identical_to_eager_launches(case, monkeypatch):
+    """fgp_fit_run replays its spectral launch sequence from a cached hipGraph (ABI 17): the fit through the graph --
+    captured on the first call, replayed from the cache on the second -- equals the eager launch sequence
+    (FGP_FIT_GRAPH=0) bit for bit: loss histories, fitted parameters.  C4's batch of shifts (k_spec_tile, the
+    deferred step), C5 per-output (the sliced tile + k_spec_step_many) and C2 on the launch per iteration."""
+    import bench
+    dev = torch.device("cuda", 0)
+    if case == "c2_per_launch":
+        monkeypatch.setenv("FGP_FIT_PERSIST", "0")
+    res = {}
+    for mode in ("0", "1", "1"):
+        monkeypatch.setenv("FGP_FIT_GRAPH", mode)
+        s0 = _graph_stats()
+        if case == "c4_batch":
+            sh = bench.Shifts(F, 5, 2 ** 17, bench.shard_seeds(0, 1, 4), dev)
+            sh.reset()
+            data = sh.batch.fit(iterations=20, stop_crit_wait_iterations=21, store_loss_hist=True)
+            lh = torch.stack([d["loss_hist"] for d in data])
+            raw = sh.batch.raw().cpu().clone()
+        else:
+            if case == "c5_per_output":
+                sg = bench.MultiOutputGP(F, 16, 3, 32, dev, per_output=True)
+            else:
+                sg = bench.SingleGP(F, "lattice", 16, 3, dev)
+            sg.reset()
+            data = sg.gp.fit(iterations=20, stop_crit_wait_iterations=21, verbose=0, store_loss_hist=True)
+            lh = data["loss_hist"]
+            raw = torch.cat([sg.gp.raw_scale.detach().reshape(-1), sg.gp.raw_lengthscales.detach().reshape(-1)]).cpu()
+        s1 = _graph_stats()
+        res.setdefault(mode, []).append((lh, raw, [b - a for a, b in zip(s0, s1)]))
+    (lh0, raw0, st0), = res["0"]
+    assert st0[0] == st0[1] == 0, st0                        # FGP_FIT_GRAPH=0: eager
+    for lh, raw, st in res["1"]:
+        assert torch.equal(lh, lh0) and torch.equal(raw, raw0)
+        assert st[0] + st[1] >= 1, st                        # the graph ran
+
+
+def test_fit_run_graph_cached_replay_equals_eager(monkeypatch):
+    """The same engine run again (its buffers unmoved): fgp_fit_run_graph replays the executable graph it cached for
+    this engine token -- bit-identical to the first (captured) run and to the eager sequence."""
+    monkeypatch.setenv("FGP_FIT_PATH", "spectral")
+    gp, _, _ = _gp("lattice", 3, 16)
+    eng = gp._fused_engine(50, 0.1)
+    raw0, prev0, step0 = eng.raw.clone(), eng.prev.clone(), eng.step.clone()
+    out = []
+    for r, mode in enumerate(("1", "1", "1", "0")):
+        monkeypatch.setenv("FGP_FIT_GRAPH", mode)
+        eng.raw.copy_(raw0)
+        eng.prev.copy_(prev0)
+        eng.step.copy_(step0)
+        eng.loss_hist.zero_()
+        s0 = _graph_stats()
+        eng.run(0, 51, final_no_update=True)
+        d = [b - a for a, b in zip(s0, _graph_stats())]
+        out.append((eng.loss_hist[:51].cpu().clone(), eng.raw.cpu().clone()))
+        assert d == ([0, 1, 0] if r == 0 else [1, 0, 0] if mode == "1" else [0, 0, 0]), (r, d)
+    for lh, raw in out[1:]:
+        assert torch.equal(lh, out[0][0]) and torch.equal(raw, out[0][1])
