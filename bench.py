@@ -373,8 +373,10 @@ def secondary_configs(F, args, device, rank=0, world=1, collect=None):
                                          stats=ROCPROF_PREDICT_STATS, sq=PMC_SQ_PREDICT,
                                          live_ms=phases.get("post_mean") if phases else None,
                                          launches=1 + (1 if sg.outputs % 4 else 0))
+        roofs = secondary_rooflines(name.split(":")[0], sg.n, d, total, args.n_mean, args.fit_iters)
         out.append({"metric": "GP fit+predict points/sec" if total == 1 else
                     "multi-output GP fit+predict output-points/sec",
+                    "roofline": roofs[0] if roofs else None, "rooflines_other": roofs[1:],
                     "value": None if giveup_err else sg.n * total / sec, "error": giveup_err,
                     "unit": "points/s" if total == 1 else "output-points/s",
                     "ms_per_step": sec * 1e3, "steps": max(5, args.steps), "n_gpus": world,
@@ -955,6 +957,106 @@ def roofline_post_mean(kernel, grid, pairs, d, nb, stats=None, sq=None, live_ms=
                        "source": os.path.relpath(sq or PMC_SQ_SUMMARY, ROOT) + " (SQ_INSTS_VALU)"}
     if live_ms is not None:
         out["phase_ms_live"] = live_ms
+    return out
+
+
+SECONDARY_STATS = os.path.join(ROOT, "profiles", "r06k_secondary_stats.json")
+FP64_MFMA_PEAK_FLOPS = 78.6e12       # MI355X FP64 matrix peak (spec; = the FP64 vector FMA rate)
+
+
+def secondary_rooflines(case, n, d, outputs, n_mean, fit_iters):
+    """Rooflines of a secondary line's kernels, priced on the committed rocprofv3 trace + PMC passes
+    of the same steps (tools/secondary_profile.sh -> tools/secondary_kernels.py, profiles/r06k_secondary_stats.json;
+    durations: the kernel trace's per-launch averages; traffic: FETCH_SIZE x2 (gfx950) + WRITE_SIZE per launch).
+    Returns [primary, others...] (primary = the line's longest kernel per step) or []."""
+    try:
+        st = json.load(open(SECONDARY_STATS))
+    except (OSError, ValueError):
+        return []
+    tr = st["trace"].get(case)
+    if not tr:
+        return []
+    src = os.path.relpath(SECONDARY_STATS, ROOT)
+
+    def find(prefix):
+        for k, v in tr.items():
+            if k.startswith(prefix):
+                return k, v
+        return None, None
+
+    def counters(k):
+        f = st.get("fetch_kb", {}).get(case, {}).get(k)
+        w = st.get("write_kb", {}).get(case, {}).get(k)
+        q = st.get("sq_insts_valu", {}).get(case, {}).get(k)
+        return (None if f is None or w is None else 2.0 * f * 1024 + w * 1024), q
+
+    def hbm(k, v, alg, what):
+        traffic, q = counters(k)
+        ach = alg / (v["avg_us"] * 1e-6) / 1e9
+        r = {"bound": "hbm", "kernel": k.split("|")[0], "grid_threads": int(k.split("=")[-1]), "algorithmic_bytes": alg,
+             "bytes_model": what, "avg_us": v["avg_us"], "launches_per_step": v["launches_per_step"],
+             "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
+             "source": src}
+        if q is not None:
+            r["valu_frac"] = q * 64 / (v["avg_us"] * 1e-6) / FP64_LANE_OPS_PEAK
+        return r
+
+    K = n // 2 + 1 if case != "C3" else n
+    out = []
+    if case in ("C2", "C3"):
+        k, v = find("k_spec_persist")
+        if k is not None:
+            traffic, q = counters(k)
+            ach = q * 64 / (v["avg_us"] * 1e-6) if q is not None else None
+            lds = 8 * K * (2 ** d + 1)        # the spectra + Y, LDS-resident, read once per iteration
+            out.append({"bound": "latency (one grid barrier + reduction + Rprop step per iteration)", "kernel": k.split("|")[0],
+                        "grid_threads": int(k.split("=")[-1]), "avg_us": v["avg_us"], "iterations": fit_iters + 1,
+                        "iteration_us": v["avg_us"] / (fit_iters + 1), "achieved": ach, "peak": FP64_LANE_OPS_PEAK,
+                        "unit": "FP64 lane-ops/s (SQ_INSTS_VALU x 64)", "frac": None if ach is None else ach / FP64_LANE_OPS_PEAK,
+                        "lds_bytes_per_iteration": lds, "hbm_traffic_per_launch": traffic,
+                        "note": "the whole 51-iteration fit in one launch (fgp_fit_persist): spectra + Y stay in LDS, so "
+                                "neither HBM nor VALU bounds the iteration; its time is the in-kernel barrier chain",
+                        "source": src})
+    if case in ("C5", "C5 mixed"):
+        k, v = find("Cijk_")
+        if k is not None:
+            flops = 2.0 * n_mean * n * outputs / v["launches_per_step"]
+            ach = flops / (v["avg_us"] * 1e-6)
+            out.append({"bound": "mfma (fp64)", "kernel": "library DGEMM (post_mean: kernel rows x coefficients)",
+                        "kernel_symbol": k.split("|")[0][:80], "flops_per_launch": flops,
+                        "flops_model": "2 N n B over its launches per step", "avg_us": v["avg_us"],
+                        "launches_per_step": v["launches_per_step"], "achieved": ach / 1e12, "peak": FP64_MFMA_PEAK_FLOPS / 1e12,
+                        "unit": "TFLOP/s", "frac": ach / FP64_MFMA_PEAK_FLOPS, "traffic": counters(k)[0], "source": src})
+        k, v = find("k_inv_cols_c2r")
+        if k is not None:
+            out.append(hbm(k, v, 32.0 * (n // 2) * outputs, "coefficients, column pass: 16 (n/2) B read + 16 (n/2) B written"))
+        k, v = find("k_inv_rows_c2r")
+        if k is not None:
+            out.append(hbm(k, v, (16.0 * (n // 2) + 8.0 * n) * outputs, "coefficients, row pass: 16 (n/2) B read + 8 n B written"))
+        k, v = find("k_spec_persist")
+        if k is not None:
+            traffic, q = counters(k)
+            out.append({"bound": "latency (single-launch fit)", "kernel": k.split("|")[0], "avg_us": v["avg_us"],
+                        "iteration_us": v["avg_us"] / (fit_iters + 1), "frac": None if q is None else
+                        q * 64 / (v["avg_us"] * 1e-6) / FP64_LANE_OPS_PEAK, "unit": "FP64 VALU fraction", "source": src})
+    if case == "C5 per-output":
+        k, v = find("k_spec_tile")
+        if k is not None:
+            out.append(hbm(k, v, 8.0 * K * (2 ** d) + 8.0 * K * outputs,
+                           "one fit iteration of %d problems sharing the spectra: 2^d spectra + Y of every problem, "
+                           "8 K bytes each (K = n/2 + 1)" % outputs))
+        k, v = find("k_spec_post_var")
+        if k is not None:
+            traffic, q = counters(k)
+            if q is not None:
+                ach = q * 64 / (v["avg_us"] * 1e-6)
+                out.append({"bound": "fp64 valu", "kernel": k.split("|")[0], "avg_us": v["avg_us"],
+                            "launches_per_step": v["launches_per_step"], "achieved": ach, "peak": FP64_LANE_OPS_PEAK,
+                            "unit": "FP64 lane-ops/s (SQ_INSTS_VALU x 64)", "frac": ach / FP64_LANE_OPS_PEAK,
+                            "traffic": traffic, "note": "post_var of the %d problems by linearity of the test points' row "
+                            "spectra: per (problem, test point, frequency) the 2^d-term polynomial" % outputs,
+                            "source": src})
+    out.sort(key=lambda r: -(r.get("avg_us", 0) * r.get("launches_per_step", 1)))
     return out
 
 

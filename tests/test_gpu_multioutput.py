@@ -358,3 +358,48 @@ def test_bench_c5_50_iterations_matches_reference(mixed):
     assert errs["scale"] <= C5_50_TOL["params"] and errs["lengthscales"] <= C5_50_TOL["params"], errs
     assert errs["pmean"] <= C5_50_TOL["pmean"], errs
     assert errs["pvar_kxx"] <= C5_50_TOL["pvar_kxx"], errs
+
+
+def test_bench_c5_per_output_50_iterations_matches_reference():
+    """The C5 per-output line (512 independent eigen-problems on one point set) exactly as bench.step_single times it,
+    50 iterations, against the REAL reference (tests/golden/make_golden_c5.py --per-output --its 50).  Over 50 sign-driven
+    Rprop steps the reference's own torch.fft and pocketfft runs fork on ONE output (profiles/r06_c5_po_backend_spread.json:
+    output 111; the other 511 end with identical parameters), so each output is held to the reference run it follows:
+    parameters 1e-10 of the torch.fft run, or -- on a forked output only -- of the pocketfft run
+    (c5_m18_d3_b512_po_it50_alt.npz); posterior means 5x the spread of the unforked outputs (2.6e-7 relative -> 1.3e-6)
+    against the run the output follows; variances 1e-8 K(x,x); the summed loss history 5x the spread (7.1e-7 -> 3.6e-6)."""
+    import argparse
+    import json
+    import numpy as np
+    import bench
+    here = os.path.dirname(__file__)
+    g = np.load(os.path.join(here, "golden", "c5_m18_d3_b512_po_it50.npz"))
+    alt = np.load(os.path.join(here, "golden", "c5_m18_d3_b512_po_it50_alt.npz"))
+    forked = set(json.load(open(os.path.join(here, "..", "profiles", "r06_c5_po_backend_spread.json")))["outputs_forked"])
+    m, d, B, its = int(g["m"]), int(g["d"]), int(g["B"]), int(g["its"])
+    dev = torch.device(DEV, 0)
+    sg = bench.MultiOutputGP(F, m, d, B, dev, per_output=True)
+    xt = torch.from_numpy(g["x_test"])
+    pm, pv = bench.step_single(sg, argparse.Namespace(fit_iters=its), xt.to(dev), xt[:g["pvar"].shape[-1]].to(dev))
+    pm, pv = pm.cpu().numpy(), pv.cpu().numpy()
+    rs = sg.gp.raw_scale.detach().cpu().numpy().reshape(B, -1)
+    rl = sg.gp.raw_lengthscales.detach().cpu().numpy().reshape(B, -1)
+    sg.reset()
+    data = sg.gp.fit(iterations=its, stop_crit_wait_iterations=its + 1, verbose=0, store_loss_hist=True)
+    assert rel_err(data["loss_hist"], g["loss_hist"]) <= 3.6e-6
+    kxx = np.abs(g["kxx_all"])
+    follows = {}
+    for b in range(B):
+        errs = []
+        for name, run in (("torch", g), ("pocketfft", alt)):
+            errs.append(max(np.abs(rs[b] - run["raw_scale"].reshape(B, -1)[b]).max(),
+                            np.abs(rl[b] - run["raw_lengthscales"].reshape(B, -1)[b]).max()))
+        if errs[0] <= 1e-10:
+            follows[b] = g
+        else:
+            assert b in forked and errs[1] <= 1e-10, (b, errs)
+            follows[b] = alt
+    pm_ref = np.stack([follows[b]["pmean"][b] for b in range(B)])
+    pv_ref = np.stack([follows[b]["pvar"][b] for b in range(B)])
+    assert np.abs(pm - pm_ref).max() <= 1.3e-6 * np.abs(pm_ref).max()
+    assert (np.abs(pv - pv_ref) / kxx).max() <= 1e-8
