@@ -347,6 +347,91 @@ __global__ __launch_bounds__(256, 2) void k_lab2(Args a) {
   }
 }
 
+// Third family (round 6): a dedicated DMA producer wave per workgroup.  Waves 0-3 compute (2
+// problems each, as the fused kernel), wave 4 only issues the LDS-DMA loads: it keeps up to RING - 1 chunks in flight,
+// and for the oldest one waits for its own loads (counted vmcnt) and publishes it by an LDS flag (full[slot] = chunk + 1);
+// a compute wave spins on that flag, computes, and counts itself done in done[slot] (ds_add), which the producer waits
+// for before it refills the slot.  No workgroup barrier in the chunk loop.
+template <int RING, int MODE>
+__global__ __launch_bounds__(320, 2) void k_lab3(Args a) {
+  extern __shared__ double lds[];
+  __shared__ int full[RING], done[RING];
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  if (a.stamps && threadIdx.x == 0) a.stamps[blockIdx.x * 2] = wall_clock64();
+  if (threadIdx.x < RING) {
+    full[threadIdx.x] = 0;
+    done[threadIdx.x] = 0;
+  }
+  __syncthreads();
+  const int nc = a.cpb;
+  const long q0 = (long)blockIdx.x * nc;
+  volatile int* vfull = full;
+  volatile int* vdone = done;
+  if (w == 4) {
+    // producer
+    int issued = 0, flagged = 0;
+    while (flagged < nc) {
+      while (issued < nc && issued < flagged + RING - 1) {
+        const int slot = issued % RING;
+        const int need = 4 * (issued / RING);          // consumers done with chunk issued - RING in this slot
+        for (int spin = 0; vdone[slot] < need && spin < (1 << 24); ++spin) __builtin_amdgcn_s_sleep(1);   // (bounded)
+        double* buf = lds + slot * TILE;
+        if (MODE != 2) {
+          const long q = q0 + issued;
+#pragma unroll
+          for (int j = 0; j < 20; ++j) {
+            const double* base = j < 16 ? a.basis + q * (NS * 64) + j * 128 : a.ysq + q * (G * 64) + (j - 16) * 128;
+            __builtin_amdgcn_global_load_lds((glb_void*)(base + lane * 2), (lds_void*)(buf + 128 * j), 16, 0, 0);
+          }
+        }
+        ++issued;
+      }
+      // the oldest chunk in flight: its 20 loads are the oldest of the wave's outstanding ones
+      const int newer = issued - 1 - flagged;
+      if (newer >= 2) asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
+      else if (newer == 1) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) vfull[flagged % RING] = flagged + 1;
+      ++flagged;
+    }
+  } else {
+    HypS h[2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const double* hp = a.hyp + (2 * w + p) * (2 + D);
+      h[p].scale = hp[0];
+      h[p].noise = hp[1];
+#pragma unroll
+      for (int j = 0; j < D; ++j) h[p].ls[j] = hp[2 + j];
+    }
+    const double rootn = 1024.0, wl = 1.0;
+    Acc acc[2];
+    for (int c = 0; c < nc; ++c) {
+      const int slot = c % RING;
+      for (int spin = 0; __builtin_amdgcn_readfirstlane(vfull[slot]) != c + 1 && spin < (1 << 24); ++spin)
+        __builtin_amdgcn_s_sleep(1);                   // (bounded: a broken hand-off ends, with wrong partials)
+      const double* buf = lds + slot * TILE;
+      if (MODE != 1) {
+        double phi[NS];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) phi[s] = buf[64 * s + lane];
+#pragma unroll
+        for (int p = 0; p < 2; ++p) terms(phi, h[p], rootn, wl, buf[64 * (NS + 2 * w + p) + lane], acc[p]);
+      } else {
+        acc[0].norm += buf[lane] + buf[64 * (NS + 2 * w) + lane];
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (lane == 0) atomicAdd(&done[slot], 1);
+    }
+#pragma unroll
+    for (int p = 0; p < 2; ++p) wave_partials(acc[p], a.partials + (long)(2 * w + p) * NQ * a.nblk + blockIdx.x, a.nblk);
+  }
+  if (a.stamps && threadIdx.x == 0) {
+    a.stamps[blockIdx.x * 2 + 1] = wall_clock64();
+    a.xcc[blockIdx.x] = __builtin_amdgcn_s_getreg((3 << 11) | 20);
+  }
+}
+
 template <typename F>
 static double time_us(F launch, int reps) {
   hipEvent_t e0, e1;
@@ -485,6 +570,11 @@ int main(int argc, char** argv) {
   run("fixed saddr r2 ppw1 1024x8 wpc4", k_lab<2, false, true, 0, 4, 1>, 2, 1024, 8, true, 512);
   if (all) run("dyn saddr r2 ppw1 res2 cpb4", k_lab<2, true, true, 0, 4, 1>, 2, 512, 4, true, 512);
   if (all) run("dyn saddr r2 ppw1 res2 cpb8", k_lab<2, true, true, 0, 4, 1>, 2, 512, 8, true, 512);
+  // third family (round 6): a DMA producer wave + 4 compute waves, LDS flags instead of barriers
+  run("lab3 producer r3", k_lab3<3, 0>, 3, 512, 16, true, 320);
+  run("lab3 producer r3 stream", k_lab3<3, 1>, 3, 512, 16, false, 320);
+  run("lab3 producer r3 compute", k_lab3<3, 2>, 3, 512, 16, false, 320);
+  run("lab3 producer r2", k_lab3<2, 0>, 2, 512, 16, true, 320);
   // second family: sub-chunks per slot, nt, prologue overlap
   run("lab2 ck1", k_lab2<1, 0, 0, 1, 0>, 2, 512, 16, true, 256, 1);
   run("lab2 ck2", k_lab2<2, 0, 0, 1, 0>, 2, 512, 8, true, 256, 2);
