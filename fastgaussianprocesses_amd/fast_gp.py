@@ -685,6 +685,13 @@ class AbstractFastGP(torch.nn.Module):
                      task_kernel=store_hists or (store_task_kernel_hist and (
                          self.raw_factor_task_kernel.requires_grad or self.raw_noise_task_kernel.requires_grad)))
         stop = (np.log(1 + stop_crit_improvement_threshold), stop_crit_wait_iterations)
+        if masks is not None and optimizer is None and loss_metric == "MLL" and self._fused_ok():
+            mk = self._masked_ysq(masks)
+            if mk is not None:
+                # only the outputs y[..., *masks] in the loss, shared hyper-parameters: the device fit on their
+                # Y = sum |ytilde_b|^2 with d_out = the selected count (abstract_gp.py:220-235, 253-260)
+                return self._fit_fused(iterations, 1e-1 if lr is None else lr, stop, hists, verbose, verbose_indent,
+                                       ysq=mk[0], d_out=mk[1])
         fused = optimizer is None and masks is None and self._fused_ok() and (
             loss_metric == "MLL" or self._alt_loss_ok(loss_metric, cv_weights))
         if optimizer is None:
@@ -728,6 +735,27 @@ class AbstractFastGP(torch.nn.Module):
                 return False
         pb = self._problem_batch()
         return pb is not None and pb[1] <= 16 and self._spec_basis(self._nh, pb[1], force=True) is not None
+
+    def _masked_ysq(self, masks):
+        """(Y [1, n], d_out) of fit(masks=...) with ONE eigen-problem (hyper-parameters shared by the outputs): Y sums
+        |ytilde_b|^2 over the selected outputs y[..., *masks] (repeats counted, as the reference's indexing does) and d_out
+        is their count (abstract_gp.py:220-224; the logdet term then weighs the shared logdet d_out times, :258-259).
+        None when the problem batch has several eigen-problems (per-output hyper-parameters: the generic path)."""
+        pb = self._problem_batch()
+        if pb is None or pb[1] != 1 or len(self.shape_batch) == 0:
+            return None
+        masks = torch.atleast_2d(masks)
+        assert masks.ndim == 2 and len(masks) <= len(self.shape_batch)
+        d_out = torch.empty(self.shape_batch)[(..., *masks)].numel()
+        n = self._nh
+        half = self._ytilde_half()
+        idx = tuple(m.to(self.device) for m in masks)
+        if half is not None:
+            sel = half[(..., *idx, slice(None))]
+            return ops.sum_sq_half(sel.reshape(-1, sel.shape[-1]).contiguous(), n, 1), d_out
+        yt = self.get_ytilde(0)
+        sel = yt[(..., *idx, slice(None))]
+        return ops.sum_sq(sel.reshape(-1, n).contiguous(), 1), d_out
 
     def _problem_batch(self):
         """G and the per-problem flags for the fused layout (None when shapes need broadcasting)."""
