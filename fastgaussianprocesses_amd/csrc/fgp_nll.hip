@@ -1426,7 +1426,8 @@ static int to_nll(const fgp_nll_desc* d, Nll& a) {
   a.cv_weight = d->cv_weight;
   if (a.loss != FGP_LOSS_MLL) {
     if (a.loss != FGP_LOSS_GCV && a.loss != FGP_LOSS_CV) return set_error(kErrInvalid, "bad loss_metric %d", a.loss);
-    if (!d->basis || mt) return set_error(kErrUnsupported, "GCV / CV fits need the spectral path (basis), one task");
+    if (!d->basis && !mt) return set_error(kErrUnsupported, "GCV / CV fits need the spectral path (basis)");
+    if (mt && a.loss != FGP_LOSS_GCV) return set_error(kErrUnsupported, "multitask spectral fits: MLL or GCV");
   }
   if (a.spec) {
     a.re = a.r2c = 0;
@@ -1454,6 +1455,7 @@ static int to_nll(const fgp_nll_desc* d, Nll& a) {
     const int64_t chunks = n / a.mt_F;
     a.nb = (int)std::min<int64_t>(kSpecBlocks, chunks);
     a.mt_cpb = (int)(chunks / a.nb);
+    if (a.loss == FGP_LOSS_GCV) a.nq = 6 + 2 * a.d;    // the single-task GCV partial layout (k_spec_loss_step)
   }
   return kOk;
 }

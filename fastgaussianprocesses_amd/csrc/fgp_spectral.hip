@@ -1043,7 +1043,8 @@ __global__ __launch_bounds__(kWG) void k_spec_loss_step(Nll a, Fit f, int iter, 
     tot[u] = s;
   }
   __syncthreads();
-  const double n = (double)((int64_t)1 << a.log2n);
+  // (multitask GCV: the trace is normalised by the points of all T tasks, util.py:379 self.n.sum())
+  const double n = (double)((int64_t)1 << a.log2n) * (a.mt > 0 ? a.mt : 1);
   const bool cv = a.loss == FGP_LOSS_CV;
   if ((int)threadIdx.x < cnt) {
     const int i = threadIdx.x;
@@ -1532,13 +1533,18 @@ __device__ __forceinline__ void mt_pair_kl(int p, int T, int& k, int& l) {
   l = k + p;
 }
 
-template <int D>
+// GCV (ABI 17, util.py:371-380 with T tasks of equal n): numer N = sum_j |z_j|^2, Tr = sum_j tr Lambda_j^-1, loss
+// N / (Tr / (T n))^2; with u = Lambda^-1 z, dN = -2 Re(u^H dLambda z) and dTr = -Re tr(Lambda^-2 dLambda), so the block
+// partials are the single-task GCV layout (k_spec_loss_step): [N, Tr, S1 (noise, scale, l_m), S2 (noise, scale, l_m)]
+// with S1 = 1/2 Re tr(W1 dLambda), W1 = z u^H + u z^H, and S2 = 1/2 Re tr(W2 dLambda), W2 = 2 Lambda^-2.
+template <int D, bool GCV = false>
 __global__ __launch_bounds__(kWG) void k_mt_spec_iter(Nll a) {
-  constexpr int NS = 1 << D, NQ = 4 + D;
+  constexpr int NS = 1 << D, NQ = GCV ? 6 + 2 * D : 4 + D;
   __shared__ double ls_pow[NS];                          // l^S
   __shared__ double kt[kMtMaxT * kMtMaxT];
-  __shared__ double2 blk[kMtF][kMtMaxT * kMtMaxT];       // Lambda_j (full), factored in place
-  __shared__ double2 wv[kMtF][kMtMaxT * (kMtMaxT + 1) / 2];   // W[l, k] of pair (k, l)
+  __shared__ double2 blk[kMtF][kMtMaxT * kMtMaxT];       // Lambda_j (full), factored in place (GCV: then W2 packed)
+  __shared__ double2 wv[kMtF][kMtMaxT * (kMtMaxT + 1) / 2];   // W[l, k] of pair (k, l)  (GCV: W1)
+  __shared__ double2 iv[GCV ? kMtF : 1][GCV ? kMtMaxT * (kMtMaxT + 1) / 2 : 1];   // GCV: Lambda^-1[l, k], l >= k
   __shared__ double red[kWG / 64];
   const int T = a.mt, NP = T * (T + 1) / 2, F = a.mt_F, tid = threadIdx.x;
   const int64_t n = (int64_t)1 << a.log2n;
@@ -1555,8 +1561,9 @@ __global__ __launch_bounds__(kWG) void k_mt_spec_iter(Nll a) {
   if (tid < T * T) kt[tid] = a.mt_kt[tid];
   const double rootn = sqrt((double)n), sn = rootn * h.scale;
   double acc_norm = 0.0, acc_ld = 0.0, acc_noise = 0.0, acc_sc = 0.0, acc_l[D];
+  double acc_noise2 = 0.0, acc_sc2 = 0.0, acc_l2[D];     // (GCV: the S2 sums; acc_ld holds Tr)
 #pragma unroll
-  for (int m = 0; m < D; ++m) acc_l[m] = 0.0;
+  for (int m = 0; m < D; ++m) acc_l[m] = acc_l2[m] = 0.0;
   for (int c = 0; c < a.mt_cpb; ++c) {
     const int64_t j0 = ((int64_t)blockIdx.x * a.mt_cpb + c) * F;
     __syncthreads();                                     // ls_pow / kt ready; previous chunk's wv consumed
@@ -1610,7 +1617,7 @@ __global__ __launch_bounds__(kWG) void k_mt_spec_iter(Nll a) {
           }
           A[i * T + k] = make_double2(s.x / dk, s.y / dk);
         }
-        acc_ld += log(fabs(dk));
+        if constexpr (!GCV) acc_ld += log(fabs(dk));
       }
       for (int k = 0; k < T; ++k) {
         if (a.spec_net) y[k] = make_double2(static_cast<const double*>(a.mt_ytilde)[(int64_t)k * n + j], 0.0);
@@ -1625,7 +1632,7 @@ __global__ __launch_bounds__(kWG) void k_mt_spec_iter(Nll a) {
           s.y -= t.y;
         }
         z[i] = s;
-        acc_norm += (s.x * s.x + s.y * s.y) / Dg[i];
+        if constexpr (!GCV) acc_norm += (s.x * s.x + s.y * s.y) / Dg[i];
       }
       for (int i = 0; i < T; ++i) z[i] = make_double2(z[i].x / Dg[i], z[i].y / Dg[i]);
       for (int i = T - 1; i >= 0; --i) {
@@ -1659,11 +1666,65 @@ __global__ __launch_bounds__(kWG) void k_mt_spec_iter(Nll a) {
             s.x += t.x / Dg[m];
             s.y += t.y / Dg[m];
           }
+          if constexpr (GCV) {
+            iv[tid][p] = s;
+            if (k == l) acc_ld += s.x;                           // Tr
+            continue;
+          }
           const double2 zz = cmulc(z[l], z[k]);                  // z_l conj(z_k)
           const double2 w = make_double2(s.x - zz.x, s.y - zz.y);
           wv[tid][p] = w;
           if (k == l) acc_noise += 0.5 * w.x * kt[k * T + k];
         }
+      if constexpr (GCV) {
+        // N, u = Lambda^-1 z (the factor: L w = z, w / D, L^H u = w), W1 = z u^H + u z^H, W2 = 2 Lambda^-2 (packed into
+        // the factor's block, which is no longer read)
+        double2 u[kMtMaxT];
+        for (int i = 0; i < T; ++i) {
+          acc_norm += z[i].x * z[i].x + z[i].y * z[i].y;
+          double2 s = z[i];
+          for (int m = 0; m < i; ++m) {
+            const double2 t = cmul(A[i * T + m], u[m]);
+            s.x -= t.x;
+            s.y -= t.y;
+          }
+          u[i] = s;
+        }
+        for (int i = 0; i < T; ++i) u[i] = make_double2(u[i].x / Dg[i], u[i].y / Dg[i]);
+        for (int i = T - 1; i >= 0; --i) {
+          double2 s = u[i];
+          for (int m = i + 1; m < T; ++m) {
+            const double2 t = cmulc(u[m], A[m * T + i]);          // conj(L[m][i]) u[m]
+            s.x -= t.x;
+            s.y -= t.y;
+          }
+          u[i] = s;
+        }
+        const double2* V = iv[tid];
+        auto inv_at = [&](int r, int c) -> double2 {            // Lambda^-1[r][c] from the packed l >= k entries
+          if (r >= c) return V[c * T - c * (c - 1) / 2 + (r - c)];
+          const double2 t = V[r * T - r * (r - 1) / 2 + (c - r)];
+          return make_double2(t.x, -t.y);
+        };
+        for (int p = 0, k = 0; k < T; ++k)
+          for (int l = k; l < T; ++l, ++p) {
+            const double2 a1 = cmulc(z[l], u[k]), a2 = cmulc(u[l], z[k]);   // z_l conj(u_k) + u_l conj(z_k)
+            const double2 w1 = make_double2(a1.x + a2.x, a1.y + a2.y);
+            double2 w2 = make_double2(0.0, 0.0);
+            for (int m = 0; m < T; ++m) {
+              const double2 t = cmul(inv_at(l, m), inv_at(m, k));
+              w2.x += t.x;
+              w2.y += t.y;
+            }
+            w2 = make_double2(2.0 * w2.x, 2.0 * w2.y);
+            wv[tid][p] = w1;
+            A[p] = w2;
+            if (k == l) {
+              acc_noise += 0.5 * w1.x * kt[k * T + k];
+              acc_noise2 += 0.5 * w2.x * kt[k * T + k];
+            }
+          }
+      }
     }
     __syncthreads();
     // (3) gradient: c = w_kl sqrt(n) scale Kt[k, l] W[l, k]; r_S = l^S Re(c Phi^{kl}_S)
@@ -1674,6 +1735,12 @@ __global__ __launch_bounds__(kWG) void k_mt_spec_iter(Nll a) {
       const double wgt = (k == l ? 0.5 : 1.0) * sn * kt[k * T + l];
       const double2 w = wv[f][p];
       const double cx = wgt * w.x, cy = wgt * w.y;
+      double c2x = 0.0, c2y = 0.0;
+      if constexpr (GCV) {
+        const double2 w2 = blk[f][p];
+        c2x = wgt * w2.x;
+        c2y = wgt * w2.y;
+      }
       const int64_t base = (int64_t)p * NS * n + j0 + f;
       constexpr int U = NS < 8 ? NS : 8;
 #pragma unroll 1
@@ -1687,6 +1754,13 @@ __global__ __launch_bounds__(kWG) void k_mt_spec_iter(Nll a) {
 #pragma unroll
           for (int m = 0; m < D; ++m)
             if (m < 3 ? ((t >> m) & 1) : ((sh >> m) & 1)) acc_l[m] += r;
+          if constexpr (GCV) {
+            const double r2 = ls_pow[S] * (c2x * ph.x - c2y * ph.y);
+            acc_sc2 += r2;
+#pragma unroll
+            for (int m = 0; m < D; ++m)
+              if (m < 3 ? ((t >> m) & 1) : ((sh >> m) & 1)) acc_l2[m] += r2;
+          }
         }
       }
     }
@@ -1698,6 +1772,12 @@ __global__ __launch_bounds__(kWG) void k_mt_spec_iter(Nll a) {
   v[3] = acc_sc;
 #pragma unroll
   for (int m = 0; m < D; ++m) v[4 + m] = acc_l[m];
+  if constexpr (GCV) {
+    v[4 + D] = acc_noise2;
+    v[5 + D] = acc_sc2;
+#pragma unroll
+    for (int m = 0; m < D; ++m) v[6 + D + m] = acc_l2[m];
+  }
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
     const double s = block_sum(v[q], red);
@@ -2070,7 +2150,8 @@ int launch_spec_iter(const Nll& a, hipStream_t st, const FitFuse* fz) {
 
 int launch_mt_spec_iter(const Nll& a, hipStream_t st) {
   return with_spec_d(a.d, [&](auto dc) {
-    k_mt_spec_iter<decltype(dc)::value><<<(unsigned)a.nb, kWG, 0, st>>>(a);
+    if (a.loss == FGP_LOSS_GCV) k_mt_spec_iter<decltype(dc)::value, true><<<(unsigned)a.nb, kWG, 0, st>>>(a);
+    else k_mt_spec_iter<decltype(dc)::value><<<(unsigned)a.nb, kWG, 0, st>>>(a);
     return check_launch("k_mt_spec_iter");
   });
 }

@@ -162,8 +162,8 @@ class FusedMLL(object):
         loss_metric: "MLL" (default), or "GCV" / "CV" (fgp_nll_desc.loss_metric, ABI 16: the spectral path only;
                 cv_weight the scalar cv_weights of AbstractGP.fit); their loss history holds [loss, numer, denom]
         """
-        if loss_metric != "MLL" and basis is None:
-            raise ValueError("GCV / CV fits run on the spectral path only (basis)")
+        if loss_metric != "MLL" and basis is None and (mt is None or loss_metric != "GCV"):
+            raise ValueError("GCV / CV fits run on the spectral path only (basis; multitask: GCV)")
         require_device(ysq, "FusedMLL")
         self.device = ysq.device
         self.family = int(family)

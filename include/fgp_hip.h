@@ -249,7 +249,10 @@ typedef struct fgp_nll_desc {
    * summed over the problems (or per problem with a per_problem fit desc), gradients in closed form.  Every
    * iteration is the per-wave partials kernel (2 + 2 (2 + d) quantities per problem and k block) plus the
    * reduction / step kernel; the tile, single-launch and persistent kernels are MLL-only.  A desc that is not
-   * per_problem holds at most 16 problems. */
+   * per_problem holds at most 16 problems.
+   * ABI 17 -- GCV of a multitask spectral fit (mt_tasks = T, equal n, fixed task kernel): numer = sum_j |z_j|^2 with
+   * z_j = Lambda_j^-1 y_j, denom = (sum_j tr Lambda_j^-1 / (T n))^2 (util.py:371-380), the gradient from u = Lambda^-1 z
+   * and Lambda^-2 per frequency block. */
   int loss_metric;
   double cv_weight;
 } fgp_nll_desc;

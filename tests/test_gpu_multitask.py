@@ -373,3 +373,40 @@ def test_multitask_gp_pickles():
     assert type(gp2) is type(gp)
     x = torch.rand((8, 2), device=DEV)
     assert torch.equal(gp2.post_mean(x), gp.post_mean(x))
+
+
+@pytest.mark.parametrize("path", ["device", "generic"])
+@pytest.mark.parametrize("name", ["deriv_net_d2_a4_equal", "deriv_lattice_d2_a2_equal"])
+def test_multitask_gcv_fit_matches_reference(name, path, monkeypatch):
+    """fit(loss_metric="GCV") of a derivative-informed GP (T = 3 tasks of equal n, fixed task kernel) against the REAL
+    reference's 6-iteration trajectory (tests/golden/make_golden_mt_gcv.py -> tests/golden/mt_gcv/*.npz), through the
+    device path (ABI 17: k_mt_spec_iter's GCV variant -- N = sum |z|^2, Tr = sum tr Lambda^-1, the closed-form
+    gradient from u = Lambda^-1 z and Lambda^-2 -- and k_spec_loss_step) and the generic autograd loop
+    (FGP_ALT_LOSS_DEVICE=0).  Tolerances of tests/test_gpu_losses.py: loss 2e-7 relative, lengthscale trajectory
+    1e-10, post_mean 1e-7 (pred_tol's for the ill-conditioned lattice fixture)."""
+    import os
+    from fastgaussianprocesses_amd import fit_engine
+    with np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "mt_gcv", name + ".npz"),
+                 allow_pickle=False) as f:
+        r = {k: f[k] for k in f.files}
+    monkeypatch.setenv("FGP_ALT_LOSS_DEVICE", "1" if path == "device" else "0")
+    seen = []
+    orig = fit_engine.FusedMLL.__init__
+
+    def init(self, *a, **k):
+        seen.append(k.get("loss_metric", "MLL"))
+        return orig(self, *a, **k)
+    monkeypatch.setattr(fit_engine.FusedMLL, "__init__", init)
+    g = load_golden(name)
+    gp = product_mt(g)
+    assert gp._mt_fused_ok()
+    its = len(r["loss_hist"]) - 1
+    data = gp.fit(loss_metric="GCV", iterations=its, store_hists=True, verbose=0, stop_crit_wait_iterations=its + 5)
+    assert seen == (["GCV"] if path == "device" else []), seen
+    assert data["iterations"] == its
+    assert rel_err(data["loss_hist"], r["loss_hist"]) <= 2e-7
+    assert rel_err(data["lengthscales_hist"], r["lengthscales_hist"]) <= 1e-10
+    assert rel_err(gp.raw_lengthscales, r["raw_lengthscales"]) <= 1e-10
+    xd = torch.from_numpy(g["x_test"]).to(DEV)
+    # (deriv_lattice_d2_a2_equal: the ill-conditioned posterior mean's documented tolerance, PRED_TOL)
+    assert rel_err(gp.post_mean(xd), r["pmean"]) <= pred_tol(name, "fit_pmean", 1e-7)
