@@ -12,7 +12,7 @@ import torch
 
 _LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
 LIB_PATH = os.environ.get("FGP_LIB_PATH") or os.path.join(_LIB_DIR, "libfgp_hip.so")   # override: experiments
-ABI_VERSION = 17
+ABI_VERSION = 18
 MT_MAX_TASKS = 16
 MAX_D = 8
 PARTS_ARRAY = 0

@@ -1427,7 +1427,6 @@ static int to_nll(const fgp_nll_desc* d, Nll& a) {
   if (a.loss != FGP_LOSS_MLL) {
     if (a.loss != FGP_LOSS_GCV && a.loss != FGP_LOSS_CV) return set_error(kErrInvalid, "bad loss_metric %d", a.loss);
     if (!d->basis && !mt) return set_error(kErrUnsupported, "GCV / CV fits need the spectral path (basis)");
-    if (mt && a.loss != FGP_LOSS_GCV) return set_error(kErrUnsupported, "multitask spectral fits: MLL or GCV");
   }
   if (a.spec) {
     a.re = a.r2c = 0;
@@ -1455,7 +1454,7 @@ static int to_nll(const fgp_nll_desc* d, Nll& a) {
     const int64_t chunks = n / a.mt_F;
     a.nb = (int)std::min<int64_t>(kSpecBlocks, chunks);
     a.mt_cpb = (int)(chunks / a.nb);
-    if (a.loss == FGP_LOSS_GCV) a.nq = 6 + 2 * a.d;    // the single-task GCV partial layout (k_spec_loss_step)
+    if (a.loss != FGP_LOSS_MLL) a.nq = 6 + 2 * a.d;    // the single-task GCV / CV partial layout (k_spec_loss_step)
   }
   return kOk;
 }
@@ -1840,7 +1839,8 @@ int fgp_nll_partials_len(const fgp_nll_desc* desc, int64_t* len) {
   if (rc != kOk) return rc;
   if (!len) return set_error(kErrInvalid, "fgp_nll_partials_len: null len");
   const int64_t nb_doc = std::max<int64_t>(1, ((int64_t)1 << a.log2n) >> 12);
-  *len = (int64_t)a.G * a.nq * (std::max<int64_t>(a.nb, nb_doc) + 1) + a.G;
+  const int64_t gp = (a.mt > 0 && a.loss == FGP_LOSS_CV) ? a.mt : a.G;   // multitask CV: partials per task
+  *len = gp * a.nq * (std::max<int64_t>(a.nb, nb_doc) + 1) + gp;
   if (a.spec) {   // level-1 + level-2 partials + counters of the fused spectral step (fgp_spectral.hip)
     int64_t off;
     int cnt;

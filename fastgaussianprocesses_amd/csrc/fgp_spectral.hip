@@ -1044,8 +1044,9 @@ __global__ __launch_bounds__(kWG) void k_spec_loss_step(Nll a, Fit f, int iter, 
   }
   __syncthreads();
   // (multitask GCV: the trace is normalised by the points of all T tasks, util.py:379 self.n.sum())
-  const double n = (double)((int64_t)1 << a.log2n) * (a.mt > 0 ? a.mt : 1);
+  // (multitask CV: I_t over the n points of task t)
   const bool cv = a.loss == FGP_LOSS_CV;
+  const double n = (double)((int64_t)1 << a.log2n) * (a.mt > 0 && !cv ? a.mt : 1);
   if ((int)threadIdx.x < cnt) {
     const int i = threadIdx.x;
     const double N1 = tot[i * NQ + 0], T = tot[i * NQ + 1];
@@ -1537,8 +1538,15 @@ __device__ __forceinline__ void mt_pair_kl(int p, int T, int& k, int& l) {
 // N / (Tr / (T n))^2; with u = Lambda^-1 z, dN = -2 Re(u^H dLambda z) and dTr = -Re tr(Lambda^-2 dLambda), so the block
 // partials are the single-task GCV layout (k_spec_loss_step): [N, Tr, S1 (noise, scale, l_m), S2 (noise, scale, l_m)]
 // with S1 = 1/2 Re tr(W1 dLambda), W1 = z u^H + u z^H, and S2 = 1/2 Re tr(W2 dLambda), W2 = 2 Lambda^-2.
-template <int D, bool GCV = false>
+// CV (ABI 18, util.py:381-394 + abstract_gp.py:261-272 with T tasks of equal n): K^-1's diagonal is constant over the
+// points of task t, I_t = (1/n) sum_j Lambda_j^-1[t, t] (K^-1's block (t, t) is ift diag(Lambda^-1[t, t]) ft), and
+// sum_i coeffs_{t,i}^2 = N_t = sum_j |z_{j,t}|^2 (Parseval), so loss = w sum_t N_t / I_t^2 -- the single-task CV of each
+// task.  Workgroup (block, t) = blockIdx (x, y): with v = Lambda^-1 e_t (column t of the inverse) and u = v z_t,
+// dN_t = -2 Re(u^H dLambda z) and d(n I_t) = -v^H dLambda v: the GCV layout per task, W1 = z u^H + u z^H, W2 = 2 v v^H,
+// partials [t][N_t, n I_t, S1, S2] read by k_spec_loss_step as T problems of one loss.
+template <int D, bool GCV = false, bool CV = false>
 __global__ __launch_bounds__(kWG) void k_mt_spec_iter(Nll a) {
+  static_assert(!CV || GCV, "CV uses the GCV machinery");
   constexpr int NS = 1 << D, NQ = GCV ? 6 + 2 * D : 4 + D;
   __shared__ double ls_pow[NS];                          // l^S
   __shared__ double kt[kMtMaxT * kMtMaxT];
@@ -1547,6 +1555,7 @@ __global__ __launch_bounds__(kWG) void k_mt_spec_iter(Nll a) {
   __shared__ double2 iv[GCV ? kMtF : 1][GCV ? kMtMaxT * (kMtMaxT + 1) / 2 : 1];   // GCV: Lambda^-1[l, k], l >= k
   __shared__ double red[kWG / 64];
   const int T = a.mt, NP = T * (T + 1) / 2, F = a.mt_F, tid = threadIdx.x;
+  const int tcv = CV ? (int)blockIdx.y : -1;             // CV: this workgroup's task
   const int64_t n = (int64_t)1 << a.log2n;
   stamp_begin(a);
   Hyp h;
@@ -1668,7 +1677,7 @@ __global__ __launch_bounds__(kWG) void k_mt_spec_iter(Nll a) {
           }
           if constexpr (GCV) {
             iv[tid][p] = s;
-            if (k == l) acc_ld += s.x;                           // Tr
+            if (k == l && (!CV || k == tcv)) acc_ld += s.x;      // Tr (CV: n I_t)
             continue;
           }
           const double2 zz = cmulc(z[l], z[k]);                  // z_l conj(z_k)
@@ -1680,7 +1689,35 @@ __global__ __launch_bounds__(kWG) void k_mt_spec_iter(Nll a) {
         // N, u = Lambda^-1 z (the factor: L w = z, w / D, L^H u = w), W1 = z u^H + u z^H, W2 = 2 Lambda^-2 (packed into
         // the factor's block, which is no longer read)
         double2 u[kMtMaxT];
-        for (int i = 0; i < T; ++i) {
+        const double2* V = iv[tid];
+        auto inv_at = [&](int r, int c) -> double2 {            // Lambda^-1[r][c] from the packed l >= k entries
+          if (r >= c) return V[c * T - c * (c - 1) / 2 + (r - c)];
+          const double2 t = V[r * T - r * (r - 1) / 2 + (c - r)];
+          return make_double2(t.x, -t.y);
+        };
+        if constexpr (CV) {
+          // N_t, v = Lambda^-1 e_t, u = v z_t, W1 = z u^H + u z^H, W2 = 2 v v^H
+          acc_norm += z[tcv].x * z[tcv].x + z[tcv].y * z[tcv].y;
+          double2 v[kMtMaxT];
+          for (int i = 0; i < T; ++i) {
+            v[i] = inv_at(i, tcv);
+            u[i] = cmul(v[i], z[tcv]);
+          }
+          for (int p = 0, k = 0; k < T; ++k)
+            for (int l = k; l < T; ++l, ++p) {
+              const double2 a1 = cmulc(z[l], u[k]), a2 = cmulc(u[l], z[k]);
+              const double2 w1 = make_double2(a1.x + a2.x, a1.y + a2.y);
+              const double2 vv = cmulc(v[l], v[k]);                    // v_l conj(v_k)
+              const double2 w2 = make_double2(2.0 * vv.x, 2.0 * vv.y);
+              wv[tid][p] = w1;
+              A[p] = w2;
+              if (k == l) {
+                acc_noise += 0.5 * w1.x * kt[k * T + k];
+                acc_noise2 += 0.5 * w2.x * kt[k * T + k];
+              }
+            }
+        }
+        for (int i = 0; i < T && !CV; ++i) {
           acc_norm += z[i].x * z[i].x + z[i].y * z[i].y;
           double2 s = z[i];
           for (int m = 0; m < i; ++m) {
@@ -1690,8 +1727,8 @@ __global__ __launch_bounds__(kWG) void k_mt_spec_iter(Nll a) {
           }
           u[i] = s;
         }
-        for (int i = 0; i < T; ++i) u[i] = make_double2(u[i].x / Dg[i], u[i].y / Dg[i]);
-        for (int i = T - 1; i >= 0; --i) {
+        for (int i = 0; i < T && !CV; ++i) u[i] = make_double2(u[i].x / Dg[i], u[i].y / Dg[i]);
+        for (int i = T - 1; i >= 0 && !CV; --i) {
           double2 s = u[i];
           for (int m = i + 1; m < T; ++m) {
             const double2 t = cmulc(u[m], A[m * T + i]);          // conj(L[m][i]) u[m]
@@ -1700,13 +1737,7 @@ __global__ __launch_bounds__(kWG) void k_mt_spec_iter(Nll a) {
           }
           u[i] = s;
         }
-        const double2* V = iv[tid];
-        auto inv_at = [&](int r, int c) -> double2 {            // Lambda^-1[r][c] from the packed l >= k entries
-          if (r >= c) return V[c * T - c * (c - 1) / 2 + (r - c)];
-          const double2 t = V[r * T - r * (r - 1) / 2 + (c - r)];
-          return make_double2(t.x, -t.y);
-        };
-        for (int p = 0, k = 0; k < T; ++k)
+        for (int p = 0, k = 0; k < T && !CV; ++k)
           for (int l = k; l < T; ++l, ++p) {
             const double2 a1 = cmulc(z[l], u[k]), a2 = cmulc(u[l], z[k]);   // z_l conj(u_k) + u_l conj(z_k)
             const double2 w1 = make_double2(a1.x + a2.x, a1.y + a2.y);
@@ -1781,7 +1812,7 @@ __global__ __launch_bounds__(kWG) void k_mt_spec_iter(Nll a) {
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
     const double s = block_sum(v[q], red);
-    if (tid == 0) *part_ptr(a, 0, q, blockIdx.x) = s;
+    if (tid == 0) *part_ptr(a, CV ? tcv : 0, q, blockIdx.x) = s;
   }
   stamp_end(a);
 }
@@ -2034,6 +2065,17 @@ int launch_spec_loss_iter(const Nll& a, hipStream_t st) {
 }
 
 int launch_spec_loss_step(const Nll& a, const Fit& f, int iter, int do_update, hipStream_t st) {
+  if (a.mt > 0 && a.loss == FGP_LOSS_CV) {
+    // multitask CV: the T tasks' partials as T problems of ONE loss (k_mt_spec_iter<D, true, true>)
+    Nll b = a;
+    b.G = a.mt;
+    Fit g = f;
+    g.per_problem = 0;
+    return with_spec_d(a.d, [&](auto dc) {
+      k_spec_loss_step<decltype(dc)::value><<<1, kWG, 0, st>>>(b, g, iter, do_update);
+      return check_launch("k_spec_loss_step");
+    });
+  }
   if (!f.per_problem && a.G > 16) return set_error(kErrUnsupported, "GCV / CV fits: one loss over at most 16 problems");
   if (a.nb > kSpecBlocks) return set_error(kErrInvalid, "k_spec_loss_step: nb > %d", kSpecBlocks);
   return with_spec_d(a.d, [&](auto dc) {
@@ -2150,7 +2192,8 @@ int launch_spec_iter(const Nll& a, hipStream_t st, const FitFuse* fz) {
 
 int launch_mt_spec_iter(const Nll& a, hipStream_t st) {
   return with_spec_d(a.d, [&](auto dc) {
-    if (a.loss == FGP_LOSS_GCV) k_mt_spec_iter<decltype(dc)::value, true><<<(unsigned)a.nb, kWG, 0, st>>>(a);
+    if (a.loss == FGP_LOSS_CV) k_mt_spec_iter<decltype(dc)::value, true, true><<<dim3((unsigned)a.nb, (unsigned)a.mt), kWG, 0, st>>>(a);
+    else if (a.loss == FGP_LOSS_GCV) k_mt_spec_iter<decltype(dc)::value, true><<<(unsigned)a.nb, kWG, 0, st>>>(a);
     else k_mt_spec_iter<decltype(dc)::value><<<(unsigned)a.nb, kWG, 0, st>>>(a);
     return check_launch("k_mt_spec_iter");
   });

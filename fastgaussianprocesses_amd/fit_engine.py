@@ -160,10 +160,11 @@ class FusedMLL(object):
         mt:     multitask spectral fit (include/fgp_hip.h mt_tasks; G = 1, ysq only gives n): dict with
                 `basis` the pair spectra [T (T+1)/2, 2^d, n], `ytilde` [T, n], `kt` the task kernel [T, T]
         loss_metric: "MLL" (default), or "GCV" / "CV" (fgp_nll_desc.loss_metric, ABI 16: the spectral path only;
-                cv_weight the scalar cv_weights of AbstractGP.fit); their loss history holds [loss, numer, denom]
+                multitask: GCV ABI 17, CV ABI 18; cv_weight the scalar cv_weights of AbstractGP.fit); their loss
+                history holds [loss, numer, denom] (CV: [loss, nan, nan])
         """
-        if loss_metric != "MLL" and basis is None and (mt is None or loss_metric != "GCV"):
-            raise ValueError("GCV / CV fits run on the spectral path only (basis; multitask: GCV)")
+        if loss_metric != "MLL" and basis is None and mt is None:
+            raise ValueError("GCV / CV fits run on the spectral path only (basis, or the multitask spectra)")
         require_device(ysq, "FusedMLL")
         self.device = ysq.device
         self.family = int(family)

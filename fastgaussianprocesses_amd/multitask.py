@@ -489,8 +489,8 @@ class MultiTaskFastGP(AbstractFastGP):
         return self._cached(("mt_pair_spec", tuple(lo.nsrt), tuple(lo.active)), f, grad_sensitive=False)
 
     def _fused_engine(self, iterations, lr, ysq=None, d_out=None, loss_metric="MLL", cv_weight=1.0):
-        """FusedMLL in multitask spectral mode (G = 1; loss_metric MLL or GCV, ABI 17); the general engine
-        (MtGeneralEngine, MLL) outside its domain (_mt_fused_ok: equal n, fixed task kernel)."""
+        """FusedMLL in multitask spectral mode (G = 1; loss_metric MLL, GCV (ABI 17) or CV (ABI 18)); the general
+        engine (MtGeneralEngine, MLL) outside its domain (_mt_fused_ok: equal n, fixed task kernel)."""
         if not self._mt_fused_ok():
             return MtGeneralEngine(self, lr, min(iterations + 1, 64))
         n, T = self._ns[0], self.num_tasks
@@ -501,7 +501,7 @@ class MultiTaskFastGP(AbstractFastGP):
                         logdet_weight=1.0, mll_const=mll_constant(1, T * n),
                         requires_grad=(self.raw_scale.requires_grad, self.raw_lengthscales.requires_grad,
                                        self.raw_noise.requires_grad),
-                        lr=lr, max_iters=min(iterations + 1, 64), loss_metric=loss_metric,
+                        lr=lr, max_iters=min(iterations + 1, 64), loss_metric=loss_metric, cv_weight=cv_weight,
                         mt=dict(basis=self._mt_spectra(n), ytilde=yt, kt=self.gram_matrix_tasks.detach()))
 
     # ------------------------------------------------------------------ kernel parts and kernels
@@ -772,11 +772,17 @@ class MultiTaskFastGP(AbstractFastGP):
         assert isinstance(stop_crit_wait_iterations, int) and stop_crit_wait_iterations > 0
         assert masks is None or isinstance(masks, torch.Tensor)
         loss_metric = loss_metric.upper()
-        gcv_dev = (loss_metric == "GCV" and default_optimizer and masks is None and self._mt_fused_ok()
+        alt_dev = (loss_metric in ("GCV", "CV") and default_optimizer and masks is None and self._mt_fused_ok()
                    and os.environ.get("FGP_ALT_LOSS_DEVICE", "1")[:1] != "0")
-        if gcv_dev:
-            # GCV of T tasks with equal n and a fixed task kernel (derivative-informed GPs) on the device:
-            # k_mt_spec_iter's GCV variant + k_spec_loss_step (ABI 17; util.py:371-380, abstract_gp.py:242-251)
+        if loss_metric == "CV":
+            # (one task: the reference's inv_diag is the single-task formula without the noise, util.py:383-386; a
+            # per-point cv_weights needs the points' coefficients, not their Parseval sum)
+            alt_dev = alt_dev and self.num_tasks > 1 and (
+                np.isscalar(cv_weights) or (torch.is_tensor(cv_weights) and cv_weights.numel() == 1))
+        if alt_dev:
+            # GCV / CV of T tasks with equal n and a fixed task kernel (derivative-informed GPs) on the device:
+            # k_mt_spec_iter's GCV / CV variants + k_spec_loss_step (ABI 17 / 18; util.py:371-394,
+            # abstract_gp.py:242-272)
             hists = dict(loss=store_hists or store_loss_hist,
                          scale=store_hists or (store_scale_hist and self.raw_scale.requires_grad),
                          lengthscales=store_hists or (store_lengthscales_hist and self.raw_lengthscales.requires_grad),
@@ -784,7 +790,8 @@ class MultiTaskFastGP(AbstractFastGP):
                          task_kernel=store_hists)                # (the task kernel is fixed on this path)
             return self._fit_fused(iterations, 1e-1 if lr is None else lr,
                                    (np.log(1 + stop_crit_improvement_threshold), stop_crit_wait_iterations), hists,
-                                   verbose, verbose_indent, loss_metric="GCV")
+                                   verbose, verbose_indent, loss_metric=loss_metric,
+                                   cv_weight=float(cv_weights) if loss_metric == "CV" else 1.0)
         if loss_metric == "MLL" and default_optimizer and masks is None and (self._mt_fused_ok() or
                                                                             self._mt_general_ok()):
             learned_tk = self.raw_factor_task_kernel.requires_grad or self.raw_noise_task_kernel.requires_grad

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define FGP_ABI_VERSION 17
+#define FGP_ABI_VERSION 18
 
 #define FGP_OK 0
 #define FGP_ERR_INVALID (-1)     /* bad argument (shape, stride, null pointer) */
@@ -252,7 +252,11 @@ typedef struct fgp_nll_desc {
    * per_problem holds at most 16 problems.
    * ABI 17 -- GCV of a multitask spectral fit (mt_tasks = T, equal n, fixed task kernel): numer = sum_j |z_j|^2 with
    * z_j = Lambda_j^-1 y_j, denom = (sum_j tr Lambda_j^-1 / (T n))^2 (util.py:371-380), the gradient from u = Lambda^-1 z
-   * and Lambda^-2 per frequency block. */
+   * and Lambda^-2 per frequency block.
+   * ABI 18 -- CV of a multitask spectral fit (mt_tasks = T >= 2, equal n, fixed task kernel; util.py:381-394,
+   * abstract_gp.py:261-272): K^-1's diagonal over the points of task t is I_t = (1/n) sum_j Lambda_j^-1[t, t] and
+   * sum_i coeffs_{t,i}^2 = N_t = sum_j |z_{j,t}|^2, so loss = cv_weight sum_t N_t / I_t^2 (history [loss, nan, nan]);
+   * one partials workgroup per (frequency block, task). */
   int loss_metric;
   double cv_weight;
 } fgp_nll_desc;

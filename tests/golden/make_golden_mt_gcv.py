@@ -1,13 +1,14 @@
-"""Golden vectors for fit(loss_metric="GCV") of multitask GPs with equal n per task and a fixed task kernel (the
-derivative-informed setting: util.py:371-380 with T tasks, abstract_gp.py:242-251) from the REAL reference, on the
+"""Golden vectors for fit(loss_metric="GCV" / "CV") of multitask GPs with equal n per task and a fixed task kernel (the
+derivative-informed setting: util.py:371-394 with T tasks, abstract_gp.py:242-272) from the REAL reference, on the
 inputs of the committed fixtures deriv_net_d2_a4_equal / deriv_lattice_d2_a2_equal (make_golden_multitask.py):
 
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_mt_gcv.py
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_mt_gcv.py [--metric GCV|CV]
 
-Writes tests/golden/mt_gcv/<fixture>.npz: the 6-iteration GCV fit's loss / scale / lengthscale histories, the fitted
-raw parameters and post_mean at the fixture's test points after the fit.  (A lattice fixture is skipped if the
+Writes tests/golden/mt_gcv/<fixture>.npz (GCV) or tests/golden/mt_cv/<fixture>.npz (CV): the 6-iteration fit's loss /
+scale / lengthscale histories, the fitted raw parameters and post_mean at the fixture's test points after the fit.  (A lattice fixture is skipped if the
 reference's complex-valued lattice GCV makes its fit raise, as it does for one task.)
 """
+import argparse
 import os
 import sys
 
@@ -24,10 +25,14 @@ ITS = 6
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--metric", default="GCV", choices=["GCV", "CV"])
+    metric = ap.parse_args().metric
+    sub = "mt_gcv" if metric == "GCV" else "mt_cv"
     torch.set_default_dtype(torch.float64)
     fg = import_reference()
     import qmcpy
-    os.makedirs(os.path.join(HERE, "mt_gcv"), exist_ok=True)
+    os.makedirs(os.path.join(HERE, sub), exist_ok=True)
     for name in NAMES:
         g = dict(np.load(os.path.join(HERE, name + ".npz")))
         d, ns = int(g["d"]), [int(v) for v in g["ns"]]
@@ -46,7 +51,7 @@ def main():
             assert np.array_equal(xs[l].numpy(), g["x_%d" % l])
         gp.add_y_next([torch.from_numpy(g["y_%d" % l]) for l in range(T)])
         try:
-            data = gp.fit(loss_metric="GCV", iterations=ITS, store_hists=True, verbose=0,
+            data = gp.fit(loss_metric=metric, iterations=ITS, store_hists=True, verbose=0,
                           stop_crit_wait_iterations=ITS + 5)
         except TypeError as e:
             print("skip", name, "(the reference's fit raised: %s)" % e)
@@ -57,7 +62,7 @@ def main():
                    lengthscales_hist=data["lengthscales_hist"].detach().numpy(),
                    raw_scale=gp.raw_scale.detach().numpy(), raw_lengthscales=gp.raw_lengthscales.detach().numpy(),
                    pmean=gp.post_mean(xt).detach().numpy())
-        fn = os.path.join(HERE, "mt_gcv", name + ".npz")
+        fn = os.path.join(HERE, sub, name + ".npz")
         np.savez_compressed(fn, **out)
         print("wrote", fn, out["loss_hist"][:3])
 

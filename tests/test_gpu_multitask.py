@@ -375,18 +375,22 @@ def test_multitask_gp_pickles():
     assert torch.equal(gp2.post_mean(x), gp.post_mean(x))
 
 
+@pytest.mark.parametrize("metric", ["GCV", "CV"])
 @pytest.mark.parametrize("path", ["device", "generic"])
 @pytest.mark.parametrize("name", ["deriv_net_d2_a4_equal", "deriv_lattice_d2_a2_equal"])
-def test_multitask_gcv_fit_matches_reference(name, path, monkeypatch):
-    """fit(loss_metric="GCV") of a derivative-informed GP (T = 3 tasks of equal n, fixed task kernel) against the REAL
-    reference's 6-iteration trajectory (tests/golden/make_golden_mt_gcv.py -> tests/golden/mt_gcv/*.npz), through the
-    device path (ABI 17: k_mt_spec_iter's GCV variant -- N = sum |z|^2, Tr = sum tr Lambda^-1, the closed-form
-    gradient from u = Lambda^-1 z and Lambda^-2 -- and k_spec_loss_step) and the generic autograd loop
-    (FGP_ALT_LOSS_DEVICE=0).  Tolerances of tests/test_gpu_losses.py: loss 2e-7 relative, lengthscale trajectory
-    1e-10, post_mean 1e-7 (pred_tol's for the ill-conditioned lattice fixture)."""
+def test_multitask_gcv_fit_matches_reference(name, path, metric, monkeypatch):
+    """fit(loss_metric="GCV" / "CV") of a derivative-informed GP (T = 3 tasks of equal n, fixed task kernel) against the
+    REAL reference's 6-iteration trajectory (tests/golden/make_golden_mt_gcv.py [--metric CV] ->
+    tests/golden/mt_gcv/*.npz, mt_cv/*.npz), through the device path (GCV, ABI 17: k_mt_spec_iter's GCV variant -- N =
+    sum |z|^2, Tr = sum tr Lambda^-1, the closed-form gradient from u = Lambda^-1 z and Lambda^-2; CV, ABI 18: per task
+    N_t and I_t = mean_j Lambda_j^-1[t, t], the gradient from v = Lambda^-1 e_t -- and k_spec_loss_step) and the generic
+    autograd loop (FGP_ALT_LOSS_DEVICE=0; CV: the dense inverse diagonal, util.py:387-393).  Tolerances of
+    tests/test_gpu_losses.py: loss 2e-7 relative, lengthscale trajectory 1e-10, post_mean 1e-7 (pred_tol's for the
+    ill-conditioned lattice fixture)."""
     import os
     from fastgaussianprocesses_amd import fit_engine
-    with np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "mt_gcv", name + ".npz"),
+    sub = "mt_gcv" if metric == "GCV" else "mt_cv"
+    with np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", sub, name + ".npz"),
                  allow_pickle=False) as f:
         r = {k: f[k] for k in f.files}
     monkeypatch.setenv("FGP_ALT_LOSS_DEVICE", "1" if path == "device" else "0")
@@ -401,8 +405,8 @@ def test_multitask_gcv_fit_matches_reference(name, path, monkeypatch):
     gp = product_mt(g)
     assert gp._mt_fused_ok()
     its = len(r["loss_hist"]) - 1
-    data = gp.fit(loss_metric="GCV", iterations=its, store_hists=True, verbose=0, stop_crit_wait_iterations=its + 5)
-    assert seen == (["GCV"] if path == "device" else []), seen
+    data = gp.fit(loss_metric=metric, iterations=its, store_hists=True, verbose=0, stop_crit_wait_iterations=its + 5)
+    assert seen == ([metric] if path == "device" else []), seen
     assert data["iterations"] == its
     assert rel_err(data["loss_hist"], r["loss_hist"]) <= 2e-7
     assert rel_err(data["lengthscales_hist"], r["lengthscales_hist"]) <= 1e-10
