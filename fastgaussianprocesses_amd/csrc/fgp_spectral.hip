@@ -445,7 +445,8 @@ __device__ __forceinline__ int spec_slot_param(const Nll& a, int g, int k, int d
 template <int D>
 __device__ __forceinline__ void spec_finish(const Nll& a, const Fit& f, const double* tot, int g0, int cnt, int iter,
                                             int do_update, const RpState& in, const RpState& out, bool write,
-                                            double* newraw, int state_write = -1, const double* pf = nullptr) {
+                                            double* newraw, int state_write = -1, const double* pf = nullptr,
+                                            double* best = nullptr) {
   const bool wstate = state_write < 0 ? write : state_write != 0;   // the new state to `out` (default: with write)
   const int tf = tid_fresh(), i = tf >> 4, k = tf & 15;
   if (i >= cnt) return;
@@ -483,6 +484,7 @@ __device__ __forceinline__ void spec_finish(const Nll& a, const Fit& f, const do
   // (pf: this thread's state, prefetched by the caller beside its other loads)
   const double raw_p = pf ? pf[0] : in.raw[p], prev_p = pf ? pf[1] : in.prev[p], step_p = pf ? pf[2] : in.step[p];
   if (k == dl + 1) gp = exp(raw_p) * v[2];
+  if (best) best[p] = raw_p;                     // (k_spec_persist: this iteration's parameters are the best iterate)
   if (write) {
     f.raw_hist[(int64_t)iter * f.n_params + p] = raw_p;
     f.grad_out[p] = gp;
@@ -702,10 +704,11 @@ __global__ __launch_bounds__(kWG) void k_spec_persist(Nll a, Fit f, int iters, d
   constexpr int NS = 1 << D, NQ = 4 + D, MAXG = kSpecBlocks / kSpecGroup;
   extern __shared__ double lds[];                  // [bpw][kpl][NS + 1][64] spectra + Y of this workgroup's blocks
   __shared__ double st_raw[kSpecScratch], st_prev[kSpecScratch], st_step[kSpecScratch];
+  __shared__ double st_best[kSpecScratch];         // the best iterate's parameters (AbstractGP.fit's best_params)
   __shared__ double gsum[NQ * MAXG];
   __shared__ double tot[NQ];
   __shared__ double es[3];                         // early stopping: best, save, waited
-  __shared__ int brk_s, fail_s;
+  __shared__ int brk_s, fail_s, isb_s, bi_s;
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int W = gridDim.x, kpl = a.spec_kpl, np = spec_nparams(a), ng = spec_groups(a);
   const int64_t main = a.spec_main, B = 64 * (int64_t)kpl;
@@ -724,6 +727,7 @@ __global__ __launch_bounds__(kWG) void k_spec_persist(Nll a, Fit f, int iters, d
   }
   for (int p = tid; p < np; p += kWG) {
     st_raw[p] = f.raw[p];
+    st_best[p] = st_raw[p];                        // (no finite loss at all: iteration 0's, the host rule's best_i = 0)
     st_prev[p] = f.prev[p];
     st_step[p] = f.step[p];
   }
@@ -733,6 +737,7 @@ __global__ __launch_bounds__(kWG) void k_spec_persist(Nll a, Fit f, int iters, d
     es[2] = 0.0;
     brk_s = 0;
     fail_s = 0;
+    bi_s = 0;
   }
   __syncthreads();
   const double rootn = sqrt((double)((int64_t)1 << a.log2n)), wl = a.logdet_weight;
@@ -858,7 +863,11 @@ __global__ __launch_bounds__(kWG) void k_spec_persist(Nll a, Fit f, int iters, d
       // AbstractGP.fit's bookkeeping on the loss of this iteration (the value spec_finish records)
       const double lv = 0.5 * (tot[0] + a.logdet_weight * tot[1] + f.mll_const);
       double best = es[0], save = es[1], waited = es[2];
-      if (lv < best) best = lv;
+      isb_s = lv < best ? 1 : 0;                   // (NaN never best: the host rule `lv < best`)
+      if (lv < best) {
+        best = lv;
+        bi_s = it;
+      }
       if ((save - lv) > logtol) {
         waited = 0.0;
         save = best;
@@ -872,19 +881,25 @@ __global__ __launch_bounds__(kWG) void k_spec_persist(Nll a, Fit f, int iters, d
     }
     __syncthreads();
     const int brk = brk_s;
-    spec_finish<D>(a, f, tot, 0, 1, it, brk ? 0 : 1, st, st, blockIdx.x == 0, nullptr, 1);
+    spec_finish<D>(a, f, tot, 0, 1, it, brk ? 0 : 1, st, st, blockIdx.x == 0, nullptr, 1, nullptr,
+                   isb_s ? st_best : nullptr);
     // (the new state is in LDS; workgroup 0's history stores stay in flight -- drained by the next iteration's
     // vmcnt(0) before its grid barrier, under its compute: a __syncthreads here cost ~1 us per iteration)
     barrier_keep_vm();
     stamp(it, 4);
     if (brk) {
       if (blockIdx.x == 0) {
+        // raw <- the BEST iterate (what AbstractGP.fit restores; fgp_fit_persist, ABI 18), prev / step <- the final
+        // Rprop state; out[0] the last iteration, out[2] the best one
         for (int p = tid; p < np; p += kWG) {
-          f.raw[p] = st_raw[p];
+          f.raw[p] = st_best[p];
           f.prev[p] = st_prev[p];
           f.step[p] = st_step[p];
         }
-        if (tid == 0) out[0] = it;
+        if (tid == 0) {
+          out[0] = it;
+          out[2] = bi_s;
+        }
       }
       return;
     }
@@ -2295,10 +2310,10 @@ int launch_spec_persist(const Nll& a, const Fit& f, int iters, double logtol, in
   size_t shm;
   int rc = spec_persist_geometry(a, &W, &bpw, &shm);
   if (rc != kOk) return rc;
-  // the three partial buffers empty (kPartEmpty: all bytes 0xff), the control words out[0..1] cleared
+  // the three partial buffers empty (kPartEmpty: all bytes 0xff), the control words out[0..2] cleared
   (void)counter;
   if (hipMemsetAsync(a.partials, 0xff, 3 * sizeof(double) * (size_t)a.nq * (size_t)a.nb, st) != hipSuccess ||
-      hipMemsetAsync(out, 0, 2 * sizeof(int), st) != hipSuccess)
+      hipMemsetAsync(out, 0, 3 * sizeof(int), st) != hipSuccess)
     return set_error(kErrHip, "fgp_fit_persist: workspace reset failed");
   return with_spec_d(a.d, [&](auto dc) {
     constexpr int D = decltype(dc)::value;

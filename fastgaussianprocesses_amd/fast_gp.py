@@ -831,7 +831,21 @@ class AbstractFastGP(torch.nn.Module):
         total = iterations + 1
         done = False
         losses = []
-        if getattr(eng, "persist_ok", lambda: False)():
+        persist = getattr(eng, "persist_ok", lambda: False)()
+        if persist and not verbose and not any(hists.values()):
+            # the whole fit in one launch (fgp_fit_persist), which leaves the best iterate in the engine's raw
+            # parameters (ABI 18): they are restored while the launch runs, and the control word is read after
+            # that (the host work overlaps the fit instead of following it)
+            ip = eng.run_persist(iterations, logtol, wait_max, defer=True)
+            if ip is not None:
+                self._restore_best(eng, eng.raw)
+                if ip < 0:
+                    ip = eng.persist_result()
+                if ip is not None:
+                    eng.release_inputs()
+                    return {"iterations": ip}
+            persist = False       # a barrier give-up restored the entry state: the launch per iteration below
+        if persist:
             # the whole fit in one launch (fgp_fit_persist: the early-stopping rule on the device); the last
             # iteration and the failure word are read back.  A barrier give-up (None) restored the entry state:
             # the fit then runs below on the launch per iteration (the same trajectory bit for bit).
@@ -894,17 +908,7 @@ class AbstractFastGP(torch.nn.Module):
         s_raw, l_raw, nz_raw = eng.split_raw(raw_hist)
         # (a device index tensor: index_select, not raw_hist[t] -- a 0-d index tensor is read back to the host)
         best_row = raw_hist.index_select(0, best_i.reshape(1))[0] if torch.is_tensor(best_i) else raw_hist[best_i]
-        b_s, b_l, b_n = eng.split_raw(best_row)
-        restore = [("raw_scale", b_s), ("raw_lengthscales", b_l), ("raw_noise", b_n)]
-        if hasattr(eng, "split_task"):                  # the general multitask engine also learns the task kernel
-            b_f, b_v = eng.split_task(best_row)
-            restore += [("raw_factor_task_kernel", b_f), ("raw_noise_task_kernel", b_v)]
-        with torch.no_grad():
-            for name, val in restore:
-                old = getattr(self, name)
-                setattr(self, name, torch.nn.Parameter(val.reshape(old.shape).clone(), requires_grad=old.requires_grad))
-        self._cache = {k: v for k, v in self._cache.items() if not k[2]}    # keep data-only entries (ytilde, spectra)
-        self._snap = None
+        self._restore_best(eng, best_row)
         if hasattr(eng, "release_inputs"):
             eng.release_inputs()
         data = {"iterations": i}
@@ -924,6 +928,21 @@ class AbstractFastGP(torch.nn.Module):
                 data["task_kernel_hist"] = self.gram_matrix_tasks.detach().cpu()[None].expand(
                     (i + 1,) + self.gram_matrix_tasks.shape).clone()
         return data
+
+    def _restore_best(self, eng, best_row):
+        """The best iterate's raw parameters (a device row of the engine's layout) as this GP's Parameters
+        (abstract_gp.py:285-296), the hyper-parameter-dependent caches dropped."""
+        b_s, b_l, b_n = eng.split_raw(best_row)
+        restore = [("raw_scale", b_s), ("raw_lengthscales", b_l), ("raw_noise", b_n)]
+        if hasattr(eng, "split_task"):                  # the general multitask engine also learns the task kernel
+            b_f, b_v = eng.split_task(best_row)
+            restore += [("raw_factor_task_kernel", b_f), ("raw_noise_task_kernel", b_v)]
+        with torch.no_grad():
+            for name, val in restore:
+                old = getattr(self, name)
+                setattr(self, name, torch.nn.Parameter(val.reshape(old.shape).clone(), requires_grad=old.requires_grad))
+        self._cache = {k: v for k, v in self._cache.items() if not k[2]}    # keep data-only entries (ytilde, spectra)
+        self._snap = None
 
     def _loss_generic(self, loss_metric, masks, cv_weights, d_out):
         n = self._nh

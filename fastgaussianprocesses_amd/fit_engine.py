@@ -392,16 +392,18 @@ class FusedMLL(object):
         N.call("fgp_fit_persist_ok", self._nll, ctypes.byref(ok))
         return ok.value
 
-    def run_persist(self, iterations, logtol, wait_max):
+    def run_persist(self, iterations, logtol, wait_max, defer=False):
         """AbstractGP.fit's iterations 0 .. iterations with its early-stopping rule, in one launch
-        (fgp_fit_persist); returns the last iteration evaluated (its row applied no update).
+        (fgp_fit_persist); returns the last iteration evaluated (its row applied no update).  Afterwards `raw` holds
+        the BEST iterate's parameters (ABI 18), the ones AbstractGP.fit restores.
 
-        The 4-int control word is read back at once (one small device-to-host read): when an in-kernel barrier
-        gave up (the workgroups were not co-resident after all -- e.g. CUs taken by other work), the entry
-        parameters are restored (the kernel leaves Rprop's state untouched and sets the parameters to NaN) and
-        None is returned, so the caller re-runs the fit on the launch per iteration, which gives the same
-        trajectory bit for bit.  Inside a hipGraph capture nothing can be read: the word is kept for
-        check_persist at the next eager call, and a failure shows as NaN parameters and parameter history."""
+        The 4-int control word is read back at once (one small device-to-host read), or with `defer` by
+        persist_result() once the caller has enqueued its own work behind the launch (-1 is returned): when an
+        in-kernel barrier gave up (the workgroups were not co-resident after all -- e.g. CUs taken by other work), the
+        entry parameters are restored (the kernel leaves Rprop's state untouched and sets the parameters to NaN) and
+        None is returned, so the caller re-runs the fit on the launch per iteration, which gives the same trajectory
+        bit for bit.  Inside a hipGraph capture nothing can be read: the word is kept for check_persist at the next
+        eager call, and a failure shows as NaN parameters and parameter history."""
         self.check_persist()
         self.ensure_history(iterations + 1)
         ctrl = torch.empty((4,), dtype=torch.int32, device=self.device)   # (the launch clears the words it reports)
@@ -412,6 +414,14 @@ class FusedMLL(object):
         if capturing:
             self._ctrl = ctrl
             return int(iterations)
+        self._pending = (ctrl, raw0)
+        return -1 if defer else self.persist_result()
+
+    def persist_result(self):
+        """The control word of the last run_persist: its last iteration, or None after a barrier give-up (the entry
+        parameters restored); synchronises."""
+        ctrl, raw0 = self._pending
+        self._pending = None
         c = ctrl.cpu().tolist()
         if c[2]:
             self.raw.copy_(raw0)

@@ -554,6 +554,9 @@ int fgp_sum_sq_half(const void* x, int64_t x_row_stride, int64_t R, int64_t G, i
  * stop_crit_wait_iterations) -- with the multi-launch fgp_fit_run's arithmetic (bit-identical histories).
  * The last evaluated iteration applies no update.  ctrl: device scratch of >= 16 bytes; afterwards
  * ((int*)ctrl)[1] = the last iteration, ((int*)ctrl)[2] = 1 if an in-kernel barrier gave up (an error).
+ * ABI 18: ((int*)ctrl)[3] = the best iteration (the first minimum of the loss history, NaN never best) and the fit
+ * desc's raw holds ITS parameters (AbstractGP.fit's restored best_params, :285-296) -- rprop_prev / rprop_step the
+ * final Rprop state -- so a caller restores the best iterate without reading anything back.
  * fgp_fit_persist_ok: *ok = the workgroup count it would use, 0 when the desc is outside its domain. */
 int fgp_fit_persist_ok(const fgp_nll_desc* nll, int* ok);
 int fgp_fit_persist(const fgp_nll_desc* nll, const fgp_fit_desc* fit, int iters, double logtol, int wait_max, void* ctrl,
