@@ -1559,6 +1559,14 @@ class FastGPLattice(AbstractFastGP):
         HBM reads per fit iteration.  FGP_PARTS_GEN=0 disables it."""
         if os.environ.get("FGP_PARTS_GEN", "1") == "0" or not isinstance(self.seq, _seqs.Lattice):
             return None
+        memo = getattr(self, "_pgen_memo", None)      # (a function of the point set and n only)
+        if memo is not None and memo[0] == n and memo[1] is self.seq:
+            return memo[2]
+        gen = self._parts_gen_new(n)
+        self._pgen_memo = (n, self.seq, gen)
+        return gen
+
+    def _parts_gen_new(self, n):
         m = int(n).bit_length() - 1
         z = [int(v) for v in self.seq.z[:self.d]]
         if len(z) != self.d or not all(0 < v < 2 ** (53 - m) for v in z) or len(set(self._alphas)) != 1:
