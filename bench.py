@@ -853,9 +853,9 @@ def graph_fit_us(eng, iters, reps=5):
 
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r06m_pmc_fit_kernels.json")
-PMC_SQ_SUMMARY = os.path.join(ROOT, "profiles", "r06m_pmc_sq_fit_kernels.json")
-ROCPROF_GRID_STATS = os.path.join(ROOT, "profiles", "r06m_bench_timed_region_stats.txt")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r06x_pmc_fit_kernels.json")
+PMC_SQ_SUMMARY = os.path.join(ROOT, "profiles", "r06x_pmc_sq_fit_kernels.json")
+ROCPROF_GRID_STATS = os.path.join(ROOT, "profiles", "r06x_bench_timed_region_stats.txt")
 # the read floor of the spectral iteration's footprint: tools/stream_microbench.hip over the same 168 MB,
 # re-read back to back, 24.0-24.3 us per pass (7.0 TB/s; profiles/r03v_stream_and_stamps.jsonl)
 STREAM_FLOOR_US = 24.0
@@ -865,8 +865,8 @@ FP64_LANE_OPS_PEAK = 256 * 4 * 16 * 2.4e9
 CPU_FIDELITY = os.path.join(ROOT, "profiles", "r02_cpu_fidelity.json")
 # the prediction kernels (tools/predict_kernels.py: C4's batched post_mean / post_var, C5 per-output's post_mean):
 # rocprofv3 kernel-trace summary and SQ counter pass
-ROCPROF_PREDICT_STATS = os.path.join(ROOT, "profiles", "r06m_predict_kernel_grid_stats.txt")
-PMC_SQ_PREDICT = os.path.join(ROOT, "profiles", "r06m_pmc_sq_predict.json")
+ROCPROF_PREDICT_STATS = os.path.join(ROOT, "profiles", "r06x_predict_kernel_grid_stats.txt")
+PMC_SQ_PREDICT = os.path.join(ROOT, "profiles", "r06x_pmc_sq_predict.json")
 
 
 def pmc_traffic(kernel, grid):

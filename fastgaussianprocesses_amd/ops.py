@@ -312,19 +312,24 @@ class _FWHT(torch.autograd.Function):
         return fwht_raw(g, ctx.stable), None
 
 
+def _graph_wanted(x):
+    # (no autograd node when nothing needs one: the Function's bookkeeping is most of a small transform's host time)
+    return torch.is_grad_enabled() and x.requires_grad
+
+
 def fftbr(x, stable=False):
     """Drop-in for qmcpy.fftbr_torch (stable=False) or AbstractFastGP.ft on lattices (stable=True)."""
-    return _FFTBR.apply(x, stable)
+    return _FFTBR.apply(x, stable) if _graph_wanted(x) else fftbr_raw(x, stable)
 
 
 def ifftbr(x, stable=False):
     """Drop-in for qmcpy.ifftbr_torch (stable=False) or AbstractFastGP.ift on lattices (stable=True)."""
-    return _IFFTBR.apply(x, stable)
+    return _IFFTBR.apply(x, stable) if _graph_wanted(x) else ifftbr_raw(x, stable)
 
 
 def fwht(x, stable=False):
     """Drop-in for qmcpy.fwht_torch (stable=False) or AbstractFastGP.ft/ift on nets (stable=True)."""
-    return _FWHT.apply(x, stable)
+    return _FWHT.apply(x, stable) if _graph_wanted(x) else fwht_raw(x, stable)
 
 
 # ------------------------------------------------------------------------------------- kernel parts
