@@ -430,6 +430,10 @@ def test_single_launch_fit_give_up_inside_replayed_graph_raises(monkeypatch):
     with pytest.raises(RuntimeError, match="give-up"):
         E.check_replayed_fits(before)
     E.persist_giveups(reset=True)
+    # (the captured engine, kept by fit_engine.cached_engine, still holds the failed replay's control word, which its
+    # next eager fit would report: drop it, so later tests of the same geometry start clean)
+    del g
+    E._ENGINES.clear()
 
 
 def _graph_stats():
