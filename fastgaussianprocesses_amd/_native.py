@@ -49,6 +49,7 @@ class NllDesc(ctypes.Structure):
         ("basis", _c_vp), ("basis_stride", _c_i64), ("ysq_chunked", _c_int),
         ("mt_tasks", _c_int), ("mt_basis", _c_vp), ("mt_ytilde", _c_vp), ("mt_kt", _c_vp),
         ("loss_metric", _c_int), ("cv_weight", _c_dbl),
+        ("mt_task_rg", _c_int), ("mt_rank", _c_int), ("mt_vexp", _c_int),
     ]
 
 

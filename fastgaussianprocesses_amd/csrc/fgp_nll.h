@@ -55,6 +55,9 @@ struct Nll {
   const void* mt_basis;
   const void* mt_ytilde;
   const double* mt_kt;
+  // ... a learned task kernel (ABI 18, GCV / CV): bit 0 / 1 = the factor / task noise require grad (0: mt_kt is the
+  // fixed task kernel); F [T][mt_rank] at raw[mt_f_off], the task noise [T] at raw[mt_v_off] (exp when mt_vexp)
+  int mt_learn, mt_rank, mt_vexp, mt_f_off, mt_v_off;
   int64_t out_stride;                // fgp_fftbr_real_half: row stride of the half spectra (grad_lam)
   int loss;                          // FGP_LOSS_MLL / GCV / CV (ABI 16; GCV / CV: k_spec_loss_iter + k_spec_loss_step)
   double cv_weight;
@@ -610,7 +613,9 @@ struct FitFuse {
 };
 constexpr int kSpecStateMax = 64;                  // Rprop parameters of a persistent k_spec_tile (LDS copies)
 // parameters of a spectral fit (the raw vector's length: the noise block is last)
-__host__ __device__ __forceinline__ int spec_nparams(const Nll& a) { return a.noise_off + (a.noise_pp ? a.G : 1); }
+__host__ __device__ __forceinline__ int spec_nparams(const Nll& a) {
+  return a.noise_off + (a.noise_pp ? a.G : 1) + (a.mt_learn ? a.mt * (a.mt_rank + 1) : 0);
+}
 constexpr int kHandoffWords = 32 * 8 * 16;         // XOR words of the check buffer (groups x G x nq, at most)
 int launch_re_bwd_fused(const Nll& a, const FitFuse& fz, const Tables* tb, hipStream_t st);
 
@@ -662,7 +667,8 @@ int launch_spec_post_var(const Nll& a, const double2* psi, int N, const double* 
 // multitask spectral fit (ABI 12): at most kMtMaxT tasks, kMtF frequencies per chunk
 constexpr int kMtMaxT = 8;
 constexpr int kMtF = 32;
-int launch_mt_spec_iter(const Nll& a, hipStream_t st);   // loss / gradient partials of one iteration
+int launch_mt_spec_iter(const Nll& a, hipStream_t st);
+int launch_mt_learn_step(const Nll& a, const Fit& f, int iter, int do_update, hipStream_t st);   // learned task kernel   // loss / gradient partials of one iteration
 // lattice spectra of the subsets s0 .. s0 + cnt - 1 (log2n >= 17) by the fused R2C pair: products formed in
 // the row kernel, real parts k <= n/2 written by the column kernel (work: 16 n cnt bytes)
 struct GenSpec;

@@ -1443,6 +1443,17 @@ static int to_nll(const fgp_nll_desc* d, Nll& a) {
   a.mt_basis = d->mt_basis;
   a.mt_ytilde = d->mt_ytilde;
   a.mt_kt = d->mt_kt;
+  a.mt_learn = a.mt_rank = a.mt_vexp = a.mt_f_off = a.mt_v_off = 0;
+  if (d->mt_task_rg) {
+    if (!mt || a.loss == FGP_LOSS_MLL || d->mt_task_rg < 0 || d->mt_task_rg > 3 || d->mt_rank < 0 ||
+        d->mt_rank > d->mt_tasks || a.noise_pp || a.G != 1)
+      return set_error(kErrUnsupported, "learned task kernel: multitask spectral GCV / CV, rank 0 .. T");
+    a.mt_learn = d->mt_task_rg;
+    a.mt_rank = d->mt_rank;
+    a.mt_vexp = d->mt_vexp ? 1 : 0;
+    a.mt_f_off = a.noise_off + 1;
+    a.mt_v_off = a.mt_f_off + d->mt_tasks * d->mt_rank;
+  }
   if (mt) {
     // one chunk of kMtF frequencies per step, up to kSpecBlocks blocks (the spectral reduction's limit)
     const int64_t n = (int64_t)1 << d->log2n;
@@ -1455,6 +1466,8 @@ static int to_nll(const fgp_nll_desc* d, Nll& a) {
     a.nb = (int)std::min<int64_t>(kSpecBlocks, chunks);
     a.mt_cpb = (int)(chunks / a.nb);
     if (a.loss != FGP_LOSS_MLL) a.nq = 6 + 2 * a.d;    // the single-task GCV / CV partial layout (k_spec_loss_step)
+    // (a learned task kernel: + the two streams of dL/dK_task per task pair, k_mt_learn_step)
+    if (a.mt_learn) a.nq += a.mt * (a.mt + 1);
   }
   return kOk;
 }
@@ -1640,6 +1653,7 @@ static int check_per_problem(const Nll& a, const Fit& f) {
 }
 
 static int fit_step(const Nll& a, const Fit& f, int iter, int do_update, hipStream_t st, bool counter_zero = false) {
+  if (a.mt && a.mt_learn) return launch_mt_learn_step(a, f, iter, do_update, st);
   if (a.spec && a.loss != FGP_LOSS_MLL) return launch_spec_loss_step(a, f, iter, do_update, st);
   if (f.per_problem && a.spec) return launch_spec_reduce_step(a, f, iter, do_update, st);
   if (a.spec && a.nb <= kSpecBlocks && !getenv_off("FGP_SPEC_STEP_MANY")) {

@@ -1138,6 +1138,116 @@ __global__ __launch_bounds__(kWG) void k_spec_loss_step(Nll a, Fit f, int iter, 
   }
 }
 
+// Reduction + loss + Rprop of a multitask GCV / CV fit with a LEARNED task kernel (ABI 18; k_mt_spec_iter<.., LEARN>'s
+// partials): one workgroup.  The totals of every (problem, quantity) -- problems: 1 (GCV) or the T tasks (CV) --
+// in k_spec_loss_step's two-level order, the loss and the factors c1, c2 of each problem as there, the scale /
+// lengthscale / noise gradients as there, and dL/dK_task of pair p = sum_i c1_i K1_ip + c2_i K2_ip, then the chain rule
+// through K_task = F F^T + diag(v): dL/dF[t, r] = sum_p dK_p (F[l_p, r] [k_p == t] + F[k_p, r] [l_p == t]) (ascending p),
+// dL/draw_v[t] = dK_(t, t) (v_t when exp); torch.optim.Rprop on every parameter (rprop_update).
+template <int D>
+__global__ __launch_bounds__(kWG) void k_mt_learn_step(Nll a, Fit f, int iter, int do_update) {
+  constexpr int NQ0 = 6 + 2 * D, NPM = kMtMaxT * (kMtMaxT + 1) / 2;
+  __shared__ double tot[kMtMaxT * (NQ0 + 2 * NPM)];
+  __shared__ double lossg[kMtMaxT], c1s[kMtMaxT], c2s[kMtMaxT], dk[NPM];
+  __shared__ int rgs[kSpecScratch];
+  const bool cv = a.loss == FGP_LOSS_CV;
+  const int T = a.mt, NP = T * (T + 1) / 2, P = cv ? T : 1, nq = a.nq, ng = spec_groups(a), R = a.mt_rank;
+  for (int t = threadIdx.x; t < P * nq; t += kWG) {
+    const int g = t / nq, q = t - g * nq;
+    double sum = 0.0;
+    for (int grp = 0; grp < ng; ++grp) sum += spec_group_sum<false>(a, g, q, grp);
+    tot[t] = sum;
+  }
+  __syncthreads();
+  // (GCV: the trace is normalised by the points of all T tasks, util.py:379; CV: I_t over the n points of task t)
+  const double n = (double)((int64_t)1 << a.log2n) * (cv ? 1 : T);
+  if ((int)threadIdx.x < P) {
+    const int i = threadIdx.x;
+    const double N1 = tot[i * nq + 0], Tr = tot[i * nq + 1];
+    if (cv) {
+      const double I = Tr / n, w = a.cv_weight;
+      lossg[i] = w * N1 / (I * I);
+      c1s[i] = -2.0 * w / (I * I);
+      c2s[i] = 2.0 * w * N1 / (n * I * I * I);
+    } else {
+      const double Dn = (Tr / n) * (Tr / n);
+      lossg[i] = N1 / Dn;
+      c1s[i] = -2.0 / Dn;
+      c2s[i] = 2.0 * N1 * Tr / (n * n * Dn * Dn);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double L = 0.0;
+    for (int i = 0; i < P; ++i) L += lossg[i];
+    f.loss_hist[(int64_t)iter * 3 + 0] = L;
+    f.loss_hist[(int64_t)iter * 3 + 1] = cv ? NAN : tot[0];
+    f.loss_hist[(int64_t)iter * 3 + 2] = cv ? NAN : (tot[1] / n) * (tot[1] / n);
+  }
+  for (int p = threadIdx.x; p < NP; p += kWG) {
+    double s = 0.0;
+    for (int i = 0; i < P; ++i) s += c1s[i] * tot[i * nq + NQ0 + p] + c2s[i] * tot[i * nq + NQ0 + NP + p];
+    dk[p] = s;
+  }
+  __syncthreads();
+  const int dl = a.ls_pd ? a.d : 1, np = spec_nparams(a);
+  const double* Fm = f.raw + a.mt_f_off;
+  for (int pi = threadIdx.x; pi < np; pi += kWG) {
+    double gp = 0.0;
+    int rg;
+    if (pi >= a.mt_v_off) {                               // task noise v_t
+      const int t = pi - a.mt_v_off;
+      gp = dk[t * T - t * (t - 1) / 2];
+      if (a.mt_vexp) gp *= exp(f.raw[pi]);
+      rg = (a.mt_learn >> 1) & 1;
+    } else if (pi >= a.mt_f_off) {                        // task factor F[t, r]
+      const int t = (pi - a.mt_f_off) / R, r = (pi - a.mt_f_off) - t * R;
+      for (int p = 0, k = 0; k < T; ++k)
+        for (int l = k; l < T; ++l, ++p) {
+          if (k == t) gp += dk[p] * Fm[l * R + r];
+          if (l == t) gp += dk[p] * Fm[k * R + r];
+        }
+      rg = a.mt_learn & 1;
+    } else {
+      rg = -1;
+      for (int i = 0; i < P; ++i) {
+        const double* v = tot + i * nq;
+        for (int k = 0; k < 2 + dl; ++k) {
+          if (spec_slot_param(a, 0, k, dl) != pi) continue;
+          double s1, s2;
+          if (k == 0) {
+            s1 = v[3];
+            s2 = v[5 + D];
+            rg = f.scale_rg;
+          } else if (k <= dl) {
+            s1 = s2 = 0.0;
+            for (int j = 0; j < D; ++j)
+              if (a.ls_pd ? j == k - 1 : true) {
+                s1 += v[4 + j];
+                s2 += v[6 + D + j];
+              }
+            rg = f.ls_rg;
+          } else {
+            const double nz = exp(f.raw[pi]);
+            s1 = nz * v[2];
+            s2 = nz * v[4 + D];
+            rg = f.noise_rg;
+          }
+          gp += c1s[i] * s1 + c2s[i] * s2;
+        }
+      }
+    }
+    rgs[pi] = rg;
+    if (rg < 0) continue;
+    f.raw_hist[(int64_t)iter * f.n_params + pi] = f.raw[pi];
+    f.grad_out[pi] = gp;
+  }
+  // (every gradient reads the factor before any update: the steps after a barrier)
+  __syncthreads();
+  for (int pi = threadIdx.x; pi < np; pi += kWG)
+    if (do_update && rgs[pi] > 0) rprop_update(f, pi, f.grad_out[pi]);
+}
+
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void glb_void;
 
@@ -1559,9 +1669,15 @@ __device__ __forceinline__ void mt_pair_kl(int p, int T, int& k, int& l) {
 // task.  Workgroup (block, t) = blockIdx (x, y): with v = Lambda^-1 e_t (column t of the inverse) and u = v z_t,
 // dN_t = -2 Re(u^H dLambda z) and d(n I_t) = -v^H dLambda v: the GCV layout per task, W1 = z u^H + u z^H, W2 = 2 v v^H,
 // partials [t][N_t, n I_t, S1, S2] read by k_spec_loss_step as T problems of one loss.
-template <int D, bool GCV = false, bool CV = false>
+// LEARN (ABI 18, GCV / CV): K_task = F F^T + diag(v) from raw (k_mt_learn_step's parameters) and, per task pair p = (k, l),
+// the two streams of dK = w_kl Re(W[l, k] dLambda[k, l] / dK_task[k, l]) = w_kl Re(W[l, k] (sqrt(n) scale P_kl +
+// noise [k == l])) for W = W1, W2 -- partials q = NQ + p and NQ + NP + p.  Thread it of the phase-3 loop holds pair
+// it / F in its slot it / kWG; a slot's F threads of a pair are summed in ascending f at the end (fixed order).
+constexpr int kMtSlots = (kMtMaxT * (kMtMaxT + 1) / 2 * kMtF + kWG - 1) / kWG;
+template <int D, bool GCV = false, bool CV = false, bool LEARN = false>
 __global__ __launch_bounds__(kWG) void k_mt_spec_iter(Nll a) {
   static_assert(!CV || GCV, "CV uses the GCV machinery");
+  static_assert(!LEARN || GCV, "a learned task kernel on the GCV / CV paths");
   constexpr int NS = 1 << D, NQ = GCV ? 6 + 2 * D : 4 + D;
   __shared__ double ls_pow[NS];                          // l^S
   __shared__ double kt[kMtMaxT * kMtMaxT];
@@ -1582,10 +1698,25 @@ __global__ __launch_bounds__(kWG) void k_mt_spec_iter(Nll a) {
       if ((tid >> j) & 1) pw *= h.ls[j];
     ls_pow[tid] = pw;
   }
-  if (tid < T * T) kt[tid] = a.mt_kt[tid];
+  if (tid < T * T) {
+    if constexpr (LEARN) {
+      // K_task[ka, kb] = sum_r F[ka, r] F[kb, r] + [ka == kb] v_ka (util.py:157-162, ascending r)
+      const int ka = tid / T, kb = tid - ka * T, R = a.mt_rank;
+      const double* Fm = a.raw + a.mt_f_off;
+      double s = 0.0;
+      for (int r = 0; r < R; ++r) s += Fm[ka * R + r] * Fm[kb * R + r];
+      if (ka == kb) s += a.mt_vexp ? exp(a.raw[a.mt_v_off + ka]) : a.raw[a.mt_v_off + ka];
+      kt[tid] = s;
+    } else {
+      kt[tid] = a.mt_kt[tid];
+    }
+  }
   const double rootn = sqrt((double)n), sn = rootn * h.scale;
   double acc_norm = 0.0, acc_ld = 0.0, acc_noise = 0.0, acc_sc = 0.0, acc_l[D];
   double acc_noise2 = 0.0, acc_sc2 = 0.0, acc_l2[D];     // (GCV: the S2 sums; acc_ld holds Tr)
+  double kta[LEARN ? kMtSlots : 1], ktb[LEARN ? kMtSlots : 1];   // LEARN: the pairs' dK streams, per slot
+#pragma unroll
+  for (int s2 = 0; s2 < (LEARN ? kMtSlots : 1); ++s2) kta[s2] = ktb[s2] = 0.0;
 #pragma unroll
   for (int m = 0; m < D; ++m) acc_l[m] = acc_l2[m] = 0.0;
   for (int c = 0; c < a.mt_cpb; ++c) {
@@ -1774,19 +1905,25 @@ __global__ __launch_bounds__(kWG) void k_mt_spec_iter(Nll a) {
     }
     __syncthreads();
     // (3) gradient: c = w_kl sqrt(n) scale Kt[k, l] W[l, k]; r_S = l^S Re(c Phi^{kl}_S)
-    for (int it = tid; it < NP * F; it += kWG) {
+    for (int it = tid, slot = 0; it < NP * F; it += kWG, ++slot) {
       const int p = it / F, f = it - p * F;
       int k, l;
       mt_pair_kl(p, T, k, l);
-      const double wgt = (k == l ? 0.5 : 1.0) * sn * kt[k * T + l];
+      const double wkl = (k == l ? 0.5 : 1.0);
+      const double wgt = wkl * sn * kt[k * T + l];
       const double2 w = wv[f][p];
       const double cx = wgt * w.x, cy = wgt * w.y;
       double c2x = 0.0, c2y = 0.0;
+      double2 w2v = make_double2(0.0, 0.0);
       if constexpr (GCV) {
         const double2 w2 = blk[f][p];
+        w2v = w2;
         c2x = wgt * w2.x;
         c2y = wgt * w2.y;
       }
+      // (LEARN: the same products without K_task -- d Lambda / d K_task)
+      const double ex = wkl * sn * w.x, ey = wkl * sn * w.y, e2x = wkl * sn * w2v.x, e2y = wkl * sn * w2v.y;
+      double rk1 = 0.0, rk2 = 0.0;
       const int64_t base = (int64_t)p * NS * n + j0 + f;
       constexpr int U = NS < 8 ? NS : 8;
 #pragma unroll 1
@@ -1807,9 +1944,46 @@ __global__ __launch_bounds__(kWG) void k_mt_spec_iter(Nll a) {
             for (int m = 0; m < D; ++m)
               if (m < 3 ? ((t >> m) & 1) : ((sh >> m) & 1)) acc_l2[m] += r2;
           }
+          if constexpr (LEARN) {
+            rk1 = __builtin_fma(ls_pow[S], ex * ph.x - ey * ph.y, rk1);
+            rk2 = __builtin_fma(ls_pow[S], e2x * ph.x - e2y * ph.y, rk2);
+          }
         }
       }
+      if constexpr (LEARN) {
+        if (k == l) {
+          rk1 += 0.5 * h.noise * w.x;
+          rk2 += 0.5 * h.noise * w2v.x;
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < kMtSlots; ++s2)
+          if (s2 == slot) {
+            kta[s2] += rk1;
+            ktb[s2] += rk2;
+          }
+      }
     }
+  }
+  if constexpr (LEARN) {
+    // the pairs' sums: slot s2 holds pairs kWG s2 / F .. (kWG s2 + kWG) / F - 1, F consecutive threads each
+    __shared__ double pr[kWG];
+    const int pc = kWG / F;
+    for (int s2 = 0; s2 < kMtSlots && (kWG * s2) / F < NP; ++s2)
+      for (int stream = 0; stream < 2; ++stream) {
+        __syncthreads();
+        double mine = 0.0;
+#pragma unroll
+        for (int u = 0; u < kMtSlots; ++u)
+          if (u == s2) mine = stream ? ktb[u] : kta[u];
+        pr[tid] = mine;
+        __syncthreads();
+        const int p = (kWG * s2) / F + tid;
+        if (tid < pc && p < NP) {
+          double sum = 0.0;
+          for (int f2 = 0; f2 < F; ++f2) sum += pr[tid * F + f2];
+          *part_ptr(a, CV ? tcv : 0, NQ + stream * NP + p, blockIdx.x) = sum;
+        }
+      }
   }
   double v[NQ];
   v[0] = acc_norm;
@@ -2099,6 +2273,15 @@ int launch_spec_loss_step(const Nll& a, const Fit& f, int iter, int do_update, h
   });
 }
 
+int launch_mt_learn_step(const Nll& a, const Fit& f, int iter, int do_update, hipStream_t st) {
+  if (a.mt > kMtMaxT || a.nb > kSpecBlocks || spec_nparams(a) > kSpecScratch)
+    return set_error(kErrInvalid, "k_mt_learn_step: shape");
+  return with_spec_d(a.d, [&](auto dc) {
+    k_mt_learn_step<decltype(dc)::value><<<1, kWG, 0, st>>>(a, f, iter, do_update);
+    return check_launch("k_mt_learn_step");
+  });
+}
+
 int64_t spec_chunks(bool net, int log2n) {
   const int64_t n = (int64_t)1 << log2n, K = net ? n : n / 2 + 1;
   return (K + 63) / 64;
@@ -2207,8 +2390,11 @@ int launch_spec_iter(const Nll& a, hipStream_t st, const FitFuse* fz) {
 
 int launch_mt_spec_iter(const Nll& a, hipStream_t st) {
   return with_spec_d(a.d, [&](auto dc) {
-    if (a.loss == FGP_LOSS_CV) k_mt_spec_iter<decltype(dc)::value, true, true><<<dim3((unsigned)a.nb, (unsigned)a.mt), kWG, 0, st>>>(a);
-    else if (a.loss == FGP_LOSS_GCV) k_mt_spec_iter<decltype(dc)::value, true><<<(unsigned)a.nb, kWG, 0, st>>>(a);
+    constexpr int DD = decltype(dc)::value;
+    if (a.loss == FGP_LOSS_CV && a.mt_learn) k_mt_spec_iter<DD, true, true, true><<<dim3((unsigned)a.nb, (unsigned)a.mt), kWG, 0, st>>>(a);
+    else if (a.loss == FGP_LOSS_CV) k_mt_spec_iter<DD, true, true><<<dim3((unsigned)a.nb, (unsigned)a.mt), kWG, 0, st>>>(a);
+    else if (a.loss == FGP_LOSS_GCV && a.mt_learn) k_mt_spec_iter<DD, true, false, true><<<(unsigned)a.nb, kWG, 0, st>>>(a);
+    else if (a.loss == FGP_LOSS_GCV) k_mt_spec_iter<DD, true><<<(unsigned)a.nb, kWG, 0, st>>>(a);
     else k_mt_spec_iter<decltype(dc)::value><<<(unsigned)a.nb, kWG, 0, st>>>(a);
     return check_launch("k_mt_spec_iter");
   });

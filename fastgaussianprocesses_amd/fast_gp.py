@@ -922,8 +922,9 @@ class AbstractFastGP(torch.nn.Module):
         if hists["noise"]:
             data["noise_hist"] = self.tf_noise(nz_raw.reshape((-1,) + self.raw_noise.shape)).cpu()
         if hists["task_kernel"]:
-            if hasattr(eng, "task_kernel_rows"):
-                data["task_kernel_hist"] = eng.task_kernel_rows(raw_hist).detach().cpu()
+            tkr = eng.task_kernel_rows(raw_hist) if hasattr(eng, "task_kernel_rows") else None
+            if tkr is not None:
+                data["task_kernel_hist"] = tkr.detach().cpu()
             else:
                 data["task_kernel_hist"] = self.gram_matrix_tasks.detach().cpu()[None].expand(
                     (i + 1,) + self.gram_matrix_tasks.shape).clone()
@@ -934,8 +935,9 @@ class AbstractFastGP(torch.nn.Module):
         (abstract_gp.py:285-296), the hyper-parameter-dependent caches dropped."""
         b_s, b_l, b_n = eng.split_raw(best_row)
         restore = [("raw_scale", b_s), ("raw_lengthscales", b_l), ("raw_noise", b_n)]
-        if hasattr(eng, "split_task"):                  # the general multitask engine also learns the task kernel
-            b_f, b_v = eng.split_task(best_row)
+        tsk = eng.split_task(best_row) if hasattr(eng, "split_task") else None
+        if tsk is not None:                             # a multitask engine that also learns the task kernel
+            b_f, b_v = tsk
             restore += [("raw_factor_task_kernel", b_f), ("raw_noise_task_kernel", b_v)]
         with torch.no_grad():
             for name, val in restore:

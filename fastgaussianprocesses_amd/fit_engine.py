@@ -207,6 +207,17 @@ class FusedMLL(object):
         self.n_params = S + Sl * Dl + Sn
         self.raw = torch.cat([raw_scale.reshape(-1), raw_lengthscales.reshape(-1), raw_noise.reshape(-1)]).to(
             device=self.device, dtype=torch.float64).contiguous()
+        tk = mt.get("task") if mt is not None else None
+        self.task = None
+        if tk is not None:
+            # a learned task kernel (ABI 18, GCV / CV): raw = [scale, lengthscales, noise, F [T][R], task noise [T]]
+            fr = tk["factor"].detach().to(device=self.device, dtype=torch.float64)
+            vr = tk["noise"].detach().to(device=self.device, dtype=torch.float64).reshape(-1)
+            T, R = fr.shape
+            self.task = dict(T=int(T), R=int(R), off=self.n_params, rg=tuple(bool(r) for r in tk["rg"]),
+                             vexp=bool(tk["vexp"]))
+            self.raw = torch.cat([self.raw, fr.reshape(-1), vr]).contiguous()
+            self.n_params += int(T) * (int(R) + 1)
         cdt = torch.complex128 if self.family == 0 else torch.float64
         self.work = torch.empty((G, n), dtype=cdt, device=self.device) if (self.m > 12 and basis is None and
                                                                            mt is None) else None
@@ -263,6 +274,11 @@ class FusedMLL(object):
             self._nll.mt_basis = self.mt["basis"].data_ptr()
             self._nll.mt_ytilde = self.mt["ytilde"].data_ptr()
             self._nll.mt_kt = self.mt["kt"].data_ptr()
+            if self.task is not None:
+                rg = self.task["rg"]
+                self._nll.mt_task_rg = int(rg[0]) | (int(rg[1]) << 1)
+                self._nll.mt_rank = self.task["R"]
+                self._nll.mt_vexp = int(self.task["vexp"])
         plen = ctypes.c_int64(0)
         N.call("fgp_nll_partials_len", self._nll, ctypes.byref(plen))
         self.partials = torch.empty((plen.value,), dtype=torch.float64, device=self.device)
@@ -522,6 +538,23 @@ class FusedMLL(object):
     def split_raw(self, raw_vec):
         S, L, Nn = self.sizes
         return raw_vec[..., :S], raw_vec[..., S:S + L], raw_vec[..., S + L:S + L + Nn]
+
+    def split_task(self, raw_vec):
+        """(raw task factor [.., T R], raw task noise [.., T]) of a learned task kernel's raw vector(s); None without."""
+        if self.task is None:
+            return None
+        o, T, R = self.task["off"], self.task["T"], self.task["R"]
+        return raw_vec[..., o:o + T * R], raw_vec[..., o + T * R:o + T * (R + 1)]
+
+    def task_kernel_rows(self, raw_rows):
+        """K_task = F F^T + diag(v) of every history row (util.py:157-162); None without a learned task kernel."""
+        if self.task is None:
+            return None
+        f, v = self.split_task(raw_rows)
+        T, R = self.task["T"], self.task["R"]
+        F = f.reshape(f.shape[:-1] + (T, R))
+        vv = torch.exp(v) if self.task["vexp"] else v
+        return torch.einsum("...il,...kl->...ik", F, F) + torch.diag_embed(vv)
 
 
 _ENGINES = collections.OrderedDict()

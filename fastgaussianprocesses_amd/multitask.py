@@ -356,6 +356,32 @@ class MultiTaskFastGP(AbstractFastGP):
         return tuple(self.raw_scale.shape) == (1,) and tuple(self.raw_noise.shape) == (1,) and \
             tuple(self.raw_lengthscales.shape) in ((1,), (self.d,))
 
+    def _mt_learn_ok(self):
+        """fit(loss_metric="GCV" / "CV") on the device with the task kernel LEARNED (ABI 18: k_mt_spec_iter's LEARN
+        variants + k_mt_learn_step; the reference's default for num_tasks > 1, abstract_gp.py:116-139): _mt_fused_ok's
+        domain except the fixed task kernel -- the factor [T, R] with the identity transform, the task noise [T] with the
+        exp or the identity transform, no parameter batch."""
+        if os.environ.get("FGP_MT_FUSED", "1")[:1] == "0":
+            return False
+        if not (self.raw_factor_task_kernel.requires_grad or self.raw_noise_task_kernel.requires_grad):
+            return False
+        ns = self._ns
+        n, T = ns[0], self.num_tasks
+        if not (n >= 16 and all(v == n for v in ns) and 2 <= T <= 8 and self.d <= 6):
+            return False
+        if self.adaptive_nugget or len(self.shape_batch):
+            return False
+        if any(self._tfs[k][1] is not _exp for k in ("scale", "lengthscales", "noise")):
+            return False
+        if self.tf_factor_task_kernel is not _identity or self.tf_noise_task_kernel not in (_exp, _identity):
+            return False
+        if tuple(self.raw_factor_task_kernel.shape[:-1]) != (T,) or tuple(self.raw_noise_task_kernel.shape) != (T,):
+            return False
+        if (T * (T + 1) // 2) * (1 << self.d) * n * 16 > MT_SPECTRA_CAP:
+            return False
+        return tuple(self.raw_scale.shape) == (1,) and tuple(self.raw_noise.shape) == (1,) and \
+            tuple(self.raw_lengthscales.shape) in ((1,), (self.d,))
+
     def _mt_param_rows(self):
         """Parameter batches (docs/examples/batch_multitask/fgp_lattice.ipynb cell 6; abstract_gp.py:73-139: each
         parameter's batch dimensions are the TRAILING dimensions of shape_batch): None when no parameter has batch
@@ -491,18 +517,24 @@ class MultiTaskFastGP(AbstractFastGP):
     def _fused_engine(self, iterations, lr, ysq=None, d_out=None, loss_metric="MLL", cv_weight=1.0):
         """FusedMLL in multitask spectral mode (G = 1; loss_metric MLL, GCV (ABI 17) or CV (ABI 18)); the general
         engine (MtGeneralEngine, MLL) outside its domain (_mt_fused_ok: equal n, fixed task kernel)."""
-        if not self._mt_fused_ok():
+        learn = loss_metric != "MLL" and not self._mt_fused_ok() and self._mt_learn_ok()
+        if not self._mt_fused_ok() and not learn:
             return MtGeneralEngine(self, lr, min(iterations + 1, 64))
         n, T = self._ns[0], self.num_tasks
         yt = torch.stack([self.get_ytilde(k).reshape(n) for k in range(T)])
         ls = self.raw_lengthscales.detach()
+        mt = dict(basis=self._mt_spectra(n), ytilde=yt, kt=self.gram_matrix_tasks.detach())
+        if learn:
+            # the task kernel's parameters in the engine's raw vector (FusedMLL: K_task formed on the device)
+            mt["task"] = dict(factor=self.raw_factor_task_kernel, noise=self.raw_noise_task_kernel,
+                              rg=(self.raw_factor_task_kernel.requires_grad, self.raw_noise_task_kernel.requires_grad),
+                              vexp=self.tf_noise_task_kernel is _exp)
         return FusedMLL(self._FAMILY, None, torch.zeros((1, n), device=self.device),
                         self.raw_scale.detach().reshape(-1), ls.reshape(1, -1), self.raw_noise.detach().reshape(-1),
                         logdet_weight=1.0, mll_const=mll_constant(1, T * n),
                         requires_grad=(self.raw_scale.requires_grad, self.raw_lengthscales.requires_grad,
                                        self.raw_noise.requires_grad),
-                        lr=lr, max_iters=min(iterations + 1, 64), loss_metric=loss_metric, cv_weight=cv_weight,
-                        mt=dict(basis=self._mt_spectra(n), ytilde=yt, kt=self.gram_matrix_tasks.detach()))
+                        lr=lr, max_iters=min(iterations + 1, 64), loss_metric=loss_metric, cv_weight=cv_weight, mt=mt)
 
     # ------------------------------------------------------------------ kernel parts and kernels
     # (_pair_spec, _kargs, _parts_pairs, _kernel_from_parts: AbstractFastGP, fast_gp.py)
@@ -772,8 +804,8 @@ class MultiTaskFastGP(AbstractFastGP):
         assert isinstance(stop_crit_wait_iterations, int) and stop_crit_wait_iterations > 0
         assert masks is None or isinstance(masks, torch.Tensor)
         loss_metric = loss_metric.upper()
-        alt_dev = (loss_metric in ("GCV", "CV") and default_optimizer and masks is None and self._mt_fused_ok()
-                   and os.environ.get("FGP_ALT_LOSS_DEVICE", "1")[:1] != "0")
+        alt_dev = (loss_metric in ("GCV", "CV") and default_optimizer and masks is None and
+                   (self._mt_fused_ok() or self._mt_learn_ok()) and os.environ.get("FGP_ALT_LOSS_DEVICE", "1")[:1] != "0")
         if loss_metric == "CV":
             # (one task: the reference's inv_diag is the single-task formula without the noise, util.py:383-386; a
             # per-point cv_weights needs the points' coefficients, not their Parseval sum)
@@ -787,7 +819,8 @@ class MultiTaskFastGP(AbstractFastGP):
                          scale=store_hists or (store_scale_hist and self.raw_scale.requires_grad),
                          lengthscales=store_hists or (store_lengthscales_hist and self.raw_lengthscales.requires_grad),
                          noise=store_hists or (store_noise_hist and self.raw_noise.requires_grad),
-                         task_kernel=store_hists)                # (the task kernel is fixed on this path)
+                         task_kernel=store_hists or (store_task_kernel_hist and (
+                             self.raw_factor_task_kernel.requires_grad or self.raw_noise_task_kernel.requires_grad)))
             return self._fit_fused(iterations, 1e-1 if lr is None else lr,
                                    (np.log(1 + stop_crit_improvement_threshold), stop_crit_wait_iterations), hists,
                                    verbose, verbose_indent, loss_metric=loss_metric,

@@ -259,6 +259,15 @@ typedef struct fgp_nll_desc {
    * one partials workgroup per (frequency block, task). */
   int loss_metric;
   double cv_weight;
+  /* ABI 18 -- a LEARNED task kernel on the multitask spectral path (GCV / CV, mt_tasks = T, equal n; the reference's
+   * default for num_tasks > 1, abstract_gp.py:116-139): mt_task_rg != 0 (bit 0: the factor, bit 1: the task noise
+   * require grad) makes K_task = F F^T + diag(v) from raw itself -- raw = [scale, lengthscales, noise, F [T][mt_rank],
+   * task noise [T]], v = exp (mt_vexp = 1) or the identity of the raw task noise; mt_kt is then not read -- and adds
+   * the task parameters' closed-form gradients (dL/dK_task per task pair, the chain rule through F F^T + diag(v)) and
+   * their Rprop steps (fgp_fit_desc.n_params covers them). */
+  int mt_task_rg;
+  int mt_rank;
+  int mt_vexp;
 } fgp_nll_desc;
 
 #define FGP_LOSS_MLL 0

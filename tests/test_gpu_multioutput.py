@@ -212,8 +212,9 @@ def _sharded_worker(rank, world, port, B, m, d, its, q):
         x = gp.get_x_next(n).cpu()
         gp.add_y_next(_c5_data(x, B)[a:b].to("cuda:0"))
         data = fit_sharded(gp, B, iterations=its, store_loss_hist=True, stop_crit_wait_iterations=10)
-        q.put((rank, data["iterations"], data["loss_hist"].clone(), gp.raw_lengthscales.detach().cpu().clone(),
-               gp.raw_scale.detach().cpu().clone()))
+        # (numpy by value: a tensor would travel as a shared file descriptor, lost if the worker exits first)
+        q.put((rank, data["iterations"], data["loss_hist"].numpy().copy(), gp.raw_lengthscales.detach().cpu().numpy().copy(),
+               gp.raw_scale.detach().cpu().numpy().copy()))
     finally:
         dist.destroy_process_group()
 
@@ -238,6 +239,7 @@ def test_fit_sharded_two_processes_equals_unsharded(B, m, its):
     full.add_y_next(_c5_data(x, B).to(DEV))
     ref = full.fit(iterations=its, verbose=0, store_loss_hist=True, stop_crit_wait_iterations=10)
     for _, its, lh, ls, sc in res:
+        lh, ls, sc = torch.from_numpy(lh), torch.from_numpy(ls), torch.from_numpy(sc)
         assert its == ref["iterations"]
         assert rel_err(lh, ref["loss_hist"]) < 1e-10           # Y summed in another order
         assert rel_err(ls, full.raw_lengthscales) < 1e-10

@@ -68,7 +68,7 @@ def _ysq_worker(rank, world, port, q):
     yt = ft_stable(y[a:b], fftbr)
     ysq = (yt.abs() ** 2).sum(0)
     allreduce_sum_(ysq)
-    q.put((rank, (a, b), ysq))
+    q.put((rank, (a, b), ysq.numpy().copy()))   # (by value: a tensor would travel as a shared fd, lost at exit)
     dist.destroy_process_group()
 
 
@@ -89,8 +89,9 @@ def test_two_rank_multi_output_ysq_allreduce():
     torch.manual_seed(5)
     y = torch.randn(7, 64, dtype=torch.float64)
     full = (ft_stable(y, fftbr).abs() ** 2).sum(0)
-    assert torch.equal(res[0][2], res[1][2])               # every rank holds the same Y
-    assert torch.allclose(res[0][2], full, rtol=1e-13, atol=0)
+    r0, r1 = torch.from_numpy(res[0][2]), torch.from_numpy(res[1][2])
+    assert torch.equal(r0, r1)                             # every rank holds the same Y
+    assert torch.allclose(r0, full, rtol=1e-13, atol=0)
 
 
 def test_output_shard_partition():
