@@ -179,9 +179,13 @@ class SingleGP(object):
         gp._y[0] = gp._y[0][..., :0]
         gp._nh = 0
         gp.add_y_next(self.y)
+        # fresh initial parameters: one copy of the three, each a Parameter over its slice
+        flat = torch.cat([v.reshape(-1) for v in self.raw0])
+        o = 0
         for name, v in zip(("raw_scale", "raw_lengthscales", "raw_noise"), self.raw0):
             old = getattr(gp, name)
-            setattr(gp, name, torch.nn.Parameter(v.clone(), requires_grad=old.requires_grad))
+            setattr(gp, name, torch.nn.Parameter(flat[o:o + v.numel()].view(v.shape), requires_grad=old.requires_grad))
+            o += v.numel()
         gp._cache, gp._snap = {}, None
 
 

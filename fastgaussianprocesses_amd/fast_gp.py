@@ -140,6 +140,9 @@ class AbstractFastGP(torch.nn.Module):
     _XBDTYPE = None
     _FTOUTDTYPE = None
     _MULTITASK = False
+    # host-side attributes the fit / ingest path reassigns on every call (never Parameters, buffers or sub-modules)
+    _PLAIN_ATTRS = frozenset(("_cache", "_snap", "_nh", "_y", "_yt_state", "_n_t", "_m_t", "_iters_for_log",
+                              "_pgen_memo", "_task_unit_memo", "_pts_T", "_pts_n", "_x", "_xb"))
 
     def __new__(cls, *args, **kwargs):
         if not cls._MULTITASK and cls._FAMILY is not None and _wants_multitask(cls, args, kwargs):
@@ -252,6 +255,44 @@ class AbstractFastGP(torch.nn.Module):
         self._parts = {}       # n -> [d, n] first-column parts
         self._cache = {}       # derived quantities keyed by (name, n) + parameter snapshot
         self._snap = None
+
+    def __setattr__(self, name, value):
+        """nn.Module.__setattr__ costs ~3 us a call (its Parameter / buffer / sub-module bookkeeping) and a fit + ingest
+        makes ~20 of them: the plain host attributes above are set directly, and a Parameter replacing an existing one
+        (AbstractGP.fit's best-iterate restore, abstract_gp.py:295-296) goes straight into _parameters, which is where
+        register_parameter would put it (global parameter-registration hooks are not run for such replacements)."""
+        if name in self._PLAIN_ATTRS:
+            object.__setattr__(self, name, value)
+        elif type(value) is torch.nn.Parameter and name in self.__dict__["_parameters"]:
+            self.__dict__["_parameters"][name] = value
+        else:
+            super().__setattr__(name, value)
+
+    @property
+    def n(self):
+        """Samples so far ([1] int64 on the device, the reference's gp.n): formed when first read after add_y_next
+        (the fit path reads the host mirror _nh; two device fills per ingest saved)."""
+        t = self._n_t
+        if t is None:
+            t = self._n_t = torch.full((1,), self._nh, dtype=torch.int64, device=self.device)
+        return t
+
+    @n.setter
+    def n(self, v):
+        self._n_t = v
+
+    @property
+    def m(self):
+        """log2 of n ([1] int64 on the device, -1 without samples), formed on first read like n."""
+        t = self._m_t
+        if t is None:
+            t = self._m_t = torch.full((1,), self._nh.bit_length() - 1 if self._nh > 0 else -1, dtype=torch.int64,
+                                       device=self.device)
+        return t
+
+    @m.setter
+    def m(self, v):
+        self._m_t = v
 
     # ------------------------------------------------------------------ construction helpers
     def _resolve_seq(self, seqs, seed_for_seq):
@@ -423,9 +464,8 @@ class AbstractFastGP(torch.nn.Module):
             self._yt_state = None           # only an append keeps the cached prefix transform valid
         self._y[0] = torch.cat([self._y[0].to(self.data_dtype), y], -1)
         self._nh = int(self._y[0].size(-1))
-        # device fills, not host->device copies (a pageable copy blocks the host)
-        self.n = torch.full((1,), self._nh, dtype=torch.int64, device=self.device)
-        self.m = torch.full((1,), self._nh.bit_length() - 1 if self._nh > 0 else -1, dtype=torch.int64, device=self.device)
+        # gp.n / gp.m: device fills on first read (properties above), not host->device copies (a pageable copy blocks)
+        self._n_t = self._m_t = None
         self._cache = {}
         assert self._nh == 0 or (self._nh & (self._nh - 1)) == 0, "total samples must be power of 2"
 
@@ -939,10 +979,11 @@ class AbstractFastGP(torch.nn.Module):
         if tsk is not None:                             # a multitask engine that also learns the task kernel
             b_f, b_v = tsk
             restore += [("raw_factor_task_kernel", b_f), ("raw_noise_task_kernel", b_v)]
+        params = self._parameters
         with torch.no_grad():
             for name, val in restore:
-                old = getattr(self, name)
-                setattr(self, name, torch.nn.Parameter(val.reshape(old.shape).clone(), requires_grad=old.requires_grad))
+                old = params[name]
+                params[name] = torch.nn.Parameter(val.reshape(old.shape).clone(), requires_grad=old.requires_grad)
         self._cache = {k: v for k, v in self._cache.items() if not k[2]}    # keep data-only entries (ytilde, spectra)
         self._snap = None
 

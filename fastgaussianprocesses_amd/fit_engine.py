@@ -99,6 +99,21 @@ def spectral_wanted(family, n, d, G, nbases=1):
     return t_spec < t_tr and (2 ** d) * nbases * K * 8 <= (16 << 30)
 
 
+_SPEC_WORK = {}
+
+
+def _spec_work_bytes(family, m, d):
+    """Work bytes of fgp_spec_basis(_gen) for (family, log2 n, d): one subset's transform at least, all 2^d at
+    once up to SPEC_WORK_CAP (fgp_spec_basis_work; memoised, a pure function of its arguments)."""
+    key = (int(family), int(m), int(d))
+    w = _SPEC_WORK.get(key)
+    if w is None:
+        total = ctypes.c_int64(0)
+        N.call("fgp_spec_basis_work", key[0], key[1], key[2], ctypes.byref(total))
+        w = _SPEC_WORK[key] = max(total.value >> d, min(total.value, SPEC_WORK_CAP))
+    return w
+
+
 def spec_basis(family, parts, n):
     """Part-product spectra (fgp_spec_basis): parts [d, n] -> [Q, 2^d, 64], or [P, d, n] -> [P, Q, 2^d, 64]
     (chunks of 64 frequencies; spec_dense gives [2^d, K]); lambda = scale sum_S l^S Phi_S for every
@@ -109,10 +124,7 @@ def spec_basis(family, parts, n):
     m = log2_exact(n)
     P = parts.shape[0] if parts.dim() == 3 else 1
     Q = spec_chunks(family, n)
-    total = ctypes.c_int64(0)
-    N.call("fgp_spec_basis_work", int(family), m, int(d), ctypes.byref(total))
-    one = total.value >> d
-    wbytes = max(one, min(total.value, SPEC_WORK_CAP))
+    wbytes = _spec_work_bytes(family, m, d)
     work = torch.empty((wbytes,), dtype=torch.uint8, device=parts.device)
     out = torch.empty(((P,) if parts.dim() == 3 else ()) + (Q, 2 ** d, 64), dtype=torch.float64, device=parts.device)
     N.call("fgp_spec_basis", int(family), N.ptr(parts), d * n, P, m, int(d), N.ptr(out), N.ptr(work), wbytes,
@@ -131,10 +143,7 @@ def spec_basis_gen(gen, n, device, force=False):
     if not on or not (17 <= m <= 24) or d > 6 or len(set(int(a) for a in gen.alphas)) != 1:
         return None
     Q = spec_chunks(LATTICE, n)
-    total = ctypes.c_int64(0)
-    N.call("fgp_spec_basis_work", LATTICE, m, int(d), ctypes.byref(total))
-    one = total.value >> d
-    wbytes = max(one, min(total.value, SPEC_WORK_CAP))
+    wbytes = _spec_work_bytes(LATTICE, m, d)
     work = torch.empty((wbytes,), dtype=torch.uint8, device=device)
     out = torch.empty((Q, 2 ** d, 64), dtype=torch.float64, device=device)
     N.call("fgp_spec_basis_gen", N.int64_array(gen.z), m, int(d), 2 * int(gen.alphas[0]),
@@ -324,6 +333,7 @@ class FusedMLL(object):
         group's HBM-bound column kernel (measured slower, see groups()).  Every problem's arithmetic is
         the same as in the single launch sequence (bit-identical results)."""
         self.ensure_history(iter0 + iters)
+        self._raw_entry = None
         groups = self.groups()
         if groups <= 1:
             if iters >= FIT_GRAPH_MIN_ITERS and os.environ.get("FGP_FIT_GRAPH", "1")[:1] != "0":
@@ -367,7 +377,11 @@ class FusedMLL(object):
         else:
             self.ysq.copy_(ysq)
         self.ysq_rows = ysq
-        self.raw.copy_(torch.cat([raw_scale.reshape(-1), raw_lengthscales.reshape(-1), raw_noise.reshape(-1)]))
+        src = [raw_scale.reshape(-1), raw_lengthscales.reshape(-1), raw_noise.reshape(-1)]
+        torch.cat(src, out=self.raw)
+        # run_persist's entry state (a barrier give-up restores it): the caller's tensors themselves, not a copy (the
+        # fit replaces a GP's Parameters by new ones, abstract_gp.py:295-296, it never writes into them)
+        self._raw_entry = src
         self.prev.zero_()
         self.step.fill_(float(lr))
 
@@ -404,9 +418,12 @@ class FusedMLL(object):
         all be co-resident on this device)."""
         if os.environ.get("FGP_FIT_PERSIST", "1")[:1] == "0" or self.G != 1 or not self._nll.basis:
             return 0
-        ok = ctypes.c_int(0)
-        N.call("fgp_fit_persist_ok", self._nll, ctypes.byref(ok))
-        return ok.value
+        wg = getattr(self, "_persist_wg", None)      # (a function of the engine's geometry and the device only)
+        if wg is None:
+            ok = ctypes.c_int(0)
+            N.call("fgp_fit_persist_ok", self._nll, ctypes.byref(ok))
+            wg = self._persist_wg = ok.value
+        return wg
 
     def run_persist(self, iterations, logtol, wait_max, defer=False):
         """AbstractGP.fit's iterations 0 .. iterations with its early-stopping rule, in one launch
@@ -424,7 +441,8 @@ class FusedMLL(object):
         self.ensure_history(iterations + 1)
         ctrl = torch.empty((4,), dtype=torch.int32, device=self.device)   # (the launch clears the words it reports)
         capturing = torch.cuda.is_current_stream_capturing()
-        raw0 = None if capturing else self.raw.clone()
+        entry, self._raw_entry = getattr(self, "_raw_entry", None), None
+        raw0 = None if capturing else (entry if entry is not None else self.raw.clone())
         N.call("fgp_fit_persist", self._nll, self._fit, int(iterations), float(logtol), int(wait_max),
                ctrl.data_ptr(), self.stream())
         if capturing:
@@ -440,7 +458,10 @@ class FusedMLL(object):
         self._pending = None
         c = ctrl.cpu().tolist()
         if c[2]:
-            self.raw.copy_(raw0)
+            if isinstance(raw0, list):
+                torch.cat(raw0, out=self.raw)
+            else:
+                self.raw.copy_(raw0)
             self.persist_failures = getattr(self, "persist_failures", 0) + 1
             return None
         return int(c[1])
@@ -519,6 +540,7 @@ class FusedMLL(object):
     def evaluate(self, slot=0):
         """Loss terms and gradient at the current raw parameters (no update); synchronises."""
         self.ensure_history(slot + 1)
+        self._raw_entry = None
         st = self.stream()
         N.call("fgp_nll_fwd", self._nll, st)
         N.call("fgp_nll_bwd", self._nll, st)
@@ -529,6 +551,7 @@ class FusedMLL(object):
     def fit_step(self, slot, update=True):
         """Enqueue the reduction + Rprop step of history slot `slot` (fgp_fit_step)."""
         self.ensure_history(slot + 1)
+        self._raw_entry = None
         N.call("fgp_fit_step", self._nll, self._fit, int(slot), int(bool(update)), self.stream())
 
     def stage(self, k):

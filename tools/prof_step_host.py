@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--family", default="lattice")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--detail", action="store_true", help="also print the callees of the fit's host functions")
     args = ap.parse_args()
     import bench
     import fastgaussianprocesses_amd as F
@@ -95,6 +96,11 @@ def main():
     print("%9s %9s %6s  %s" % ("cum_us/5", "self_us/5", "calls", "function"))
     for (fn, ln, name), (cc, nc, tt, ct, _) in rows:
         print("%9.1f %9.1f %6d  %s:%d(%s)" % (ct * 2e5, tt * 2e5, nc, os.path.basename(fn), ln, name))
+    if args.detail:
+        ps = pstats.Stats(pr)
+        for fn in ("_fused_engine", "_spec_basis", "_ysq", "cached_engine", "refill", "reset", "add_y_next",
+                   "_restore_best", "run_persist", "persist_result", "_parts_gen", "spec_basis_gen", "fit"):
+            ps.print_callees(r"\b%s\b" % fn)
 
 
 if __name__ == "__main__":
