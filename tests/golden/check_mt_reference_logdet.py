@@ -1,4 +1,14 @@
-import sys, os; sys.path.insert(0,'.'); sys.path.insert(0,'tests/golden')
+"""Reproduces the note in tests/test_oracle_multitask.py: the REAL reference's multitask inverse / logdet cache for a
+derivative-informed lattice GP (T = 3, d = 2, n = 128 per task) against a dense per-frequency block check, run in the
+build container through oracle/refshim (it prints the three logdets, which agree to 1e-10).
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/check_mt_reference_logdet.py
+"""
+import os
+import sys
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+sys.path.insert(0, HERE)
 import torch, numpy as np
 torch.set_default_dtype(torch.float64)
 from oracle.refshim.load_reference import import_reference

@@ -17,7 +17,7 @@ MT_NAMES = golden_names(multitask=True)
 # reference's unpivoted complex Schur recursion (util.py:301-323) pivots on it and its complement S
 # comes out as 0.0049 - 0.0039i, where a Hermitian matrix's Schur complement is real.  Its logdet is
 # -1381.633 against -1382.114 from slogdet, eigvalsh and Cholesky of the very same lams blocks (all
-# three agree to 1e-10; tools/diag_mt_reference.py reproduces this).  Quantities that go through the
+# three agree to 1e-10; tests/golden/check_mt_reference_logdet.py reproduces this).  Quantities that go through the
 # inverse are therefore compared at that error; everything before the inverse (parts, lam, ytilde)
 # at the usual tolerances.
 REF_INVERSE_ERROR = {"deriv_lattice_d2_a3_equal": 2e-2}
