@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--detail", action="store_true", help="also print the callees of the fit's host functions")
+    ap.add_argument("--segments", action="store_true",
+                    help="host time of each piece of the eager fit, called one by one (no profiler overhead)")
     args = ap.parse_args()
     import bench
     import fastgaussianprocesses_amd as F
@@ -84,6 +86,8 @@ def main():
     print(json.dumps({"family": args.family, "eager_events_ms_median": ev[len(ev) // 2],
                       "eager_host_ms_median": 1e3 * walls[len(walls) // 2], "graph_ms": gms, "graph_after_idle_ms_median": gap[len(gap) // 2] if gap else None,
                       "graph_info": info, "persist_giveups_during_replays": gu1 - gu0}), flush=True)
+    if args.segments:
+        segments(sg, args)
     pr = cProfile.Profile()
     torch.cuda.synchronize()
     pr.enable()
@@ -101,6 +105,41 @@ def main():
         for fn in ("_fused_engine", "_spec_basis", "_ysq", "cached_engine", "refill", "reset", "add_y_next",
                    "_restore_best", "run_persist", "persist_result", "_parts_gen", "spec_basis_gen", "fit"):
             ps.print_callees(r"\b%s\b" % fn)
+
+
+def segments(sg, args):
+    """Median host microseconds of the pieces FastGP.fit runs before / after the single-launch fit's launch, each
+    called on its own (the device drained before each rep, so a piece's time is its host work + launch calls)."""
+    import math
+    gp = sg.gp
+    rows = {}
+
+    def t(name, fn):
+        t0 = time.perf_counter()
+        r = fn()
+        rows.setdefault(name, []).append(1e6 * (time.perf_counter() - t0))
+        return r
+    for _ in range(args.reps):
+        torch.cuda.synchronize()
+        t("reset (bench)", sg.reset)
+        n = gp._nh
+        t("fit checks (_fused_ok)", gp._fused_ok)
+        t("spectra (_spec_basis)", lambda: gp._spec_basis(n, 1))
+        t("ytilde (get_ytilde)", gp.get_ytilde)
+        t("Y (_ysq)", lambda: gp._ysq(None, 1))
+        eng = t("engine (_fused_engine, inputs cached)", lambda: gp._fused_engine(args.iters, 0.1))
+        t("persist launch (run_persist)", lambda: eng.run_persist(args.iters, math.log(1.05), args.iters + 1, defer=True))
+        t("restore best (_restore_best)", lambda: gp._restore_best(eng, eng.raw))
+        t("control word (persist_result, waits)", eng.persist_result)
+        eng.release_inputs()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        sg.reset()
+        gp.fit(iterations=args.iters, stop_crit_wait_iterations=args.iters + 1, verbose=0)
+        rows.setdefault("whole reset + fit (host, until return)", []).append(1e6 * (time.perf_counter() - t0))
+    for k, v in rows.items():
+        v.sort()
+        print("%-44s %8.1f us" % (k, v[len(v) // 2]), flush=True)
 
 
 if __name__ == "__main__":
