@@ -150,6 +150,33 @@ def test_doctest_invariants(family):
     assert torch.allclose(gp.post_cubature_var(), pcvar_f)
 
 
+@pytest.mark.parametrize("family", ["lattice", "net"])
+def test_module_attributes_after_ingest_and_fit(family):
+    """gp.n / gp.m (formed on first read after add_y_next) and the Parameters fit() leaves behind (new Parameter
+    objects, abstract_gp.py:295-296, set past nn.Module.__setattr__): registered, the entry ones untouched."""
+    d = 3
+    gp = F.FastGPLattice(F.Lattice(d, seed=7), device=DEV) if family == "lattice" else \
+        F.FastGPDigitalNetB2(F.DigitalNetB2(d, seed=7), device=DEV)
+    assert gp.n.tolist() == [0] and gp.m.tolist() == [-1]
+    from oracle.fgp_oracle import f_ackley
+    gp.add_y_next(f_ackley(gp.get_x_next(2 ** 12)))
+    assert gp.n.tolist() == [2 ** 12] and gp.m.tolist() == [12] and gp.n.device.type == "cuda"
+    gp.add_y_next(f_ackley(gp.get_x_next(2 ** 13)))        # (the points 2^12 .. 2^13)
+    assert gp.n.tolist() == [2 ** 13] and gp.m.tolist() == [13]
+    before = {k: (p, p.detach().clone()) for k, p in gp.named_parameters()}
+    gp.fit(iterations=10, verbose=0)
+    after = dict(gp.named_parameters())
+    assert set(after) == set(before) and set(gp.state_dict()) == set(before)
+    for k in ("raw_scale", "raw_lengthscales", "raw_noise"):
+        p = getattr(gp, k)
+        assert type(p) is torch.nn.Parameter and p is after[k] and p is not before[k][0]
+        assert torch.equal(before[k][0].detach(), before[k][1])          # the entry Parameter is not written into
+        assert p.requires_grad == before[k][0].requires_grad
+    assert not torch.equal(gp.raw_lengthscales.detach(), before["raw_lengthscales"][1])   # the fit moved them
+    gp.n = torch.tensor([5], device=DEV)                                  # assignable, as in the reference
+    assert gp.n.tolist() == [5]
+
+
 @pytest.mark.parametrize("family,m", [("lattice", 10), ("lattice", 14), ("net", 13)])
 def test_fit_batched_equals_individual_fits(family, m):
     """fit_batched (one fused device loop over independent GPs) returns exactly what each GP's own
