@@ -567,7 +567,16 @@ class AbstractFastGP(torch.nn.Module):
                 b = spec_basis_gen(gen, n, self.device)      # the parts regenerated in the transform
                 if b is not None:
                     return b
-            parts = ops.lattice_parts_gen(gen.z, gen.shift[0], gen.alphas, n) if gen is not None else self._k1parts(n)
+            if gen is not None:
+                # the regenerated parts, kept per n like the parts array (_k1parts): a function of the points only,
+                # so a later add_y_next at this n (or new data at the same points) does not regenerate them
+                memo = self.__dict__.setdefault("_parts_regen", {})
+                hit = memo.get(n)
+                if hit is None or hit[0] is not gen:
+                    hit = memo[n] = (gen, ops.lattice_parts_gen(gen.z, gen.shift[0], gen.alphas, n))
+                parts = hit[1]
+            else:
+                parts = self._k1parts(n)
             return spec_basis(self._FAMILY, parts, n)
         return self._cached(("basis", n), f, grad_sensitive=False)
 

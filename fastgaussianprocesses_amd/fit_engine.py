@@ -240,6 +240,7 @@ class FusedMLL(object):
         st = blob[:3 * np_].view(3, np_)
         st[1].fill_(float(lr))
         self.prev, self.step, self.grad = st[0], st[1], st[2]
+        self._rprop_state = st[:2]                      # (prev, step) adjacent: refill resets both with one copy
         self.loss_hist = blob[3 * np_:3 * np_ + hmax * hg * 3].view(hmax, hg, 3)
         self.raw_hist = blob[3 * np_ + hmax * hg * 3:].view(hmax, np_)
         self.max_iters = hmax
@@ -382,8 +383,12 @@ class FusedMLL(object):
         # run_persist's entry state (a barrier give-up restores it): the caller's tensors themselves, not a copy (the
         # fit replaces a GP's Parameters by new ones, abstract_gp.py:295-296, it never writes into them)
         self._raw_entry = src
-        self.prev.zero_()
-        self.step.fill_(float(lr))
+        init = getattr(self, "_rprop_init", None)      # [[0 ...], [lr ...]] on the device, kept per lr
+        if init is None or init[0] != float(lr):
+            t = torch.zeros_like(self._rprop_state)
+            t[1].fill_(float(lr))
+            init = self._rprop_init = (float(lr), t)
+        self._rprop_state.copy_(init[1])
 
     def release_inputs(self):
         """Drop the references to the fit's inputs (spectra, Y rows) after the fit is enqueued: a cached engine must not
