@@ -113,6 +113,38 @@ __device__ __forceinline__ void spec_terms(const double* phi, const Hyp& h, doub
   for (int j = 0; j < D; ++j) acc.gl[j] = __builtin_fma(g, dp[j], acc.gl[j]);
 }
 
+// spec_terms split in two (k_spec_persist): the per-frequency values of a chunk, then their accumulation -- two chunks'
+// values computed side by side (independent chains a single wave per SIMD can overlap) and accumulated in chunk
+// order, so the sums are spec_terms' bit for bit.
+template <int D>
+struct SpecTerm {
+  double Y, r, m, g, P;
+  double dp[D];
+  int ex;
+};
+
+template <int D>
+__device__ __forceinline__ void spec_term_values(const double* phi, const Hyp& h, double rootn, double wl, double Y,
+                                                 SpecTerm<D>& t) {
+  t.P = mlin<D>(phi, h.ls, t.dp);
+  const double e = __builtin_fma(rootn, h.scale * t.P, h.noise);
+  t.r = rcp_nr(e);
+  t.Y = Y;
+  t.m = frexp(fabs(e), &t.ex);
+  t.g = t.r * __builtin_fma(-Y, t.r, wl);
+}
+
+template <int D>
+__device__ __forceinline__ void spec_term_add(const SpecTerm<D>& t, SpecAcc<D>& acc) {
+  acc.norm = __builtin_fma(t.Y, t.r, acc.norm);
+  acc.mant *= t.m;
+  acc.ex += t.ex;
+  acc.ge += t.g;
+  acc.gs = __builtin_fma(t.g, t.P, acc.gs);
+#pragma unroll
+  for (int j = 0; j < D; ++j) acc.gl[j] = __builtin_fma(t.g, t.dp[j], acc.gl[j]);
+}
+
 // One lane of a double through a DPP pattern (two 32-bit moves; every source lane valid for the patterns used)
 template <int CTRL>
 __device__ __forceinline__ double dpp_f64(double v) {
@@ -774,14 +806,25 @@ __global__ __launch_bounds__(kWG) void k_spec_persist(Nll a, Fit f, int iters, d
       if (blk >= a.nb) break;
       SpecAcc<D> acc;
       const double* lb = lds + (int64_t)t * per_blk;
-      for (int i = 0; i < kpl; ++i) {
+      // two chunks per pass: both chunks' terms first, then their accumulation in chunk order (spec_term_*)
+      for (int i = 0; i < kpl; i += 2) {
         const int64_t k = (int64_t)blk * B + lane + 64 * i;
         if (k >= main) break;
-        const double* cb = lb + i * (NS + 1) * 64 + lane;
-        double phi[NS];
+        const bool two = i + 1 < kpl && k + 64 < main;
+        const double* cb0 = lb + i * (NS + 1) * 64 + lane;
+        const double* cb1 = two ? cb0 + (NS + 1) * 64 : cb0;
+        double phi0[NS], phi1[NS];
 #pragma unroll
-        for (int s = 0; s < NS; ++s) phi[s] = cb[64 * s];
-        spec_terms<D>(phi, h, rootn, wl, cb[64 * NS], acc);
+        for (int s = 0; s < NS; ++s) {
+          phi0[s] = cb0[64 * s];
+          phi1[s] = cb1[64 * s];
+        }
+        SpecTerm<D> t0, t1;
+        spec_term_values<D>(phi0, h, rootn, wl, cb0[64 * NS], t0);
+        spec_term_values<D>(phi1, h, rootn, wl, cb1[64 * NS], t1);
+        spec_term_add<D>(t0, acc);
+        if (!two) break;
+        spec_term_add<D>(t1, acc);
       }
       spec_block_partials<D, NET>(a, h, 0, blk, rootn, wl, acc, !single, pbase, corr);
     }
